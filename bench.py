@@ -1,0 +1,215 @@
+"""Benchmark: BASELINE.json metric — cell-updates/s (node) for 3-D advection
+with halo exchange, and the % of HBM roofline of the advection sweep kernel.
+
+Workload (BASELINE config 3, tests/advection): level-0 base 128 x 128 x
+(128 * N) with cubic cells of length 1/128, maximum refinement level 2
+(512^3-equivalent per GPU), neighborhood length 0 (face neighbors), periodic
+in x and y, non-periodic in z, the reference's initial condition (hump +
+rotating velocity, tests/advection/initialize.hpp) and its pre-refinement
+criterion (adapter.hpp check_for_adaptation, refine side).  The mesh is then
+frozen; one step = halo update of the density (RCCL, N > 1) overlapped with
+the inner-cell sweep, then the outer-cell sweep, fused flux + apply.  Weak
+scaling: every GPU owns one 128^3-base slab (block partition of level-0 ids,
+children inherit the owner).
+
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+NAMES = ("density", "vx", "vy", "vz", "lx", "ly", "lz")
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--base", type=int, default=128, help="level-0 cells per dimension per GPU")
+    p.add_argument("--max-ref-lvl", type=int, default=2)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    return p.parse_args()
+
+
+def build_grid(dccrg_amd, rank, size, base, R, uid):
+    nx, ny, nz = base, base, base * size
+    g = dccrg_amd.Dccrg(rank, size, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g.set_initial_length((nx, ny, nz)).set_neighborhood_length(0).set_maximum_refinement_level(R)
+    g.set_periodic(True, True, False).initialize()
+    g.set_geometry((0.0, 0.0, 0.0), (1.0 / nx, 1.0 / ny, 1.0 / nx))
+    f = [g.add_field(n, np.float64, n == "density") for n in NAMES]
+    # pre-refinement (tests/advection/2d.cpp:260-285), refine side
+    for _ in range(R):
+        g.advection_initialize(f)
+        for c in g.advection_refine_candidates(f[0], 0.025 / R, 0.25):
+            g.refine_completely(int(c))
+        g.stop_refining()
+    g.advection_initialize(f)
+    return g, f
+
+
+def cpu_baseline(seconds):
+    """The oracle (CPU restatement, one core) on a bounded sample of the same
+    workload: 32 x 32 x 4 base, R = 2, same pre-refinement, time steps until
+    ~`seconds` of CPU time."""
+    from oracle import oracle as O
+
+    base = (32, 32, 4)
+    o = O.Grid(base, 2, (True, True, False), 0, 1)
+    o.set_geometry((0, 0, 0), (1 / 32, 1 / 32, 1 / 32))
+    o.adv_prerefine(0.025, 0.25)
+    ids, _ = o.cells()
+    dt = o.adv_max_time_step()
+    o.adv_steps(1, 0.5 * dt)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.adv_steps(5, 0.5 * dt)
+        steps += 5
+    el = time.perf_counter() - t0
+    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
+                sample=f"oracle restatement, 32x32x4 base R=2 pre-refined ({ids.size} cells), {steps} steps, "
+                       f"{el:.1f} s on 1 host core")
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    import dccrg_amd
+
+    uid = None
+    if world > 1:
+        obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+
+    t_setup = time.perf_counter()
+    g, f = build_grid(dccrg_amd, rank, world, a.base, a.max_ref_lvl, uid)
+    setup_s = time.perf_counter() - t_setup
+    dt = 0.5 * g.advection_max_time_step(f)  # cfl 0.5 (2d.cpp:121-123)
+    c = g.counts
+    n_local = c["inner"] + c["outer"]
+    ptr, _, _ = g.csr("face")
+    face_entries = int(ptr[-1])
+
+    def step():
+        g.start_remote_neighbor_copy_updates()
+        g.advection_step(f, dt, "inner")
+        g.wait_remote_neighbor_copy_update_receives()
+        g.advection_step(f, dt, "outer")
+        g.wait_remote_neighbor_copy_update_sends()
+        g.advection_commit(f[0])
+
+    for _ in range(a.warmup):
+        step()
+    g.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    g.kernel_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    g.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms, kern_n = g.kernel_timing(0)
+
+    stats = torch.tensor([el, float(n_local), float(c["recv"]), kern_ms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el_max, total_cells = float(mx[0]), int(sm[1])
+    else:
+        el_max, total_cells = el, n_local
+
+    # algorithmic bytes of the sweep per local cell:
+    # read density, vx, vy, vz, lx, ly, lz + write density = 64 B, plus the
+    # face CSR (4 B per entry, 4 B row pointer)
+    alg_bytes_step = 64 * n_local + 4 * face_entries + 4 * (n_local + 1)
+    kern_s = kern_ms / 1e3
+    achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
+    launches_per_step = kern_n / a.steps if a.steps else 0
+
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a.cpu_seconds)
+
+    if rank == 0:
+        value = total_cells * a.steps / el_max
+        line = {
+            "metric": "cell-updates/s (node) for 3D advection w/ halo exchange; % of HBM roofline",
+            "value": value,
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": el_max / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: reference initial condition (tests/advection/initialize.hpp), pre-refined mesh",
+            "config": {
+                "workload": "advection3d (BASELINE config 3): base 128x128x128 per GPU, max_ref_lvl 2, "
+                            "face neighbors, periodic x,y, frozen mesh",
+                "base": [a.base, a.base, a.base * world],
+                "max_ref_lvl": a.max_ref_lvl,
+                "cells_total": total_cells,
+                "cells_rank0": n_local,
+                "halo_cells_rank0": c["recv"],
+                "partition": "block (level-0 z-slabs, children inherit)",
+                "parallelism": f"domain decomposition x{world}",
+                "setup_s": setup_s,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
+                "traffic": traffic,
+                "kernel": "advection_kernel",
+                "alg_bytes_per_step": alg_bytes_step,
+                "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
+                "launches_per_step": launches_per_step,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    g.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

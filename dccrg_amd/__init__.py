@@ -1,0 +1,11 @@
+"""dccrg_amd — MI355X-native neighbor-stencil + remote-neighbor halo path of
+dccrg (distributed cartesian cell-refinable grid).
+
+The compute path is the HIP/RCCL library ``libdccrgx.so`` (C ABI:
+include/dccrgx.h); this package is the Python mirror of the reference's
+``dccrg::Dccrg`` host interface on top of it.
+"""
+from ._lib import DccrgError, header_symbols, lib  # noqa: F401
+from .grid import Dccrg, Field  # noqa: F401
+
+__all__ = ["Dccrg", "Field", "DccrgError", "lib", "header_symbols"]

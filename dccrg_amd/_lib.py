@@ -1,0 +1,122 @@
+"""ctypes binding of dccrg_amd/libdccrgx.so (C ABI declared in include/dccrgx.h).
+
+The product path is the HIP library; there is no CPU fallback.  Importing
+this module fails loudly if the library has not been built.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdccrgx.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "dccrgx.h")
+
+_lib = None
+
+u64 = C.c_uint64
+i64 = C.c_int64
+i32 = C.c_int32
+sz = C.c_size_t
+vp = C.c_void_p
+P = C.POINTER
+
+_SIGS = {
+    "dccrgx_last_error": (C.c_char_p, []),
+    "dccrgx_abi_version": (C.c_int, []),
+    "dccrgx_get_unique_id": (C.c_int, [vp]),
+    "dccrgx_create": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, P(vp)]),
+    "dccrgx_destroy": (C.c_int, [vp]),
+    "dccrgx_set_initial_length": (C.c_int, [vp, P(u64)]),
+    "dccrgx_set_maximum_refinement_level": (C.c_int, [vp, C.c_int]),
+    "dccrgx_get_maximum_refinement_level": (C.c_int, [vp, P(C.c_int)]),
+    "dccrgx_set_periodic": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
+    "dccrgx_set_neighborhood_length": (C.c_int, [vp, C.c_uint]),
+    "dccrgx_initialize": (C.c_int, [vp]),
+    "dccrgx_set_geometry": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
+    "dccrgx_get_cell_from_indices": (u64, [vp, P(u64), C.c_int]),
+    "dccrgx_get_indices": (C.c_int, [vp, u64, P(u64)]),
+    "dccrgx_get_refinement_level": (C.c_int, [vp, u64]),
+    "dccrgx_get_last_cell": (u64, [vp]),
+    "dccrgx_get_cells": (C.c_int, [vp, C.c_int, vp, sz, P(sz)]),
+    "dccrgx_get_counts": (C.c_int, [vp, P(sz), P(sz), P(sz), P(sz)]),
+    "dccrgx_get_neighbors_of": (C.c_int, [vp, u64, vp, vp, sz, P(sz)]),
+    "dccrgx_get_slot_ids": (C.c_int, [vp, vp, sz, P(sz)]),
+    "dccrgx_download_csr": (C.c_int, [vp, C.c_int, vp, vp, vp, sz, P(sz)]),
+    "dccrgx_get_neighbors_to": (C.c_int, [vp, u64, vp, sz, P(sz)]),
+    "dccrgx_get_face_neighbors_of": (C.c_int, [vp, u64, vp, vp, sz, P(sz)]),
+    "dccrgx_is_local": (C.c_int, [vp, u64]),
+    "dccrgx_get_process": (C.c_int, [vp, u64]),
+    "dccrgx_get_slot": (i64, [vp, u64]),
+    "dccrgx_get_peers": (C.c_int, [vp, vp, sz, P(sz)]),
+    "dccrgx_get_cells_to_send": (C.c_int, [vp, C.c_int, vp, sz, P(sz)]),
+    "dccrgx_get_cells_to_receive": (C.c_int, [vp, C.c_int, vp, sz, P(sz)]),
+    "dccrgx_get_number_of_update_cells": (C.c_int, [vp, P(u64), P(u64)]),
+    "dccrgx_refine_completely": (C.c_int, [vp, u64]),
+    "dccrgx_stop_refining": (C.c_int, [vp, vp, sz, P(sz)]),
+    "dccrgx_get_new_cells": (C.c_int, [vp, vp, sz, P(sz)]),
+    "dccrgx_set_cells": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_pin": (C.c_int, [vp, u64, C.c_int]),
+    "dccrgx_unpin": (C.c_int, [vp, u64]),
+    "dccrgx_balance_load": (C.c_int, [vp]),
+    "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
+    "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),
+    "dccrgx_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp)]),
+    "dccrgx_field_upload": (C.c_int, [vp, C.c_int, sz, sz, vp]),
+    "dccrgx_field_download": (C.c_int, [vp, C.c_int, sz, sz, vp]),
+    "dccrgx_update_copies_of_remote_neighbors": (C.c_int, [vp]),
+    "dccrgx_start_remote_neighbor_copy_updates": (C.c_int, [vp]),
+    "dccrgx_wait_remote_neighbor_copy_update_receives": (C.c_int, [vp]),
+    "dccrgx_wait_remote_neighbor_copy_update_sends": (C.c_int, [vp]),
+    "dccrgx_wait_remote_neighbor_copy_updates": (C.c_int, [vp]),
+    "dccrgx_gol_step": (C.c_int, [vp, C.c_int, C.c_int]),
+    "dccrgx_gol_commit": (C.c_int, [vp, C.c_int]),
+    "dccrgx_advection_step": (C.c_int, [vp, P(C.c_int), C.c_double, C.c_int]),
+    "dccrgx_advection_commit": (C.c_int, [vp, C.c_int]),
+    "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),
+    "dccrgx_advection_max_time_step": (C.c_int, [vp, P(C.c_int), P(C.c_double)]),
+    "dccrgx_advection_refine_candidates": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, vp, sz, P(sz)]),
+    "dccrgx_allreduce_f64": (C.c_int, [vp, P(C.c_double), C.c_int, C.c_int]),
+    "dccrgx_barrier": (C.c_int, [vp]),
+    "dccrgx_synchronize": (C.c_int, [vp]),
+    "dccrgx_compute_stream": (vp, [vp]),
+    "dccrgx_kernel_timing": (C.c_int, [vp, C.c_int, P(C.c_double), P(i64)]),
+}
+
+
+def header_symbols():
+    """Every function the C header declares."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(dccrgx_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"dccrg_amd native library missing: {LIB_PATH} (run python -m dccrg_amd.build)")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class DccrgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"dccrgx error {code}: {msg}")
+        self.code = code
+
+
+OK, EINVAL, EHIP, ECOMM, ERANGE, ENOTFOUND = 0, -1, -2, -3, -4, -5
+
+
+def check(rc):
+    if rc != 0:
+        raise DccrgError(rc, lib().dccrgx_last_error().decode())
+    return rc

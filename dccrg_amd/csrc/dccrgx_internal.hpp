@@ -1,0 +1,216 @@
+// Internal state of one dccrgx grid (one per process / GPU).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/dccrgx.h"
+#include "dccrgx_mapping.hpp"
+#include "dccrgx_neighbors.hpp"
+
+namespace dccrgx {
+
+struct Error : std::runtime_error {
+	int code;
+	Error(int c, const std::string& s) : std::runtime_error(s), code(c) {}
+};
+
+#define DX_STR2(x) #x
+#define DX_STR(x) DX_STR2(x)
+#define HIP_CHECK(expr)                                                                                        \
+	do {                                                                                                       \
+		hipError_t e_ = (expr);                                                                                \
+		if (e_ != hipSuccess)                                                                                  \
+			throw ::dccrgx::Error(DCCRGX_EHIP, std::string(__FILE__ ":" DX_STR(__LINE__) " ") + #expr + ": " + \
+			                                       hipGetErrorString(e_));                                     \
+	} while (0)
+#define NCCL_CHECK(expr)                                                                                        \
+	do {                                                                                                        \
+		ncclResult_t r_ = (expr);                                                                               \
+		if (r_ != ncclSuccess)                                                                                  \
+			throw ::dccrgx::Error(DCCRGX_ECOMM, std::string(__FILE__ ":" DX_STR(__LINE__) " ") + #expr + ": " + \
+			                                        ncclGetErrorString(r_));                                    \
+	} while (0)
+#define DX_REQUIRE(cond, msg)                                                     \
+	do {                                                                          \
+		if (!(cond)) throw ::dccrgx::Error(DCCRGX_EINVAL, std::string(msg)); \
+	} while (0)
+
+// Owning device buffer.
+template <class T>
+struct DBuf {
+	T* p = nullptr;
+	size_t n = 0;
+	DBuf() = default;
+	DBuf(const DBuf&) = delete;
+	DBuf& operator=(const DBuf&) = delete;
+	DBuf(DBuf&& o) noexcept : p(o.p), n(o.n) {
+		o.p = nullptr;
+		o.n = 0;
+	}
+	DBuf& operator=(DBuf&& o) noexcept {
+		if (this != &o) {
+			release();
+			p = o.p;
+			n = o.n;
+			o.p = nullptr;
+			o.n = 0;
+		}
+		return *this;
+	}
+	~DBuf() { release(); }
+	void release() {
+		if (p) (void)hipFree(p);
+		p = nullptr;
+		n = 0;
+	}
+	void alloc(size_t count) {
+		if (count == n && p) return;
+		release();
+		if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+		n = count;
+	}
+	void swap(DBuf& o) {
+		std::swap(p, o.p);
+		std::swap(n, o.n);
+	}
+};
+
+struct Field {
+	std::string name;
+	size_t elem = 0;
+	bool transfer = false;
+	DBuf<uint8_t> data;     // n_slots * elem
+	DBuf<uint8_t> scratch;  // double buffer for sweeps (allocated on demand)
+};
+
+struct Grid {
+	// communicator
+	int rank = 0, size = 1, device = 0;
+	ncclComm_t comm = nullptr;
+	hipStream_t s_comp = nullptr, s_comm = nullptr;
+	hipEvent_t ev_comp = nullptr, ev_halo = nullptr;
+	bool halo_in_flight = false;
+
+	// setup (dccrg.hpp:8120-8230)
+	uint64_t len[3] = {1, 1, 1};
+	int R = 0;
+	int per[3] = {0, 0, 0};
+	unsigned hood_len = 1;
+	bool initialized = false;
+	MapCtx m{};
+	std::vector<int32_t> hood;     // neighborhood_of, 3 per item
+	std::vector<int32_t> hood_to;  // neighborhood_to (negated)
+	double start[3] = {0, 0, 0}, l0[3] = {1, 1, 1};
+
+	// global leaves (like cell_process, dccrg.hpp:7197): sorted ids + owners
+	std::vector<uint64_t> leaves;
+	std::vector<int32_t> owners;
+	std::unordered_map<uint64_t, int> pins;
+	std::vector<uint64_t> refine_requests;
+	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
+
+	// local layout
+	size_t n_inner = 0, n_outer = 0, n_local = 0, n_recv = 0, n_slots = 0;
+	std::vector<int> peers;                                     // union of send/recv peers, ascending
+	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;    // ascending ids per peer
+	std::map<int, size_t> recv_slot0;                           // first halo slot per peer
+	std::map<int, size_t> send_off;                             // offset into send_slots per peer
+	size_t n_send_total = 0;
+	std::vector<uint64_t> extra_remote;                         // remote neighbors_to-only cells
+	std::vector<uint64_t> slot_ids_h;                           // host mirror of slot -> id
+	bool slot_ids_h_valid = false;
+
+	// device structures
+	DBuf<int32_t> owner_by_id;  // last_cell + 1 entries, -1 = not a leaf
+	DBuf<int32_t> slot_by_id;   // last_cell + 1 entries, -1 = no slot on this rank
+	DBuf<uint64_t> slot_ids;    // n_slots
+	DBuf<int32_t> d_hood, d_hood_to;
+	// full CSR (built lazily): neighbors_of (stencil order), neighbors_to (ascending)
+	bool csr_valid = false;
+	DBuf<uint32_t> nof_ptr, nto_ptr, it_ptr;
+	DBuf<uint64_t> nof_id, nto_id;
+	DBuf<int32_t> nof_off, nof_slot, it_slot;
+	// face CSR (built lazily): entry = slot * 8 + dir (dir 0..5 = -x,+x,-y,+y,-z,+z)
+	bool face_valid = false;
+	DBuf<uint32_t> face_ptr;
+	DBuf<int32_t> face_ent;
+	// halo
+	DBuf<int32_t> send_slots;
+	DBuf<uint8_t> sendbuf;
+
+	std::vector<Field> fields;
+
+	// timing of sweep kernels (HIP events on s_comp)
+	bool timing = false;
+	double timed_ms = 0;
+	int64_t timed_count = 0;
+	std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+
+	bool uniform() const { return R == 0; }
+};
+
+// --- launchers implemented in build_kernels.hip -----------------------------
+void k_fill_i32(int32_t* p, size_t n, int32_t v, hipStream_t s);
+void k_scatter_owner(int32_t* owner_by_id, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s);
+void k_scatter_slots(int32_t* slot_by_id, const uint64_t* slot_ids, size_t n, hipStream_t s);
+// flag local cells that have a remote neighbors_of / neighbors_to entry
+void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
+                    int rank, const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s);
+// local ids -> slots: inner first, outer second, both ascending
+void k_assign_slots2(const uint32_t* flag, const uint32_t* scan_outer, size_t n, size_t n_inner, const uint64_t* cells,
+                     uint64_t* slot_ids, hipStream_t s);
+void k_fill_neighbors_of(const MapCtx& m, const int32_t* hood, int nh, const int32_t* owner_by_id,
+                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
+                         int32_t* offs, hipStream_t s);
+void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
+                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
+                         hipStream_t s);
+void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
+                  const uint64_t* slot_ids, size_t row0, size_t nrows, uint32_t* nof_cnt, uint32_t* nto_cnt,
+                  hipStream_t s);
+// remote (owner != rank) entries of an id array as composite keys owner*(last+1)+id
+size_t k_extract_remote(const uint64_t* ids, size_t n, const int32_t* owner_by_id, int rank, uint64_t stride,
+                        uint64_t* keys_out, hipStream_t s);
+// keys for the send side: for each neighbors_to entry with a remote owner,
+// owner*(last+1) + the row's own id
+size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
+                      size_t nrows, const int32_t* owner_by_id, int rank, uint64_t stride, uint64_t* keys_out,
+                      hipStream_t s);
+size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s);  // in place
+uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
+void k_lookup_slots(const uint64_t* ids, size_t n, const int32_t* slot_by_id, int32_t* out, int32_t* err_flag,
+                    hipStream_t s);
+void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
+                      const int32_t* nof_slot, size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr,
+                      int32_t* it_slot, int pass, hipStream_t s);
+void k_face_lists(const MapCtx& m, const int32_t* owner_by_id, const int32_t* slot_by_id, const uint64_t* slot_ids,
+                  size_t nrows, uint32_t* cnt, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass,
+                  hipStream_t s);
+void k_remap_field2(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const int32_t* new_slot_by_id,
+                    uint64_t last, uint8_t* new_data, size_t elem, hipStream_t s);
+void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int32_t* slot_by_id, const MapCtx& m,
+                   const uint8_t* old_data, const int32_t* old_slot_by_id, size_t elem, hipStream_t s);
+
+// --- launchers implemented in sweep_kernels.hip -----------------------------
+void k_pack(const uint8_t* field, size_t elem, const int32_t* slots, size_t n, uint8_t* out, hipStream_t s);
+void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
+               size_t s1, hipStream_t s);
+void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
+void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
+                 size_t s0, size_t s1, double dt, hipStream_t s);
+void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
+size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
+                        const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
+                        uint64_t* out, hipStream_t s);
+void k_time_begin(Grid& g);
+void k_time_end(Grid& g);
+
+}  // namespace dccrgx

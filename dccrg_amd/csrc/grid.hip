@@ -1,0 +1,1436 @@
+// dccrgx: host side of the MI355X-native dccrg hot path + the C ABI
+// (include/dccrgx.h).  Owns the global leaf set (the reference's
+// cell_process, dccrg.hpp:7197), drives the device neighbor build, the halo
+// exchange over RCCL and the built-in sweeps.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <set>
+#include <unordered_set>
+
+#include "dccrgx_internal.hpp"
+
+namespace dccrgx {
+
+static thread_local std::string g_last_error;
+
+template <class F>
+static int guard(F&& f) {
+	try {
+		return f();
+	} catch (const Error& e) {
+		g_last_error = e.what();
+		return e.code;
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return DCCRGX_EINVAL;
+	}
+}
+
+static inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u) {
+	size_t g = (n + per_block - 1) / per_block;
+	if (g > cap) g = cap;
+	if (g == 0) g = 1;
+	return unsigned(g);
+}
+
+// ---------------------------------------------------------------------------
+// small kernels local to the host driver
+__global__ void block_owner_kernel(int32_t* owner_by_id, uint64_t total, uint64_t P) {
+	// create_level_0_cells (dccrg.hpp:7967-8013): contiguous id blocks, the
+	// first `fewer` processes get one cell less
+	uint64_t cpp = total < P ? 1 : (total % P ? total / P + 1 : total / P);
+	const uint64_t fewer = cpp * P - total;
+	const uint64_t K = fewer * (cpp - 1);
+	for (uint64_t k = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x; k < total; k += uint64_t(gridDim.x) * blockDim.x) {
+		uint64_t p;
+		if (k < K) p = k / (cpp - 1);
+		else p = fewer + (k - K) / cpp;
+		owner_by_id[k + 1] = int32_t(p);
+	}
+}
+
+__global__ void iota_u64_kernel(uint64_t* out, uint64_t first, size_t n) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		out[i] = first + i;
+}
+
+__global__ void unpack_kernel(const uint8_t* in, size_t elem, const int32_t* slots, size_t n, uint8_t* field) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * elem; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t k = i / elem, b = i - k * elem;
+		field[size_t(slots[k]) * elem + b] = in[i];
+	}
+}
+
+// ---------------------------------------------------------------------------
+// block partition on the host (same formula as block_owner_kernel)
+static void block_range(uint64_t total, uint64_t P, uint64_t p, uint64_t& first, uint64_t& count) {
+	const uint64_t cpp = total < P ? 1 : (total % P ? total / P + 1 : total / P);
+	const uint64_t fewer = cpp * P - total;
+	if (p < fewer) {
+		first = 1 + p * (cpp - 1);
+		count = cpp - 1;
+	} else {
+		first = 1 + fewer * (cpp - 1) + (p - fewer) * cpp;
+		count = cpp;
+	}
+}
+
+struct HostExists {
+	const Grid* g;
+	bool operator()(uint64_t id) const {
+		if (id == error_cell || id > g->m.last) return false;
+		if (g->leaves.empty()) return id < g->m.first[1];  // implicit uniform level-0 grid
+		return std::binary_search(g->leaves.begin(), g->leaves.end(), id);
+	}
+};
+
+static bool implicit_mesh(const Grid& g) { return g.leaves.empty(); }
+
+static void materialize(Grid& g) {
+	if (!implicit_mesh(g)) return;
+	const uint64_t total = g.m.first[1] - 1;
+	g.leaves.resize(total);
+	g.owners.resize(total);
+	for (int p = 0; p < g.size; p++) {
+		uint64_t f, c;
+		block_range(total, uint64_t(g.size), uint64_t(p), f, c);
+		for (uint64_t i = 0; i < c; i++) {
+			g.leaves[f - 1 + i] = f + i;
+			g.owners[f - 1 + i] = p;
+		}
+	}
+}
+
+static int host_owner(const Grid& g, uint64_t id) {
+	if (id == error_cell || id > g.m.last) return -1;
+	if (implicit_mesh(g)) {
+		if (id >= g.m.first[1]) return -1;
+		const uint64_t total = g.m.first[1] - 1;
+		for (int p = 0; p < g.size; p++) {
+			uint64_t f, c;
+			block_range(total, uint64_t(g.size), uint64_t(p), f, c);
+			if (id >= f && id < f + c) return p;
+		}
+		return -1;
+	}
+	auto it = std::lower_bound(g.leaves.begin(), g.leaves.end(), id);
+	if (it == g.leaves.end() || *it != id) return -1;
+	return g.owners[size_t(it - g.leaves.begin())];
+}
+
+template <class T>
+static void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
+	d.alloc(h.size());
+	if (!h.empty()) HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+template <class T>
+static std::vector<T> download(const T* d, size_t n, hipStream_t s) {
+	std::vector<T> h(n);
+	if (n) {
+		HIP_CHECK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	return h;
+}
+
+static void decode_keys(const std::vector<uint64_t>& keys, uint64_t stride, std::map<int, std::vector<uint64_t>>& out) {
+	out.clear();
+	for (uint64_t k : keys) out[int(k / stride)].push_back(k % stride);
+}
+
+// ---------------------------------------------------------------------------
+// (Re)build every local structure from the global leaf set.  Field payloads
+// of cells that stay on this rank are carried over (old slot -> new slot);
+// freshly created children inherit their parent's payload.
+static void rebuild(Grid& g) {
+	hipStream_t s = g.s_comp;
+	const MapCtx& m = g.m;
+	const int nh = int(g.hood.size() / 3);
+
+	DBuf<uint64_t> old_slot_ids;
+	old_slot_ids.swap(g.slot_ids);
+	DBuf<int32_t> old_slot_by_id;
+	old_slot_by_id.swap(g.slot_by_id);
+	const size_t old_n_local = g.n_local;
+
+	// 1. global owner table (replaces the cell_process hash map)
+	g.owner_by_id.alloc(m.last + 1);
+	k_fill_i32(g.owner_by_id.p, m.last + 1, -1, s);
+	DBuf<uint64_t> d_local;
+	if (implicit_mesh(g)) {
+		const uint64_t total = m.first[1] - 1;
+		block_owner_kernel<<<grid_for(total, 256), 256, 0, s>>>(g.owner_by_id.p, total, uint64_t(g.size));
+		HIP_CHECK(hipGetLastError());
+		uint64_t f, c;
+		block_range(total, uint64_t(g.size), uint64_t(g.rank), f, c);
+		d_local.alloc(c);
+		if (c) {
+			iota_u64_kernel<<<grid_for(c, 256), 256, 0, s>>>(d_local.p, f, c);
+			HIP_CHECK(hipGetLastError());
+		}
+		g.n_local = c;
+	} else {
+		DBuf<uint64_t> dl;
+		DBuf<int32_t> dow;
+		upload(dl, g.leaves, s);
+		upload(dow, g.owners, s);
+		k_scatter_owner(g.owner_by_id.p, dl.p, dow.p, g.leaves.size(), s);
+		std::vector<uint64_t> local;
+		for (size_t i = 0; i < g.leaves.size(); i++)
+			if (g.owners[i] == g.rank) local.push_back(g.leaves[i]);
+		upload(d_local, local, s);
+		g.n_local = local.size();
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	const size_t nl = g.n_local;
+
+	// 2. inner / outer classification (update_remote_neighbor_info 8992-9095)
+	DBuf<uint32_t> flag, scan;
+	flag.alloc(nl + 1);
+	scan.alloc(nl + 1);
+	HIP_CHECK(hipMemsetAsync(flag.p, 0, (nl + 1) * sizeof(uint32_t), s));
+	if (g.size > 1) k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, g.owner_by_id.p, g.rank, d_local.p, nl, flag.p, s);
+	g.n_outer = scan_exclusive_u32(flag.p, scan.p, nl, s);
+	g.n_inner = nl - g.n_outer;
+	DBuf<uint64_t> local_slots;
+	local_slots.alloc(nl);
+	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
+	d_local.release();
+
+	// 3. neighbor lists of outer cells -> send / receive lists (8590-8752)
+	g.send_ids.clear();
+	g.recv_ids.clear();
+	g.extra_remote.clear();
+	const uint64_t stride = m.last + 1;
+	if (g.n_outer > 0) {
+		const size_t no = g.n_outer;
+		DBuf<uint32_t> c_of, c_to, p_of, p_to;
+		c_of.alloc(no + 1);
+		c_to.alloc(no + 1);
+		p_of.alloc(no + 1);
+		p_to.alloc(no + 1);
+		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, g.owner_by_id.p, local_slots.p, g.n_inner, no, c_of.p, c_to.p,
+		             s);
+		const size_t t_of = scan_exclusive_u32(c_of.p, p_of.p, no, s);
+		const size_t t_to = scan_exclusive_u32(c_to.p, p_to.p, no, s);
+		DBuf<uint64_t> of_id, to_id, keys;
+		DBuf<int32_t> of_off;
+		of_id.alloc(t_of);
+		of_off.alloc(3 * t_of);
+		to_id.alloc(t_to);
+		keys.alloc(std::max(t_of, t_to) + 1);
+		k_fill_neighbors_of(m, g.d_hood.p, nh, g.owner_by_id.p, local_slots.p, g.n_inner, no, p_of.p, of_id.p,
+		                    of_off.p, s);
+		k_fill_neighbors_to(m, g.d_hood_to.p, nh, g.owner_by_id.p, local_slots.p, g.n_inner, no, p_to.p, to_id.p, s);
+		size_t nk = k_extract_remote(of_id.p, t_of, g.owner_by_id.p, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		decode_keys(download(keys.p, nk, s), stride, g.recv_ids);
+		nk = k_extract_send(to_id.p, p_to.p, local_slots.p, g.n_inner, no, g.owner_by_id.p, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		decode_keys(download(keys.p, nk, s), stride, g.send_ids);
+		nk = k_extract_remote(to_id.p, t_to, g.owner_by_id.p, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		std::map<int, std::vector<uint64_t>> rem_to;
+		decode_keys(download(keys.p, nk, s), stride, rem_to);
+		std::set<uint64_t> extra;
+		for (auto& kv : rem_to) {
+			const auto& rv = g.recv_ids[kv.first];
+			for (uint64_t id : kv.second)
+				if (!std::binary_search(rv.begin(), rv.end(), id)) extra.insert(id);
+		}
+		for (auto it = g.recv_ids.begin(); it != g.recv_ids.end();) {
+			if (it->second.empty()) it = g.recv_ids.erase(it);
+			else ++it;
+		}
+		g.extra_remote.assign(extra.begin(), extra.end());
+	}
+	std::set<int> peerset;
+	for (auto& kv : g.send_ids) peerset.insert(kv.first);
+	for (auto& kv : g.recv_ids) peerset.insert(kv.first);
+	g.peers.assign(peerset.begin(), peerset.end());
+
+	// 4. slots: local | halo (per peer, ascending) | remote neighbors_to-only
+	std::vector<uint64_t> halo;
+	g.recv_slot0.clear();
+	for (auto& kv : g.recv_ids) {
+		g.recv_slot0[kv.first] = nl + halo.size();
+		halo.insert(halo.end(), kv.second.begin(), kv.second.end());
+	}
+	g.n_recv = halo.size();
+	halo.insert(halo.end(), g.extra_remote.begin(), g.extra_remote.end());
+	g.n_slots = nl + halo.size();
+	g.slot_ids.alloc(g.n_slots);
+	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, local_slots.p, nl * 8, hipMemcpyDeviceToDevice, s));
+	if (!halo.empty())
+		HIP_CHECK(hipMemcpyAsync(g.slot_ids.p + nl, halo.data(), halo.size() * 8, hipMemcpyHostToDevice, s));
+	g.slot_by_id.alloc(m.last + 1);
+	k_fill_i32(g.slot_by_id.p, m.last + 1, -1, s);
+	k_scatter_slots(g.slot_by_id.p, g.slot_ids.p, g.n_slots, s);
+
+	// 5. send slots (ascending id per peer = wire order)
+	std::vector<uint64_t> sids;
+	g.send_off.clear();
+	for (auto& kv : g.send_ids) {
+		g.send_off[kv.first] = sids.size();
+		sids.insert(sids.end(), kv.second.begin(), kv.second.end());
+	}
+	g.n_send_total = sids.size();
+	{
+		DBuf<uint64_t> d;
+		upload(d, sids, s);
+		g.send_slots.alloc(sids.size());
+		DBuf<int32_t> err;
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+		k_lookup_slots(d.p, sids.size(), g.slot_by_id.p, g.send_slots.p, err.p, s);
+		int32_t herr = 0;
+		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		DX_REQUIRE(herr == 0, "internal error: send cell without a slot");
+	}
+
+	// 6. carry field payloads over
+	for (auto& f : g.fields) {
+		DBuf<uint8_t> nd;
+		nd.alloc(g.n_slots * f.elem);
+		if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
+		if (f.data.p && old_slot_ids.p) {
+			k_remap_field2(f.data.p, old_slot_ids.p, old_n_local, g.slot_by_id.p, m.last, nd.p, f.elem, s);
+			k_parent_fill(nd.p, g.slot_ids.p, nl, g.slot_by_id.p, m, f.data.p, old_slot_by_id.p, f.elem, s);
+		}
+		f.data.swap(nd);
+		f.scratch.release();
+	}
+	HIP_CHECK(hipStreamSynchronize(s));
+	g.csr_valid = false;
+	g.face_valid = false;
+	g.slot_ids_h_valid = false;
+}
+
+// full neighbors_of / neighbors_to / iterator CSR for all local rows
+static void ensure_csr(Grid& g) {
+	if (g.csr_valid) return;
+	hipStream_t s = g.s_comp;
+	const int nh = int(g.hood.size() / 3);
+	const size_t nl = g.n_local;
+	DBuf<uint32_t> c_of, c_to;
+	c_of.alloc(nl + 1);
+	c_to.alloc(nl + 1);
+	g.nof_ptr.alloc(nl + 1);
+	g.nto_ptr.alloc(nl + 1);
+	g.it_ptr.alloc(nl + 1);
+	k_count_rows(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, c_of.p, c_to.p, s);
+	const size_t t_of = scan_exclusive_u32(c_of.p, g.nof_ptr.p, nl, s);
+	const size_t t_to = scan_exclusive_u32(c_to.p, g.nto_ptr.p, nl, s);
+	g.nof_id.alloc(t_of);
+	g.nof_off.alloc(3 * t_of);
+	g.nof_slot.alloc(t_of);
+	g.nto_id.alloc(t_to);
+	k_fill_neighbors_of(g.m, g.d_hood.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, g.nof_ptr.p, g.nof_id.p,
+	                    g.nof_off.p, s);
+	k_fill_neighbors_to(g.m, g.d_hood_to.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, g.nto_ptr.p, g.nto_id.p, s);
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	k_lookup_slots(g.nof_id.p, t_of, g.slot_by_id.p, g.nof_slot.p, err.p, s);
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, nl, c_of.p, nullptr, nullptr, 0, s);
+	const size_t t_it = scan_exclusive_u32(c_of.p, g.it_ptr.p, nl, s);
+	g.it_slot.alloc(t_it);
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, nl, nullptr, g.it_ptr.p, g.it_slot.p, 1, s);
+	int32_t herr = 0;
+	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(herr == 0, "neighbor list references a cell unknown to this rank (unbalanced mesh?)");
+	g.csr_valid = true;
+}
+
+static void ensure_face(Grid& g) {
+	if (g.face_valid) return;
+	hipStream_t s = g.s_comp;
+	const size_t nl = g.n_local;
+	DBuf<uint32_t> cnt;
+	cnt.alloc(nl + 1);
+	g.face_ptr.alloc(nl + 1);
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	k_face_lists(g.m, g.owner_by_id.p, g.slot_by_id.p, g.slot_ids.p, nl, cnt.p, nullptr, nullptr, err.p, 0, s);
+	const size_t t = scan_exclusive_u32(cnt.p, g.face_ptr.p, nl, s);
+	g.face_ent.alloc(t);
+	k_face_lists(g.m, g.owner_by_id.p, g.slot_by_id.p, g.slot_ids.p, nl, nullptr, g.face_ptr.p, g.face_ent.p, err.p, 1,
+	             s);
+	int32_t herr = 0;
+	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
+	g.face_valid = true;
+}
+
+static const std::vector<uint64_t>& slot_ids_host(Grid& g) {
+	if (!g.slot_ids_h_valid) {
+		g.slot_ids_h = download(g.slot_ids.p, g.n_slots, g.s_comp);
+		g.slot_ids_h_valid = true;
+	}
+	return g.slot_ids_h;
+}
+
+static int64_t slot_of(Grid& g, uint64_t id) {
+	if (id == error_cell || id > g.m.last || !g.initialized) return -1;
+	int32_t s = -1;
+	HIP_CHECK(hipMemcpy(&s, g.slot_by_id.p + id, 4, hipMemcpyDeviceToHost));
+	return s;
+}
+
+static Field& field(Grid& g, int fid) {
+	DX_REQUIRE(fid >= 0 && size_t(fid) < g.fields.size(), "invalid field id");
+	return g.fields[size_t(fid)];
+}
+
+static void ensure_scratch(Grid& g, Field& f) {
+	if (f.scratch.n != f.data.n) f.scratch.alloc(f.data.n);
+}
+
+// commit a double-buffered sweep: swap, and carry the current remote copies
+// over so they hold the last received values (as the reference's copies do)
+static void commit(Grid& g, Field& f) {
+	DX_REQUIRE(f.scratch.n == f.data.n && f.data.p, "nothing to commit");
+	const size_t halo = (g.n_slots - g.n_local) * f.elem;
+	if (halo)
+		HIP_CHECK(hipMemcpyAsync(f.scratch.p + g.n_local * f.elem, f.data.p + g.n_local * f.elem, halo,
+		                         hipMemcpyDeviceToDevice, g.s_comp));
+	f.data.swap(f.scratch);
+}
+
+static void region_range(const Grid& g, int region, size_t& s0, size_t& s1) {
+	switch (region) {
+	case DCCRGX_REGION_ALL: s0 = 0; s1 = g.n_local; break;
+	case DCCRGX_REGION_INNER: s0 = 0; s1 = g.n_inner; break;
+	case DCCRGX_REGION_OUTER: s0 = g.n_inner; s1 = g.n_local; break;
+	default: throw Error(DCCRGX_EINVAL, "invalid region");
+	}
+}
+
+void k_time_begin(Grid& g) {
+	if (!g.timing) return;
+	hipEvent_t a, b;
+	HIP_CHECK(hipEventCreate(&a));
+	HIP_CHECK(hipEventCreate(&b));
+	HIP_CHECK(hipEventRecord(a, g.s_comp));
+	g.pending_events.push_back({a, b});
+}
+
+void k_time_end(Grid& g) {
+	if (!g.timing) return;
+	HIP_CHECK(hipEventRecord(g.pending_events.back().second, g.s_comp));
+}
+
+static void drain_timing(Grid& g) {
+	for (auto& ab : g.pending_events) {
+		HIP_CHECK(hipEventSynchronize(ab.second));
+		float ms = 0;
+		HIP_CHECK(hipEventElapsedTime(&ms, ab.first, ab.second));
+		g.timed_ms += ms;
+		g.timed_count++;
+		(void)hipEventDestroy(ab.first);
+		(void)hipEventDestroy(ab.second);
+	}
+	g.pending_events.clear();
+}
+
+// --------------------------------------------------------------------------- halo
+static void halo_start(Grid& g) {
+	if (g.size == 1 || g.peers.empty()) return;
+	DX_REQUIRE(g.comm, "halo exchange needs a communicator (grid created without an RCCL id)");
+	DX_REQUIRE(!g.halo_in_flight, "remote neighbor update already in flight");
+	std::vector<Field*> tf;
+	size_t bytes_per_cell = 0;
+	for (auto& f : g.fields)
+		if (f.transfer) {
+			tf.push_back(&f);
+			bytes_per_cell += f.elem;
+		}
+	if (tf.empty()) return;
+	if (g.sendbuf.n < g.n_send_total * bytes_per_cell) g.sendbuf.alloc(g.n_send_total * bytes_per_cell);
+	HIP_CHECK(hipEventRecord(g.ev_comp, g.s_comp));
+	HIP_CHECK(hipStreamWaitEvent(g.s_comm, g.ev_comp, 0));
+	size_t off = 0;
+	std::vector<size_t> foff;
+	for (Field* f : tf) {
+		foff.push_back(off);
+		k_pack(f->data.p, f->elem, g.send_slots.p, g.n_send_total, g.sendbuf.p + off, g.s_comm);
+		off += g.n_send_total * f->elem;
+	}
+	NCCL_CHECK(ncclGroupStart());
+	for (int p : g.peers) {
+		auto si = g.send_ids.find(p);
+		auto ri = g.recv_ids.find(p);
+		for (size_t k = 0; k < tf.size(); k++) {
+			Field* f = tf[k];
+			if (si != g.send_ids.end() && !si->second.empty())
+				NCCL_CHECK(ncclSend(g.sendbuf.p + foff[k] + g.send_off[p] * f->elem, si->second.size() * f->elem,
+				                    ncclUint8, p, g.comm, g.s_comm));
+			if (ri != g.recv_ids.end() && !ri->second.empty())
+				NCCL_CHECK(ncclRecv(f->data.p + g.recv_slot0[p] * f->elem, ri->second.size() * f->elem, ncclUint8, p,
+				                    g.comm, g.s_comm));
+		}
+	}
+	NCCL_CHECK(ncclGroupEnd());
+	HIP_CHECK(hipEventRecord(g.ev_halo, g.s_comm));
+	g.halo_in_flight = true;
+}
+
+static void halo_wait(Grid& g) {
+	if (!g.halo_in_flight) return;
+	HIP_CHECK(hipStreamWaitEvent(g.s_comp, g.ev_halo, 0));
+	g.halo_in_flight = false;
+}
+
+// --------------------------------------------------------------------------- collectives
+static void allgather_u64(Grid& g, const std::vector<uint64_t>& mine, std::vector<std::vector<uint64_t>>& all) {
+	all.assign(size_t(g.size), {});
+	DX_REQUIRE(g.size == 1 || g.comm, "collective needs a communicator (grid created without an RCCL id)");
+	if (g.size == 1) {
+		all[0] = mine;
+		return;
+	}
+	hipStream_t s = g.s_comm;
+	DBuf<uint64_t> cnt, cnts;
+	cnt.alloc(1);
+	cnts.alloc(size_t(g.size));
+	uint64_t n = mine.size();
+	HIP_CHECK(hipMemcpyAsync(cnt.p, &n, 8, hipMemcpyHostToDevice, s));
+	NCCL_CHECK(ncclAllGather(cnt.p, cnts.p, 1, ncclUint64, g.comm, s));
+	std::vector<uint64_t> hc = download(cnts.p, size_t(g.size), s);
+	const uint64_t mx = std::max<uint64_t>(1, *std::max_element(hc.begin(), hc.end()));
+	DBuf<uint64_t> buf, out;
+	buf.alloc(mx);
+	out.alloc(mx * uint64_t(g.size));
+	if (n) HIP_CHECK(hipMemcpyAsync(buf.p, mine.data(), n * 8, hipMemcpyHostToDevice, s));
+	NCCL_CHECK(ncclAllGather(buf.p, out.p, mx, ncclUint64, g.comm, s));
+	std::vector<uint64_t> h = download(out.p, mx * uint64_t(g.size), s);
+	for (int p = 0; p < g.size; p++) all[size_t(p)].assign(h.begin() + p * mx, h.begin() + p * mx + hc[size_t(p)]);
+}
+
+static void allreduce_f64(Grid& g, double* v, int count, int op) {
+	if (g.size == 1) return;
+	DX_REQUIRE(g.comm, "collective needs a communicator (grid created without an RCCL id)");
+	DBuf<double> d;
+	d.alloc(size_t(count));
+	HIP_CHECK(hipMemcpyAsync(d.p, v, size_t(count) * 8, hipMemcpyHostToDevice, g.s_comm));
+	const ncclRedOp_t rop = op == 0 ? ncclSum : (op == 1 ? ncclMin : ncclMax);
+	NCCL_CHECK(ncclAllReduce(d.p, d.p, size_t(count), ncclFloat64, rop, g.comm, g.s_comm));
+	HIP_CHECK(hipMemcpyAsync(v, d.p, size_t(count) * 8, hipMemcpyDeviceToHost, g.s_comm));
+	HIP_CHECK(hipStreamSynchronize(g.s_comm));
+}
+
+// --------------------------------------------------------------------------- refinement
+// induce_refines (dccrg.hpp:9591-9720): close the request set under "a
+// neighbors_of / neighbors_to entry coarser than a refined cell is refined
+// too", then execute_refines (10104-10554): children inherit the owner.
+static std::vector<uint64_t> stop_refining_impl(Grid& g) {
+	std::vector<std::vector<uint64_t>> all;
+	allgather_u64(g, g.refine_requests, all);
+	g.refine_requests.clear();
+	materialize(g);
+	std::unordered_set<uint64_t> S;
+	std::vector<uint64_t> fresh;
+	const HostExists ex{&g};
+	for (auto& v : all)
+		for (uint64_t c : v)
+			if (ex(c) && map_level(g.m, c) < g.R && S.insert(c).second) fresh.push_back(c);
+	const int nh = int(g.hood.size() / 3);
+	while (!fresh.empty()) {
+		std::vector<uint64_t> next;
+		for (uint64_t r : fresh) {
+			uint64_t c[3];
+			const int lvl = map_indices(g.m, r, c[0], c[1], c[2]);
+			auto consider = [&](uint64_t n) {
+				if (n == error_cell || !ex(n)) return;
+				if (map_level(g.m, n) < lvl && S.insert(n).second) next.push_back(n);
+			};
+			for (int k = 0; k < nh; k++) {
+				ItemOut o;
+				nof_item(g.m, c, lvl, &g.hood[3 * k], ex, o);
+				for (int i = 0; i < o.n; i++) consider(o.id[i]);
+			}
+			for (int k = 0; k < 10 * nh; k++) consider(nto_candidate(g.m, c, lvl, g.hood_to.data(), nh, k, ex));
+		}
+		fresh.swap(next);
+	}
+	if (S.empty()) return {};
+	std::vector<uint64_t> nl;
+	std::vector<int32_t> no;
+	std::vector<std::pair<uint64_t, int32_t>> created;
+	for (size_t i = 0; i < g.leaves.size(); i++) {
+		if (S.count(g.leaves[i])) {
+			uint64_t ch[8];
+			map_all_children(g.m, g.leaves[i], ch);
+			for (auto c : ch) created.push_back({c, g.owners[i]});
+		} else {
+			nl.push_back(g.leaves[i]);
+			no.push_back(g.owners[i]);
+		}
+	}
+	std::vector<std::pair<uint64_t, int32_t>> merged;
+	merged.reserve(nl.size() + created.size());
+	for (size_t i = 0; i < nl.size(); i++) merged.push_back({nl[i], no[i]});
+	merged.insert(merged.end(), created.begin(), created.end());
+	std::sort(merged.begin(), merged.end());
+	g.leaves.resize(merged.size());
+	g.owners.resize(merged.size());
+	for (size_t i = 0; i < merged.size(); i++) {
+		g.leaves[i] = merged[i].first;
+		g.owners[i] = merged[i].second;
+	}
+	rebuild(g);
+	std::vector<uint64_t> mine;
+	for (auto& c : created)
+		if (c.second == g.rank) mine.push_back(c.first);
+	std::sort(mine.begin(), mine.end());
+	return mine;
+}
+
+// --------------------------------------------------------------------------- load balance
+// balance_load with pins (dccrg.hpp:1024-1044, make_new_partition 8426-8518,
+// migration continue_balance_load 3899-3934): pinned cells move, the rest
+// keep their owner; payloads of moved cells travel over RCCL.
+static void balance_load_impl(Grid& g) {
+	std::vector<uint64_t> mine;
+	for (auto& kv : g.pins) {
+		mine.push_back(kv.first);
+		mine.push_back(uint64_t(kv.second));
+	}
+	std::vector<std::vector<uint64_t>> all;
+	allgather_u64(g, mine, all);
+	materialize(g);
+	std::vector<int32_t> new_owner = g.owners;
+	for (auto& v : all)
+		for (size_t i = 0; i + 1 < v.size(); i += 2) {
+			auto it = std::lower_bound(g.leaves.begin(), g.leaves.end(), v[i]);
+			if (it == g.leaves.end() || *it != v[i]) continue;
+			if (int64_t(v[i + 1]) < 0 || int64_t(v[i + 1]) >= g.size) continue;
+			new_owner[size_t(it - g.leaves.begin())] = int32_t(v[i + 1]);
+		}
+	// migration plan: ascending id per (source, destination)
+	std::map<int, std::vector<uint64_t>> out, in;
+	for (size_t i = 0; i < g.leaves.size(); i++) {
+		if (g.owners[i] == new_owner[i]) continue;
+		if (g.owners[i] == g.rank) out[new_owner[i]].push_back(g.leaves[i]);
+		if (new_owner[i] == g.rank) in[g.owners[i]].push_back(g.leaves[i]);
+	}
+	hipStream_t s = g.s_comp;
+	std::vector<DBuf<uint8_t>> sbufs(g.fields.size()), rbufs(g.fields.size());
+	std::vector<uint64_t> out_ids, in_ids;
+	std::map<int, size_t> out_off, in_off;
+	for (auto& kv : out) {
+		out_off[kv.first] = out_ids.size();
+		out_ids.insert(out_ids.end(), kv.second.begin(), kv.second.end());
+	}
+	for (auto& kv : in) {
+		in_off[kv.first] = in_ids.size();
+		in_ids.insert(in_ids.end(), kv.second.begin(), kv.second.end());
+	}
+	if (g.size > 1) {
+		DBuf<uint64_t> dids;
+		upload(dids, out_ids, s);
+		DBuf<int32_t> oslots, err;
+		oslots.alloc(out_ids.size());
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+		k_lookup_slots(dids.p, out_ids.size(), g.slot_by_id.p, oslots.p, err.p, s);
+		for (size_t k = 0; k < g.fields.size(); k++) {
+			Field& f = g.fields[k];
+			sbufs[k].alloc(out_ids.size() * f.elem);
+			rbufs[k].alloc(in_ids.size() * f.elem);
+			k_pack(f.data.p, f.elem, oslots.p, out_ids.size(), sbufs[k].p, s);
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+		if (!g.fields.empty()) {
+			NCCL_CHECK(ncclGroupStart());
+			for (size_t k = 0; k < g.fields.size(); k++) {
+				const size_t e = g.fields[k].elem;
+				for (auto& kv : out)
+					NCCL_CHECK(ncclSend(sbufs[k].p + out_off[kv.first] * e, kv.second.size() * e, ncclUint8, kv.first,
+					                    g.comm, s));
+				for (auto& kv : in)
+					NCCL_CHECK(ncclRecv(rbufs[k].p + in_off[kv.first] * e, kv.second.size() * e, ncclUint8, kv.first,
+					                    g.comm, s));
+			}
+			NCCL_CHECK(ncclGroupEnd());
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	g.owners = new_owner;
+	g.pins.clear();
+	rebuild(g);
+	if (!in_ids.empty()) {
+		DBuf<uint64_t> dids;
+		upload(dids, in_ids, s);
+		DBuf<int32_t> islots, err;
+		islots.alloc(in_ids.size());
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+		k_lookup_slots(dids.p, in_ids.size(), g.slot_by_id.p, islots.p, err.p, s);
+		for (size_t k = 0; k < g.fields.size(); k++) {
+			Field& f = g.fields[k];
+			unpack_kernel<<<grid_for(in_ids.size() * f.elem, 256), 256, 0, s>>>(rbufs[k].p, f.elem, islots.p,
+			                                                                    in_ids.size(), f.data.p);
+			HIP_CHECK(hipGetLastError());
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+}
+
+}  // namespace dccrgx
+
+// ============================================================================
+// C ABI
+// ============================================================================
+using namespace dccrgx;
+
+struct dccrgx_grid {
+	Grid g;
+};
+
+#define GRID_OR_FAIL(gp) \
+	if (!(gp)) throw Error(DCCRGX_EINVAL, "null grid"); \
+	Grid& g = (gp)->g
+
+static int copy_out_u64(const std::vector<uint64_t>& v, uint64_t* out, size_t cap, size_t* n) {
+	if (n) *n = v.size();
+	if (v.size() > cap || (!out && !v.empty())) return DCCRGX_ERANGE;
+	if (!v.empty()) std::memcpy(out, v.data(), v.size() * 8);
+	return DCCRGX_OK;
+}
+
+extern "C" {
+
+const char* dccrgx_last_error(void) { return g_last_error.c_str(); }
+int dccrgx_abi_version(void) { return 1; }
+
+int dccrgx_get_unique_id(void* out) {
+	return guard([&] {
+		ncclUniqueId id;
+		NCCL_CHECK(ncclGetUniqueId(&id));
+		std::memcpy(out, &id, sizeof(id));
+		return 0;
+	});
+}
+
+int dccrgx_create(int rank, int size, int device, const void* nccl_id, dccrgx_grid** out) {
+	return guard([&] {
+		DX_REQUIRE(out && size >= 1 && rank >= 0 && rank < size, "invalid rank/size");
+		HIP_CHECK(hipSetDevice(device));
+		auto* h = new dccrgx_grid();
+		Grid& g = h->g;
+		g.rank = rank;
+		g.size = size;
+		g.device = device;
+		HIP_CHECK(hipStreamCreateWithFlags(&g.s_comp, hipStreamNonBlocking));
+		HIP_CHECK(hipStreamCreateWithFlags(&g.s_comm, hipStreamNonBlocking));
+		HIP_CHECK(hipEventCreateWithFlags(&g.ev_comp, hipEventDisableTiming));
+		HIP_CHECK(hipEventCreateWithFlags(&g.ev_halo, hipEventDisableTiming));
+		if (size > 1 && nccl_id) {  // without an id: a detached view of one rank (no halo transport)
+			ncclUniqueId id;
+			std::memcpy(&id, nccl_id, sizeof(id));
+			NCCL_CHECK(ncclCommInitRank(&g.comm, size, id, rank));
+		}
+		*out = h;
+		return 0;
+	});
+}
+
+int dccrgx_destroy(dccrgx_grid* gp) {
+	return guard([&] {
+		if (!gp) return 0;
+		Grid& g = gp->g;
+		(void)hipDeviceSynchronize();
+		drain_timing(g);
+		if (g.comm) ncclCommDestroy(g.comm);
+		if (g.ev_comp) (void)hipEventDestroy(g.ev_comp);
+		if (g.ev_halo) (void)hipEventDestroy(g.ev_halo);
+		if (g.s_comp) (void)hipStreamDestroy(g.s_comp);
+		if (g.s_comm) (void)hipStreamDestroy(g.s_comm);
+		delete gp;
+		return 0;
+	});
+}
+
+int dccrgx_set_initial_length(dccrgx_grid* gp, const uint64_t length[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_initial_length after initialize");
+		for (int d = 0; d < 3; d++) DX_REQUIRE(length[d] > 0, "grid length must be > 0");
+		for (int d = 0; d < 3; d++) g.len[d] = length[d];
+		return 0;
+	});
+}
+
+int dccrgx_set_maximum_refinement_level(dccrgx_grid* gp, int level) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_maximum_refinement_level after initialize");
+		// dccrg_mapping.hpp:316-329: the largest level whose ids fit in 64 bits
+		const double gl = double(g.len[0]) * double(g.len[1]) * double(g.len[2]);
+		int lvl = 0;
+		double cur = 0;
+		while (cur <= double(~uint64_t(0))) {
+			cur += gl * std::pow(8.0, double(lvl));
+			lvl++;
+		}
+		const int maxpos = lvl - 2;
+		if (level < 0) level = maxpos;
+		DX_REQUIRE(level <= maxpos && level < kMaxLevels, "refinement level too large for the grid");
+		g.R = level;
+		return 0;
+	});
+}
+
+int dccrgx_get_maximum_refinement_level(dccrgx_grid* gp, int* level) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		*level = g.R;
+		return 0;
+	});
+}
+
+int dccrgx_set_periodic(dccrgx_grid* gp, int x, int y, int z) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_periodic after initialize");
+		g.per[0] = x != 0;
+		g.per[1] = y != 0;
+		g.per[2] = z != 0;
+		return 0;
+	});
+}
+
+int dccrgx_set_neighborhood_length(dccrgx_grid* gp, unsigned length) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_neighborhood_length after initialize");
+		DX_REQUIRE(length <= 8, "neighborhood length > 8 not supported");
+		g.hood_len = length;
+		return 0;
+	});
+}
+
+int dccrgx_initialize(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "already initialized");
+		map_init(g.m, g.len, g.R, g.per);
+		std::vector<int32_t> h(3 * 2000);
+		const int nh = default_hood(g.hood_len, h.data());
+		g.hood.assign(h.begin(), h.begin() + 3 * nh);
+		g.hood_to.resize(g.hood.size());
+		for (size_t i = 0; i < g.hood.size(); i++) g.hood_to[i] = -g.hood[i];
+		upload(g.d_hood, g.hood, g.s_comp);
+		upload(g.d_hood_to, g.hood_to, g.s_comp);
+		g.leaves.clear();
+		g.owners.clear();
+		rebuild(g);
+		g.initialized = true;
+		return 0;
+	});
+}
+
+int dccrgx_set_geometry(dccrgx_grid* gp, const double start[3], const double l0[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		for (int d = 0; d < 3; d++) DX_REQUIRE(l0[d] > 0, "cell length must be > 0");
+		for (int d = 0; d < 3; d++) {
+			g.start[d] = start[d];
+			g.l0[d] = l0[d];
+		}
+		return 0;
+	});
+}
+
+uint64_t dccrgx_get_cell_from_indices(dccrgx_grid* gp, const uint64_t ind[3], int level) {
+	if (!gp) return error_cell;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return map_from_indices(m, ind[0], ind[1], ind[2], level);
+}
+
+int dccrgx_get_indices(dccrgx_grid* gp, uint64_t cell, uint64_t ind[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		MapCtx m;
+		map_init(m, g.len, g.R, g.per);
+		const int l = map_indices(m, cell, ind[0], ind[1], ind[2]);
+		return l < 0 ? DCCRGX_ENOTFOUND : 0;
+	});
+}
+
+int dccrgx_get_refinement_level(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return map_level(m, cell);
+}
+
+uint64_t dccrgx_get_last_cell(dccrgx_grid* gp) {
+	if (!gp) return 0;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return m.last;
+}
+
+int dccrgx_get_counts(dccrgx_grid* gp, size_t* ni, size_t* no, size_t* nr, size_t* ns) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (ni) *ni = g.n_inner;
+		if (no) *no = g.n_outer;
+		if (nr) *nr = g.n_recv;
+		if (ns) *ns = g.n_slots;
+		return 0;
+	});
+}
+
+int dccrgx_get_cells(dccrgx_grid* gp, int which, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		const auto& ids = slot_ids_host(g);
+		std::vector<uint64_t> v;
+		switch (which) {
+		case DCCRGX_CELLS_LOCAL: v.assign(ids.begin(), ids.begin() + g.n_local); break;
+		case DCCRGX_CELLS_INNER: v.assign(ids.begin(), ids.begin() + g.n_inner); break;
+		case DCCRGX_CELLS_OUTER: v.assign(ids.begin() + g.n_inner, ids.begin() + g.n_local); break;
+		case DCCRGX_CELLS_REMOTE: v.assign(ids.begin() + g.n_local, ids.end()); break;
+		case DCCRGX_CELLS_ALL: v = ids; break;
+		default: throw Error(DCCRGX_EINVAL, "invalid selection");
+		}
+		std::sort(v.begin(), v.end());
+		return copy_out_u64(v, out, cap, n);
+	});
+}
+
+int dccrgx_get_slot_ids(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		return copy_out_u64(slot_ids_host(g), out, cap, n);
+	});
+}
+
+int dccrgx_get_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32_t* offs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = slot_of(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_csr(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.nof_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) {
+			HIP_CHECK(hipMemcpy(ids, g.nof_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
+			if (offs) HIP_CHECK(hipMemcpy(offs, g.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_get_neighbors_to(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = slot_of(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_csr(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.nto_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) HIP_CHECK(hipMemcpy(ids, g.nto_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32_t* dirs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = slot_of(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_face(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.face_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		std::vector<int32_t> ent(k);
+		if (k) HIP_CHECK(hipMemcpy(ent.data(), g.face_ent.p + be[0], k * 4, hipMemcpyDeviceToHost));
+		const auto& sid = slot_ids_host(g);
+		static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
+		for (size_t i = 0; i < k; i++) {
+			ids[i] = sid[size_t(ent[i] >> 3)];
+			if (dirs) dirs[i] = dmap[ent[i] & 7];
+		}
+		return 0;
+	});
+}
+
+/* bulk download of a local CSR in slot order:
+   kind 0 neighbors_of (aux = offsets x3), 1 neighbors_to, 2 face (aux = dir),
+   3 iterator neighbors_of (ids only) */
+int dccrgx_download_csr(dccrgx_grid* gp, int kind, uint32_t* ptr, uint64_t* ids, int32_t* aux, size_t cap,
+                        size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const size_t nl = g.n_local;
+		const uint32_t* dptr = nullptr;
+		if (kind == 2) {
+			ensure_face(g);
+			dptr = g.face_ptr.p;
+		} else {
+			ensure_csr(g);
+			dptr = kind == 0 ? g.nof_ptr.p : kind == 1 ? g.nto_ptr.p : g.it_ptr.p;
+		}
+		std::vector<uint32_t> hp = download(dptr, nl + 1, g.s_comp);
+		const size_t tot = hp[nl];
+		if (n) *n = tot;
+		if (tot > cap) return DCCRGX_ERANGE;
+		std::memcpy(ptr, hp.data(), (nl + 1) * 4);
+		if (!tot) return 0;
+		const auto& sid = slot_ids_host(g);
+		if (kind == 0) {
+			HIP_CHECK(hipMemcpy(ids, g.nof_id.p, tot * 8, hipMemcpyDeviceToHost));
+			if (aux) HIP_CHECK(hipMemcpy(aux, g.nof_off.p, tot * 12, hipMemcpyDeviceToHost));
+		} else if (kind == 1) {
+			HIP_CHECK(hipMemcpy(ids, g.nto_id.p, tot * 8, hipMemcpyDeviceToHost));
+		} else if (kind == 2) {
+			std::vector<int32_t> ent = download(g.face_ent.p, tot, g.s_comp);
+			static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
+			for (size_t i = 0; i < tot; i++) {
+				ids[i] = sid[size_t(ent[i] >> 3)];
+				if (aux) aux[i] = dmap[ent[i] & 7];
+			}
+		} else {
+			std::vector<int32_t> sl = download(g.it_slot.p, tot, g.s_comp);
+			for (size_t i = 0; i < tot; i++) ids[i] = sid[size_t(sl[i])];
+		}
+		return 0;
+	});
+}
+
+int dccrgx_is_local(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return 0;
+	return host_owner(gp->g, cell) == gp->g.rank ? 1 : 0;
+}
+
+int dccrgx_get_process(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	return host_owner(gp->g, cell);
+}
+
+int64_t dccrgx_get_slot(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	try {
+		return slot_of(gp->g, cell);
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return -1;
+	}
+}
+
+int dccrgx_get_peers(dccrgx_grid* gp, int32_t* peers, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (n) *n = g.peers.size();
+		if (g.peers.size() > cap) return DCCRGX_ERANGE;
+		for (size_t i = 0; i < g.peers.size(); i++) peers[i] = g.peers[i];
+		return 0;
+	});
+}
+
+int dccrgx_get_cells_to_send(dccrgx_grid* gp, int peer, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		auto it = g.send_ids.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == g.send_ids.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_get_cells_to_receive(dccrgx_grid* gp, int peer, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		auto it = g.recv_ids.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == g.recv_ids.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* nr) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (ns) *ns = g.n_send_total;
+		if (nr) *nr = g.n_recv;
+		return 0;
+	});
+}
+
+int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (host_owner(g, cell) != g.rank) return DCCRGX_ENOTFOUND;  // 2449-2459: only local cells
+		if (map_level(g.m, cell) >= g.R) return 0;                   // 2474-2477: no-op at max level
+		g.refine_requests.push_back(cell);
+		return 0;
+	});
+}
+
+int dccrgx_stop_refining(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		g.last_new_cells = stop_refining_impl(g);
+		if (!out) {
+			if (n) *n = g.last_new_cells.size();
+			return 0;
+		}
+		return copy_out_u64(g.last_new_cells, out, cap, n);
+	});
+}
+
+int dccrgx_get_new_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		return copy_out_u64(g.last_new_cells, out, cap, n);
+	});
+}
+
+int dccrgx_set_cells(dccrgx_grid* gp, const uint64_t* ids, const int32_t* owners, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		std::vector<uint64_t> L(ids, ids + n);
+		std::vector<int32_t> O(owners, owners + n);
+		for (size_t i = 0; i < n; i++) {
+			DX_REQUIRE(L[i] != error_cell && L[i] <= g.m.last, "invalid cell id");
+			DX_REQUIRE(i == 0 || L[i] > L[i - 1], "cell ids must be strictly ascending");
+			DX_REQUIRE(O[i] >= 0 && O[i] < g.size, "invalid owner");
+		}
+		g.leaves.swap(L);
+		g.owners.swap(O);
+		rebuild(g);
+		return 0;
+	});
+}
+
+int dccrgx_pin(dccrgx_grid* gp, uint64_t cell, int process) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(process >= 0 && process < g.size, "invalid process");
+		if (host_owner(g, cell) != g.rank) return DCCRGX_ENOTFOUND;
+		g.pins[cell] = process;
+		return 0;
+	});
+}
+
+int dccrgx_unpin(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.pins.erase(cell);
+		return 0;
+	});
+}
+
+int dccrgx_balance_load(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		balance_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_add_field(dccrgx_grid* gp, const char* name, size_t elem, int transfer, int* fid) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(elem > 0, "element size must be > 0");
+		Field f;
+		f.name = name ? name : "";
+		f.elem = elem;
+		f.transfer = transfer != 0;
+		g.fields.push_back(std::move(f));
+		Field& nf = g.fields.back();
+		if (g.initialized) {
+			nf.data.alloc(g.n_slots * elem);
+			if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+		}
+		*fid = int(g.fields.size() - 1);
+		return 0;
+	});
+}
+
+int dccrgx_set_field_transfer(dccrgx_grid* gp, int fid, int transfer) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		field(g, fid).transfer = transfer != 0;
+		return 0;
+	});
+}
+
+int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		*ptr = field(g, fid).data.p;
+		return 0;
+	});
+}
+
+int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const void* host) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+		if (n) HIP_CHECK(hipMemcpy(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice));
+		return 0;
+	});
+}
+
+int dccrgx_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_t n, void* host) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		if (n) HIP_CHECK(hipMemcpy(host, f.data.p + slot0 * f.elem, n * f.elem, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_update_copies_of_remote_neighbors(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_start(g);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_start_remote_neighbor_copy_updates(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_start(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_update_receives(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_update_sends(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_updates(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_gol_step(dccrgx_grid* gp, int sf, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, sf);
+		DX_REQUIRE(f.elem == 4, "game of life state must be a 4-byte field");
+		ensure_scratch(g, f);
+		size_t s0, s1;
+		region_range(g, region, s0, s1);
+		if (s1 <= s0) return 0;
+		const bool structured = g.R == 0 && g.hood_len == 1 && g.n_outer == 0 && g.n_slots == g.n_local && s0 == 0 &&
+		                        s1 == g.n_local && implicit_mesh(g) && g.size == 1;
+		k_time_begin(g);
+		if (structured) {
+			k_gol_structured((const uint32_t*)f.data.p, (uint32_t*)f.scratch.p, g.len, g.per, g.s_comp);
+		} else {
+			ensure_csr(g);
+			k_gol_csr((const uint32_t*)f.data.p, (uint32_t*)f.scratch.p, g.it_ptr.p, g.it_slot.p, s0, s1, g.s_comp);
+		}
+		k_time_end(g);
+		return 0;
+	});
+}
+
+int dccrgx_gol_commit(dccrgx_grid* gp, int sf) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		commit(g, field(g, sf));
+		return 0;
+	});
+}
+
+static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
+	for (int k = 0; k < 7; k++) {
+		Field& F = field(g, fids[k]);
+		DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+		f[k] = (const double*)F.data.p;
+	}
+}
+
+int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		ensure_face(g);
+		const double* f[7];
+		adv_fields(g, fids, f);
+		Field& rho = field(g, fids[0]);
+		ensure_scratch(g, rho);
+		size_t s0, s1;
+		region_range(g, region, s0, s1);
+		if (s1 <= s0) return 0;
+		k_time_begin(g);
+		k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, s0, s1, dt, g.s_comp);
+		k_time_end(g);
+		return 0;
+	});
+}
+
+int dccrgx_advection_commit(dccrgx_grid* gp, int df) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		commit(g, field(g, df));
+		return 0;
+	});
+}
+
+// tests/advection/initialize.hpp:36-82 + Cartesian_Geometry get_center /
+// get_length (dccrg_cartesian_geometry.hpp:282-362), evaluated on the host
+// with the reference's expression order so the initial state is bitwise the
+// reference's.
+int dccrgx_advection_initialize(dccrgx_grid* gp, const int fids[7]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		// local cells and remote copies alike: the analytic initial state of a
+		// remote copy is what initialize() + update_copies_of_remote_neighbors()
+		// with transfer_all_data = true would deliver (initialize.hpp:80)
+		const auto& ids = slot_ids_host(g);
+		const size_t n = g.n_slots;
+		std::vector<double> a[7];
+		for (auto& v : a) v.resize(n);
+		for (size_t i = 0; i < n; i++) {
+			uint64_t ind[3];
+			const int lvl = map_indices(g.m, ids[i], ind[0], ind[1], ind[2]);
+			const double sf = 1.0 / double(uint64_t(1) << lvl);
+			double L[3], c[3];
+			for (int d = 0; d < 3; d++) L[d] = g.l0[d] * sf;
+			for (int d = 0; d < 3; d++)
+				c[d] = g.start[d] + double(ind[d]) * g.l0[d] / double(uint64_t(1) << g.R) + L[d] / 2;
+			const double radius = 0.15;
+			const double hr = std::min(std::sqrt(std::pow(c[0] - 0.25, 2.0) + std::pow(c[1] - 0.5, 2.0)), radius) / radius;
+			a[0][i] = 0.25 * (1 + std::cos(M_PI * hr));
+			a[1][i] = -c[1] + 0.5;
+			a[2][i] = +c[0] - 0.5;
+			a[3][i] = 0;
+			a[4][i] = L[0];
+			a[5][i] = L[1];
+			a[6][i] = L[2];
+		}
+		for (int k = 0; k < 7; k++) {
+			Field& F = field(g, fids[k]);
+			DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+			if (n) HIP_CHECK(hipMemcpy(F.data.p, a[k].data(), n * 8, hipMemcpyHostToDevice));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_advection_max_time_step(dccrgx_grid* gp, const int fids[7], double* out) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const double* f[7];
+		adv_fields(g, fids, f);
+		const size_t nb = 512;
+		DBuf<double> part;
+		part.alloc(nb);
+		k_adv_dt(f, g.n_local, part.p, nb, g.s_comp);
+		auto h = download(part.p, nb, g.s_comp);
+		*out = *std::min_element(h.begin(), h.end());
+		return 0;
+	});
+}
+
+int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_increase, double diff_threshold,
+                                       uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		ensure_face(g);
+		Field& F = field(g, df);
+		DBuf<uint64_t> d;
+		d.alloc(g.n_local + 1);
+		const size_t k = k_adv_candidates(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p,
+		                                  g.n_local, diff_increase, diff_threshold, d.p, g.s_comp);
+		auto v = download(d.p, k, g.s_comp);
+		std::sort(v.begin(), v.end());
+		return copy_out_u64(v, out, cap, n);
+	});
+}
+
+int dccrgx_allreduce_f64(dccrgx_grid* gp, double* v, int count, int op) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		allreduce_f64(g, v, count, op);
+		return 0;
+	});
+}
+
+int dccrgx_barrier(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		double z = 0;
+		allreduce_f64(g, &z, 1, 0);
+		return 0;
+	});
+}
+
+int dccrgx_synchronize(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comm));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		return 0;
+	});
+}
+
+void* dccrgx_compute_stream(dccrgx_grid* gp) { return gp ? (void*)gp->g.s_comp : nullptr; }
+
+int dccrgx_kernel_timing(dccrgx_grid* gp, int enable, double* total_ms, int64_t* count) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		drain_timing(g);
+		if (total_ms) *total_ms = g.timed_ms;
+		if (count) *count = g.timed_count;
+		if (enable == 1) {
+			g.timing = true;
+			g.timed_ms = 0;
+			g.timed_count = 0;
+		} else if (enable == 0) {
+			g.timing = false;
+		}
+		return 0;
+	});
+}
+
+}  // extern "C"

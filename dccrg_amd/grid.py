@@ -1,0 +1,394 @@
+"""Python mirror of the reference's ``dccrg::Dccrg<Cell_Data, Geometry>`` host
+interface (dccrg.hpp:145-7072) over the C ABI in ``include/dccrgx.h``.
+
+Method names, argument meaning and chaining follow the reference so that
+ports of its tests read like the originals; cell payloads are SoA device
+fields instead of a ``Cell_Data`` struct.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._lib import ENOTFOUND, ERANGE, DccrgError, check, lib
+
+REGION = {"all": 0, "inner": 1, "outer": 2}
+CELLS = {"local": 0, "inner": 1, "outer": 2, "remote": 3, "all": 4}
+CSR_KIND = {"of": 0, "to": 1, "face": 2, "iterator": 3}
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class Field:
+    """One SoA payload array over all slots (local cells, then remote copies)."""
+
+    def __init__(self, grid, fid, name, dtype, transfer):
+        self.grid, self.id, self.name, self.dtype, self.transfer = grid, fid, name, np.dtype(dtype), transfer
+
+    def device_ptr(self):
+        p = C.c_void_p()
+        check(lib().dccrgx_field_device_ptr(self.grid.h, self.id, C.byref(p)))
+        return p.value
+
+    def get(self, slot0=0, n=None):
+        if n is None:
+            n = self.grid.n_slots - slot0
+        out = np.empty(n, self.dtype)
+        check(lib().dccrgx_field_download(self.grid.h, self.id, slot0, n, _ptr(out)))
+        return out
+
+    def set(self, values, slot0=0):
+        a = np.ascontiguousarray(values, dtype=self.dtype)
+        check(lib().dccrgx_field_upload(self.grid.h, self.id, slot0, a.size, _ptr(a)))
+
+    def set_transfer(self, transfer: bool):
+        self.transfer = bool(transfer)
+        check(lib().dccrgx_set_field_transfer(self.grid.h, self.id, int(transfer)))
+
+
+class Dccrg:
+    """One grid per process; ``rank``/``size`` and an RCCL bootstrap id replace
+    the reference's ``MPI_Comm`` (initialize(comm), dccrg.hpp:472)."""
+
+    def __init__(self, rank=0, size=1, device=0, unique_id: bytes | None = None):
+        L = lib()
+        h = C.c_void_p()
+        uid = None
+        if size > 1 and unique_id is not None:
+            # without a unique id the grid is a detached view of rank `rank`
+            # (structures only, no halo transport / collectives)
+            uid = C.create_string_buffer(bytes(unique_id), 128)
+        check(L.dccrgx_create(rank, size, device, uid, C.byref(h)))
+        self.h = h
+        self.rank, self.size, self.device = rank, size, device
+        self.fields = {}
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().dccrgx_get_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def from_torch_distributed(cls, device=None):
+        """Bootstrap from an initialized torch.distributed process group."""
+        import torch.distributed as dist
+
+        rank, size = dist.get_rank(), dist.get_world_size()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", rank))
+        obj = [cls.unique_id() if rank == 0 else None]
+        if size > 1:
+            dist.broadcast_object_list(obj, src=0)
+        return cls(rank, size, device, obj[0] if size > 1 else None)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dccrgx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- setup (dccrg.hpp:8120-8230), chainable ----------------------------
+    def set_initial_length(self, length):
+        a = (C.c_uint64 * 3)(*[int(x) for x in length])
+        check(lib().dccrgx_set_initial_length(self.h, a))
+        self.length = tuple(int(x) for x in length)
+        return self
+
+    def set_maximum_refinement_level(self, level):
+        check(lib().dccrgx_set_maximum_refinement_level(self.h, int(level)))
+        return self
+
+    def get_maximum_refinement_level(self):
+        v = C.c_int()
+        check(lib().dccrgx_get_maximum_refinement_level(self.h, C.byref(v)))
+        return v.value
+
+    def set_periodic(self, x, y, z):
+        check(lib().dccrgx_set_periodic(self.h, int(x), int(y), int(z)))
+        return self
+
+    def set_neighborhood_length(self, n):
+        check(lib().dccrgx_set_neighborhood_length(self.h, int(n)))
+        return self
+
+    def initialize(self):
+        check(lib().dccrgx_initialize(self.h))
+        return self
+
+    def set_geometry(self, start, level_0_cell_length):
+        s = (C.c_double * 3)(*start)
+        l0 = (C.c_double * 3)(*level_0_cell_length)
+        check(lib().dccrgx_set_geometry(self.h, s, l0))
+        return self
+
+    # ---- mapping ------------------------------------------------------------
+    def get_cell_from_indices(self, indices, level):
+        a = (C.c_uint64 * 3)(*[int(x) for x in indices])
+        return int(lib().dccrgx_get_cell_from_indices(self.h, a, int(level)))
+
+    def get_indices(self, cell):
+        a = (C.c_uint64 * 3)()
+        rc = lib().dccrgx_get_indices(self.h, int(cell), a)
+        if rc == ENOTFOUND:
+            return None
+        check(rc)
+        return tuple(a)
+
+    def get_refinement_level(self, cell):
+        return int(lib().dccrgx_get_refinement_level(self.h, int(cell)))
+
+    def get_last_cell(self):
+        return int(lib().dccrgx_get_last_cell(self.h))
+
+    # ---- queries ------------------------------------------------------------
+    @property
+    def counts(self):
+        v = [C.c_size_t() for _ in range(4)]
+        check(lib().dccrgx_get_counts(self.h, *[C.byref(x) for x in v]))
+        return dict(inner=v[0].value, outer=v[1].value, recv=v[2].value, slots=v[3].value)
+
+    @property
+    def n_slots(self):
+        return self.counts["slots"]
+
+    @property
+    def n_local(self):
+        c = self.counts
+        return c["inner"] + c["outer"]
+
+    def _u64_query(self, fn, *args, cap=None):
+        n = C.c_size_t()
+        rc = fn(self.h, *args, None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        out = np.empty(n.value, np.uint64)
+        check(fn(self.h, *args, _ptr(out), out.size, C.byref(n)))
+        return out
+
+    def get_cells(self, which="local"):
+        """Sorted ids of a cell selection (get_cells(..., sorted=true), 651)."""
+        return self._u64_query(lib().dccrgx_get_cells, CELLS[which])
+
+    def local_cells(self):
+        return self.get_cells("local")
+
+    def inner_cells(self):
+        return self.get_cells("inner")
+
+    def outer_cells(self):
+        return self.get_cells("outer")
+
+    def remote_cells(self):
+        return self.get_cells("remote")
+
+    def slot_ids(self):
+        return self._u64_query(lib().dccrgx_get_slot_ids)
+
+    def get_neighbors_of(self, cell):
+        """[(id, (x, y, z)), ...] in stencil order (get_neighbors_of, 819), or
+        None for a cell that is not local (the reference returns nullptr)."""
+        n = C.c_size_t()
+        cap = 4096
+        ids = np.empty(cap, np.uint64)
+        offs = np.empty(3 * cap, np.int32)
+        rc = lib().dccrgx_get_neighbors_of(self.h, int(cell), _ptr(ids), _ptr(offs), cap, C.byref(n))
+        if rc == ENOTFOUND:
+            return None
+        check(rc)
+        k = n.value
+        return [(int(ids[i]), tuple(int(v) for v in offs[3 * i: 3 * i + 3])) for i in range(k)]
+
+    def get_neighbors_to(self, cell):
+        n = C.c_size_t()
+        cap = 8192
+        ids = np.empty(cap, np.uint64)
+        rc = lib().dccrgx_get_neighbors_to(self.h, int(cell), _ptr(ids), cap, C.byref(n))
+        if rc == ENOTFOUND:
+            return None
+        check(rc)
+        return [(int(i), (0, 0, 0)) for i in ids[: n.value]]
+
+    def get_face_neighbors_of(self, cell):
+        n = C.c_size_t()
+        ids = np.empty(64, np.uint64)
+        dirs = np.empty(64, np.int32)
+        rc = lib().dccrgx_get_face_neighbors_of(self.h, int(cell), _ptr(ids), _ptr(dirs), 64, C.byref(n))
+        if rc == ENOTFOUND:
+            return None
+        check(rc)
+        return [(int(ids[i]), int(dirs[i])) for i in range(n.value)]
+
+    def csr(self, kind="of"):
+        """Bulk download (ptr, ids, aux) of a local CSR in slot order."""
+        k = CSR_KIND[kind]
+        n = C.c_size_t()
+        nl = self.n_local
+        ptr = np.empty(nl + 1, np.uint32)
+        rc = lib().dccrgx_download_csr(self.h, k, _ptr(ptr), None, None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        tot = n.value
+        ids = np.empty(max(tot, 1), np.uint64)
+        aux = np.empty(max(3 * tot, 1), np.int32) if k in (0, 2) else None
+        check(lib().dccrgx_download_csr(self.h, k, _ptr(ptr), _ptr(ids), _ptr(aux), tot, C.byref(n)))
+        ids = ids[:tot]
+        if k == 0:
+            aux = aux[: 3 * tot].reshape(tot, 3)
+        elif k == 2:
+            aux = aux[:tot]
+        return ptr, ids, aux
+
+    def is_local(self, cell):
+        return bool(lib().dccrgx_is_local(self.h, int(cell)))
+
+    def get_process(self, cell):
+        return int(lib().dccrgx_get_process(self.h, int(cell)))
+
+    def get_slot(self, cell):
+        return int(lib().dccrgx_get_slot(self.h, int(cell)))
+
+    def get_peers(self):
+        n = C.c_size_t()
+        buf = np.empty(max(self.size, 1), np.int32)
+        check(lib().dccrgx_get_peers(self.h, _ptr(buf), buf.size, C.byref(n)))
+        return [int(x) for x in buf[: n.value]]
+
+    def get_cells_to_send(self, peer):
+        return self._u64_query(lib().dccrgx_get_cells_to_send, int(peer))
+
+    def get_cells_to_receive(self, peer):
+        return self._u64_query(lib().dccrgx_get_cells_to_receive, int(peer))
+
+    def get_number_of_update_send_cells(self):
+        s, r = C.c_uint64(), C.c_uint64()
+        check(lib().dccrgx_get_number_of_update_cells(self.h, C.byref(s), C.byref(r)))
+        return s.value
+
+    def get_number_of_update_receive_cells(self):
+        s, r = C.c_uint64(), C.c_uint64()
+        check(lib().dccrgx_get_number_of_update_cells(self.h, C.byref(s), C.byref(r)))
+        return r.value
+
+    # ---- refinement -------------------------------------------------------------
+    def refine_completely(self, cell):
+        rc = lib().dccrgx_refine_completely(self.h, int(cell))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def stop_refining(self):
+        """Executes the collected refines (collective); returns the local new cells."""
+        n = C.c_size_t()
+        check(lib().dccrgx_stop_refining(self.h, None, 0, C.byref(n)))
+        return self._u64_query(lib().dccrgx_get_new_cells)
+
+    def set_cells(self, ids, owners):
+        """Replace the global leaf set + partition (identical on every rank)."""
+        ids = np.ascontiguousarray(ids, np.uint64)
+        owners = np.ascontiguousarray(owners, np.int32)
+        check(lib().dccrgx_set_cells(self.h, _ptr(ids), _ptr(owners), ids.size))
+        return self
+
+    # ---- partition ------------------------------------------------------------
+    def pin(self, cell, process):
+        rc = lib().dccrgx_pin(self.h, int(cell), int(process))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def unpin(self, cell):
+        check(lib().dccrgx_unpin(self.h, int(cell)))
+        return True
+
+    def balance_load(self, use_zoltan=False):
+        check(lib().dccrgx_balance_load(self.h))
+        return self
+
+    # ---- fields ---------------------------------------------------------------
+    def add_field(self, name, dtype, transfer=True):
+        fid = C.c_int()
+        dt = np.dtype(dtype)
+        check(lib().dccrgx_add_field(self.h, name.encode(), dt.itemsize, int(transfer), C.byref(fid)))
+        f = Field(self, fid.value, name, dt, transfer)
+        self.fields[name] = f
+        return f
+
+    # ---- halo -------------------------------------------------------------------
+    def update_copies_of_remote_neighbors(self):
+        check(lib().dccrgx_update_copies_of_remote_neighbors(self.h))
+        return True
+
+    def start_remote_neighbor_copy_updates(self):
+        check(lib().dccrgx_start_remote_neighbor_copy_updates(self.h))
+        return True
+
+    def wait_remote_neighbor_copy_update_receives(self):
+        check(lib().dccrgx_wait_remote_neighbor_copy_update_receives(self.h))
+        return True
+
+    def wait_remote_neighbor_copy_update_sends(self):
+        check(lib().dccrgx_wait_remote_neighbor_copy_update_sends(self.h))
+        return True
+
+    def wait_remote_neighbor_copy_updates(self):
+        check(lib().dccrgx_wait_remote_neighbor_copy_updates(self.h))
+        return True
+
+    # ---- built-in sweeps ------------------------------------------------------------
+    def gol_step(self, state: Field, region="all"):
+        check(lib().dccrgx_gol_step(self.h, state.id, REGION[region]))
+
+    def gol_commit(self, state: Field):
+        check(lib().dccrgx_gol_commit(self.h, state.id))
+
+    @staticmethod
+    def _fids(fields):
+        assert len(fields) == 7
+        return (C.c_int * 7)(*[f.id for f in fields])
+
+    def advection_step(self, fields, dt, region="all"):
+        check(lib().dccrgx_advection_step(self.h, self._fids(fields), float(dt), REGION[region]))
+
+    def advection_commit(self, density: Field):
+        check(lib().dccrgx_advection_commit(self.h, density.id))
+
+    def advection_initialize(self, fields):
+        check(lib().dccrgx_advection_initialize(self.h, self._fids(fields)))
+
+    def advection_max_time_step(self, fields):
+        v = C.c_double()
+        check(lib().dccrgx_advection_max_time_step(self.h, self._fids(fields), C.byref(v)))
+        return self.allreduce(v.value, "min")
+
+    def advection_refine_candidates(self, density, diff_increase, diff_threshold):
+        return self._u64_query(lib().dccrgx_advection_refine_candidates, density.id, float(diff_increase),
+                               float(diff_threshold))
+
+    # ---- collectives / sync -------------------------------------------------------
+    def allreduce(self, value, op="sum"):
+        v = C.c_double(float(value))
+        check(lib().dccrgx_allreduce_f64(self.h, C.byref(v), 1, {"sum": 0, "min": 1, "max": 2}[op]))
+        return v.value
+
+    def barrier(self):
+        check(lib().dccrgx_barrier(self.h))
+
+    def synchronize(self):
+        check(lib().dccrgx_synchronize(self.h))
+
+    def kernel_timing(self, enable=-1):
+        ms, cnt = C.c_double(), C.c_int64()
+        check(lib().dccrgx_kernel_timing(self.h, int(enable), C.byref(ms), C.byref(cnt)))
+        return ms.value, cnt.value

@@ -1,0 +1,186 @@
+/*
+ * dccrgx — C ABI of the MI355X-native dccrg neighbor-stencil + halo path.
+ *
+ * One opaque grid per process (one process per GPU).  Cell payloads live in
+ * HBM as structure-of-arrays "fields"; every field is indexed by a *slot*:
+ *
+ *     [0, n_inner)              local cells without remote neighbors, ascending id
+ *     [n_inner, n_local)        local cells with remote neighbors,     ascending id
+ *     [n_local, n_local+n_recv) copies of remote neighbors, grouped by owner
+ *                               (ascending rank), ascending id inside a group
+ *                               = the halo exchange wire order
+ *     [.., n_slots)             remote cells that only have local cells as
+ *                               neighbors_to (no payload is ever received)
+ *
+ * Every entry point returns 0 on success and a negative code on failure;
+ * dccrgx_last_error() then describes the failure.  Every function cites the
+ * reference interface (lkotipal/dccrg @ 2024-10-24, dccrg.hpp unless noted)
+ * it replaces.
+ */
+#ifndef DCCRGX_H
+#define DCCRGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dccrgx_grid dccrgx_grid;
+
+#define DCCRGX_OK 0
+#define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
+#define DCCRGX_EHIP -2     /* HIP runtime failure */
+#define DCCRGX_ECOMM -3    /* RCCL failure */
+#define DCCRGX_ERANGE -4   /* caller buffer too small; *n holds the needed size */
+#define DCCRGX_ENOTFOUND -5 /* unknown cell (reference returns nullptr) */
+
+/* cell selections for dccrgx_get_cells (iterator ranges dccrg.hpp:7478-7602) */
+#define DCCRGX_CELLS_LOCAL 0   /* local_cells()  */
+#define DCCRGX_CELLS_INNER 1   /* inner_cells()  */
+#define DCCRGX_CELLS_OUTER 2   /* outer_cells()  */
+#define DCCRGX_CELLS_REMOTE 3  /* remote_cells() = remote_cells_on_process_boundary */
+#define DCCRGX_CELLS_ALL 4     /* all_cells()    */
+
+/* sweep regions */
+#define DCCRGX_REGION_ALL 0
+#define DCCRGX_REGION_INNER 1
+#define DCCRGX_REGION_OUTER 2
+
+const char* dccrgx_last_error(void);
+int dccrgx_abi_version(void);
+
+/* ---- communicator / lifetime ---------------------------------------------
+ * dccrgx_get_unique_id: rank 0 creates the 128-byte RCCL bootstrap id that the
+ * caller broadcasts (replaces Dccrg::initialize(MPI_Comm) 472-552's
+ * MPI_Comm_dup, 7622-7687).  nccl_id may be NULL when size == 1. */
+int dccrgx_get_unique_id(void* out_128_bytes);
+int dccrgx_create(int rank, int size, int device, const void* nccl_id, dccrgx_grid** out);
+int dccrgx_destroy(dccrgx_grid* g);
+
+/* ---- setup, before initialize (dccrg.hpp:8120-8230) ---------------------- */
+int dccrgx_set_initial_length(dccrgx_grid* g, const uint64_t length[3]);   /* 8120 */
+int dccrgx_set_maximum_refinement_level(dccrgx_grid* g, int level);        /* 8154 */
+int dccrgx_set_periodic(dccrgx_grid* g, int x, int y, int z);              /* 8183 */
+int dccrgx_set_neighborhood_length(dccrgx_grid* g, unsigned length);       /* 8206 */
+int dccrgx_get_maximum_refinement_level(dccrgx_grid* g, int* level);
+/* initialize(): level-0 cells, block partition (create_level_0_cells
+ * 7967-8102), device neighbor build (initialize_neighbors 8240-8289 and
+ * update_remote_neighbor_info / send-receive lists 8590-9309).  472 */
+int dccrgx_initialize(dccrgx_grid* g);
+/* Cartesian_Geometry::set (dccrg_cartesian_geometry.hpp:184) */
+int dccrgx_set_geometry(dccrgx_grid* g, const double start[3], const double level_0_cell_length[3]);
+
+/* ---- mapping (dccrg_mapping.hpp) — host-side scalar queries -------------- */
+uint64_t dccrgx_get_cell_from_indices(dccrgx_grid* g, const uint64_t indices[3], int level); /* 153 */
+int dccrgx_get_indices(dccrgx_grid* g, uint64_t cell, uint64_t indices[3]);                 /* 217 */
+int dccrgx_get_refinement_level(dccrgx_grid* g, uint64_t cell);                             /* 261 */
+uint64_t dccrgx_get_last_cell(dccrgx_grid* g);                                              /* 651 */
+
+/* ---- queries ------------------------------------------------------------- */
+/* get_cells(criteria={}, sorted=true) restricted to a selection; 651 */
+int dccrgx_get_cells(dccrgx_grid* g, int which, uint64_t* out, size_t cap, size_t* n);
+int dccrgx_get_counts(dccrgx_grid* g, size_t* n_inner, size_t* n_outer, size_t* n_recv, size_t* n_slots);
+/* get_neighbors_of 819 (stencil order, error cells dropped as in 4634);
+ * offsets as int32 x,y,z triples.  Returns DCCRGX_ENOTFOUND for non-local cells. */
+int dccrgx_get_neighbors_of(dccrgx_grid* g, uint64_t cell, uint64_t* ids, int32_t* offsets, size_t cap, size_t* n);
+/* all slot ids (slot order, see the layout above) */
+int dccrgx_get_slot_ids(dccrgx_grid* g, uint64_t* out, size_t cap, size_t* n);
+/* bulk download of a local CSR in slot order (rows = local slots):
+ * kind 0 neighbors_of (aux = x,y,z offsets), 1 neighbors_to, 2 face
+ * neighbors (aux = direction), 3 iterator cell.neighbors_of (ids only).
+ * ptr has n_local + 1 entries; *n = number of entries. */
+int dccrgx_download_csr(dccrgx_grid* g, int kind, uint32_t* ptr, uint64_t* ids, int32_t* aux, size_t cap, size_t* n);
+/* get_neighbors_to 883 (ascending id, offsets 0) */
+int dccrgx_get_neighbors_to(dccrgx_grid* g, uint64_t cell, uint64_t* ids, size_t cap, size_t* n);
+/* get_face_neighbors_of 2806 (dirs -1,+1,-2,+2,-3,+3) */
+int dccrgx_get_face_neighbors_of(dccrgx_grid* g, uint64_t cell, uint64_t* ids, int32_t* dirs, size_t cap, size_t* n);
+/* is_local 3270, get_process 5807 (-1 for unknown cells) */
+int dccrgx_is_local(dccrgx_grid* g, uint64_t cell);
+int dccrgx_get_process(dccrgx_grid* g, uint64_t cell);
+/* slot of a local cell or remote copy (-1 if none) */
+int64_t dccrgx_get_slot(dccrgx_grid* g, uint64_t cell);
+/* peers of this rank and their send/receive lists (cells_to_send /
+ * cells_to_receive 6900-6914, 8590-8752; ascending id = wire order) */
+int dccrgx_get_peers(dccrgx_grid* g, int32_t* peers, size_t cap, size_t* n);
+int dccrgx_get_cells_to_send(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
+int dccrgx_get_cells_to_receive(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
+/* get_number_of_update_send_cells / _receive_cells 5382-5490 */
+int dccrgx_get_number_of_update_cells(dccrgx_grid* g, uint64_t* n_send, uint64_t* n_receive);
+
+/* ---- refinement (refine_completely 2434, stop_refining 3461 -> induce_refines
+ * 9591, execute_refines 10104; unrefine is not provided) ------------------ */
+int dccrgx_refine_completely(dccrgx_grid* g, uint64_t cell);
+int dccrgx_stop_refining(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t* n);
+/* the local cells created by the last stop_refining (ascending) */
+int dccrgx_get_new_cells(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t* n);
+
+/* Replace the whole leaf set and its partition (every rank passes the same
+ * global list: ids strictly ascending, owners in [0, size)).  Stands in for
+ * a mesh + partition handed over from outside (load_grid_data 1089-2425 /
+ * an external partitioner); payloads of cells that stay local are kept. */
+int dccrgx_set_cells(dccrgx_grid* g, const uint64_t* ids, const int32_t* owners, size_t n);
+
+/* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024) ------------
+ * balance_load applies the pinned owners (no third-party partitioner:
+ * Zoltan is out of scope), migrates every field of moved cells over RCCL and
+ * rebuilds all neighbor structures on the device. */
+int dccrgx_pin(dccrgx_grid* g, uint64_t cell, int process);
+int dccrgx_unpin(dccrgx_grid* g, uint64_t cell);
+int dccrgx_balance_load(dccrgx_grid* g);
+
+/* ---- fields (replaces Cell_Data + get_mpi_datatype, dccrg_get_cell_datatype.hpp:40-340)
+ * transfer != 0: the field is part of update_copies_of_remote_neighbors. */
+int dccrgx_add_field(dccrgx_grid* g, const char* name, size_t elem_bytes, int transfer, int* field_id);
+int dccrgx_set_field_transfer(dccrgx_grid* g, int field_id, int transfer);
+int dccrgx_field_device_ptr(dccrgx_grid* g, int field_id, void** ptr);
+/* host <-> device copies of whole slot ranges [slot0, slot0+n) */
+int dccrgx_field_upload(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const void* host);
+int dccrgx_field_download(dccrgx_grid* g, int field_id, size_t slot0, size_t n, void* host);
+
+/* ---- halo (update_copies_of_remote_neighbors 966-1000 and its split form
+ * start_remote_neighbor_copy_updates 5010, wait_* 5267-5367) ------------- */
+int dccrgx_update_copies_of_remote_neighbors(dccrgx_grid* g);
+int dccrgx_start_remote_neighbor_copy_updates(dccrgx_grid* g);
+int dccrgx_wait_remote_neighbor_copy_update_receives(dccrgx_grid* g);
+int dccrgx_wait_remote_neighbor_copy_update_sends(dccrgx_grid* g);
+int dccrgx_wait_remote_neighbor_copy_updates(dccrgx_grid* g);
+
+/* ---- built-in sweeps (user stencils of tests/ and examples/) ------------- */
+/* game of life over cell.neighbors_of (examples/game_of_life.cpp:54-79,
+ * tests/game_of_life/scalability3d.cpp:130-165); state is a uint32 field.
+ * Reads state, writes the next state into a scratch buffer; the field's
+ * device pointer is swapped when dccrgx_gol_commit is called. */
+int dccrgx_gol_step(dccrgx_grid* g, int state_field, int region);
+int dccrgx_gol_commit(dccrgx_grid* g, int state_field);
+/* first-order upwind advection over face neighbors, flux + apply fused
+ * (tests/advection/solve.hpp:44-279).  fields: density, vx, vy, vz, lx, ly, lz
+ * (all fp64).  Writes the new density into a scratch buffer; commit swaps. */
+int dccrgx_advection_step(dccrgx_grid* g, const int fields[7], double dt, int region);
+int dccrgx_advection_commit(dccrgx_grid* g, int density_field);
+/* advection helpers: initial condition (tests/advection/initialize.hpp:36-82)
+ * and max_time_step (solve.hpp:289-333, local part; caller reduces MIN) */
+int dccrgx_advection_initialize(dccrgx_grid* g, const int fields[7]);
+int dccrgx_advection_max_time_step(dccrgx_grid* g, const int fields[7], double* local_min);
+/* refine candidates of check_for_adaptation (tests/advection/adapter.hpp:47-178):
+ * local cells whose max face relative difference exceeds (lvl+1)*diff_increase */
+int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double diff_increase,
+                                       double diff_threshold, uint64_t* out, size_t cap, size_t* n);
+
+/* ---- collectives for user kernels (MPI_Allreduce in solve.hpp:317) ------- */
+int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 sum, 1 min, 2 max */);
+int dccrgx_barrier(dccrgx_grid* g);
+
+/* ---- stream / timing ----------------------------------------------------- */
+int dccrgx_synchronize(dccrgx_grid* g);
+void* dccrgx_compute_stream(dccrgx_grid* g);
+/* average duration (ms) of the last `count` sweep kernels measured with HIP
+ * events on the compute stream; enable=1 starts recording */
+int dccrgx_kernel_timing(dccrgx_grid* g, int enable, double* total_ms, int64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCCRGX_H */

@@ -193,6 +193,9 @@ struct Grid {
 	std::unordered_map<uint64_t, int> cell_process;
 	std::unordered_map<uint64_t, std::array<uint64_t, 6>> neighbors_;
 	std::unordered_map<uint64_t, nlist> nof, nto;
+	// iterator lists are cached like the reference's update_cell_pointers
+	// (11314-11628) caches them; cleared on every rebuild
+	mutable std::unordered_map<uint64_t, nlist> it_cache;
 	std::unordered_set<uint64_t> to_refine;
 	std::unordered_map<uint64_t, int> pins;
 	// Cartesian geometry (dccrg_cartesian_geometry.hpp)
@@ -488,6 +491,7 @@ struct Grid {
 
 	// dccrg.hpp:9313-9319 then 8240-8289 / 8894-8963
 	void rebuild() {
+		it_cache.clear();
 		neighbors_.clear();
 		for (const auto& cp : cell_process) update_neighbors_(cp.first);
 		nof.clear();
@@ -603,6 +607,12 @@ struct Grid {
 
 	// iterator neighbor ranges, update_cell_pointers 11451-11500:
 	// neighbors_of range = only_of (sorted set) followed by both (sorted set)
+	const nlist& iter_of(uint64_t c) const {
+		auto it = it_cache.find(c);
+		if (it != it_cache.end()) return it->second;
+		return it_cache.emplace(c, iterator_neighbors_of(c)).first->second;
+	}
+
 	nlist iterator_neighbors_of(uint64_t c) const {
 		std::set<std::pair<uint64_t, off3>> ids_of, ids_to, only_of, both;
 		for (const auto& n : nof.at(c))
@@ -630,7 +640,7 @@ static void gol_step(const Grid& g, std::unordered_map<uint64_t, uint32_t>& aliv
 	std::unordered_map<uint64_t, uint32_t> count;
 	for (const auto& cp : g.cell_process) {
 		uint32_t k = 0;
-		for (const auto& n : g.iterator_neighbors_of(cp.first))
+		for (const auto& n : g.iter_of(cp.first))
 			if (alive.at(n.first) > 0) k++;
 		count[cp.first] = k;
 	}
@@ -680,7 +690,7 @@ static void adv_cell_fluxes(const Grid& g, uint64_t cid, double dt, std::unorder
 	const double cd = cell.d[0];
 	const double cv = cell.d[6] * cell.d[7] * cell.d[8];
 	const int clen = int(g.m.cell_len(cid));
-	for (const auto& nb : g.iterator_neighbors_of(cid)) {
+	for (const auto& nb : g.iter_of(cid)) {
 		const int nlen = int(g.m.cell_len(nb.first));
 		int overlaps = 0, direction = 0;
 		const int x = nb.second[0], y = nb.second[1], z = nb.second[2];

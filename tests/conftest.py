@@ -16,3 +16,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """GPU session: torch is imported first so the process has one HIP
+    runtime (torch's), exactly as in bench.py."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import dccrg_amd
+
+    dccrg_amd.lib()
+    return torch

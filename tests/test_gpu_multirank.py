@@ -1,0 +1,138 @@
+"""Multi-rank structures on one GPU: detached per-rank views (no transport)
+vs the oracle's per-rank views (update_remote_neighbor_info 8992-9095,
+recalculate_neighbor_update_send_receive_lists 8590-8752), plus an emulated
+halo exchange that moves field payloads between the views in wire order
+and runs the inner/outer split sweeps — results must equal one rank's."""
+import numpy as np
+import pytest
+
+import dccrg_amd
+from helpers import make_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def views(length, R, periodic, hood, nprocs, rounds=0, frac=0.1, seed=0):
+    out = []
+    o = None
+    for r in range(nprocs):
+        g, o = make_pair(length, R, periodic, hood, rounds, frac, seed, nprocs=nprocs, rank=r)
+        out.append(g)
+    return out, o
+
+
+CASES = [((10, 6, 5), 0, (False, False, False), 1, 2, 0), ((10, 6, 5), 0, (True, True, True), 1, 3, 0),
+         ((8, 8, 4), 0, (False, True, False), 2, 4, 0), ((7, 5, 3), 0, (True, False, True), 0, 5, 0),
+         ((6, 6, 6), 2, (False, False, False), 1, 3, 2), ((6, 6, 4), 2, (True, True, False), 0, 4, 2)]
+
+
+@pytest.mark.parametrize("length,R,periodic,hood,P,rounds", CASES)
+def test_rank_views_match_oracle(gpu, length, R, periodic, hood, P, rounds):
+    gs, o = views(length, R, periodic, hood, P, rounds, 0.15, 7)
+    for r, g in enumerate(gs):
+        assert np.array_equal(g.local_cells(), o.rank_cells(r, "local"))
+        assert np.array_equal(g.inner_cells(), o.rank_cells(r, "inner"))
+        assert np.array_equal(g.outer_cells(), o.rank_cells(r, "outer"))
+        assert np.array_equal(g.remote_cells(), o.rank_cells(r, "remote_bdy"))
+        for p in range(P):
+            if p == r:
+                continue
+            assert np.array_equal(g.get_cells_to_send(p), o.cells_to_send(r, p)), (r, p)
+            assert np.array_equal(g.get_cells_to_receive(p), o.cells_to_receive(r, p)), (r, p)
+            # wire consistency: what r sends to p is what p expects from r
+            assert np.array_equal(g.get_cells_to_send(p), gs[p].get_cells_to_receive(r))
+    for g in gs:
+        g.close()
+
+
+def emulated_exchange(gs, fields):
+    """The wire protocol of update_copies_of_remote_neighbors: per peer, the
+    payloads of cells_to_send in ascending id order land in the receiver's
+    halo slots of that peer (same order)."""
+    for r, g in enumerate(gs):
+        for p in g.get_peers():
+            send = g.get_cells_to_send(p)
+            if send.size == 0:
+                continue
+            src_slots = np.array([g.get_slot(int(c)) for c in send])
+            dst_slots = np.array([gs[p].get_slot(int(c)) for c in send])
+            assert np.all(np.diff(dst_slots) == 1)  # contiguous halo block per peer
+            for name in fields:
+                vals = g.fields[name].get()[src_slots]
+                gs[p].fields[name].set(vals, slot0=int(dst_slots[0]))
+
+
+def test_multirank_gol_equals_single_rank(gpu):
+    length, P, steps = (12, 10, 8), 3, 5
+    gs, o = views(length, 0, (True, False, True), 1, P)
+    ref, _ = make_pair(length, 0, (True, False, True), 1)
+    rng = np.random.default_rng(1)
+    ids_all = ref.slot_ids()
+    a0 = (rng.random(ids_all.size) < 0.3).astype(np.uint32)
+    val = dict(zip(ids_all.tolist(), a0.tolist()))
+    rs = ref.add_field("is_alive", np.uint32)
+    rs.set(a0)
+    for g in gs:
+        st = g.add_field("is_alive", np.uint32)
+        sl = g.slot_ids()[: g.n_local]
+        st.set(np.array([val[int(c)] for c in sl], np.uint32))
+    for _ in range(steps):
+        emulated_exchange(gs, ["is_alive"])
+        for g in gs:
+            g.gol_step(g.fields["is_alive"], "inner")
+            g.gol_step(g.fields["is_alive"], "outer")
+            g.gol_commit(g.fields["is_alive"])
+        ref.gol_step(rs)
+        ref.gol_commit(rs)
+    final = dict(zip(ids_all.tolist(), rs.get().tolist()))
+    for g in gs:
+        sl = g.slot_ids()[: g.n_local]
+        got = g.fields["is_alive"].get(0, g.n_local)
+        assert np.array_equal(got, np.array([final[int(c)] for c in sl], np.uint32))
+    for g in gs + [ref]:
+        g.close()
+
+
+def test_multirank_advection_equals_single_rank(gpu):
+    from test_gpu_advection import NAMES, gpu_grid, prerefine
+
+    base, R, P, steps = (12, 12, 4), 2, 3, 10
+    ref, rf = gpu_grid(base, R)
+    prerefine(ref, rf, R)
+    leaves = np.sort(ref.local_cells())
+    # block partition of level-0 parents, children follow (execute_refines 10228-10237)
+    m = dccrg_amd.Dccrg(0, 1, 0).set_initial_length(base).set_maximum_refinement_level(R).initialize()
+    n0 = int(np.prod(base))
+    l0p = np.array([m.get_cell_from_indices(m.get_indices(int(c)), 0) for c in leaves], np.int64)
+    owners = ((l0p - 1) * P // n0).astype(np.int32)
+    m.close()
+    gs = []
+    for r in range(P):
+        g = dccrg_amd.Dccrg(r, P, 0).set_initial_length(base).set_neighborhood_length(0)
+        g.set_maximum_refinement_level(R).set_periodic(True, True, False).initialize()
+        g.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
+        for n in NAMES:
+            g.add_field(n, np.float64, n == "density")
+        g.set_cells(leaves, owners)
+        g.advection_initialize([g.fields[n] for n in NAMES])
+        gs.append(g)
+    dt = ref.advection_max_time_step(rf)
+    for _ in range(steps):
+        emulated_exchange(gs, ["density"])
+        for g in gs:
+            f = [g.fields[n] for n in NAMES]
+            g.advection_step(f, 0.5 * dt, "inner")
+            g.advection_step(f, 0.5 * dt, "outer")
+            g.advection_commit(f[0])
+        ref.advection_step(rf, 0.5 * dt)
+        ref.advection_commit(rf[0])
+    final = dict(zip(ref.slot_ids()[: ref.n_local].tolist(), rf[0].get(0, ref.n_local).tolist()))
+    for g in gs:
+        assert g.counts["outer"] > 0
+        sl = g.slot_ids()[: g.n_local]
+        got = g.fields["density"].get(0, g.n_local)
+        exp = np.array([final[int(c)] for c in sl])
+        # identical face sets and operand order: bitwise equal
+        assert np.array_equal(got, exp)
+    for g in gs + [ref]:
+        g.close()

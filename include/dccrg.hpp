@@ -1,0 +1,252 @@
+/*
+ * dccrg.hpp — C++ drop-in facade of dccrg::Dccrg<Cell_Data, Geometry> over
+ * the MI355X-native C ABI (include/dccrgx.h, libdccrgx.so).
+ *
+ * Keeps the reference's namespace, class template, chainable setters and
+ * query names (reference dccrg.hpp:145-7072).  Differences, by design:
+ *   - the communicator is (rank, size, 128-byte RCCL id) instead of MPI_Comm
+ *     (initialize 472-552); Dccrg::unique_id() makes the id on rank 0;
+ *   - Cell_Data lives on the GPU as one AoS payload array over slots (local
+ *     cells, then remote copies); the WHOLE struct is the halo payload
+ *     (get_mpi_datatype 152-206 is not consulted).  operator[] returns a
+ *     pointer into a host staging copy: call download() before reading and
+ *     upload() after writing host-side, exactly where the reference would
+ *     have touched cell data outside a device sweep;
+ *   - device-side work uses SoA fields (add_field) and the built-in sweeps.
+ */
+#ifndef DCCRG_AMD_DCCRG_HPP
+#define DCCRG_AMD_DCCRG_HPP
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dccrgx.h"
+
+namespace dccrg {
+
+static const uint64_t error_cell = 0;                     // dccrg_mapping.hpp:37
+static const uint64_t error_index = 0xFFFFFFFFFFFFFFFFull;  // dccrg_mapping.hpp:40
+static const int default_neighborhood_id = -0xDCC;        // dccrg.hpp:112 (value irrelevant here)
+
+// dccrg_no_geometry.hpp / dccrg_cartesian_geometry.hpp parameter stand-ins
+struct No_Geometry {
+	struct Parameters {};
+};
+struct Cartesian_Geometry {
+	struct Parameters {
+		std::array<double, 3> start{{0, 0, 0}}, level_0_cell_length{{1, 1, 1}};
+	};
+};
+
+namespace detail {
+inline void check(int rc) {
+	if (rc != DCCRGX_OK) throw std::runtime_error(std::string("dccrgx: ") + dccrgx_last_error());
+}
+}  // namespace detail
+
+template <class Cell_Data, class Geometry = No_Geometry>
+class Dccrg {
+public:
+	Dccrg() = default;
+	Dccrg(const Dccrg&) = delete;
+	Dccrg& operator=(const Dccrg&) = delete;
+	~Dccrg() {
+		if (g_) dccrgx_destroy(g_);
+	}
+
+	static std::array<char, 128> unique_id() {
+		std::array<char, 128> id{};
+		detail::check(dccrgx_get_unique_id(id.data()));
+		return id;
+	}
+
+	// ---- setup (dccrg.hpp:8120-8230) ----------------------------------------
+	Dccrg& set_initial_length(const std::array<uint64_t, 3>& l) {
+		length_ = l;
+		return *this;
+	}
+	Dccrg& set_maximum_refinement_level(const int l) {
+		max_ref_ = l;
+		return *this;
+	}
+	Dccrg& set_periodic(bool x, bool y, bool z) {
+		periodic_ = {{x, y, z}};
+		return *this;
+	}
+	Dccrg& set_neighborhood_length(unsigned n) {
+		hood_ = n;
+		return *this;
+	}
+	Dccrg& set_load_balancing_method(const std::string&) { return *this; }  // Zoltan: out of scope
+
+	// initialize(comm) 472: comm = (rank, size, device, RCCL id or nullptr)
+	Dccrg& initialize(int rank = 0, int size = 1, int device = 0, const void* rccl_id = nullptr) {
+		detail::check(dccrgx_create(rank, size, device, rccl_id, &g_));
+		detail::check(dccrgx_set_initial_length(g_, length_.data()));
+		detail::check(dccrgx_set_maximum_refinement_level(g_, max_ref_));
+		detail::check(dccrgx_set_periodic(g_, periodic_[0], periodic_[1], periodic_[2]));
+		detail::check(dccrgx_set_neighborhood_length(g_, hood_));
+		detail::check(dccrgx_initialize(g_));
+		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
+		rank_ = rank;
+		return *this;
+	}
+
+	Dccrg& set_geometry(const typename Geometry::Parameters& p) {
+		set_geometry_impl(p);
+		return *this;
+	}
+
+	dccrgx_grid* native() const { return g_; }
+	int get_rank() const { return rank_; }
+
+	// ---- mapping (dccrg_mapping.hpp) -----------------------------------------
+	uint64_t get_cell_from_indices(const std::array<uint64_t, 3>& ind, int lvl) const {
+		return dccrgx_get_cell_from_indices(g_, ind.data(), lvl);
+	}
+	std::array<uint64_t, 3> get_indices(uint64_t cell) const {
+		std::array<uint64_t, 3> r{{error_index, error_index, error_index}};
+		dccrgx_get_indices(g_, cell, r.data());
+		return r;
+	}
+	int get_refinement_level(uint64_t cell) const { return dccrgx_get_refinement_level(g_, cell); }
+	int get_maximum_refinement_level() const {
+		int l = 0;
+		detail::check(dccrgx_get_maximum_refinement_level(g_, &l));
+		return l;
+	}
+
+	// ---- queries ----------------------------------------------------------------
+	// get_cells (651), sorted ascending; selection instead of criteria
+	std::vector<uint64_t> get_cells(int which = DCCRGX_CELLS_LOCAL) const {
+		return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells(g_, which, o, c, n); });
+	}
+	std::vector<uint64_t> local_cells() const { return get_cells(DCCRGX_CELLS_LOCAL); }
+	std::vector<uint64_t> inner_cells() const { return get_cells(DCCRGX_CELLS_INNER); }
+	std::vector<uint64_t> outer_cells() const { return get_cells(DCCRGX_CELLS_OUTER); }
+	std::vector<uint64_t> remote_cells() const { return get_cells(DCCRGX_CELLS_REMOTE); }
+
+	// get_neighbors_of (819): empty optional-like result (nullptr in the
+	// reference) is signalled by `found == false`
+	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_of(uint64_t cell, bool* found = nullptr) const {
+		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
+		size_t n = 0;
+		int rc = dccrgx_get_neighbors_of(g_, cell, nullptr, nullptr, 0, &n);
+		if (found) *found = rc != DCCRGX_ENOTFOUND;
+		if (rc == DCCRGX_ENOTFOUND) return r;
+		if (rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> ids(n);
+		std::vector<int32_t> off(3 * n);
+		detail::check(dccrgx_get_neighbors_of(g_, cell, ids.data(), off.data(), n, &n));
+		for (size_t i = 0; i < n; i++) r.push_back({ids[i], {{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}});
+		return r;
+	}
+	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_to(uint64_t cell) const {
+		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
+		size_t n = 0;
+		int rc = dccrgx_get_neighbors_to(g_, cell, nullptr, 0, &n);
+		if (rc == DCCRGX_ENOTFOUND) return r;
+		if (rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> ids(n);
+		detail::check(dccrgx_get_neighbors_to(g_, cell, ids.data(), n, &n));
+		for (auto i : ids) r.push_back({i, {{0, 0, 0}}});
+		return r;
+	}
+	std::vector<std::pair<uint64_t, int>> get_face_neighbors_of(uint64_t cell) const {  // 2806
+		std::vector<std::pair<uint64_t, int>> r;
+		uint64_t ids[64];
+		int32_t dirs[64];
+		size_t n = 0;
+		int rc = dccrgx_get_face_neighbors_of(g_, cell, ids, dirs, 64, &n);
+		if (rc == DCCRGX_ENOTFOUND) return r;
+		detail::check(rc);
+		for (size_t i = 0; i < n; i++) r.push_back({ids[i], dirs[i]});
+		return r;
+	}
+	bool is_local(uint64_t cell) const { return dccrgx_is_local(g_, cell) == 1; }  // 3270
+	int get_process(uint64_t cell) const { return dccrgx_get_process(g_, cell); }   // 5807
+
+	// ---- refinement / partition ----------------------------------------------
+	bool refine_completely(uint64_t cell) { return dccrgx_refine_completely(g_, cell) == DCCRGX_OK; }
+	std::vector<uint64_t> stop_refining() {
+		size_t n = 0;
+		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
+		return fetch([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+	}
+	bool pin(uint64_t cell, int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
+	bool unpin(uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
+	Dccrg& balance_load(bool /*use_zoltan*/ = true) {
+		detail::check(dccrgx_balance_load(g_));
+		return *this;
+	}
+
+	// ---- Cell_Data payload (host staging) -----------------------------------
+	void download() {
+		size_t ns = 0;
+		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
+		host_.resize(ns);
+		ids_ = fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_slot_ids(g_, o, c, n); });
+		if (ns) detail::check(dccrgx_field_download(g_, payload_, 0, ns, host_.data()));
+	}
+	void upload() {
+		if (!host_.empty()) detail::check(dccrgx_field_upload(g_, payload_, 0, host_.size(), host_.data()));
+	}
+	// operator[] (756): local cell or remote copy in the host staging copy
+	Cell_Data* operator[](uint64_t cell) {
+		const int64_t s = dccrgx_get_slot(g_, cell);
+		if (s < 0 || size_t(s) >= host_.size()) return nullptr;
+		return &host_[size_t(s)];
+	}
+
+	// ---- halo (966, 5010-5367) -------------------------------------------------
+	bool update_copies_of_remote_neighbors() { return dccrgx_update_copies_of_remote_neighbors(g_) == DCCRGX_OK; }
+	bool start_remote_neighbor_copy_updates() { return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK; }
+	bool wait_remote_neighbor_copy_update_receives() {
+		return dccrgx_wait_remote_neighbor_copy_update_receives(g_) == DCCRGX_OK;
+	}
+	bool wait_remote_neighbor_copy_update_sends() {
+		return dccrgx_wait_remote_neighbor_copy_update_sends(g_) == DCCRGX_OK;
+	}
+	bool wait_remote_neighbor_copy_updates() { return dccrgx_wait_remote_neighbor_copy_updates(g_) == DCCRGX_OK; }
+
+	// ---- device SoA fields ------------------------------------------------------
+	template <class T>
+	int add_field(const std::string& name, bool transfer) {
+		int id = -1;
+		detail::check(dccrgx_add_field(g_, name.c_str(), sizeof(T), transfer ? 1 : 0, &id));
+		return id;
+	}
+	int payload_field() const { return payload_; }
+
+private:
+	template <class F>
+	static std::vector<uint64_t> fetch(F&& f) {
+		size_t n = 0;
+		int rc = f(nullptr, 0, &n);
+		if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> v(n);
+		if (n) detail::check(f(v.data(), n, &n));
+		return v;
+	}
+	void set_geometry_impl(const No_Geometry::Parameters&) {}
+	void set_geometry_impl(const Cartesian_Geometry::Parameters& p) {
+		detail::check(dccrgx_set_geometry(g_, p.start.data(), p.level_0_cell_length.data()));
+	}
+
+	dccrgx_grid* g_ = nullptr;
+	int rank_ = 0, payload_ = -1;
+	std::array<uint64_t, 3> length_{{1, 1, 1}};
+	int max_ref_ = 0;
+	std::array<bool, 3> periodic_{{false, false, false}};
+	unsigned hood_ = 1;
+	std::vector<Cell_Data> host_;
+	std::vector<uint64_t> ids_;
+};
+
+}  // namespace dccrg
+
+#endif

@@ -38,7 +38,51 @@ def parse():
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--workload", choices=["advection", "gol"], default="advection",
+                   help="advection = BASELINE metric (default); gol = config 2 game of life line")
     return p.parse_args()
+
+
+def gol_main(a, dccrgx_mod, torch):
+    """BASELINE config 2: game of life 1024 x 1024 x 64, 26-point stencil,
+    uint32 state, 1 GPU (algorithmic 8 B per cell-update)."""
+    nx, ny, nz = 1024, 1024, 64
+    g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((nx, ny, nz)).set_neighborhood_length(1)
+    g.set_maximum_refinement_level(0).initialize()
+    st = g.add_field("is_alive", np.uint32)
+    ids = np.arange(1, nx * ny * nz + 1, dtype=np.uint64)
+    z = (ids ^ np.uint64(0x5DEECE66D)) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    st.set((z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32))
+    for _ in range(a.warmup):
+        g.gol_step(st)
+        g.gol_commit(st)
+    g.synchronize()
+    torch.cuda.synchronize()
+    g.kernel_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.gol_step(st)
+        g.gol_commit(st)
+    g.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms, kn = g.kernel_timing(0)
+    n = nx * ny * nz
+    ach = 8.0 * n * a.steps / (kms / 1e3) / 1e9
+    print(json.dumps({
+        "metric": "cell-updates/s, game of life 3D (BASELINE config 2)", "value": n * a.steps / el,
+        "unit": "cell-updates/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic: seeded alive(id) rule, p=0.2",
+        "config": {"workload": "game of life 1024x1024x64, neighborhood 1, non-periodic (config 2)"},
+        "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                     "traffic": None, "kernel": "gol_structured_kernel", "alg_bytes_per_step": 8 * n,
+                     "kernel_ms_per_step": kms / a.steps},
+        "cpu_baseline": None}), flush=True)
+    g.close()
 
 
 def build_grid(dccrg_amd, rank, size, base, R, uid):
@@ -94,6 +138,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     import dccrg_amd
 
+    if a.workload == "gol":
+        return gol_main(a, dccrg_amd, torch)
     uid = None
     if world > 1:
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
@@ -106,8 +152,12 @@ def main():
     dt = 0.5 * g.advection_max_time_step(f)  # cfl 0.5 (2d.cpp:121-123)
     c = g.counts
     n_local = c["inner"] + c["outer"]
-    ptr, _, _ = g.csr("face")
-    face_entries = int(ptr[-1])
+    ptr, _, fdir = g.csr("face")
+    # finer faces = (cell, direction) pairs with 4 face neighbors
+    rows = np.repeat(np.arange(n_local), np.diff(ptr.astype(np.int64)))
+    pair = rows * 8 + (fdir + 3)
+    _, cnt = np.unique(pair, return_counts=True)
+    n_fine = int(np.sum(cnt == 4))
 
     def step():
         g.start_remote_neighbor_copy_updates()
@@ -144,10 +194,11 @@ def main():
     else:
         el_max, total_cells = el, n_local
 
-    # algorithmic bytes of the sweep per local cell:
-    # read density, vx, vy, vz, lx, ly, lz + write density = 64 B, plus the
-    # face CSR (4 B per entry, 4 B row pointer)
-    alg_bytes_step = 64 * n_local + 4 * face_entries + 4 * (n_local + 1)
+    # algorithmic bytes of the sweep: per cell read density,
+    # vx, vy, vz, lx, ly, lz + write density = 64 B, plus the face table the
+    # kernel reads: 6 x int32 per cell and 4 x int32 per finer face
+    alg_core = 64 * n_local
+    alg_bytes_step = alg_core + 24 * n_local + 16 * n_fine
     kern_s = kern_ms / 1e3
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
     launches_per_step = kern_n / a.steps if a.steps else 0
@@ -200,6 +251,8 @@ def main():
                 "traffic": traffic,
                 "kernel": "advection_kernel",
                 "alg_bytes_per_step": alg_bytes_step,
+                "alg_bytes_core_per_step": alg_core,
+                "finer_faces": n_fine,
                 "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
                 "launches_per_step": launches_per_step,
             },

@@ -341,6 +341,50 @@ __global__ void parent_fill_kernel(uint8_t* data, const uint64_t* slot_ids, size
 	}
 }
 
+__device__ __forceinline__ uint64_t spread3(uint64_t v) {
+	v &= 0x1FFFFFull;
+	v = (v | (v << 32)) & 0x1F00000000FFFFull;
+	v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+	v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+	v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+	v = (v | (v << 2)) & 0x1249249249249249ull;
+	return v;
+}
+
+__global__ void morton_keys_kernel(MapCtx m, const uint64_t* ids, size_t n, uint64_t* keys) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t x, y, z;
+		map_indices(m, ids[i], x, y, z);
+		keys[i] = spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+	}
+}
+
+// fixed-width face table: per local slot and direction one int32 = the
+// neighbor's slot (same size or coarser), -1 (no neighbor), or -2 - k for a
+// finer face whose 4 slots are fine[4k..4k+3] (reference order)
+__global__ void face_ell_kernel(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine,
+                                unsigned int* nfine) {
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
+		int32_t row[6] = {-1, -1, -1, -1, -1, -1};
+		uint32_t e = ptr[r];
+		const uint32_t e1 = ptr[r + 1];
+		while (e < e1) {
+			const int d = ent[e] & 7;
+			uint32_t k = e + 1;
+			while (k < e1 && (ent[k] & 7) == d) k++;
+			if (k - e == 1) {
+				row[d] = ent[e] >> 3;
+			} else {
+				const unsigned int f = atomicAdd(nfine, 1u);
+				for (int i = 0; i < 4; i++) fine[4 * size_t(f) + i] = ent[e + i] >> 3;
+				row[d] = -2 - int32_t(f);
+			}
+			e = k;
+		}
+		for (int d = 0; d < 6; d++) ell[6 * r + d] = row[d];
+	}
+}
+
 int nto_cap(int nh) {
 	int P = 1;
 	while (P < 10 * nh) P <<= 1;
@@ -512,6 +556,38 @@ void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int3
 	if (!n) return;
 	parent_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(data, slot_ids, n, m, old_data, old_slot_by_id, elem);
 	HIP_CHECK(hipGetLastError());
+}
+
+size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s) {
+	if (!nrows) return 0;
+	DBuf<unsigned int> ctr;
+	ctr.alloc(1);
+	HIP_CHECK(hipMemsetAsync(ctr.p, 0, 4, s));
+	face_ell_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(ptr, ent, nrows, ell, fine, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	unsigned int h = 0;
+	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	return h;
+}
+
+// Reorder a run of cell ids along the Morton (z-order) curve of their min
+// corners at finest-level resolution (leaves have distinct min corners).
+void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s) {
+	if (n < 2) return;
+	DBuf<uint64_t> keys, keys2, ids2;
+	keys.alloc(n);
+	keys2.alloc(n);
+	ids2.alloc(n);
+	morton_keys_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, ids, n, keys.p);
+	HIP_CHECK(hipGetLastError());
+	size_t bytes = 0;
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys.p, keys2.p, ids, ids2.p, int(n), 0, 63, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(bytes);
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, keys.p, keys2.p, ids, ids2.p, int(n), 0, 63, s));
+	HIP_CHECK(hipMemcpyAsync(ids, ids2.p, n * 8, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace dccrgx

@@ -142,6 +142,8 @@ struct Grid {
 	bool face_valid = false;
 	DBuf<uint32_t> face_ptr;
 	DBuf<int32_t> face_ent;
+	DBuf<int32_t> face_ell, face_fine;  // fixed-width form used by the advection sweep
+	size_t n_fine_faces = 0;
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;
@@ -153,6 +155,11 @@ struct Grid {
 	double timed_ms = 0;
 	int64_t timed_count = 0;
 	std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+
+	// slot order inside the inner and outer runs: 0 = ascending id (raster,
+	// needed by the structured uniform kernels), 1 = Morton order of the min
+	// corners (locality for refined meshes)
+	int slot_order = -1;  // -1: Morton when R > 0, else id
 
 	bool uniform() const { return R == 0; }
 };
@@ -185,6 +192,8 @@ size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uin
                       size_t nrows, const int32_t* owner_by_id, int rank, uint64_t stride, uint64_t* keys_out,
                       hipStream_t s);
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s);  // in place
+void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
+size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
 void k_lookup_slots(const uint64_t* ids, size_t n, const int32_t* slot_by_id, int32_t* out, int32_t* err_flag,
                     hipStream_t s);
@@ -205,7 +214,7 @@ void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, con
                size_t s1, hipStream_t s);
 void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
-                 size_t s0, size_t s1, double dt, hipStream_t s);
+                 const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                         const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,

@@ -200,6 +200,15 @@ static void rebuild(Grid& g) {
 	local_slots.alloc(nl);
 	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
 	d_local.release();
+	int order = g.slot_order;
+	if (const char* e = getenv("DCCRGX_SLOT_ORDER")) order = atoi(e);
+	if (order < 0) order = g.R > 0 ? 1 : 0;
+	bool fits = true;
+	for (int d = 0; d < 3; d++) fits = fits && m.glen[d] <= (uint64_t(1) << 21);
+	if (order == 1 && fits) {
+		k_morton_sort(m, local_slots.p, g.n_inner, s);
+		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
+	}
 
 	// 3. neighbor lists of outer cells -> send / receive lists (8590-8752)
 	g.send_ids.clear();
@@ -367,6 +376,9 @@ static void ensure_face(Grid& g) {
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
+	g.face_ell.alloc(6 * nl);
+	g.face_fine.alloc(t / 4 + 4);
+	g.n_fine_faces = k_face_ell(g.face_ptr.p, g.face_ent.p, nl, g.face_ell.p, g.face_fine.p, s);
 	g.face_valid = true;
 }
 
@@ -1301,7 +1313,8 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		region_range(g, region, s0, s1);
 		if (s1 <= s0) return 0;
 		k_time_begin(g);
-		k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, s0, s1, dt, g.s_comp);
+		k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p, g.face_fine.p, s0, s1, dt,
+		            g.s_comp);
 		k_time_end(g);
 		return 0;
 	});

@@ -4,8 +4,11 @@
  * One opaque grid per process (one process per GPU).  Cell payloads live in
  * HBM as structure-of-arrays "fields"; every field is indexed by a *slot*:
  *
- *     [0, n_inner)              local cells without remote neighbors, ascending id
- *     [n_inner, n_local)        local cells with remote neighbors,     ascending id
+ *     [0, n_inner)              local cells without remote neighbors
+ *     [n_inner, n_local)        local cells with remote neighbors
+ *                               (both runs in ascending id on unrefined grids,
+ *                               in Morton order of the cells' min corners when
+ *                               max refinement level > 0, for locality)
  *     [n_local, n_local+n_recv) copies of remote neighbors, grouped by owner
  *                               (ascending rank), ascending id inside a group
  *                               = the halo exchange wire order

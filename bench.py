@@ -152,12 +152,16 @@ def main():
     dt = 0.5 * g.advection_max_time_step(f)  # cfl 0.5 (2d.cpp:121-123)
     c = g.counts
     n_local = c["inner"] + c["outer"]
-    ptr, _, fdir = g.csr("face")
-    # finer faces = (cell, direction) pairs with 4 face neighbors
-    rows = np.repeat(np.arange(n_local), np.diff(ptr.astype(np.int64)))
-    pair = rows * 8 + (fdir + 3)
-    _, cnt = np.unique(pair, return_counts=True)
-    n_fine = int(np.sum(cnt == 4))
+    variant = int(os.environ.get("DCCRGX_ADV_VARIANT", "11"))
+    layout = g.advection_layout() if variant == 11 else None
+    if layout is None:
+        ptr, _, fdir = g.csr("face")
+        # finer faces = (cell, direction) pairs with 4 face neighbors
+        rows = np.repeat(np.arange(n_local), np.diff(ptr.astype(np.int64)))
+        _, cnt = np.unique(rows * 8 + (fdir + 3), return_counts=True)
+        n_fine = int(np.sum(cnt == 4))
+    else:
+        n_fine = layout["finer_faces"]
 
     def step():
         g.start_remote_neighbor_copy_updates()
@@ -195,10 +199,13 @@ def main():
         el_max, total_cells = el, n_local
 
     # algorithmic bytes of the sweep: per cell read density,
-    # vx, vy, vz, lx, ly, lz + write density = 64 B, plus the face table the
-    # kernel reads: 6 x int32 per cell and 4 x int32 per finer face
+    # vx, vy, vz, lx, ly, lz + write density = 64 B, plus the face structure
+    # the kernel reads: tiled sweep = 12 B face row per cell + 4 B per
+    # distinct out-of-tile neighbor of a tile + 8 B per finer face + 8 B per
+    # tile (dccrgx_advection_layout); ELL sweeps = 6 x int32 per cell + 16 B
+    # per finer face
     alg_core = 64 * n_local
-    alg_bytes_step = alg_core + 24 * n_local + 16 * n_fine
+    alg_bytes_step = layout["alg_bytes"] if layout else alg_core + 24 * n_local + 16 * n_fine
     kern_s = kern_ms / 1e3
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
     launches_per_step = kern_n / a.steps if a.steps else 0
@@ -249,7 +256,8 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "advection_kernel",
+                "kernel": "advection_tiles_kernel" if layout else f"advection_kernel variant {variant}",
+                "layout": layout,
                 "alg_bytes_per_step": alg_bytes_step,
                 "alg_bytes_core_per_step": alg_core,
                 "finer_faces": n_fine,

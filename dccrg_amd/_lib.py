@@ -77,6 +77,7 @@ _SIGS = {
     "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),
     "dccrgx_advection_max_time_step": (C.c_int, [vp, P(C.c_int), P(C.c_double)]),
     "dccrgx_advection_refine_candidates": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, vp, sz, P(sz)]),
+    "dccrgx_advection_layout": (C.c_int, [vp, P(u64)]),
     "dccrgx_allreduce_f64": (C.c_int, [vp, P(C.c_double), C.c_int, C.c_int]),
     "dccrgx_barrier": (C.c_int, [vp]),
     "dccrgx_synchronize": (C.c_int, [vp]),

@@ -83,6 +83,22 @@ struct DBuf {
 	}
 };
 
+template <class T>
+inline void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
+	d.alloc(h.size());
+	if (!h.empty()) HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+}
+
+template <class T>
+inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
+	std::vector<T> h(n);
+	if (n) {
+		HIP_CHECK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	return h;
+}
+
 struct Field {
 	std::string name;
 	size_t elem = 0;
@@ -144,6 +160,20 @@ struct Grid {
 	DBuf<int32_t> face_ent;
 	DBuf<int32_t> face_ell, face_fine;  // fixed-width form used by the advection sweep
 	size_t n_fine_faces = 0;
+	// face tiles (built lazily from the face CSR): the inner and the outer run
+	// of slots are cut into tiles of `tile` consecutive slots; per tile the
+	// distinct out-of-tile face neighbors (`ext`, ascending slot) and per cell
+	// six 16-bit tile-local neighbor indices (< tile: a slot of the tile,
+	// tile + k: ext[k] of the tile, 0x8000 | j: finer face j of the tile whose
+	// four tile-local indices are in `tfine`, 0xffff: no face neighbor)
+	bool tiles_valid = false;
+	int tile = 0;
+	size_t n_tiles_inner = 0, n_tiles_outer = 0, max_ext = 0, total_ext = 0;
+	DBuf<uint32_t> tell;       // 3 x u32 per local slot (6 x u16)
+	DBuf<uint32_t> ext_ptr;    // n_tiles + 1
+	DBuf<uint32_t> ext;        // total_ext slots
+	DBuf<uint32_t> fine_base;  // n_tiles: index of the tile's first finer face
+	DBuf<uint32_t> tfine;      // 2 x u32 per finer face (4 x u16)
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;
@@ -208,6 +238,14 @@ void k_remap_field2(const uint8_t* old_data, const uint64_t* old_ids, size_t n_o
 void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int32_t* slot_by_id, const MapCtx& m,
                    const uint8_t* old_data, const int32_t* old_slot_by_id, size_t elem, hipStream_t s);
 
+// --- launchers implemented in tile_build.hip --------------------------------
+struct TileBuild {
+	size_t n_tiles_inner, n_tiles_outer, max_ext, total_ext, n_fine;
+};
+TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, size_t n_inner, size_t n_local, int tile,
+                        DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
+                        DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s);
+
 // --- launchers implemented in sweep_kernels.hip -----------------------------
 void k_pack(const uint8_t* field, size_t elem, const int32_t* slots, size_t n, uint8_t* out, hipStream_t s);
 void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
@@ -215,6 +253,11 @@ void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, con
 void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
+// tiled advection sweep over one run [r0, r1) of slots (the inner or the
+// outer run: tiles never straddle the two); gt0 = index of the run's first tile
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t r0, size_t r1, size_t gt0,
+                       double dt, hipStream_t s);
+int adv_variant();  // DCCRGX_ADV_VARIANT (11 = tiled, the default)
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                         const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,

@@ -121,22 +121,6 @@ static int host_owner(const Grid& g, uint64_t id) {
 	return g.owners[size_t(it - g.leaves.begin())];
 }
 
-template <class T>
-static void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
-	d.alloc(h.size());
-	if (!h.empty()) HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
-}
-
-template <class T>
-static std::vector<T> download(const T* d, size_t n, hipStream_t s) {
-	std::vector<T> h(n);
-	if (n) {
-		HIP_CHECK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
-	}
-	return h;
-}
-
 static void decode_keys(const std::vector<uint64_t>& keys, uint64_t stride, std::map<int, std::vector<uint64_t>>& out) {
 	out.clear();
 	for (uint64_t k : keys) out[int(k / stride)].push_back(k % stride);
@@ -317,6 +301,7 @@ static void rebuild(Grid& g) {
 	HIP_CHECK(hipStreamSynchronize(s));
 	g.csr_valid = false;
 	g.face_valid = false;
+	g.tiles_valid = false;
 	g.slot_ids_h_valid = false;
 }
 
@@ -380,6 +365,28 @@ static void ensure_face(Grid& g) {
 	g.face_fine.alloc(t / 4 + 4);
 	g.n_fine_faces = k_face_ell(g.face_ptr.p, g.face_ent.p, nl, g.face_ell.p, g.face_fine.p, s);
 	g.face_valid = true;
+}
+
+static int tile_size_setting() {
+	static const int t = [] {
+		const char* e = getenv("DCCRGX_TILE");
+		return e ? atoi(e) : 512;
+	}();
+	return t;
+}
+
+static void ensure_tiles(Grid& g) {
+	ensure_face(g);
+	const int T = tile_size_setting();
+	if (g.tiles_valid && g.tile == T) return;
+	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.n_inner, g.n_local, T, g.tell, g.ext_ptr, g.ext,
+	                                   g.fine_base, g.tfine, g.s_comp);
+	g.tile = T;
+	g.n_tiles_inner = tb.n_tiles_inner;
+	g.n_tiles_outer = tb.n_tiles_outer;
+	g.max_ext = tb.max_ext;
+	g.total_ext = tb.total_ext;
+	g.tiles_valid = true;
 }
 
 static const std::vector<uint64_t>& slot_ids_host(Grid& g) {
@@ -1313,9 +1320,33 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		region_range(g, region, s0, s1);
 		if (s1 <= s0) return 0;
 		k_time_begin(g);
-		k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p, g.face_fine.p, s0, s1, dt,
-		            g.s_comp);
+		if (adv_variant() == 11) {
+			ensure_tiles(g);
+			// tiles never straddle the inner / outer runs
+			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, s0, std::min(s1, g.n_inner), 0, dt, g.s_comp);
+			if (s1 > g.n_inner)
+				k_advection_tiles(f, (double*)rho.scratch.p, g, g.n_inner, s1, g.n_tiles_inner, dt, g.s_comp);
+		} else {
+			k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p, g.face_fine.p, s0, s1, dt,
+			            g.s_comp);
+		}
 		k_time_end(g);
+		return 0;
+	});
+}
+
+int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[6]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(out, "null output");
+		ensure_tiles(g);
+		const uint64_t nt = g.n_tiles_inner + g.n_tiles_outer;
+		out[0] = uint64_t(g.tile);
+		out[1] = nt;
+		out[2] = g.total_ext;
+		out[3] = g.max_ext;
+		out[4] = g.n_fine_faces;
+		out[5] = 76 * uint64_t(g.n_local) + 4 * uint64_t(g.total_ext) + 8 * uint64_t(g.n_fine_faces) + 8 * nt;
 		return 0;
 	});
 }

@@ -495,6 +495,205 @@ __global__ __launch_bounds__(TILE, MINW) void advection_kernel_v3(
 	rho_out[s] = cd + acc;
 }
 
+// Face flux without the division by the cell volume (applied once per cell):
+// the face velocity and the upwind flux keep the reference's expression
+// (solve.hpp:169-225), so only the per-cell rounding of the sum differs.
+__device__ __forceinline__ double adv_face_flux(int dir, double cd, double cl_a, double cl_b, double cl_c,
+                                                double cvel, double nd, double nl_a, double nl_b, double nl_c,
+                                                double nv, double dt) {
+#pragma clang fp contract(off)
+	// cl_a = the cell's length along the face normal, cl_b/cl_c transverse
+	const double min_area = fmin(cl_b * cl_c, nl_b * nl_c);
+	const double v = (cl_a * nv + nl_a * cvel) / (cl_a + nl_a);
+	if (dir & 1) return -((v >= 0 ? cd : nd) * dt * v * min_area);
+	return (v >= 0 ? nd : cd) * dt * v * min_area;
+}
+
+struct AdvNb {
+	double d, lx, ly, lz, v;
+};
+
+__device__ __forceinline__ double adv_face_flux_d(int d, double cd, double clx, double cly, double clz, double cvx,
+                                                  double cvy, double cvz, const AdvNb& n, double dt) {
+	if (d < 2) return adv_face_flux(d, cd, clx, cly, clz, cvx, n.d, n.lx, n.ly, n.lz, n.v, dt);
+	if (d < 4) return adv_face_flux(d, cd, cly, clx, clz, cvy, n.d, n.ly, n.lx, n.lz, n.v, dt);
+	return adv_face_flux(d, cd, clz, clx, cly, cvz, n.d, n.lz, n.lx, n.ly, n.v, dt);
+}
+
+// 32-bit byte offsets from a uniform base: global_load v, voff, s[base]
+// (halves the address registers of a gather; slots < 2^29, checked on the host)
+__device__ __forceinline__ double ldo(const double* __restrict__ p, uint32_t off) {
+	return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(p) + off);
+}
+
+__device__ __forceinline__ AdvNb adv_gather(const double* __restrict__ rho, const double* __restrict__ lx,
+                                            const double* __restrict__ ly, const double* __restrict__ lz,
+                                            const double* __restrict__ vdir, size_t n) {
+	const uint32_t o = uint32_t(n) << 3;
+	return AdvNb{ldo(rho, o), ldo(lx, o), ldo(ly, o), ldo(lz, o), ldo(vdir, o)};
+}
+
+// v3 with one division by the cell volume per cell instead of one per face
+template <int TILE, int MINW>
+__global__ __launch_bounds__(TILE, MINW) void advection_kernel_v6(
+    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
+    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
+    const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
+    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt, unsigned nb_real) {
+#pragma clang fp contract(off)
+	__shared__ double sh[7][TILE];
+	const unsigned nb = gridDim.x;
+	const unsigned b = blockIdx.x;
+	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
+	if (lb >= nb_real) return;  // block-uniform
+	const size_t base = s0 + size_t(lb) * TILE;
+	const size_t s = base + threadIdx.x;
+	const bool valid = s < s1;
+	double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
+	int32_t row[6] = {-1, -1, -1, -1, -1, -1};
+	if (valid) {
+		const int2* r2 = reinterpret_cast<const int2*>(ell + 6 * s);
+		const int2 a = r2[0], bb = r2[1], c = r2[2];
+		row[0] = a.x; row[1] = a.y; row[2] = bb.x; row[3] = bb.y; row[4] = c.x; row[5] = c.y;
+		cd = rho[s]; cvx = vx[s]; cvy = vy[s]; cvz = vz[s]; clx = lx[s]; cly = ly[s]; clz = lz[s];
+	}
+	sh[0][threadIdx.x] = cd;
+	sh[1][threadIdx.x] = cvx;
+	sh[2][threadIdx.x] = cvy;
+	sh[3][threadIdx.x] = cvz;
+	sh[4][threadIdx.x] = clx;
+	sh[5][threadIdx.x] = cly;
+	sh[6][threadIdx.x] = clz;
+	__syncthreads();
+	if (!valid) return;
+	AdvNb nb6[6];
+#pragma unroll
+	for (int d = 0; d < 6; d++) {
+		const size_t n = row[d] >= 0 ? size_t(row[d]) : s;
+		const size_t k = n - base;
+		if (k < size_t(TILE) && n < s1)
+			nb6[d] = AdvNb{sh[0][k], sh[4][k], sh[5][k], sh[6][k], sh[1 + (d >> 1)][k]};
+		else
+			nb6[d] = adv_gather(rho, lx, ly, lz, d < 2 ? vx : (d < 4 ? vy : vz), n);
+	}
+	double acc = 0;
+#pragma unroll
+	for (int d = 0; d < 6; d++) {
+		if (row[d] >= 0) {
+			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, nb6[d], dt);
+		} else if (row[d] <= -2) {
+			const int4 q = reinterpret_cast<const int4*>(fine)[-2 - row[d]];
+			const int32_t fs[4] = {q.x, q.y, q.z, q.w};
+			const double* vdir = d < 2 ? vx : (d < 4 ? vy : vz);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const AdvNb f = adv_gather(rho, lx, ly, lz, vdir, size_t(fs[k]));
+				acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, f, dt);
+			}
+		}
+	}
+	rho_out[s] = cd + acc / (clx * cly * clz);
+}
+
+// Tiled sweep (tables: tile_build.hip).  One workgroup per tile of T
+// consecutive slots; one thread per cell.  Phase 1 stages the tile's own
+// seven fields (coalesced) and the fields of its distinct out-of-tile face
+// neighbors (one gather per neighbor, not one per face) in LDS; phase 2
+// evaluates every face from LDS through the 16-bit tile-local index, so the
+// only global traffic is the staging and the density store.  Tiles are
+// dealt so that each XCD sweeps one contiguous eighth of the run (blocks b
+// and b + 8 share an XCD): the ext cells of a tile are the own cells of
+// tiles swept nearby in time, i.e. L2 hits.  A tile with more ext cells
+// than the LDS holds (ecap) reads the surplus from global memory.
+template <int T, int MINW>
+__global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
+    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
+    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
+    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tell,
+    const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext, const uint32_t* __restrict__ fine_base,
+    const uint32_t* __restrict__ tfine, uint32_t r0, uint32_t r1, uint32_t gt0, uint32_t ntiles, uint32_t ecap,
+    double dt) {
+#pragma clang fp contract(off)
+	extern __shared__ double shd[];  // [7][T + ecap]
+	const uint32_t W = T + ecap;
+	const unsigned nb = gridDim.x, b = blockIdx.x;
+	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
+	if (lb >= ntiles) return;  // block-uniform
+	const uint32_t gt = gt0 + lb;
+	const uint32_t ts = r0 + lb * T;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t s = ts + tid;
+	const bool valid = s < r1;
+	const uint32_t e0 = ext_ptr[gt], e1 = ext_ptr[gt + 1];
+	const uint32_t nes = min(e1 - e0, ecap);
+	const double* const fld[7] = {rho, vx, vy, vz, lx, ly, lz};
+
+	// phase 1: own cell, face row, and up to two ext cells per thread
+	double c[7] = {0, 0, 0, 0, 1, 1, 1};
+	uint32_t row[3] = {~0u, ~0u, ~0u};
+	const uint32_t ja = tid, jb = tid + T;
+	const uint32_t xa = ja < nes ? ext[e0 + ja] : 0u, xb = jb < nes ? ext[e0 + jb] : 0u;
+	if (valid) {
+		row[0] = tell[3 * size_t(s)];
+		row[1] = tell[3 * size_t(s) + 1];
+		row[2] = tell[3 * size_t(s) + 2];
+		const uint32_t o = s << 3;
+#pragma unroll
+		for (int k = 0; k < 7; k++) c[k] = ldo(fld[k], o);
+	}
+	double va[7], vb[7];
+	if (ja < nes) {
+		const uint32_t o = xa << 3;
+#pragma unroll
+		for (int k = 0; k < 7; k++) va[k] = ldo(fld[k], o);
+	}
+	if (jb < nes) {
+		const uint32_t o = xb << 3;
+#pragma unroll
+		for (int k = 0; k < 7; k++) vb[k] = ldo(fld[k], o);
+	}
+#pragma unroll
+	for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
+	if (ja < nes)
+#pragma unroll
+		for (int k = 0; k < 7; k++) shd[k * W + T + ja] = va[k];
+	if (jb < nes)
+#pragma unroll
+		for (int k = 0; k < 7; k++) shd[k * W + T + jb] = vb[k];
+	for (uint32_t j = tid + 2 * T; j < nes; j += T) {
+		const uint32_t o = ext[e0 + j] << 3;
+#pragma unroll
+		for (int k = 0; k < 7; k++) shd[k * W + T + j] = ldo(fld[k], o);
+	}
+	__syncthreads();
+	if (!valid) return;
+
+	// phase 2: faces from LDS, in the reference's face order
+	auto fetch = [&](uint32_t li, int d) -> AdvNb {
+		const int dv = 1 + (d >> 1);
+		if (li < T + nes) return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[dv * W + li]};
+		const uint32_t o = ext[e0 + li - T] << 3;  // beyond the LDS capacity of this tile
+		return AdvNb{ldo(rho, o), ldo(lx, o), ldo(ly, o), ldo(lz, o), ldo(fld[dv], o)};
+	};
+	const double cd = c[0], cvx = c[1], cvy = c[2], cvz = c[3], clx = c[4], cly = c[5], clz = c[6];
+	double acc = 0;
+#pragma unroll
+	for (int d = 0; d < 6; d++) {
+		const uint32_t code = (row[d >> 1] >> (16 * (d & 1))) & 0xffffu;
+		if (code == 0xffffu) continue;
+		if (code & 0x8000u) {
+			const uint32_t fk = fine_base[gt] + (code & 0x7fffu);
+			const uint32_t q0 = tfine[2 * size_t(fk)], q1 = tfine[2 * size_t(fk) + 1];
+			const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
+#pragma unroll
+			for (int k = 0; k < 4; k++) acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
+		} else {
+			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
+		}
+	}
+	rho_out[s] = cd + acc / (clx * cly * clz);
+}
+
 // max_time_step local part (solve.hpp:289-333): block minima
 __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __restrict__ vy,
                               const double* __restrict__ vz, const double* __restrict__ lx,
@@ -597,7 +796,7 @@ void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 int adv_variant() {
 	static int v = [] {
 		const char* e = getenv("DCCRGX_ADV_VARIANT");
-		return e ? atoi(e) : 3;
+		return e ? atoi(e) : 11;
 	}();
 	return v;
 }
@@ -605,7 +804,23 @@ int adv_variant() {
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s) {
 	if (s1 <= s0) return;
-	if (adv_variant() >= 3) {
+	if (adv_variant() == 9 || adv_variant() == 10) {
+		constexpr int T = 256;
+		const size_t nb_real = (s1 - s0 + T - 1) / T;
+		const size_t nb = (nb_real + 7) / 8 * 8;
+		if (adv_variant() == 9)
+			advection_kernel_v6<T, 6><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
+			                                                    face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
+		else
+			advection_kernel_v6<T, 8><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
+			                                                    face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
+	} else if (adv_variant() == 6) {
+		constexpr int T = 512;
+		const size_t nb_real = (s1 - s0 + T - 1) / T;
+		const size_t nb = (nb_real + 7) / 8 * 8;
+		advection_kernel_v6<T, 4><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, face_ell,
+		                                                 face_fine, s0, s1, dt, unsigned(nb_real));
+	} else if (adv_variant() >= 3) {
 		const int tile = adv_variant() == 4 ? 256 : 512;
 		const size_t nb_real = (s1 - s0 + tile - 1) / tile;
 		const size_t nb = (nb_real + 7) / 8 * 8;
@@ -633,6 +848,37 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 		advection_kernel_v1<<<unsigned(nb), ADV_BLOCK, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
 		                                                       face_ptr, face_ent, s0, s1, dt, unsigned(nb_real));
 	}
+	HIP_CHECK(hipGetLastError());
+}
+
+// LDS rows for ext cells: a compact T-cell box has about T^(2/3) * 6 of them
+// (384 for an 8x8x8 box); larger lists spill to global reads
+static uint32_t tile_ecap(int T, size_t max_ext) {
+	static const int env = [] {
+		const char* e = getenv("DCCRGX_TILE_ECAP");
+		return e ? atoi(e) : -1;
+	}();
+	const size_t cap = env >= 0 ? size_t(env) : (T >= 512 ? size_t(3 * T / 4) : size_t(T));
+	return uint32_t(std::min(cap, max_ext));
+}
+
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t r0, size_t r1, size_t gt0,
+                       double dt, hipStream_t s) {
+	if (r1 <= r0) return;
+	const int T = g.tile;
+	const size_t ntiles = (r1 - r0 + T - 1) / T;
+	const size_t nb = (ntiles + 7) / 8 * 8;
+	const uint32_t ecap = tile_ecap(T, g.max_ext);
+	const size_t lds = size_t(7) * (T + ecap) * sizeof(double);
+#define DX_ADV_TILES(TT, W)                                                                                          \
+	advection_tiles_kernel<TT, W><<<unsigned(nb), TT, lds, s>>>(                                                       \
+	    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tell.p, g.ext_ptr.p, g.ext.p, g.fine_base.p, g.tfine.p,  \
+	    uint32_t(r0), uint32_t(r1), uint32_t(gt0), uint32_t(ntiles), ecap, dt)
+	if (T == 512) DX_ADV_TILES(512, 6);
+	else if (T == 256) DX_ADV_TILES(256, 5);
+	else if (T == 1024) DX_ADV_TILES(1024, 4);
+	else throw Error(DCCRGX_EINVAL, "unsupported advection tile size");
+#undef DX_ADV_TILES
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -372,6 +372,14 @@ class Dccrg:
         check(lib().dccrgx_advection_max_time_step(self.h, self._fids(fields), C.byref(v)))
         return self.allreduce(v.value, "min")
 
+    def advection_layout(self):
+        """Tile layout of the advection sweep and its algorithmic HBM bytes per
+        sweep over all local cells (see include/dccrgx.h)."""
+        out = (C.c_uint64 * 6)()
+        check(lib().dccrgx_advection_layout(self.h, out))
+        keys = ("tile", "tiles", "ext_total", "ext_max", "finer_faces", "alg_bytes")
+        return dict(zip(keys, (int(v) for v in out)))
+
     def advection_refine_candidates(self, density, diff_increase, diff_threshold):
         return self._u64_query(lib().dccrgx_advection_refine_candidates, density.id, float(diff_increase),
                                float(diff_threshold))

@@ -171,6 +171,14 @@ int dccrgx_advection_max_time_step(dccrgx_grid* g, const int fields[7], double* 
 int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double diff_increase,
                                        double diff_threshold, uint64_t* out, size_t cap, size_t* n);
 
+/* data layout of the advection sweep (built on first use): out[0] tile size,
+ * [1] tiles, [2] distinct out-of-tile face neighbors summed over tiles,
+ * [3] largest per-tile count, [4] finer faces, [5] algorithmic HBM bytes of
+ * one sweep over all local cells (own fields 64 B/cell + face rows 12 B/cell
+ * + 4 B per out-of-tile neighbor + 8 B per finer face + 8 B per tile).
+ * No reference counterpart (layout introspection for the roofline). */
+int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[6]);
+
 /* ---- collectives for user kernels (MPI_Allreduce in solve.hpp:317) ------- */
 int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 sum, 1 min, 2 max */);
 int dccrgx_barrier(dccrgx_grid* g);

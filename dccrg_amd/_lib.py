@@ -10,7 +10,9 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdccrgx.so")
+# DCCRGX_LIB selects another build of the same library (kernel A/B runs);
+# default: the in-tree build
+LIB_PATH = os.environ.get("DCCRGX_LIB") or os.path.join(HERE, "libdccrgx.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "dccrgx.h")
 
 _lib = None

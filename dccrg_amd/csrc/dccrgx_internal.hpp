@@ -161,7 +161,8 @@ struct Grid {
 	DBuf<int32_t> face_ell, face_fine;  // fixed-width form used by the advection sweep
 	size_t n_fine_faces = 0;
 	// face tiles (built lazily from the face CSR): the inner and the outer run
-	// of slots are cut into tiles of `tile` consecutive slots; per tile the
+	// of slots are cut into tiles of at most `tile` consecutive slots
+	// (boundaries `tstart`, on aligned Morton boxes where possible); per tile the
 	// distinct out-of-tile face neighbors (`ext`, ascending slot) and per cell
 	// six 16-bit tile-local neighbor indices (< tile: a slot of the tile,
 	// tile + k: ext[k] of the tile, 0x8000 | j: finer face j of the tile whose
@@ -169,6 +170,7 @@ struct Grid {
 	bool tiles_valid = false;
 	int tile = 0;
 	size_t n_tiles_inner = 0, n_tiles_outer = 0, max_ext = 0, total_ext = 0;
+	DBuf<uint32_t> tstart;     // n_tiles + 1
 	DBuf<uint32_t> tell;       // 3 x u32 per local slot (6 x u16)
 	DBuf<uint32_t> ext_ptr;    // n_tiles + 1
 	DBuf<uint32_t> ext;        // total_ext slots
@@ -190,6 +192,7 @@ struct Grid {
 	// needed by the structured uniform kernels), 1 = Morton order of the min
 	// corners (locality for refined meshes)
 	int slot_order = -1;  // -1: Morton when R > 0, else id
+	bool morton_slots = false;  // the order in effect
 
 	bool uniform() const { return R == 0; }
 };
@@ -242,7 +245,8 @@ void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int3
 struct TileBuild {
 	size_t n_tiles_inner, n_tiles_outer, max_ext, total_ext, n_fine;
 };
-TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, size_t n_inner, size_t n_local, int tile,
+TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& m,
+                        bool morton, size_t n_inner, size_t n_local, int tile, DBuf<uint32_t>& tstart,
                         DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
                         DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s);
 
@@ -253,10 +257,10 @@ void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, con
 void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
-// tiled advection sweep over one run [r0, r1) of slots (the inner or the
-// outer run: tiles never straddle the two); gt0 = index of the run's first tile
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t r0, size_t r1, size_t gt0,
-                       double dt, hipStream_t s);
+// tiled advection sweep over tiles [gt0, gt0 + ntiles) (the inner or the
+// outer run: tiles never straddle the two)
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t gt0, size_t ntiles, double dt,
+                       hipStream_t s);
 int adv_variant();  // DCCRGX_ADV_VARIANT (11 = tiled, the default)
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,

@@ -189,7 +189,8 @@ static void rebuild(Grid& g) {
 	if (order < 0) order = g.R > 0 ? 1 : 0;
 	bool fits = true;
 	for (int d = 0; d < 3; d++) fits = fits && m.glen[d] <= (uint64_t(1) << 21);
-	if (order == 1 && fits) {
+	g.morton_slots = order == 1 && fits;
+	if (g.morton_slots) {
 		k_morton_sort(m, local_slots.p, g.n_inner, s);
 		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
 	}
@@ -379,8 +380,8 @@ static void ensure_tiles(Grid& g) {
 	ensure_face(g);
 	const int T = tile_size_setting();
 	if (g.tiles_valid && g.tile == T) return;
-	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.n_inner, g.n_local, T, g.tell, g.ext_ptr, g.ext,
-	                                   g.fine_base, g.tfine, g.s_comp);
+	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.slot_ids.p, g.m, g.morton_slots, g.n_inner,
+	                                   g.n_local, T, g.tstart, g.tell, g.ext_ptr, g.ext, g.fine_base, g.tfine, g.s_comp);
 	g.tile = T;
 	g.n_tiles_inner = tb.n_tiles_inner;
 	g.n_tiles_outer = tb.n_tiles_outer;
@@ -1323,9 +1324,9 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		if (adv_variant() == 11) {
 			ensure_tiles(g);
 			// tiles never straddle the inner / outer runs
-			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, s0, std::min(s1, g.n_inner), 0, dt, g.s_comp);
+			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, g.n_tiles_inner, dt, g.s_comp);
 			if (s1 > g.n_inner)
-				k_advection_tiles(f, (double*)rho.scratch.p, g, g.n_inner, s1, g.n_tiles_inner, dt, g.s_comp);
+				k_advection_tiles(f, (double*)rho.scratch.p, g, g.n_tiles_inner, g.n_tiles_outer, dt, g.s_comp);
 		} else {
 			k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p, g.face_fine.p, s0, s1, dt,
 			            g.s_comp);
@@ -1346,7 +1347,7 @@ int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[6]) {
 		out[2] = g.total_ext;
 		out[3] = g.max_ext;
 		out[4] = g.n_fine_faces;
-		out[5] = 76 * uint64_t(g.n_local) + 4 * uint64_t(g.total_ext) + 8 * uint64_t(g.n_fine_faces) + 8 * nt;
+		out[5] = 76 * uint64_t(g.n_local) + 4 * uint64_t(g.total_ext) + 8 * uint64_t(g.n_fine_faces) + 12 * nt;
 		return 0;
 	});
 }

@@ -595,48 +595,78 @@ __global__ __launch_bounds__(TILE, MINW) void advection_kernel_v6(
 	rho_out[s] = cd + acc / (clx * cly * clz);
 }
 
-// Tiled sweep (tables: tile_build.hip).  One workgroup per tile of T
-// consecutive slots; one thread per cell.  Phase 1 stages the tile's own
+// Tiled sweep (tables: tile_build.hip).  One workgroup per tile of at most
+// T consecutive slots; one thread per cell.  Phase 1 stages the tile's own
 // seven fields (coalesced) and the fields of its distinct out-of-tile face
 // neighbors (one gather per neighbor, not one per face) in LDS; phase 2
 // evaluates every face from LDS through the 16-bit tile-local index, so the
 // only global traffic is the staging and the density store.  Tiles are
-// dealt so that each XCD sweeps one contiguous eighth of the run (blocks b
-// and b + 8 share an XCD): the ext cells of a tile are the own cells of
-// tiles swept nearby in time, i.e. L2 hits.  A tile with more ext cells
+// dealt to the XCDs in runs of Morton-consecutive tiles (see the block
+// mapping below): the ext cells of a tile are mostly own cells of tiles
+// swept nearby in time, i.e. cache hits.  A tile with more ext cells
 // than the LDS holds (ecap) reads the surplus from global memory.
-template <int T, int MINW>
+template <int T, int MINW, int DIAG>
 __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
     const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
     const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tell,
-    const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext, const uint32_t* __restrict__ fine_base,
-    const uint32_t* __restrict__ tfine, uint32_t r0, uint32_t r1, uint32_t gt0, uint32_t ntiles, uint32_t ecap,
-    double dt) {
+    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tstart,
+    const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext,
+    const uint32_t* __restrict__ fine_base, const uint32_t* __restrict__ tfine, uint32_t gt0, uint32_t ntiles,
+    uint32_t ecap, double dt, int map) {
 #pragma clang fp contract(off)
 	extern __shared__ double shd[];  // [7][T + ecap]
 	const uint32_t W = T + ecap;
 	const unsigned nb = gridDim.x, b = blockIdx.x;
-	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
+	// block b runs on XCD b % 8 as that XCD's (b / 8)-th block; each XCD
+	// sweeps runs of `map` consecutive (Morton-adjacent) tiles, the eight
+	// XCDs side by side, so a tile's out-of-tile neighbors are mostly tiles
+	// its own XCD swept just before or sweeps concurrently (L2 hits) and the
+	// rest were read recently by another XCD (Infinity Cache hits); map == 0:
+	// one contiguous eighth per XCD, map == 1: no XCD awareness
+	unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
+	if (map == 1) lb = b;
+	else if (map >= 2) {
+		const unsigned G = unsigned(map), x = b & 7u, k = b >> 3;
+		lb = ((k / G) * 8u + x) * G + (k % G);
+	}
 	if (lb >= ntiles) return;  // block-uniform
 	const uint32_t gt = gt0 + lb;
-	const uint32_t ts = r0 + lb * T;
+	const uint32_t ts = tstart[gt], te = tstart[gt + 1];
 	const uint32_t tid = threadIdx.x;
 	const uint32_t s = ts + tid;
-	const bool valid = s < r1;
+	const bool valid = s < te;
 	const uint32_t e0 = ext_ptr[gt], e1 = ext_ptr[gt + 1];
-	const uint32_t nes = min(e1 - e0, ecap);
+	const uint32_t nes = DIAG >= 1 ? 0u : min(e1 - e0, ecap);
 	const double* const fld[7] = {rho, vx, vy, vz, lx, ly, lz};
+	if (DIAG == 3) {
+		if (!valid) return;
+		const uint32_t o = s << 3;
+		double a = 0;
+#pragma unroll
+		for (int k = 0; k < 7; k++) a += ldo(fld[k], o);
+		rho_out[s] = a;
+		return;
+	}
 
 	// phase 1: own cell, face row, and up to two ext cells per thread
 	double c[7] = {0, 0, 0, 0, 1, 1, 1};
 	uint32_t row[3] = {~0u, ~0u, ~0u};
 	const uint32_t ja = tid, jb = tid + T;
-	const uint32_t xa = ja < nes ? ext[e0 + ja] : 0u, xb = jb < nes ? ext[e0 + jb] : 0u;
+	uint32_t xa = ja < nes ? ext[e0 + ja] : 0u, xb = jb < nes ? ext[e0 + jb] : 0u;
+	if (DIAG == 4) {  // same dependent loads, but the gathers hit the tile's own lines
+		xa = ts + (xa & 255u);
+		xb = ts + (xb & 255u);
+	}
 	if (valid) {
-		row[0] = tell[3 * size_t(s)];
-		row[1] = tell[3 * size_t(s) + 1];
-		row[2] = tell[3 * size_t(s) + 2];
+		if (DIAG == 2) {
+			row[0] = (tid ^ 1) | ((tid ^ 1) << 16);
+			row[1] = (tid ^ 2) | ((tid ^ 2) << 16);
+			row[2] = (tid ^ 4) | ((tid ^ 4) << 16);
+		} else {
+			row[0] = tell[3 * size_t(s)];
+			row[1] = tell[3 * size_t(s) + 1];
+			row[2] = tell[3 * size_t(s) + 2];
+		}
 		const uint32_t o = s << 3;
 #pragma unroll
 		for (int k = 0; k < 7; k++) c[k] = ldo(fld[k], o);
@@ -672,6 +702,7 @@ __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
 	auto fetch = [&](uint32_t li, int d) -> AdvNb {
 		const int dv = 1 + (d >> 1);
 		if (li < T + nes) return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[dv * W + li]};
+		if (DIAG >= 1) return AdvNb{c[0], c[4], c[5], c[6], c[dv]};
 		const uint32_t o = ext[e0 + li - T] << 3;  // beyond the LDS capacity of this tile
 		return AdvNb{ldo(rho, o), ldo(lx, o), ldo(ly, o), ldo(lz, o), ldo(fld[dv], o)};
 	};
@@ -862,23 +893,41 @@ static uint32_t tile_ecap(int T, size_t max_ext) {
 	return uint32_t(std::min(cap, max_ext));
 }
 
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t r0, size_t r1, size_t gt0,
-                       double dt, hipStream_t s) {
-	if (r1 <= r0) return;
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t gt0, size_t ntiles, double dt,
+                       hipStream_t s) {
+	if (ntiles == 0) return;
 	const int T = g.tile;
-	const size_t ntiles = (r1 - r0 + T - 1) / T;
-	const size_t nb = (ntiles + 7) / 8 * 8;
 	const uint32_t ecap = tile_ecap(T, g.max_ext);
-	const size_t lds = size_t(7) * (T + ecap) * sizeof(double);
+	size_t lds = size_t(7) * (T + ecap) * sizeof(double);
+	static const int diag = [] {
+		const char* e = getenv("DCCRGX_ADV_DIAG");
+		return e ? atoi(e) : 0;
+	}();
+	if (diag == 3) lds = 0;
+	static const int amap = [] {
+		const char* e = getenv("DCCRGX_ADV_MAP");
+		return e ? atoi(e) : 128;
+	}();
+	// whole rounds of 8 x map tiles, so that the block -> tile map is onto
+	// (blocks past the last tile exit at once)
+	const size_t round = amap >= 2 ? size_t(8) * size_t(amap) : size_t(8);
+	const size_t nb = (ntiles + round - 1) / round * round;
+#define DX_ADV_TILES1(TT, W, M)                                                                                      \
+	advection_tiles_kernel<TT, W, M><<<unsigned(nb), TT, lds, s>>>(                                                       \
+	    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, g.tell.p, g.ext_ptr.p, g.ext.p, g.fine_base.p, \
+	    g.tfine.p, uint32_t(gt0), uint32_t(ntiles), ecap, dt, amap)
 #define DX_ADV_TILES(TT, W)                                                                                          \
-	advection_tiles_kernel<TT, W><<<unsigned(nb), TT, lds, s>>>(                                                       \
-	    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tell.p, g.ext_ptr.p, g.ext.p, g.fine_base.p, g.tfine.p,  \
-	    uint32_t(r0), uint32_t(r1), uint32_t(gt0), uint32_t(ntiles), ecap, dt)
+	if (diag == 1) DX_ADV_TILES1(TT, W, 1);                                                                          \
+	else if (diag == 2) DX_ADV_TILES1(TT, W, 2);                                                                     \
+	else if (diag == 3) DX_ADV_TILES1(TT, W, 3);                                                                     \
+	else if (diag == 4) DX_ADV_TILES1(TT, W, 4);                                                                     \
+	else DX_ADV_TILES1(TT, W, 0)
 	if (T == 512) DX_ADV_TILES(512, 6);
 	else if (T == 256) DX_ADV_TILES(256, 5);
 	else if (T == 1024) DX_ADV_TILES(1024, 4);
 	else throw Error(DCCRGX_EINVAL, "unsupported advection tile size");
 #undef DX_ADV_TILES
+#undef DX_ADV_TILES1
 	HIP_CHECK(hipGetLastError());
 }
 

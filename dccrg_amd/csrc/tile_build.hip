@@ -1,9 +1,9 @@
 // Face tiles for the advection sweep (built once per mesh, from the face CSR
 // of get_face_neighbors_of, dccrg.hpp:2806-2933).
 //
-// The inner and the outer run of local slots are cut into tiles of T
-// consecutive slots (Morton order on refined grids, so a tile is a compact
-// box of space).  A tile's sweep stages its own cells and the distinct
+// The inner and the outer run of local slots are cut into tiles of at most
+// T consecutive slots (Morton order on refined grids; cuts on aligned box
+// corners where possible, so a tile is a compact box of space).  A tile's sweep stages its own cells and the distinct
 // cells just outside it ("ext") in LDS; every face of every cell then reads
 // its neighbor from LDS through a 16-bit tile-local index.  Construction:
 //   1. one key (tile << 32 | slot) per out-of-tile face entry,
@@ -27,17 +27,33 @@ inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u
 }
 
 struct TileGeom {
-	uint32_t n_inner, n_local, T, nti;  // nti = tiles of the inner run
+	const uint32_t* tstart;  // ntiles + 1 tile boundaries (slots)
+	uint32_t ntiles, n_local;
 	// tile of row r: global tile index, first and one-past-last slot
 	__device__ void of(uint32_t r, uint32_t& gt, uint32_t& ts, uint32_t& te) const {
-		const bool inner = r < n_inner;
-		const uint32_t r0 = inner ? 0u : n_inner, r1 = inner ? n_inner : n_local;
-		const uint32_t tl = (r - r0) / T;
-		gt = (inner ? 0u : nti) + tl;
-		ts = r0 + tl * T;
-		te = min(ts + T, r1);
+		uint32_t lo = 0, hi = ntiles;  // last tile with tstart <= r
+		while (hi - lo > 1) {
+			const uint32_t mid = (lo + hi) / 2;
+			if (tstart[mid] <= r) lo = mid;
+			else hi = mid;
+		}
+		gt = lo;
+		ts = tstart[lo];
+		te = tstart[lo + 1];
 	}
 };
+
+// alignment of each slot's min corner on the Morton curve: the number of
+// trailing zero 3-bit groups of its finest-level key (a tile that starts at
+// a slot with alignment k starts on the corner of a 2^k-box)
+__global__ void align_kernel(MapCtx m, const uint64_t* __restrict__ ids, uint32_t n, uint8_t* __restrict__ al) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		uint64_t x, y, z;
+		map_indices(m, ids[i], x, y, z);
+		const uint64_t k = x | y | z;  // a key has 3k trailing zeros iff all three indices have k
+		al[i] = uint8_t(k ? __builtin_ctzll(k) : 63);
+	}
+}
 
 __global__ void ext_keys_kernel(TileGeom tg, const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
                                 uint64_t* __restrict__ keys) {
@@ -86,16 +102,14 @@ __global__ void fine_count_kernel(uint32_t n, const uint32_t* __restrict__ ptr, 
 	}
 }
 
-__global__ void fine_base_kernel(TileGeom tg, uint32_t ntiles, const uint32_t* __restrict__ fine_idx,
-                                 uint32_t* __restrict__ fine_base) {
-	for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
-		const uint32_t ts = t < tg.nti ? t * tg.T : tg.n_inner + (t - tg.nti) * tg.T;
-		fine_base[t] = fine_idx[ts];
-	}
+__global__ void fine_base_kernel(TileGeom tg, const uint32_t* __restrict__ fine_idx, uint32_t* __restrict__ fine_base) {
+	for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < tg.ntiles; t += gridDim.x * blockDim.x)
+		fine_base[t] = fine_idx[tg.tstart[t]];
 }
 
 __device__ uint32_t local_index(uint32_t n, uint32_t ts, uint32_t te, uint32_t T, const uint32_t* ext, uint32_t e0,
                                 uint32_t e1, int* err) {
+	// T = the tile capacity: ext entries follow the largest possible tile
 	if (n >= ts && n < te) return n - ts;
 	uint32_t lo = e0, hi = e1;
 	while (lo < hi) {
@@ -110,7 +124,7 @@ __device__ uint32_t local_index(uint32_t n, uint32_t ts, uint32_t te, uint32_t T
 	return T + (lo - e0);
 }
 
-__global__ void tile_ell_kernel(TileGeom tg, const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
+__global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
                                 const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext,
                                 const uint32_t* __restrict__ fine_idx, const uint32_t* __restrict__ fine_base,
                                 uint32_t* __restrict__ tell, uint32_t* __restrict__ tfine, int* err) {
@@ -127,10 +141,10 @@ __global__ void tile_ell_kernel(TileGeom tg, const uint32_t* __restrict__ ptr, c
 			uint32_t k = e + 1;
 			while (k < eend && (ent[k] & 7) == d) k++;
 			if (k - e == 1) {
-				code[d] = local_index(uint32_t(ent[e] >> 3), ts, te, tg.T, ext, e0, e1, err);
+				code[d] = local_index(uint32_t(ent[e] >> 3), ts, te, T, ext, e0, e1, err);
 			} else {
 				uint32_t li[4];
-				for (int i = 0; i < 4; i++) li[i] = local_index(uint32_t(ent[e + i] >> 3), ts, te, tg.T, ext, e0, e1, err);
+				for (int i = 0; i < 4; i++) li[i] = local_index(uint32_t(ent[e + i] >> 3), ts, te, T, ext, e0, e1, err);
 				tfine[2 * size_t(fk)] = li[0] | (li[1] << 16);
 				tfine[2 * size_t(fk) + 1] = li[2] | (li[3] << 16);
 				code[d] = 0x8000u | (fk - fine_base[gt]);
@@ -146,22 +160,61 @@ __global__ void tile_ell_kernel(TileGeom tg, const uint32_t* __restrict__ ptr, c
 
 }  // namespace
 
-TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, size_t n_inner, size_t n_local, int tile,
+// Tile boundaries of one run [r0, r1): greedy, each tile ends at the
+// best-aligned slot among the last three quarters of its allowed length
+// (the latest one on ties), so that on
+// Morton-ordered slots tiles coincide with aligned boxes wherever the mesh
+// allows (fewer distinct out-of-tile neighbors than arbitrary cuts).
+static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, uint32_t T, std::vector<uint32_t>& out) {
+	uint32_t a = r0;
+	while (a < r1) {
+		out.push_back(a);
+		if (r1 - a <= T) break;
+		uint32_t best = a + T;
+		int best_al = -1;
+		for (uint32_t b = a + T; b >= a + T / 4 && b > a; b--) {
+			const int v = al.empty() ? 0 : int(al[b]);
+			if (v > best_al) {
+				best_al = v;
+				best = b;
+			}
+		}
+		a = best;
+	}
+}
+
+TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& mc,
+                        bool morton, size_t n_inner, size_t n_local, int tile, DBuf<uint32_t>& tstart,
                         DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
                         DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s) {
 	DX_REQUIRE(tile > 0 && tile <= 4096, "tile size out of range");
 	DX_REQUIRE(n_local < (size_t(1) << 31), "too many local cells for 32-bit slots");
 	TileBuild out{};
 	const uint32_t T = uint32_t(tile);
-	TileGeom tg{uint32_t(n_inner), uint32_t(n_local), T, uint32_t((n_inner + T - 1) / T)};
-	out.n_tiles_inner = tg.nti;
-	out.n_tiles_outer = (n_local - n_inner + T - 1) / T;
-	const size_t ntiles = out.n_tiles_inner + out.n_tiles_outer;
+	std::vector<uint8_t> al;
+	if (morton && n_local) {
+		DBuf<uint8_t> dal;
+		dal.alloc(n_local);
+		align_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(mc, slot_ids, uint32_t(n_local), dal.p);
+		HIP_CHECK(hipGetLastError());
+		al = download(dal.p, n_local, s);
+	}
+	std::vector<uint32_t> hts;
+	cut_run(al, 0, uint32_t(n_inner), T, hts);
+	out.n_tiles_inner = hts.size();
+	cut_run(al, uint32_t(n_inner), uint32_t(n_local), T, hts);
+	out.n_tiles_outer = hts.size() - out.n_tiles_inner;
+	const size_t ntiles = hts.size();
+	hts.push_back(uint32_t(n_local));
+	tstart.alloc(ntiles + 1);
+	HIP_CHECK(hipMemcpyAsync(tstart.p, hts.data(), (ntiles + 1) * 4, hipMemcpyHostToDevice, s));
+	TileGeom tg{tstart.p, uint32_t(ntiles), uint32_t(n_local)};
 	tell.alloc(3 * n_local + 3);
 	ext_ptr.alloc(ntiles + 1);
 	fine_base.alloc(ntiles + 1);
 	if (n_local == 0) {
 		HIP_CHECK(hipMemsetAsync(ext_ptr.p, 0, 4, s));
+		HIP_CHECK(hipStreamSynchronize(s));
 		ext.alloc(1);
 		tfine.alloc(2);
 		return out;
@@ -199,14 +252,14 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, size_
 	HIP_CHECK(hipGetLastError());
 	out.n_fine = scan_exclusive_u32(cnt.p, fine_idx.p, n_local, s);
 	tfine.alloc(2 * out.n_fine + 2);
-	fine_base_kernel<<<grid_for(ntiles, 256), 256, 0, s>>>(tg, uint32_t(ntiles), fine_idx.p, fine_base.p);
+	fine_base_kernel<<<grid_for(ntiles, 256), 256, 0, s>>>(tg, fine_idx.p, fine_base.p);
 	HIP_CHECK(hipGetLastError());
 
 	// 5: tile-local rows
 	DBuf<int> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
-	tile_ell_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(tg, face_ptr, face_ent, ext_ptr.p, ext.p, fine_idx.p,
+	tile_ell_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(tg, T, face_ptr, face_ent, ext_ptr.p, ext.p, fine_idx.p,
 	                                                       fine_base.p, tell.p, tfine.p, err.p);
 	HIP_CHECK(hipGetLastError());
 	int herr = 0;

@@ -175,7 +175,7 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double
  * [1] tiles, [2] distinct out-of-tile face neighbors summed over tiles,
  * [3] largest per-tile count, [4] finer faces, [5] algorithmic HBM bytes of
  * one sweep over all local cells (own fields 64 B/cell + face rows 12 B/cell
- * + 4 B per out-of-tile neighbor + 8 B per finer face + 8 B per tile).
+ * + 4 B per out-of-tile neighbor + 8 B per finer face + 12 B per tile).
  * No reference counterpart (layout introspection for the roofline). */
 int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[6]);
 

@@ -210,12 +210,17 @@ def main():
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
     launches_per_step = kern_n / a.steps if a.steps else 0
 
+    # HBM bytes per launch of the sweep kernel from the committed PMC passes
+    # (FETCH_SIZE x measured read correction + WRITE_SIZE, scripts/traffic.py);
+    # only valid for the same mesh, so it is dropped for any other cell count
     traffic = None
     tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and layout is not None:
         try:
-            traffic = json.load(open(tf)).get("hbm_bytes_per_step")
-        except Exception:
+            t = json.load(open(tf))
+            if t.get("cells") == n_local and world == 1:
+                traffic = t.get("hbm_bytes_per_dispatch")
+        except (OSError, ValueError):
             traffic = None
 
     cpu = None

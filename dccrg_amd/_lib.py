@@ -37,6 +37,7 @@ _SIGS = {
     "dccrgx_set_neighborhood_length": (C.c_int, [vp, C.c_uint]),
     "dccrgx_initialize": (C.c_int, [vp]),
     "dccrgx_set_geometry": (C.c_int, [vp, P(C.c_double), P(C.c_double)]),
+    "dccrgx_geometry_batch": (C.c_int, [vp, vp, sz, vp, vp]),
     "dccrgx_get_cell_from_indices": (u64, [vp, P(u64), C.c_int]),
     "dccrgx_get_indices": (C.c_int, [vp, u64, P(u64)]),
     "dccrgx_get_refinement_level": (C.c_int, [vp, u64]),
@@ -80,6 +81,10 @@ _SIGS = {
     "dccrgx_advection_max_time_step": (C.c_int, [vp, P(C.c_int), P(C.c_double)]),
     "dccrgx_advection_refine_candidates": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, vp, sz, P(sz)]),
     "dccrgx_advection_layout": (C.c_int, [vp, P(u64)]),
+    "dccrgx_poisson_cache": (C.c_int, [vp, C.c_int, C.c_int, vp, sz, vp, sz]),
+    "dccrgx_poisson_solve": (C.c_int, [vp, C.c_uint, C.c_uint, C.c_double, C.c_double, C.c_double, C.c_int,
+                                       P(C.c_uint), P(C.c_double)]),
+    "dccrgx_poisson_field": (C.c_int, [vp, C.c_char_p, P(C.c_int)]),
     "dccrgx_allreduce_f64": (C.c_int, [vp, P(C.c_double), C.c_int, C.c_int]),
     "dccrgx_barrier": (C.c_int, [vp]),
     "dccrgx_synchronize": (C.c_int, [vp]),

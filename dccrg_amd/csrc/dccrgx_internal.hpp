@@ -107,6 +107,44 @@ struct Field {
 	DBuf<uint8_t> scratch;  // double buffer for sweeps (allocated on demand)
 };
 
+// ---- Poisson BiCG (tests/poisson/poisson_solve.hpp) ------------------------
+// device pointers of one solve: user fields rhs / solution, the solver's own
+// per-slot fields and the filtered face table (see poisson_kernels.hip)
+struct PoArrays {
+	const int32_t* ell;   // 6 per local slot: slot, -1, or -2-k -> fine[4k..4k+3] (-1 = dropped)
+	const int32_t* fine;
+	const int32_t* type;  // 0 solve, 1 boundary, 2 skip
+	const double* rhs;
+	double *sol, *best, *p0, *p1, *r0, *r1, *ap0, *sf;
+	double* f[6];  // f_x_neg, f_x_pos, f_y_neg, f_y_pos, f_z_neg, f_z_pos
+};
+
+struct PoParams {  // Poisson_Solve constructor, poisson_solve.hpp:187-201
+	unsigned max_it, min_it;
+	double stop_residual, p_of_norm, stop_increase;
+};
+
+// the solver's scalars, resident on the device (host reads them only to
+// detect termination)
+struct PoScalars {
+	double dot_r, alpha, beta, residual, residual_min, norm;
+	unsigned iteration, done, save, stop_b;
+};
+
+enum { PO_PHASE_INIT, PO_PHASE_A, PO_PHASE_B, PO_PHASE_C, PO_PHASE_FINISH, PO_PHASE_JACOBI, PO_PHASE_JACOBI_COPY };
+enum { PO_STAGE_INIT, PO_STAGE_A, PO_STAGE_B, PO_STAGE_JACOBI_INIT, PO_STAGE_JACOBI };
+
+struct PoissonState {
+	bool valid = false;        // cache_system_info done for the current mesh
+	int rhs = -1, sol = -1;    // user fields
+	int type = -1;             // int32 field: classification / final type
+	int p0 = -1, p1 = -1, r0 = -1, r1 = -1, ap0 = -1, best = -1, sf = -1, f[6] = {-1, -1, -1, -1, -1, -1};
+	DBuf<int32_t> ell, fine;
+	DBuf<double> part, red;
+	DBuf<PoScalars> st;
+	size_t n_cached = 0;       // local cells in cell_info
+};
+
 struct Grid {
 	// communicator
 	int rank = 0, size = 1, device = 0;
@@ -194,6 +232,8 @@ struct Grid {
 	int slot_order = -1;  // -1: Morton when R > 0, else id
 	bool morton_slots = false;  // the order in effect
 
+	PoissonState po;
+
 	bool uniform() const { return R == 0; }
 };
 
@@ -268,5 +308,16 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face
                         uint64_t* out, hipStream_t s);
 void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
+
+// --- launchers implemented in poisson_kernels.hip ---------------------------
+unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots
+void k_po_cache(const MapCtx& m, const double l0[3], const uint64_t* slot_ids, const int32_t* cls,
+                const int32_t* face_ell, const int32_t* face_fine, size_t n, int32_t* po_ell, int32_t* po_fine,
+                int32_t* type, const PoArrays& a, hipStream_t s);
+void k_po_phase(int phase, const PoArrays& a, size_t n, const PoParams& prm, const PoScalars* st, double* part,
+                hipStream_t s);
+void k_po_reduce(int k, const double* part, unsigned nb, double* red, PoScalars* st, const PoParams& prm, int stage,
+                 bool scalar, hipStream_t s);
+void k_po_scalar(const double* red, PoScalars* st, const PoParams& prm, int stage, hipStream_t s);
 
 }  // namespace dccrgx

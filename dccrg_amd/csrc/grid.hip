@@ -304,6 +304,7 @@ static void rebuild(Grid& g) {
 	g.face_valid = false;
 	g.tiles_valid = false;
 	g.slot_ids_h_valid = false;
+	g.po.valid = false;
 }
 
 // full neighbors_of / neighbors_to / iterator CSR for all local rows
@@ -705,6 +706,195 @@ static void balance_load_impl(Grid& g) {
 	}
 }
 
+// --------------------------------------------------------------------------- Poisson
+// Poisson_Solve (tests/poisson/poisson_solve.hpp:156-1056) over device fields.
+
+// halo update of exactly the given fields (the reference's
+// Poisson_Cell::transfer_switch, 92-140)
+static void halo_only(Grid& g, const std::vector<int>& fids) {
+	if (g.size == 1 || g.peers.empty()) return;
+	std::vector<char> saved(g.fields.size());
+	for (size_t i = 0; i < g.fields.size(); i++) {
+		saved[i] = g.fields[i].transfer;
+		g.fields[i].transfer = false;
+	}
+	for (int f : fids) field(g, f).transfer = true;
+	try {
+		halo_start(g);
+	} catch (...) {
+		for (size_t i = 0; i < g.fields.size(); i++) g.fields[i].transfer = saved[i];
+		throw;
+	}
+	for (size_t i = 0; i < g.fields.size(); i++) g.fields[i].transfer = saved[i];
+	halo_wait(g);
+}
+
+__global__ void po_classify_kernel(int32_t* cls, const int32_t* slot_by_id, const uint64_t* ids, size_t n,
+                                   uint64_t last, size_t n_local, int32_t value) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[i];
+		if (id == 0 || id > last) continue;
+		const int32_t sl = slot_by_id[id];
+		if (sl >= 0 && size_t(sl) < n_local) cls[sl] = value;  // only local cells (is_local, 839-878)
+	}
+}
+
+static int po_field(Grid& g, const char* name, size_t elem) {
+	Field f;
+	f.name = name;
+	f.elem = elem;
+	f.transfer = false;
+	g.fields.push_back(std::move(f));
+	Field& nf = g.fields.back();
+	nf.data.alloc(g.n_slots * elem);
+	if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+	return int(g.fields.size() - 1);
+}
+
+static void po_ensure_fields(Grid& g) {
+	PoissonState& P = g.po;
+	if (P.type >= 0) return;
+	P.type = po_field(g, "poisson.type", 4);
+	P.p0 = po_field(g, "poisson.p0", 8);
+	P.p1 = po_field(g, "poisson.p1", 8);
+	P.r0 = po_field(g, "poisson.r0", 8);
+	P.r1 = po_field(g, "poisson.r1", 8);
+	P.ap0 = po_field(g, "poisson.A_dot_p0", 8);
+	P.best = po_field(g, "poisson.best_solution", 8);
+	P.sf = po_field(g, "poisson.scaling_factor", 8);
+	static const char* fn[6] = {"poisson.f_x_neg", "poisson.f_x_pos", "poisson.f_y_neg",
+	                            "poisson.f_y_pos", "poisson.f_z_neg", "poisson.f_z_pos"};
+	for (int k = 0; k < 6; k++) P.f[k] = po_field(g, fn[k], 8);
+}
+
+static PoArrays po_arrays(Grid& g) {
+	PoissonState& P = g.po;
+	auto d = [&](int f) { return (double*)field(g, f).data.p; };
+	PoArrays a{};
+	a.ell = P.ell.p;
+	a.fine = P.fine.p;
+	a.type = (const int32_t*)field(g, P.type).data.p;
+	a.rhs = d(P.rhs);
+	a.sol = d(P.sol);
+	a.best = d(P.best);
+	a.p0 = d(P.p0);
+	a.p1 = d(P.p1);
+	a.r0 = d(P.r0);
+	a.r1 = d(P.r1);
+	a.ap0 = d(P.ap0);
+	a.sf = d(P.sf);
+	for (int k = 0; k < 6; k++) a.f[k] = d(P.f[k]);
+	return a;
+}
+
+// cache_system_info 827-971
+static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns, const uint64_t* skip, size_t nk) {
+	DX_REQUIRE(field(g, rhs).elem == 8 && field(g, sol).elem == 8, "rhs and solution must be fp64 fields");
+	po_ensure_fields(g);
+	PoissonState& P = g.po;
+	P.rhs = rhs;
+	P.sol = sol;
+	ensure_face(g);
+	hipStream_t s = g.s_comp;
+	const size_t nl = g.n_local;
+	int32_t* type = (int32_t*)field(g, P.type).data.p;
+	// classify: local cells boundary, then skip, then solve (836-878)
+	k_fill_i32(type, nl, 1, s);
+	for (int pass = 0; pass < 2; pass++) {
+		const uint64_t* ids = pass == 0 ? skip : solve;
+		const size_t n = pass == 0 ? nk : ns;
+		if (!n) continue;
+		DBuf<uint64_t> d;
+		d.alloc(n);
+		HIP_CHECK(hipMemcpyAsync(d.p, ids, n * 8, hipMemcpyHostToDevice, s));
+		po_classify_kernel<<<grid_for(n, 256), 256, 0, s>>>(type, g.slot_by_id.p, d.p, n, g.m.last, nl,
+		                                                    pass == 0 ? 2 : 0);
+		HIP_CHECK(hipGetLastError());
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	halo_only(g, {P.type});  // TYPE (880-881)
+	DBuf<int32_t> cls;
+	cls.alloc(g.n_slots);
+	if (g.n_slots) HIP_CHECK(hipMemcpyAsync(cls.p, type, g.n_slots * 4, hipMemcpyDeviceToDevice, s));
+	P.ell.alloc(6 * nl);
+	P.fine.alloc(g.face_fine.n);
+	const PoArrays a = po_arrays(g);
+	k_po_cache(g.m, g.l0, g.slot_ids.p, cls.p, g.face_ell.p, g.face_fine.p, nl, P.ell.p, P.fine.p, type, a, s);
+	HIP_CHECK(hipStreamSynchronize(s));
+	std::vector<int> geo{P.sf};  // GEOMETRY (969-970)
+	for (int k = 0; k < 6; k++) geo.push_back(P.f[k]);
+	halo_only(g, geo);
+	HIP_CHECK(hipStreamSynchronize(s));
+	P.valid = true;
+}
+
+// sums of the last phase -> (all ranks) -> scalar control flow
+static void po_reduce(Grid& g, int k, unsigned nb, const PoParams& prm, int stage) {
+	PoissonState& P = g.po;
+	const bool one = g.size == 1;
+	k_po_reduce(k, P.part.p, nb, P.red.p, P.st.p, prm, stage, one, g.s_comp);
+	if (!one) {
+		DX_REQUIRE(g.comm, "Poisson solve on several ranks needs a communicator");
+		NCCL_CHECK(ncclAllReduce(P.red.p, P.red.p, size_t(k), ncclFloat64, ncclSum, g.comm, g.s_comp));
+		k_po_scalar(P.red.p, P.st.p, prm, stage, g.s_comp);
+	}
+}
+
+static PoScalars po_read_scalars(Grid& g) {
+	PoScalars h{};
+	HIP_CHECK(hipMemcpyAsync(&h, g.po.st.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	return h;
+}
+
+// solve 251-522 / solve_failsafe 531-634 after po_cache; the host only
+// enqueues kernels and polls the device's `done` flag every few iterations
+static PoScalars po_solve(Grid& g, const PoParams& prm, bool failsafe) {
+	PoissonState& P = g.po;
+	DX_REQUIRE(P.valid, "Poisson system not cached for the current mesh");
+	hipStream_t s = g.s_comp;
+	const size_t n = g.n_local;
+	const unsigned nb = k_po_blocks(n);
+	if (P.part.n < 2 * size_t(nb)) P.part.alloc(2 * size_t(nb));
+	P.red.alloc(2);
+	P.st.alloc(1);
+	const PoArrays a = po_arrays(g);
+	const int poll = 8;
+	if (!failsafe) {
+		halo_only(g, {P.sol});  // INIT (983-984)
+		k_po_phase(PO_PHASE_INIT, a, n, prm, P.st.p, P.part.p, s);
+		po_reduce(g, 1, nb, prm, PO_STAGE_INIT);
+		for (unsigned it = 0; it < prm.max_it; it++) {
+			halo_only(g, {P.p0, P.p1});  // SOLVING (283-284)
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_A, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			po_reduce(g, 2, nb, prm, PO_STAGE_A);
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_B, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			po_reduce(g, 1, nb, prm, PO_STAGE_B);
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_C, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			if ((it + 1) % poll == 0 && po_read_scalars(g).done) break;
+		}
+		k_po_phase(PO_PHASE_FINISH, a, n, prm, P.st.p, P.part.p, s);
+	} else {
+		k_po_reduce(1, P.part.p, 0, P.red.p, P.st.p, prm, PO_STAGE_JACOBI_INIT, true, s);
+		for (unsigned it = 0; it < prm.max_it; it++) {
+			halo_only(g, {P.sol});  // INIT (545, 551)
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_JACOBI, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			po_reduce(g, 1, nb, prm, PO_STAGE_JACOBI);
+			k_po_phase(PO_PHASE_JACOBI_COPY, a, n, prm, P.st.p, P.part.p, s);
+			if ((it + 1) % poll == 0 && po_read_scalars(g).done) break;
+		}
+	}
+	return po_read_scalars(g);
+}
+
 }  // namespace dccrgx
 
 // ============================================================================
@@ -866,6 +1056,28 @@ int dccrgx_set_geometry(dccrgx_grid* gp, const double start[3], const double l0[
 		for (int d = 0; d < 3; d++) {
 			g.start[d] = start[d];
 			g.l0[d] = l0[d];
+		}
+		return 0;
+	});
+}
+
+int dccrgx_geometry_batch(dccrgx_grid* gp, const uint64_t* ids, size_t n, double* center, double* length) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(ids || !n, "null ids");
+		const double nan = std::numeric_limits<double>::quiet_NaN();
+		for (size_t i = 0; i < n; i++) {
+			uint64_t ind[3];
+			const int lvl = map_indices(g.m, ids[i], ind[0], ind[1], ind[2]);
+			for (int d = 0; d < 3; d++) {
+				double L = nan, c = nan;
+				if (lvl >= 0) {  // dccrg_cartesian_geometry.hpp:299-303, 334-359
+					L = g.l0[d] * (1.0 / double(uint64_t(1) << lvl));
+					c = g.start[d] + double(ind[d]) * g.l0[d] / double(uint64_t(1) << g.R) + L / 2;
+				}
+				if (length) length[3 * i + d] = L;
+				if (center) center[3 * i + d] = c;
+			}
 		}
 		return 0;
 	});
@@ -1475,6 +1687,49 @@ int dccrgx_kernel_timing(dccrgx_grid* gp, int enable, double* total_ms, int64_t*
 			g.timing = false;
 		}
 		return 0;
+	});
+}
+
+// ---- Poisson (tests/poisson/poisson_solve.hpp) ----------------------------
+int dccrgx_poisson_cache(dccrgx_grid* gp, int rhs_field, int solution_field, const uint64_t* solve_cells,
+                         size_t n_solve, const uint64_t* skip_cells, size_t n_skip) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "grid not initialized");
+		DX_REQUIRE((solve_cells || !n_solve) && (skip_cells || !n_skip), "null cell list");
+		po_cache(g, rhs_field, solution_field, solve_cells, n_solve, skip_cells, n_skip);
+		return 0;
+	});
+}
+
+int dccrgx_poisson_solve(dccrgx_grid* gp, unsigned max_iterations, unsigned min_iterations, double stop_residual,
+                         double p_of_norm, double stop_after_residual_increase, int failsafe, unsigned* iterations,
+                         double* residual) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(p_of_norm > 0, "p_of_norm must be > 0");
+		// solve() is a do-while (279-506): at least one iteration
+		const unsigned max_it = failsafe ? max_iterations : std::max(1u, max_iterations);
+		const PoParams prm{max_it, min_iterations, stop_residual, p_of_norm, stop_after_residual_increase};
+		const PoScalars st = po_solve(g, prm, failsafe != 0);
+		if (iterations) *iterations = st.iteration;
+		if (residual) *residual = failsafe ? st.norm : st.residual_min;
+		return 0;
+	});
+}
+
+int dccrgx_poisson_field(dccrgx_grid* gp, const char* name, int* fid) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(name && fid, "null argument");
+		DX_REQUIRE(g.po.type >= 0, "Poisson system not cached yet");
+		const std::string want = std::string("poisson.") + name;
+		for (size_t i = 0; i < g.fields.size(); i++)
+			if (g.fields[i].name == want) {
+				*fid = int(i);
+				return 0;
+			}
+		throw Error(DCCRGX_ENOTFOUND, "no Poisson field " + std::string(name));
 	});
 }
 

@@ -131,6 +131,21 @@ class Dccrg:
         check(lib().dccrgx_set_geometry(self.h, s, l0))
         return self
 
+    def geometry(self, cells):
+        """(centers, lengths), each (n, 3): Cartesian_Geometry get_center /
+        get_length (dccrg_cartesian_geometry.hpp:282-362) of many cells."""
+        ids = np.ascontiguousarray(cells, np.uint64)
+        c = np.empty((ids.size, 3))
+        L = np.empty((ids.size, 3))
+        check(lib().dccrgx_geometry_batch(self.h, _ptr(ids), ids.size, _ptr(c), _ptr(L)))
+        return c, L
+
+    def get_center(self, cell):
+        return tuple(self.geometry([cell])[0][0])
+
+    def get_length(self, cell):
+        return tuple(self.geometry([cell])[1][0])
+
     # ---- mapping ------------------------------------------------------------
     def get_cell_from_indices(self, indices, level):
         a = (C.c_uint64 * 3)(*[int(x) for x in indices])

@@ -75,6 +75,11 @@ int dccrgx_initialize(dccrgx_grid* g);
 /* Cartesian_Geometry::set (dccrg_cartesian_geometry.hpp:184) */
 int dccrgx_set_geometry(dccrgx_grid* g, const double start[3], const double level_0_cell_length[3]);
 
+/* Cartesian_Geometry::get_center / get_length (dccrg_cartesian_geometry.hpp:
+ * 282-362) of n cells: 3 doubles per cell each (either output may be NULL);
+ * NaN for invalid ids */
+int dccrgx_geometry_batch(dccrgx_grid* g, const uint64_t* ids, size_t n, double* center, double* length);
+
 /* ---- mapping (dccrg_mapping.hpp) — host-side scalar queries -------------- */
 uint64_t dccrgx_get_cell_from_indices(dccrgx_grid* g, const uint64_t indices[3], int level); /* 153 */
 int dccrgx_get_indices(dccrgx_grid* g, uint64_t cell, uint64_t indices[3]);                 /* 217 */
@@ -178,6 +183,26 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double
  * + 4 B per out-of-tile neighbor + 8 B per finer face + 12 B per tile).
  * No reference counterpart (layout introspection for the roofline). */
 int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[6]);
+
+/* ---- Poisson solver (tests/poisson/poisson_solve.hpp:156-1056) ----------
+ * dccrgx_poisson_cache = Poisson_Solve::cache_system_info (827-971): local
+ * cells default to boundary cells, ids in skip_cells are skipped, ids in
+ * solve_cells are solved (non-local ids are ignored, as the reference does);
+ * computes the geometry factors (set_scaling_factor 696-819) on the device and
+ * halos them.  rhs / solution are fp64 fields.
+ * dccrgx_poisson_solve = Poisson_Solve::solve (251-522, failsafe = 0) or
+ * solve_failsafe (531-634, failsafe = 1) with the constructor's parameters
+ * (187-201); solution = best solution on return.  *iterations = iterations
+ * done, *residual = smallest residual (solve) or last norm (failsafe).
+ * dccrgx_poisson_field: the solver's per-cell state as a field ("p0", "p1",
+ * "r0", "r1", "A_dot_p0", "best_solution", "scaling_factor", "f_x_neg" ...
+ * "f_z_pos", "type"), e.g. for inspection after a solve. */
+int dccrgx_poisson_cache(dccrgx_grid* g, int rhs_field, int solution_field, const uint64_t* solve_cells,
+                         size_t n_solve, const uint64_t* skip_cells, size_t n_skip);
+int dccrgx_poisson_solve(dccrgx_grid* g, unsigned max_iterations, unsigned min_iterations, double stop_residual,
+                         double p_of_norm, double stop_after_residual_increase, int failsafe, unsigned* iterations,
+                         double* residual);
+int dccrgx_poisson_field(dccrgx_grid* g, const char* name, int* field_id);
 
 /* ---- collectives for user kernels (MPI_Allreduce in solve.hpp:317) ------- */
 int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 sum, 1 min, 2 max */);

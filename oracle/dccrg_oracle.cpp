@@ -785,6 +785,251 @@ static std::vector<uint64_t> adv_refine_candidates(const Grid& g, std::unordered
 	return out;
 }
 
+/* ---------------------------------------------------------------------------
+ * Poisson BiCG — tests/poisson/poisson_solve.hpp:47-1054 (Poisson_Cell
+ * 47-141, solve 251-522, solve_failsafe 531-634, get_residual 677-687,
+ * set_scaling_factor 696-819, cache_system_info 827-971, initialize_solver
+ * 979-1054).  Single address space: remote copies are the owners' objects,
+ * which is what the reference's halo updates deliver before every use
+ * (SOLVING before A.p0, GEOMETRY once after caching, INIT before the
+ * initial residual).  Cells are visited in ascending id order; global sums
+ * are taken in that order (the reference's order is hash order + the
+ * MPI_Allreduce tree, so sums agree to rounding only).
+ * ------------------------------------------------------------------------- */
+enum { PO_SOLVE = 0, PO_BOUNDARY = 1, PO_SKIP = 2 };  // poisson_solve.hpp:146-150
+
+struct PoissonCell {  // poisson_solve.hpp:51-86
+	double rhs = 0, solution = 0, best_solution = 0, p0 = 0, p1 = 0, r0 = 0, r1 = 0, A_dot_p0 = 0, scaling_factor = 0;
+	double f[6] = {0, 0, 0, 0, 0, 0};  // f_x_neg, f_x_pos, f_y_neg, f_y_pos, f_z_neg, f_z_pos
+	int type = PO_BOUNDARY;
+};
+
+struct PoissonNb {
+	uint64_t id;
+	int direction;  // +-1..+-3
+	int rel;        // relative refinement level (+1 finer, -1 coarser)
+};
+
+// direction (+-1..+-3) -> index into PoissonCell::f (-x,+x,-y,+y,-z,+z)
+static inline int po_fi(int direction) { return 2 * (std::abs(direction) - 1) + (direction > 0 ? 1 : 0); }
+
+struct PoissonSolver {
+	unsigned max_iterations = 1000, min_iterations = 0;
+	double stop_residual = 1e-15, p_of_norm = 2, stop_after_residual_increase = 10;
+	std::vector<std::pair<uint64_t, std::vector<PoissonNb>>> cell_info;  // 647, 666
+	std::unordered_map<uint64_t, PoissonCell> cells;
+	unsigned iterations = 0;
+	double residual_min = 0;
+	bool reverse = false;
+
+	PoissonCell& at(uint64_t c) { return cells.at(c); }
+
+	// set_scaling_factor 696-819
+	void set_scaling_factor(const Grid& g, uint64_t cell, const std::vector<std::pair<uint64_t, int>>& nbs) {
+		PoissonCell& cd = at(cell);
+		const auto cl = g.get_length(cell);
+		const double chx = cl[0] / 2.0, chy = cl[1] / 2.0, chz = cl[2] / 2.0;
+		double px = +2 * chx, nx = -2 * chx, py = +2 * chy, ny = -2 * chy, pz = +2 * chz, nz = -2 * chz;
+		for (const auto& nb : nbs) {
+			const auto nl = g.get_length(nb.first);
+			const double hx = nl[0] / 2.0, hy = nl[1] / 2.0, hz = nl[2] / 2.0;
+			switch (nb.second) {
+			case +1: px = chx + hx; break;
+			case -1: nx = -1.0 * (chx + hx); break;
+			case +2: py = chy + hy; break;
+			case -2: ny = -1.0 * (chy + hy); break;
+			case +3: pz = chz + hz; break;
+			case -3: nz = -1.0 * (chz + hz); break;
+			default: throw std::runtime_error("poisson: invalid direction");
+			}
+		}
+		const double tx = px - nx, ty = py - ny, tz = pz - nz;
+		for (int k = 0; k < 6; k++) cd.f[k] = 0;
+		for (const auto& nb : nbs) {
+			switch (nb.second) {
+			case +1: cd.f[1] = +2.0 / (px * tx); break;
+			case -1: cd.f[0] = -2.0 / (nx * tx); break;
+			case +2: cd.f[3] = +2.0 / (py * ty); break;
+			case -2: cd.f[2] = -2.0 / (ny * ty); break;
+			case +3: cd.f[5] = +2.0 / (pz * tz); break;
+			case -3: cd.f[4] = -2.0 / (nz * tz); break;
+			}
+		}
+		cd.scaling_factor = -cd.f[1] - cd.f[0] - cd.f[3] - cd.f[2] - cd.f[5] - cd.f[4];
+	}
+
+	// cache_system_info 827-971; types: per local cell (every leaf here)
+	void cache_system_info(const Grid& g) {
+		std::vector<uint64_t> all;
+		for (const auto& cp : g.cell_process) all.push_back(cp.first);
+		std::sort(all.begin(), all.end());
+		// the reference walks get_cells() in hash order: any order is a faithful
+		// restatement; `reverse` gives a second one to measure the order noise
+		if (reverse) std::reverse(all.begin(), all.end());
+		cell_info.clear();
+		std::vector<uint64_t> newly_skipped;
+		for (const uint64_t cell : all) {
+			PoissonCell& cd = at(cell);
+			if (cd.type == PO_SKIP) continue;
+			const int clvl = g.m.level(cell);
+			std::vector<std::pair<uint64_t, int>> face;
+			std::vector<PoissonNb> info;
+			for (const auto& fn : g.face_neighbors_of(cell)) {
+				const PoissonCell& nd = at(fn.first);
+				if (nd.type == PO_SKIP) continue;
+				if (cd.type == PO_BOUNDARY && nd.type == PO_BOUNDARY) continue;
+				face.push_back(fn);
+				const int nlvl = g.m.level(fn.first);
+				info.push_back({fn.first, fn.second, nlvl > clvl ? 1 : (nlvl < clvl ? -1 : 0)});
+			}
+			if (face.empty()) {
+				// 953-957; applied after the loop, so every cell filters against
+				// the classification it was given (the reference's outcome for a
+				// neighbor converted here depends on its hash order)
+				newly_skipped.push_back(cell);
+				continue;
+			}
+			set_scaling_factor(g, cell, face);
+			cell_info.push_back({cell, info});
+		}
+		for (const uint64_t c : newly_skipped) at(c).type = PO_SKIP;
+	}
+
+	// get_residual 677-687
+	double get_residual() {
+		double local = 0;
+		for (const auto& ci : cell_info) local += std::pow(std::fabs(at(ci.first).r0), p_of_norm);
+		return std::pow(local, 1.0 / p_of_norm);
+	}
+
+	// initialize_solver 979-1054
+	double initialize_solver() {
+		for (const auto& ci : cell_info) {
+			PoissonCell& d = at(ci.first);
+			if (d.type != PO_SOLVE) continue;
+			d.r0 = d.rhs - d.scaling_factor * d.solution;
+			for (const auto& nb : ci.second) {
+				double mul = d.f[po_fi(nb.direction)];
+				if (nb.rel > 0) mul /= 4.0;
+				d.r0 -= mul * at(nb.id).solution;
+			}
+			d.p0 = d.p1 = d.r1 = d.r0;
+		}
+		double dot = 0;
+		for (const auto& ci : cell_info) {
+			const PoissonCell& d = at(ci.first);
+			if (d.type == PO_SOLVE) dot += d.r0 * d.r1;
+		}
+		return dot;
+	}
+
+	// solve 251-522 (after cache_system_info)
+	void solve() {
+		double residual_min_ = std::numeric_limits<double>::max();
+		double dot_r_g = initialize_solver();
+		unsigned iteration = 0;
+		do {
+			iteration++;
+			for (const auto& ci : cell_info) {  // A . p0 (290-339)
+				PoissonCell& d = at(ci.first);
+				if (d.type != PO_SOLVE) continue;
+				d.A_dot_p0 = d.scaling_factor * d.p0;
+				for (const auto& nb : ci.second) {
+					double mul = d.f[po_fi(nb.direction)];
+					if (nb.rel > 0) mul /= 4.0;
+					d.A_dot_p0 += mul * at(nb.id).p0;
+				}
+			}
+			double dot_p_g = 0;  // 341-349
+			for (const auto& ci : cell_info) {
+				const PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) dot_p_g += d.p1 * d.A_dot_p0;
+			}
+			if (dot_p_g == 0) break;
+			const double alpha = dot_r_g / dot_p_g;
+			for (const auto& ci : cell_info) {  // 364-370
+				PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) d.solution += alpha * d.p0;
+			}
+			const double residual = get_residual();
+			if (residual_min_ > residual) {  // 379-390
+				residual_min_ = residual;
+				for (const auto& ci : cell_info) {
+					PoissonCell& d = at(ci.first);
+					if (d.type == PO_SOLVE) d.best_solution = d.solution;
+				}
+			}
+			if (residual <= stop_residual && iteration >= min_iterations) break;
+			if (residual >= stop_after_residual_increase * residual_min_ && iteration >= min_iterations) break;
+			for (const auto& ci : cell_info) {  // 405-411
+				PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) d.r0 -= alpha * d.A_dot_p0;
+			}
+			for (const auto& ci : cell_info) {  // 413-470, transpose(A) . p1
+				PoissonCell& d = at(ci.first);
+				if (d.type != PO_SOLVE) continue;
+				double A_dot_p1 = d.scaling_factor * d.p1;
+				for (const auto& nb : ci.second) {
+					const PoissonCell& n = at(nb.id);
+					double mul = n.f[po_fi(-nb.direction)];
+					if (nb.rel > 0) mul /= 4.0;
+					A_dot_p1 += mul * n.p1;
+				}
+				d.r1 -= alpha * A_dot_p1;
+			}
+			if (dot_r_g == 0) break;
+			const double old = dot_r_g;
+			dot_r_g = 0;
+			for (const auto& ci : cell_info) {
+				const PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) dot_r_g += d.r0 * d.r1;
+			}
+			const double beta = dot_r_g / old;
+			for (const auto& ci : cell_info) {  // 497-504
+				PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) {
+					d.p0 = d.r0 + beta * d.p0;
+					d.p1 = d.r1 + beta * d.p1;
+				}
+			}
+		} while (iteration < max_iterations);
+		for (const auto& ci : cell_info) {
+			PoissonCell& d = at(ci.first);
+			if (d.type == PO_SOLVE) d.solution = d.best_solution;
+		}
+		iterations = iteration;
+		residual_min = residual_min_;
+	}
+
+	// solve_failsafe 531-634 (Jacobi-like); best_solution holds the next value
+	void solve_failsafe() {
+		unsigned iteration = 0;
+		double norm = std::numeric_limits<double>::max();
+		while (iteration++ < max_iterations && norm > stop_residual) {
+			norm = 0;
+			for (const auto& ci : cell_info) {
+				PoissonCell& d = at(ci.first);
+				if (d.type != PO_SOLVE) continue;
+				if (d.scaling_factor == 0) throw std::runtime_error("poisson: zero scaling factor");
+				const double inv = -1.0 / d.scaling_factor;
+				d.best_solution = -inv * d.rhs;
+				for (const auto& nb : ci.second) {
+					double mul = d.f[po_fi(nb.direction)];
+					if (nb.rel > 0) mul /= 4.0;
+					d.best_solution += inv * mul * at(nb.id).solution;
+				}
+				norm += std::fabs(d.solution - d.best_solution);
+			}
+			for (const auto& ci : cell_info) {
+				PoissonCell& d = at(ci.first);
+				if (d.type == PO_SOLVE) d.solution = d.best_solution;
+			}
+		}
+		iterations = iteration - 1;  // loop bodies executed (the test post-increments)
+		residual_min = norm;
+	}
+};
+
 }  // namespace oracle
 
 /* ===========================================================================
@@ -796,6 +1041,7 @@ struct OracleHandle {
 	Grid g;
 	std::unordered_map<uint64_t, AdvCell> adv;
 	std::unordered_map<uint64_t, uint32_t> gol;
+	PoissonSolver po;
 	std::string err;
 };
 
@@ -1116,6 +1362,70 @@ int or_adv_get(void* hp, const uint64_t* ids, size_t n, double* out9) {
 		auto* h = static_cast<OracleHandle*>(hp);
 		for (size_t i = 0; i < n; i++)
 			for (int k = 0; k < 9; k++) out9[9 * i + k] = h->adv.at(ids[i]).d[k];
+		return 0;
+	})
+}
+
+/* ---- Poisson (tests/poisson/poisson_solve.hpp) ----
+   cells: every leaf must be listed once; type 0 solve, 1 boundary, 2 skip
+   (the reference's `cells` / default / `cells_to_skip`, 836-878) */
+int or_po_set(void* hp, const uint64_t* ids, const double* rhs, const double* solution, const int32_t* type, size_t n) {
+	OR_TRY({
+		auto* h = static_cast<OracleHandle*>(hp);
+		h->po.cells.clear();
+		for (size_t i = 0; i < n; i++) {
+			PoissonCell c;
+			c.rhs = rhs[i];
+			c.solution = solution[i];
+			c.type = type[i];
+			h->po.cells[ids[i]] = c;
+		}
+		for (const auto& cp : h->g.cell_process)
+			if (!h->po.cells.count(cp.first)) throw std::runtime_error("poisson: leaf without data");
+		return 0;
+	})
+}
+
+/* solve (failsafe = 0) or solve_failsafe (1) with the given parameters
+   (constructor 187-201), cells visited in ascending (reverse = 0) or
+   descending id order; returns iterations, *residual = minimum residual
+   (solve) or last norm (failsafe) */
+int64_t or_po_solve(void* hp, unsigned max_it, unsigned min_it, double stop_residual, double p_of_norm,
+                    double stop_increase, int failsafe, int reverse, double* residual) {
+	try {
+		auto* h = static_cast<OracleHandle*>(hp);
+		PoissonSolver& s = h->po;
+		s.max_iterations = max_it;
+		s.min_iterations = min_it;
+		s.stop_residual = stop_residual;
+		s.p_of_norm = p_of_norm;
+		s.stop_after_residual_increase = stop_increase;
+		s.reverse = reverse != 0;
+		s.cache_system_info(h->g);
+		if (failsafe) s.solve_failsafe();
+		else s.solve();
+		*residual = s.residual_min;
+		return int64_t(s.iterations);
+	} catch (const std::exception& e) {
+		g_err = e.what();
+		return -1;
+	}
+}
+
+/* per cell: solution, best_solution, p0, p1, r0, r1, A_dot_p0,
+   scaling_factor, f[-x,+x,-y,+y,-z,+z], type (16 values) */
+int or_po_get(void* hp, const uint64_t* ids, size_t n, double* out16) {
+	OR_TRY({
+		auto* h = static_cast<OracleHandle*>(hp);
+		for (size_t i = 0; i < n; i++) {
+			const PoissonCell& c = h->po.cells.at(ids[i]);
+			double* o = out16 + 16 * i;
+			o[0] = c.solution; o[1] = c.best_solution; o[2] = c.p0; o[3] = c.p1; o[4] = c.r0; o[5] = c.r1;
+			o[6] = c.A_dot_p0; o[7] = c.scaling_factor;
+			for (int k = 0; k < 6; k++) o[8 + k] = c.f[k];
+			o[14] = double(c.type);
+			o[15] = 0;
+		}
 		return 0;
 	})
 }

@@ -74,6 +74,11 @@ def lib():
     L.or_adv_max_time_step.argtypes = [C.c_void_p]
     L.or_adv_steps.argtypes = [C.c_void_p, C.c_int, C.c_double]
     L.or_adv_get.argtypes = [C.c_void_p, u64p, C.c_size_t, f64p]
+    L.or_po_set.argtypes = [C.c_void_p, u64p, f64p, f64p, i32p, C.c_size_t]
+    L.or_po_solve.restype = C.c_int64
+    L.or_po_solve.argtypes = [C.c_void_p, C.c_uint, C.c_uint, C.c_double, C.c_double, C.c_double, C.c_int,
+                              C.c_int, C.POINTER(C.c_double)]
+    L.or_po_get.argtypes = [C.c_void_p, u64p, C.c_size_t, f64p]
     _LIB = L
     return L
 
@@ -264,3 +269,30 @@ class Grid:
         out = np.empty(9 * ids.size)
         self._chk(lib().or_adv_get(self.h, ids, ids.size, out))
         return out.reshape(-1, 9)
+
+    # ---- Poisson (tests/poisson/poisson_solve.hpp) ----
+    PO_FIELDS = ("solution", "best_solution", "p0", "p1", "r0", "r1", "A_dot_p0", "scaling_factor",
+                 "f_x_neg", "f_x_pos", "f_y_neg", "f_y_pos", "f_z_neg", "f_z_pos", "type")
+
+    def po_set(self, ids, rhs, solution, types):
+        """Every leaf once; types 0 solve, 1 boundary, 2 skip."""
+        ids = np.ascontiguousarray(ids, np.uint64)
+        self._chk(lib().or_po_set(self.h, ids, np.ascontiguousarray(rhs, np.float64),
+                                  np.ascontiguousarray(solution, np.float64),
+                                  np.ascontiguousarray(types, np.int32), ids.size))
+
+    def po_solve(self, max_iterations=1000, min_iterations=0, stop_residual=1e-15, p_of_norm=2.0,
+                 stop_after_residual_increase=10.0, failsafe=False, reverse=False):
+        """Returns (iterations, residual).  reverse: visit cells (and sum) in
+        descending id order — a second faithful order, to measure the
+        reference's own summation-order noise."""
+        r = C.c_double(0)
+        it = self._chk(lib().or_po_solve(self.h, max_iterations, min_iterations, stop_residual, p_of_norm,
+                                         stop_after_residual_increase, int(failsafe), int(reverse), C.byref(r)))
+        return int(it), r.value
+
+    def po_get(self, ids):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        out = np.empty(16 * ids.size)
+        self._chk(lib().or_po_get(self.h, ids, ids.size, out))
+        return out.reshape(-1, 16)

@@ -1,0 +1,52 @@
+"""Poisson test cases shared by the oracle and GPU tests: the reference's
+tests/poisson drivers restated (mesh, right-hand side, norms)."""
+import math
+
+import numpy as np
+
+
+def poisson3d_solution(c):
+    """poisson3d.cpp:44-52"""
+    return np.sin(c[:, 0]) * np.cos(2 * c[:, 1]) * np.sin(c[:, 2] / 4)
+
+
+def center_refine_select(centers, lengths):
+    """poisson3d.cpp:177-189: cells touching the point (pi, pi/2, 4 pi)."""
+    mn, mx = centers - lengths / 2, centers + lengths / 2
+    return ((mn[:, 0] < 1.01 * math.pi) & (mx[:, 0] > 0.99 * math.pi) & (mn[:, 1] < 0.51 * math.pi)
+            & (mx[:, 1] > 0.49 * math.pi) & (mn[:, 2] < 4.01 * math.pi) & (mx[:, 2] > 3.99 * math.pi))
+
+
+def poisson3d_lengths(n):
+    """poisson3d.cpp:146-149 level-0 cell lengths for an n^3 grid."""
+    return (2 * math.pi / n, 1 * math.pi / n, 8 * math.pi / n)
+
+
+def level0_avg_norm(ids, sol, centers, lengths, n, L0):
+    """get_p_norm of poisson3d.cpp:61-119 (p = 2): solution averaged over each
+    level-0 parent (weight 8^-lvl) against the analytic value at its center."""
+    lvl = np.round(np.log2(L0[0] / lengths[:, 0])).astype(int)
+    k = (np.floor(centers[:, 0] / L0[0]).astype(np.int64) + n * np.floor(centers[:, 1] / L0[1]).astype(np.int64)
+         + n * n * np.floor(centers[:, 2] / L0[2]).astype(np.int64))
+    avg = np.zeros(n ** 3)
+    np.add.at(avg, k, sol / 8.0 ** lvl)
+    j = np.arange(n ** 3)
+    c0 = np.stack([(j % n + 0.5) * L0[0], ((j // n) % n + 0.5) * L0[1], (j // (n * n) + 0.5) * L0[2]], axis=1)
+    return math.sqrt(float(np.sum((avg - poisson3d_solution(c0)) ** 2)))
+
+
+def boundary1d_solution(x):
+    """poisson1d_boundary.cpp:42-50"""
+    return np.sin(x) ** 2
+
+
+def boundary1d_rhs(x):
+    return 2 * (np.cos(x) ** 2 - np.sin(x) ** 2)
+
+
+def boundary1d_classes(ix, nx):
+    """poisson1d_boundary.cpp:141-164: outermost cells skipped, next ones
+    boundary cells, the rest solved -> (solve mask, boundary mask, skip mask)."""
+    skip = (ix == 0) | (ix == nx - 1)
+    bdy = (ix == 1) | (ix == nx - 2)
+    return ~(skip | bdy), bdy, skip

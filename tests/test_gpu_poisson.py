@@ -1,0 +1,227 @@
+"""Poisson BiCG (tests/poisson/poisson_solve.hpp) on the GPU vs the oracle.
+
+Tolerances (fp64):
+* geometry factors (set_scaling_factor 696-819) and cell types: bit-exact —
+  both sides evaluate the reference's expressions in its operand order;
+* iterated state after k BiCG iterations: |x_gpu - x_oracle| <= TOL_K *
+  max|x_oracle|.  BiCG amplifies the rounding of its global sums, whose order
+  differs everywhere (hash order + MPI tree in the reference, a fixed
+  two-level tree here, cell order in the oracle).  The reference's own
+  self-noise, measured by running the oracle with the cell order reversed on
+  the 8^3 mesh below: p0 / r0 differ by 8e-14 after 5 iterations, 2.5e-10
+  after 20 and O(1) after 200, while the solution (= best solution) differs by
+  2e-14 at every count.  Hence TOL_K = 1e-13 / 1e-11 / 1e-8 for the iterates
+  at k = 1 / 5 / 20 and 1e-12 for the solution at any k;
+* the reference's known answers (poisson3d.cpp:227 norm < 0.35,
+  poisson1d_boundary.cpp:208 non-increasing norms) through the product.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import dccrg_amd
+from oracle import oracle as O
+from poisson_cases import (boundary1d_classes, boundary1d_rhs, boundary1d_solution, center_refine_select,
+                           level0_avg_norm, poisson3d_lengths, poisson3d_solution)
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("solution", "best_solution", "p0", "p1", "r0", "r1", "A_dot_p0")
+FACTORS = ("scaling_factor", "f_x_neg", "f_x_pos", "f_y_neg", "f_y_pos", "f_z_neg", "f_z_pos")
+
+
+def build_pair(n=8, R=2, rounds=2, periodic=(True, True, True), L0=None, extra_refines=0, seed=0):
+    """Product grid + oracle with the same mesh: poisson3d.cpp's center
+    refinement (`rounds` times) plus optional random refines."""
+    L0 = L0 or poisson3d_lengths(n)
+    g = dccrg_amd.Dccrg(0, 1, 0).set_initial_length((n, n, n)).set_neighborhood_length(0)
+    g.set_maximum_refinement_level(R).set_periodic(*periodic).initialize()
+    g.set_geometry((0, 0, 0), L0)
+    o = O.Grid((n, n, n), R, periodic, 0, 1)
+    o.set_geometry((0, 0, 0), L0)
+    rng = np.random.default_rng(seed)
+    for r in range(rounds):
+        ids = g.local_cells()
+        c, L = g.geometry(ids)
+        sel = list(ids[center_refine_select(c, L)])
+        if r < extra_refines:
+            lv = np.array([g.get_refinement_level(int(i)) for i in ids])
+            cand = ids[lv < R]
+            sel += list(rng.choice(cand, size=max(1, cand.size // 20), replace=False))
+        for i in sel:
+            g.refine_completely(int(i))
+            o.refine_completely(int(i))
+        g.stop_refining()
+        o.stop_refining()
+    ids = g.local_cells()
+    oid, _ = o.cells()
+    assert np.array_equal(ids, np.sort(oid))
+    return g, o
+
+
+def setup_3d(g, o):
+    ids = g.local_cells()
+    c, L = g.geometry(ids)
+    oc, oL = o.geometry(ids)
+    assert np.array_equal(c, oc) and np.array_equal(L, oL)
+    rhs_v = -(81.0 / 16.0) * poisson3d_solution(c)
+    rhs = g.add_field("rhs", np.float64, False)
+    sol = g.add_field("solution", np.float64, False)
+    slots = g.slot_ids()[: g.n_local]
+    order = np.searchsorted(ids, slots)
+    rhs.set(rhs_v[order])
+    sol.set(np.zeros(slots.size))
+    o.po_set(ids, rhs_v, np.zeros(ids.size), np.zeros(ids.size, np.int32))
+    return ids, c, L, slots
+
+
+def gpu_state(g, slots, names):
+    out = {}
+    for nm in names:
+        f = g.fields["solution"] if nm == "solution" else dccrg_amd.Poisson_Solve.field(g, nm)
+        out[nm] = f.get(0, slots.size)
+    return out
+
+
+def compare_state(g, o, slots, tol, names=STATE):
+    got = gpu_state(g, slots, names)
+    exp = o.po_get(slots)
+    for nm in names:
+        e = exp[:, O.Grid.PO_FIELDS.index(nm)]
+        scale = max(float(np.max(np.abs(e))), 1e-300)
+        err = float(np.max(np.abs(got[nm] - e))) / scale
+        assert err <= tol, (nm, err)
+
+
+def test_cache_factors_bitwise(gpu):
+    g, o = build_pair(8, 2, 2, extra_refines=2, seed=3)
+    ids, c, L, slots = setup_3d(g, o)
+    s = dccrg_amd.Poisson_Solve(max_iterations=1)
+    s.solve(ids, g)
+    o.po_solve(max_iterations=1)
+    got = gpu_state(g, slots, FACTORS + ("type",))
+    exp = o.po_get(slots)
+    for nm in FACTORS:
+        assert np.array_equal(got[nm], exp[:, O.Grid.PO_FIELDS.index(nm)]), nm
+    assert np.array_equal(got["type"], exp[:, 14].astype(np.int32))
+
+
+@pytest.mark.parametrize("iters,tol", [(1, 1e-13), (5, 1e-11), (20, 1e-8)])
+def test_fixed_iterations_match_oracle(gpu, iters, tol):
+    g, o = build_pair(8, 2, 2, extra_refines=2, seed=1)
+    ids, c, L, slots = setup_3d(g, o)
+    s = dccrg_amd.Poisson_Solve(max_iterations=iters, min_iterations=iters)
+    it, res = s.solve(ids, g)
+    oit, ores = o.po_solve(max_iterations=iters, min_iterations=iters)
+    assert it == oit == iters
+    assert abs(res - ores) <= 1e-10 * abs(ores)
+    compare_state(g, o, slots, tol, STATE[2:])
+    compare_state(g, o, slots, 1e-12, STATE[:2])
+
+
+def test_poisson3d_kat_through_product(gpu):
+    """poisson3d.cpp:122-238 with the product: PASSED iff norm < 0.35."""
+    g, o = build_pair(8, 2, 2)
+    ids, c, L, slots = setup_3d(g, o)
+    it, res = dccrg_amd.Poisson_Solve().solve(ids, g)
+    oit, ores = o.po_solve()
+    assert it == oit
+    sol = g.fields["solution"].get(0, slots.size)
+    order = np.argsort(slots)
+    norm = level0_avg_norm(slots[order], sol[order], c, L, 8, poisson3d_lengths(8))
+    assert norm < 0.35, norm
+    compare_state(g, o, slots, 1e-12, ("solution",))
+
+
+def band_check(got, fwd, rev, floor):
+    """|gpu - oracle| within the reference's own order noise: at most 10x
+    the difference between two faithful oracle orders, or `floor`
+    (relative to max|oracle|)."""
+    scale = max(float(np.max(np.abs(fwd))), 1e-300)
+    noise = float(np.max(np.abs(rev - fwd))) / scale
+    err = float(np.max(np.abs(got - fwd))) / scale
+    assert err <= max(floor, 10 * noise), (err, noise)
+    return err, noise
+
+
+def test_config4_shape_200_iterations(gpu):
+    """SURVEY §8(d) config 4 shape at 32^3 (refined twice around the center,
+    periodic, min = max = 200 iterations).  Past ~20 iterations BiCG's
+    iterates on this system are dominated by summation-order noise, and the
+    returned best solution is the iterate at the smallest residual, a
+    discontinuous function of that noise, so the solution is compared within
+    the band two oracle orders span; the early iterates are pinned tightly by
+    test_fixed_iterations_match_oracle."""
+    g, o = build_pair(32, 2, 2)
+    ids, c, L, slots = setup_3d(g, o)
+    s = dccrg_amd.Poisson_Solve(200, 200)
+    it, res = s.solve(ids, g)
+    oit, ores = o.po_solve(200, 200)
+    fwd = o.po_get(slots)[:, 0]
+    rhs = -(81.0 / 16.0) * poisson3d_solution(c)
+    o.po_set(ids, rhs, np.zeros(ids.size), np.zeros(ids.size, np.int32))
+    rit, rres = o.po_solve(200, 200, reverse=True)
+    rev = o.po_get(slots)[:, 0]
+    assert it == oit == rit == 200
+    got = g.fields["solution"].get(0, slots.size)
+    band_check(got, fwd, rev, 1e-12)
+    lo, hi = sorted((ores, rres))
+    assert lo * (1 - 1e-6) - 1e-300 <= res <= hi * (1 + 1e-6) or abs(res - ores) <= 10 * abs(rres - ores)
+
+
+def test_poisson1d_boundary_kat_through_product(gpu):
+    """poisson1d_boundary.cpp:108-221 with skip / boundary / solve cells,
+    non-periodic; norms must not grow (the reference's check), and up to 256
+    cells every solution matches the oracle within its order-noise band
+    (these solves stop on residual <= 1e-15, a rounding-level test, so the
+    iteration count is not compared: two faithful oracle orders stop after 72
+    and 78 iterations at 64 cells)."""
+    old = float("inf")
+    cells = 8
+    while cells <= 4096:
+        nx = cells + 4
+        h = 2 * math.pi / cells
+        g = dccrg_amd.Dccrg(0, 1, 0).set_initial_length((nx, 1, 1)).set_neighborhood_length(0)
+        g.set_maximum_refinement_level(0).initialize()
+        g.set_geometry((-2 * h, 0, 0), (h, 1, 1))
+        ids = g.local_cells()
+        c, _ = g.geometry(ids)
+        x = c[:, 0]
+        solve, bdy, skip = boundary1d_classes((ids - 1).astype(np.int64), nx)
+        rhs_v = np.where(solve | bdy, boundary1d_rhs(x), 0.0)
+        sol_v = np.where(bdy, boundary1d_solution(x), 0.0)
+        rhs = g.add_field("rhs", np.float64, False)
+        sol = g.add_field("solution", np.float64, False)
+        rhs.set(rhs_v)  # unrefined: slot order = id order
+        sol.set(sol_v)
+        it, _ = dccrg_amd.Poisson_Solve(10000, 0, 1e-15, 2, 100).solve(ids[solve], g, ids[skip])
+        got = sol.get(0, ids.size)
+        norm = math.sqrt(float(np.sum((got[solve] - boundary1d_solution(x[solve])) ** 2)))
+        assert norm <= old, (cells, norm, old)
+        old = norm
+        if cells <= 256:
+            types = np.where(solve, 0, np.where(skip, 2, 1)).astype(np.int32)
+            o = O.Grid((nx, 1, 1), 0, (False, False, False), 0, 1)
+            o.set_geometry((-2 * h, 0, 0), (h, 1, 1))
+            o.po_set(ids, rhs_v, sol_v, types)
+            oit, _ = o.po_solve(10000, 0, 1e-15, 2, 100)
+            fwd = o.po_get(ids)
+            o.po_set(ids, rhs_v, sol_v, types)
+            rit, _ = o.po_solve(10000, 0, 1e-15, 2, 100, reverse=True)
+            rev = o.po_get(ids)
+            band_check(got, fwd[:, 0], rev[:, 0], 1e-10)
+            assert np.array_equal(dccrg_amd.Poisson_Solve.field(g, "type").get(0, ids.size),
+                                  fwd[:, 14].astype(np.int32))
+        g.close()
+        cells *= 2
+
+
+def test_failsafe_matches_oracle(gpu):
+    g, o = build_pair(6, 2, 1, L0=(1.0, 0.5, 2.0))
+    ids, c, L, slots = setup_3d(g, o)
+    it, norm = dccrg_amd.Poisson_Solve(50, 0, 1e-12).solve_failsafe(ids, g)
+    oit, onorm = o.po_solve(50, 0, 1e-12, failsafe=True)
+    assert it == oit
+    assert abs(norm - onorm) <= 1e-12 * abs(onorm)
+    compare_state(g, o, slots, 1e-13, ("solution",))

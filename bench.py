@@ -38,8 +38,9 @@ def parse():
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--workload", choices=["advection", "gol"], default="advection",
-                   help="advection = BASELINE metric (default); gol = config 2 game of life line")
+    p.add_argument("--workload", choices=["advection", "gol", "poisson"], default="advection",
+                   help="advection = BASELINE metric (default); gol = config 2 game of life line; "
+                        "poisson = config 4 BiCG line")
     return p.parse_args()
 
 
@@ -82,6 +83,85 @@ def gol_main(a, dccrgx_mod, torch):
                      "traffic": None, "kernel": "gol_structured_kernel", "alg_bytes_per_step": 8 * n,
                      "kernel_ms_per_step": kms / a.steps},
         "cpu_baseline": None}), flush=True)
+    g.close()
+
+
+def poisson_main(a, dccrgx_mod, torch, rank, world, uid):
+    """BASELINE config 4: Poisson BiCG (tests/poisson/poisson3d.cpp) on a
+    128^3-base grid per GPU (cell lengths 2pi/128, pi/128, 8pi/128), periodic,
+    refined twice around (pi, pi/2, 4pi); one step = one BiCG iteration over
+    every solve cell (min = max = steps iterations, as SURVEY §8(d))."""
+    import math
+
+    n = a.base
+    L0 = (2 * math.pi / n, math.pi / n, 8 * math.pi / n)
+    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g.set_initial_length((n, n, n * world)).set_neighborhood_length(0).set_maximum_refinement_level(2)
+    g.set_periodic(True, True, True).initialize()
+    g.set_geometry((0, 0, 0), L0)
+    t_setup = time.perf_counter()
+    for _ in range(2):  # poisson3d.cpp:174-192
+        ids = g.local_cells()
+        c, L = g.geometry(ids)
+        mn, mx = c - L / 2, c + L / 2
+        sel = ((mn[:, 0] < 1.01 * math.pi) & (mx[:, 0] > 0.99 * math.pi) & (mn[:, 1] < 0.51 * math.pi)
+               & (mx[:, 1] > 0.49 * math.pi) & (mn[:, 2] < 4.01 * math.pi) & (mx[:, 2] > 3.99 * math.pi))
+        for cell in ids[sel]:
+            g.refine_completely(int(cell))
+        g.stop_refining()
+    ids = g.local_cells()
+    slots = g.slot_ids()[: g.n_local]
+    c, _ = g.geometry(slots)
+    rhs = g.add_field("rhs", np.float64, False)
+    sol = g.add_field("solution", np.float64, False)
+    rhs.set(-(81.0 / 16.0) * np.sin(c[:, 0]) * np.cos(2 * c[:, 1]) * np.sin(c[:, 2] / 4))
+    sol.set(np.zeros(slots.size))
+    solver = dccrgx_mod.Poisson_Solve(a.warmup, a.warmup)
+    solver.solve(ids, g)  # cache_system_info + warm-up iterations
+    setup_s = time.perf_counter() - t_setup
+    sol.set(np.zeros(slots.size))
+    solver = dccrgx_mod.Poisson_Solve(a.steps, a.steps)
+    g.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    g.kernel_timing(1)
+    t0 = time.perf_counter()
+    it, res = solver.solve(ids, g, cache_is_up_to_date=True)
+    g.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms, kn = g.kernel_timing(0)
+    n_solve = ids.size
+    stats = torch.tensor([el, float(n_solve), kms], dtype=torch.float64, device="cuda")
+    if world > 1:
+        import torch.distributed as dist
+        mx_ = stats.clone()
+        dist.all_reduce(mx_, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        el, total = float(mx_[0]), int(sm[1])
+    else:
+        total = n_solve
+    # algorithmic bytes per solve cell and iteration: SURVEY §8(d) 3-phase
+    # minimum 272 B + the face table read by phases A and B (2 x 6 x int32)
+    per_cell = 272 + 48
+    ach = per_cell * n_solve * it / (kms / 1e3) / 1e9 if kms > 0 else None
+    if rank == 0:
+        print(json.dumps({
+            "metric": "cell-updates/s, Poisson BiCG iterations (BASELINE config 4)", "value": total * it / el,
+            "unit": "cell-updates/s", "n_gpus": world, "steps": it, "warmup": a.warmup,
+            "ms_per_step": el / it * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic: poisson3d.cpp rhs on its center-refined mesh",
+            "config": {"workload": f"poisson3d BiCG, base {n}x{n}x{n * world}, periodic, refined twice at the "
+                                   f"center, min = max = {a.steps} iterations",
+                       "solve_cells_rank0": n_solve, "setup_s": setup_s, "parallelism": f"domain decomposition x{world}"},
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                         "kernel": "po_phase_a + po_phase_b + po_phase_c", "alg_bytes_per_cell_iteration": per_cell,
+                         "kernel_ms_per_step": kms / it, "launches_per_step": kn / it, "residual_min": res},
+            "cpu_baseline": None}), flush=True)
     g.close()
 
 
@@ -145,6 +225,8 @@ def main():
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
+    if a.workload == "poisson":
+        return poisson_main(a, dccrg_amd, torch, rank, world, uid)
 
     t_setup = time.perf_counter()
     g, f = build_grid(dccrg_amd, rank, world, a.base, a.max_ref_lvl, uid)

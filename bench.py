@@ -235,15 +235,8 @@ def main():
     c = g.counts
     n_local = c["inner"] + c["outer"]
     variant = int(os.environ.get("DCCRGX_ADV_VARIANT", "11"))
-    layout = g.advection_layout() if variant == 11 else None
-    if layout is None:
-        ptr, _, fdir = g.csr("face")
-        # finer faces = (cell, direction) pairs with 4 face neighbors
-        rows = np.repeat(np.arange(n_local), np.diff(ptr.astype(np.int64)))
-        _, cnt = np.unique(rows * 8 + (fdir + 3), return_counts=True)
-        n_fine = int(np.sum(cnt == 4))
-    else:
-        n_fine = layout["finer_faces"]
+    layout = g.advection_layout()
+    n_fine = layout["finer_faces"]
 
     def step():
         g.start_remote_neighbor_copy_updates()
@@ -280,14 +273,12 @@ def main():
     else:
         el_max, total_cells = el, n_local
 
-    # algorithmic bytes of the sweep: per cell read density,
-    # vx, vy, vz, lx, ly, lz + write density = 64 B, plus the face structure
-    # the kernel reads: tiled sweep = 12 B face row per cell + 4 B per
-    # distinct out-of-tile neighbor of a tile + 8 B per finer face + 8 B per
-    # tile (dccrgx_advection_layout); ELL sweeps = 6 x int32 per cell + 16 B
-    # per finer face
-    alg_core = 64 * n_local
-    alg_bytes_step = layout["alg_bytes"] if layout else alg_core + 24 * n_local + 16 * n_fine
+    # algorithmic bytes of one sweep, as SURVEY §8(d) fixes them: per cell
+    # read density, vx, vy, vz, lx, ly, lz + write density = 64 B, plus the
+    # face structure as a CSR (4 B per face-neighbor entry + 4 B row pointer);
+    # the 64 B core alone is reported beside it
+    alg_core = layout["alg_bytes_core"]
+    alg_bytes_step = layout["alg_bytes"]
     kern_s = kern_ms / 1e3
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
     launches_per_step = kern_n / a.steps if a.steps else 0
@@ -297,7 +288,7 @@ def main():
     # only valid for the same mesh, so it is dropped for any other cell count
     traffic = None
     tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
-    if os.path.exists(tf) and layout is not None:
+    if os.path.exists(tf):
         try:
             t = json.load(open(tf))
             if t.get("cells") == n_local and world == 1:
@@ -343,10 +334,12 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "advection_tiles_kernel" if layout else f"advection_kernel variant {variant}",
+                "kernel": "advection_regular_kernel + advection_tiles_kernel" if variant == 11
+                          else f"advection_kernel variant {variant}",
                 "layout": layout,
                 "alg_bytes_per_step": alg_bytes_step,
                 "alg_bytes_core_per_step": alg_core,
+                "frac_core_64B": (alg_core * a.steps / kern_s / 1e9 / PEAK_HBM_GBS) if kern_s > 0 else None,
                 "finer_faces": n_fine,
                 "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
                 "launches_per_step": launches_per_step,

@@ -145,6 +145,14 @@ struct PoissonState {
 	size_t n_cached = 0;       // local cells in cell_info
 };
 
+// one regular advection tile (tile_build.hip): first slot and the start slot
+// of the same-level neighbor box across each side (-1: none)
+struct RegTileMeta {
+	uint32_t ts;
+	int32_t nst[6];
+	uint32_t pad;
+};
+
 struct Grid {
 	// communicator
 	int rank = 0, size = 1, device = 0;
@@ -214,6 +222,14 @@ struct Grid {
 	DBuf<uint32_t> ext;        // total_ext slots
 	DBuf<uint32_t> fine_base;  // n_tiles: index of the tile's first finer face
 	DBuf<uint32_t> tfine;      // 2 x u32 per finer face (4 x u16)
+	// regular tiles (aligned uniform 8x8x8 boxes, see tile_build.hip) are swept
+	// without face rows; tlists = [regular inner | regular outer | irregular
+	// inner | irregular outer] tile indices, tcount = the four lengths,
+	// tnb = per tile the six neighbor-box start slots (-1: none)
+	DBuf<uint32_t> tlists;
+	DBuf<int32_t> tnb;
+	size_t tcount[4] = {0, 0, 0, 0};
+	DBuf<RegTileMeta> tregmeta;  // per regular tile (list order): start slot + neighbor-box starts
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;
@@ -290,6 +306,10 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
                         DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
                         DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s);
 
+void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_inner, size_t n_tiles_outer,
+                      const uint64_t* slot_ids, const int32_t* face_ell, DBuf<uint32_t>& lists, DBuf<int32_t>& tnb,
+                      DBuf<RegTileMeta>& regmeta, size_t counts[4], hipStream_t s);
+
 // --- launchers implemented in sweep_kernels.hip -----------------------------
 void k_pack(const uint8_t* field, size_t elem, const int32_t* slots, size_t n, uint8_t* out, hipStream_t s);
 void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
@@ -297,10 +317,9 @@ void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, con
 void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
-// tiled advection sweep over tiles [gt0, gt0 + ntiles) (the inner or the
-// outer run: tiles never straddle the two)
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t gt0, size_t ntiles, double dt,
-                       hipStream_t s);
+// tiled advection sweep over the regular and the irregular tiles of one run
+// (run 0 inner, 1 outer: tiles never straddle the two)
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, int run, double dt, hipStream_t s);
 int adv_variant();  // DCCRGX_ADV_VARIANT (11 = tiled, the default)
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,

@@ -388,6 +388,8 @@ static void ensure_tiles(Grid& g) {
 	g.n_tiles_outer = tb.n_tiles_outer;
 	g.max_ext = tb.max_ext;
 	g.total_ext = tb.total_ext;
+	k_classify_tiles(g.m, g.tstart.p, g.n_tiles_inner, g.n_tiles_outer, g.slot_ids.p, g.face_ell.p, g.tlists, g.tnb,
+	                 g.tregmeta, g.tcount, g.s_comp);
 	g.tiles_valid = true;
 }
 
@@ -1536,9 +1538,8 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		if (adv_variant() == 11) {
 			ensure_tiles(g);
 			// tiles never straddle the inner / outer runs
-			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, g.n_tiles_inner, dt, g.s_comp);
-			if (s1 > g.n_inner)
-				k_advection_tiles(f, (double*)rho.scratch.p, g, g.n_tiles_inner, g.n_tiles_outer, dt, g.s_comp);
+			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
+			if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
 		} else {
 			k_advection(f, (double*)rho.scratch.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p, g.face_fine.p, s0, s1, dt,
 			            g.s_comp);
@@ -1548,18 +1549,27 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 	});
 }
 
-int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[6]) {
+int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[10]) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(out, "null output");
 		ensure_tiles(g);
 		const uint64_t nt = g.n_tiles_inner + g.n_tiles_outer;
+		uint32_t entries = 0;
+		HIP_CHECK(hipMemcpy(&entries, g.face_ptr.p + g.n_local, 4, hipMemcpyDeviceToHost));
+		const uint64_t n = g.n_local;
 		out[0] = uint64_t(g.tile);
 		out[1] = nt;
 		out[2] = g.total_ext;
 		out[3] = g.max_ext;
 		out[4] = g.n_fine_faces;
-		out[5] = 76 * uint64_t(g.n_local) + 4 * uint64_t(g.total_ext) + 8 * uint64_t(g.n_fine_faces) + 12 * nt;
+		out[5] = entries;
+		// 64 B per cell (7 fp64 fields read, density written) +
+		// the face CSR (4 B per entry + 4 B row pointer)
+		out[6] = 64 * n + 4 * (n + 1) + 4 * uint64_t(entries);
+		out[7] = 64 * n;
+		out[8] = g.tcount[0] + g.tcount[1];
+		out[9] = 512 * (g.tcount[0] + g.tcount[1]);
 		return 0;
 	});
 }

@@ -611,8 +611,8 @@ __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
     const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
     const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tstart,
     const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ fine_base, const uint32_t* __restrict__ tfine, uint32_t gt0, uint32_t ntiles,
-    uint32_t ecap, double dt, int map) {
+    const uint32_t* __restrict__ fine_base, const uint32_t* __restrict__ tfine, const uint32_t* __restrict__ list,
+    uint32_t ntiles, uint32_t ecap, double dt, int map) {
 #pragma clang fp contract(off)
 	extern __shared__ double shd[];  // [7][T + ecap]
 	const uint32_t W = T + ecap;
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
 		lb = ((k / G) * 8u + x) * G + (k % G);
 	}
 	if (lb >= ntiles) return;  // block-uniform
-	const uint32_t gt = gt0 + lb;
+	const uint32_t gt = list[lb];
 	const uint32_t ts = tstart[gt], te = tstart[gt + 1];
 	const uint32_t tid = threadIdx.x;
 	const uint32_t s = ts + tid;
@@ -723,6 +723,238 @@ __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
 		}
 	}
 	rho_out[s] = cd + acc / (clx * cly * clz);
+}
+
+
+// Regular tiles (tile_build.hip classify_tiles_kernel): an aligned 8x8x8 box
+// of same-level cells, slots ts..ts+511 in Morton order, whose face
+// neighbors across each side are the same-level cells of one neighbor box
+// starting at slot tnb[6 gt + d] (-1: no neighbor on that side).  Thread t
+// owns the cell with local Morton index t.  Own fields are staged in LDS for
+// the in-tile faces; the (at most three) out-of-tile face neighbors of a
+// cell are each used by that cell alone, so they are read straight into
+// registers, issued before the barrier.  No per-cell face rows are read.
+__device__ __forceinline__ uint32_t m9(uint32_t x, uint32_t y, uint32_t z) {
+	return (x & 1u) | ((y & 1u) << 1) | ((z & 1u) << 2) | ((x & 2u) << 2) | ((y & 2u) << 3) | ((z & 2u) << 4) |
+	       ((x & 4u) << 4) | ((y & 4u) << 5) | ((z & 4u) << 6);
+}
+
+template <int DIAG>
+__global__ __launch_bounds__(512) void advection_regular_kernel(
+    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
+    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
+    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tstart,
+    const uint32_t* __restrict__ list, const int32_t* __restrict__ tnb, uint32_t ntiles, double dt, int map) {
+#pragma clang fp contract(off)
+	__shared__ double shd[7][512];
+	const unsigned nb = gridDim.x, b = blockIdx.x;
+	unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
+	if (map == 1) lb = b;
+	else if (map >= 2) {
+		const unsigned G = unsigned(map), x = b & 7u, k = b >> 3;
+		lb = ((k / G) * 8u + x) * G + (k % G);
+	}
+	if (lb >= ntiles) return;  // block-uniform
+	const uint32_t gt = list[lb];
+	const uint32_t ts = tstart[gt];
+	const uint32_t tid = threadIdx.x;
+	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
+	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
+	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
+	const uint32_t o = (ts + tid) << 3;
+	const double* const fld[7] = {rho, vx, vy, vz, lx, ly, lz};
+	double c[7];
+#pragma unroll
+	for (int k = 0; k < 7; k++) c[k] = ldo(fld[k], o);
+	// out-of-tile neighbor per axis (a cell touches at most one side per axis)
+	AdvNb xn[3];
+	int xd[3];  // direction of that face, or -1 (inside the tile) / -2 (no neighbor)
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		xd[a] = -1;
+		xn[a] = AdvNb{0, 1, 1, 1, 0};
+		const int d = l[a] == 0 ? 2 * a : (l[a] == 7 ? 2 * a + 1 : -1);
+		if (d < 0) continue;
+		const int32_t st = DIAG ? int32_t(ts) : tnb[6 * gt + d];
+		if (st < 0) {
+			xd[a] = -2;
+			continue;
+		}
+		xd[a] = d;
+		uint32_t q[3] = {l[0], l[1], l[2]};
+		q[a] = (d & 1) ? 0u : 7u;
+		const uint32_t no = (uint32_t(st) + m9(q[0], q[1], q[2])) << 3;
+		xn[a] = AdvNb{ldo(rho, no), ldo(lx, no), ldo(ly, no), ldo(lz, no), ldo(fld[1 + a], no)};
+	}
+#pragma unroll
+	for (int k = 0; k < 7; k++) shd[k][tid] = c[k];
+	__syncthreads();
+	const double cd = c[0], cvx = c[1], cvy = c[2], cvz = c[3], clx = c[4], cly = c[5], clz = c[6];
+	double acc = 0;
+#pragma unroll
+	for (int d = 0; d < 6; d++) {
+		const int a = d >> 1;
+		const bool plus = d & 1;
+		const bool inside = plus ? l[a] < 7 : l[a] > 0;
+		AdvNb n;
+		if (inside) {
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] = plus ? q[a] + 1 : q[a] - 1;
+			const uint32_t li = m9(q[0], q[1], q[2]);
+			n = AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]};
+		} else {
+			if (xd[a] != d) continue;  // no neighbor on this side
+			n = xn[a];
+		}
+		acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, n, dt);
+	}
+	rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+}
+
+
+// Persistent, software-pipelined form of advection_regular_kernel: a fixed
+// grid (a few blocks per CU); XCD x (= block % 8) sweeps the x-th eighth of
+// the regular-tile list, its blocks taking consecutive tiles side by side
+// (block j: tiles j, j + B, j + 2B, ... of that eighth, B = blocks per XCD),
+// and every block loads tile k + B into registers while it computes tile k
+// from LDS, so a CU always has a tile of loads in flight.
+struct RegLoad {
+	double c[7];
+	AdvNb xn[3];
+	int xd[3];
+};
+
+struct AdvFields {
+	const double *rho, *vx, *vy, *vz, *lx, *ly, *lz;
+	__device__ __forceinline__ const double* v(int a) const { return a == 0 ? vx : (a == 1 ? vy : vz); }
+};
+
+__device__ __forceinline__ void reg_load(const AdvFields& F, const RegTileMeta& m, const uint32_t l[3], uint32_t tid,
+                                         RegLoad& r) {
+	const uint32_t o = (m.ts + tid) << 3;
+	r.c[0] = ldo(F.rho, o);
+	r.c[1] = ldo(F.vx, o);
+	r.c[2] = ldo(F.vy, o);
+	r.c[3] = ldo(F.vz, o);
+	r.c[4] = ldo(F.lx, o);
+	r.c[5] = ldo(F.ly, o);
+	r.c[6] = ldo(F.lz, o);
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		r.xd[a] = -1;
+		r.xn[a] = AdvNb{0, 1, 1, 1, 0};
+		const bool lo = l[a] == 0, hi = l[a] == 7;
+		if (!lo && !hi) continue;
+		// constant indices only (a runtime index into m.nst would live in scratch)
+		const int32_t st = lo ? m.nst[2 * a] : m.nst[2 * a + 1];
+		if (st < 0) {
+			r.xd[a] = -2;
+			continue;
+		}
+		r.xd[a] = lo ? 2 * a : 2 * a + 1;
+		uint32_t q[3] = {l[0], l[1], l[2]};
+		q[a] = lo ? 7u : 0u;
+		const uint32_t no = (uint32_t(st) + m9(q[0], q[1], q[2])) << 3;
+		r.xn[a] = AdvNb{ldo(F.rho, no), ldo(F.lx, no), ldo(F.ly, no), ldo(F.lz, no), ldo(F.v(a), no)};
+	}
+}
+
+// the out-of-tile neighbors of a regular tile, flattened: k = (side * 5 +
+// value) * 64 + face cell (value 0 rho, 1 lx, 2 ly, 3 lz, 4 the velocity
+// along the side's axis): 30 (side, value) rows of 64, wave w loads rows w,
+// w + 8, w + 16, w + 24, so side and value are wave-uniform (scalar pointer
+// and neighbor-box start, no private-memory lookup tables)
+struct AdvPtrs {
+	const double* p[7];  // rho, lx, ly, lz, vx, vy, vz
+};
+
+template <int MINW, int DIAG>
+__global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
+                                                                         const RegTileMeta* __restrict__ meta,
+                                                                         uint32_t ntiles, double dt) {
+#pragma clang fp contract(off)
+	__shared__ double shd[7][512];  // rho, vx, vy, vz, lx, ly, lz of the tile's cells
+	__shared__ double she[1920];
+	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
+	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
+	uint32_t t = t0 + j;
+	if (t >= t1) return;  // block-uniform
+	const uint32_t tid = threadIdx.x;
+	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
+	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
+	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
+	// index of this cell within a side of each axis (the two other coordinates)
+	const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
+	const double* __restrict__ rho = P.p[0];
+	const double* __restrict__ lx = P.p[1];
+	const double* __restrict__ ly = P.p[2];
+	const double* __restrict__ lz = P.p[3];
+	const double* __restrict__ vx = P.p[4];
+	const double* __restrict__ vy = P.p[5];
+	const double* __restrict__ vz = P.p[6];
+	// one register set: the tile being loaded
+	double c[7], e[4];
+	auto load = [&](uint32_t tt) {
+		const uint32_t ts = meta[tt].ts;
+		const uint32_t o = (ts + tid) << 3;
+		c[0] = ldo(rho, o); c[1] = ldo(vx, o); c[2] = ldo(vy, o); c[3] = ldo(vz, o);
+		c[4] = ldo(lx, o); c[5] = ldo(ly, o); c[6] = ldo(lz, o);
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
+			e[i] = 0;
+			if (row >= 30u) continue;
+			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
+			const int32_t st = meta[tt].nst[d];
+			if (st < 0 || DIAG == 1) continue;
+			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
+			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
+			e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+		}
+	};
+	load(t);
+	for (;;) {
+		__syncthreads();  // the previous tile's faces have been read from LDS
+#pragma unroll
+		for (int k = 0; k < 7; k++) shd[k][tid] = c[k];
+#pragma unroll
+		for (int i = 0; i < 4; i++)
+			if (w + 8u * i < 30u) she[(w + 8u * i) * 64u + lane] = e[i];
+		__syncthreads();
+		const uint32_t tc = t, tn = t + B;
+		const bool more = tn < t1;
+		if (more) load(tn);  // the next tile's loads fly while this one is computed
+		const uint32_t ts = meta[tc].ts;
+		const double cd = shd[0][tid], cvx = shd[1][tid], cvy = shd[2][tid], cvz = shd[3][tid], clx = shd[4][tid],
+		             cly = shd[5][tid], clz = shd[6][tid];
+		double acc = 0;
+#pragma unroll
+		for (int d = 0; d < 6; d++) {
+			if (DIAG == 2) {
+				acc += shd[1 + (d >> 1)][tid ^ (1u << (d >> 1))];
+				continue;
+			}
+			const int a = d >> 1;
+			const bool plus = d & 1;
+			const bool inside = plus ? l[a] < 7 : l[a] > 0;
+			AdvNb n;
+			if (inside) {
+				uint32_t q[3] = {l[0], l[1], l[2]};
+				q[a] = plus ? q[a] + 1 : q[a] - 1;
+				const uint32_t li = m9(q[0], q[1], q[2]);
+				n = AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]};
+			} else {
+				if (meta[tc].nst[d] < 0) continue;  // no neighbor on this side
+				const uint32_t k = uint32_t(d) * 320u + fi[a];
+				n = AdvNb{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]};
+			}
+			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, n, dt);
+		}
+		rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+		if (!more) break;
+		t = tn;
+	}
 }
 
 // max_time_step local part (solve.hpp:289-333): block minima
@@ -893,29 +1125,77 @@ static uint32_t tile_ecap(int T, size_t max_ext) {
 	return uint32_t(std::min(cap, max_ext));
 }
 
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, size_t gt0, size_t ntiles, double dt,
-                       hipStream_t s) {
-	if (ntiles == 0) return;
-	const int T = g.tile;
-	const uint32_t ecap = tile_ecap(T, g.max_ext);
-	size_t lds = size_t(7) * (T + ecap) * sizeof(double);
+void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, int run, double dt, hipStream_t s) {
 	static const int diag = [] {
 		const char* e = getenv("DCCRGX_ADV_DIAG");
 		return e ? atoi(e) : 0;
 	}();
-	if (diag == 3) lds = 0;
 	static const int amap = [] {
 		const char* e = getenv("DCCRGX_ADV_MAP");
 		return e ? atoi(e) : 128;
 	}();
+	// DCCRGX_ADV_REGULAR=0 sweeps every tile with the general kernel (A/B)
+	static const int use_regular = [] {
+		const char* e = getenv("DCCRGX_ADV_REGULAR");
+		return e ? atoi(e) : 1;
+	}();
 	// whole rounds of 8 x map tiles, so that the block -> tile map is onto
 	// (blocks past the last tile exit at once)
 	const size_t round = amap >= 2 ? size_t(8) * size_t(amap) : size_t(8);
-	const size_t nb = (ntiles + round - 1) / round * round;
+	auto blocks = [&](size_t n) { return (n + round - 1) / round * round; };
+	const int T = g.tile;
+	const uint32_t* reg = g.tlists.p + (run == 0 ? 0 : g.tcount[0]);
+	const uint32_t* irr = g.tlists.p + g.tcount[0] + g.tcount[1] + (run == 0 ? 0 : g.tcount[2]);
+	size_t n_reg = g.tcount[run], n_irr = g.tcount[2 + run];
+	std::vector<uint32_t> all_h;
+	DBuf<uint32_t> all_d;
+	if (!use_regular && n_reg) {  // one list with both kinds
+		all_h = download(reg, n_reg, s);
+		const auto ih = download(irr, n_irr, s);
+		all_h.insert(all_h.end(), ih.begin(), ih.end());
+		upload(all_d, all_h, s);
+		irr = all_d.p;
+		n_irr += n_reg;
+		n_reg = 0;
+	}
+	static const int pp_blocks = [] {  // DCCRGX_ADV_PP=k: persistent regular kernel, k blocks per CU (0: off)
+		const char* e = getenv("DCCRGX_ADV_PP");
+		return e ? atoi(e) : 2;
+	}();
+	if (n_reg && pp_blocks > 0) {
+		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
+		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * size_t(pp_blocks), (n_reg + 7) / 8 * 8));
+		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
+		if (pp_blocks >= 3)
+			advection_regular_pp_kernel<6, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else if (diag == 6)
+			advection_regular_pp_kernel<4, 1><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else if (diag == 7)
+			advection_regular_pp_kernel<4, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else
+			advection_regular_pp_kernel<4, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		HIP_CHECK(hipGetLastError());
+	} else if (n_reg) {
+		if (diag == 5)
+			advection_regular_kernel<1><<<unsigned(blocks(n_reg)), 512, 0, s>>>(
+			    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, reg, g.tnb.p, uint32_t(n_reg), dt, amap);
+		else
+			advection_regular_kernel<0><<<unsigned(blocks(n_reg)), 512, 0, s>>>(
+			    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, reg, g.tnb.p, uint32_t(n_reg), dt, amap);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (!n_irr) {
+		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
+		return;
+	}
+	const uint32_t ecap = tile_ecap(T, g.max_ext);
+	size_t lds = size_t(7) * (T + ecap) * sizeof(double);
+	if (diag == 3) lds = 0;
+	const size_t nb = blocks(n_irr);
 #define DX_ADV_TILES1(TT, W, M)                                                                                      \
 	advection_tiles_kernel<TT, W, M><<<unsigned(nb), TT, lds, s>>>(                                                       \
 	    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, g.tell.p, g.ext_ptr.p, g.ext.p, g.fine_base.p, \
-	    g.tfine.p, uint32_t(gt0), uint32_t(ntiles), ecap, dt, amap)
+	    g.tfine.p, irr, uint32_t(n_irr), ecap, dt, amap)
 #define DX_ADV_TILES(TT, W)                                                                                          \
 	if (diag == 1) DX_ADV_TILES1(TT, W, 1);                                                                          \
 	else if (diag == 2) DX_ADV_TILES1(TT, W, 2);                                                                     \
@@ -929,6 +1209,7 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 #undef DX_ADV_TILES
 #undef DX_ADV_TILES1
 	HIP_CHECK(hipGetLastError());
+	if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));  // all_d must outlive the launch
 }
 
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s) {

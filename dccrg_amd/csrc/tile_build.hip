@@ -13,6 +13,9 @@
 //   5. per cell: six tile-local indices (binary search in the tile's ext).
 #include <hipcub/hipcub.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -158,6 +161,127 @@ __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restr
 	}
 }
 
+
+// ---------------------------------------------------------------------------
+// Regular tiles: a tile of exactly 512 slots that is an aligned 8x8x8 box of
+// cells of one level whose face neighbors on each of its six sides are,
+// all of them, either absent (non-periodic boundary) or the same-level
+// cells of one neighbor box stored Morton-consecutively from a single slot.
+// Such a tile's sweep needs no per-cell face rows: neighbors are found by
+// Morton arithmetic from the tile's start slot and the six neighbor-box
+// starts.  One 512-thread block per tile; thread t = local Morton index t.
+__device__ __forceinline__ uint32_t morton9(uint32_t x, uint32_t y, uint32_t z) {
+	uint32_t m = 0;
+	for (int b = 0; b < 3; b++) m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
+	return m;
+}
+
+__global__ __launch_bounds__(512) void classify_tiles_kernel(MapCtx m, const uint32_t* __restrict__ tstart,
+                                                              const uint64_t* __restrict__ slot_ids,
+                                                              const int32_t* __restrict__ face_ell,
+                                                              uint32_t* __restrict__ treg, int32_t* __restrict__ tnb) {
+	__shared__ int ok;
+	__shared__ int32_t nst[6];
+	__shared__ int has_nb[6], no_nb[6];
+	__shared__ uint64_t corner[4];
+	const uint32_t gt = blockIdx.x, tid = threadIdx.x;
+	const uint32_t ts = tstart[gt], te = tstart[gt + 1];
+	if (tid == 0) {
+		ok = (te - ts == 512u);
+		for (int d = 0; d < 6; d++) {
+			nst[d] = -1;
+			has_nb[d] = 0;
+			no_nb[d] = 0;
+		}
+	}
+	__syncthreads();
+	if (!ok) {
+		if (tid == 0) treg[gt] = 0x10u;  // reason: not 512 slots
+		return;
+	}
+	const uint32_t s = ts + tid;
+	uint64_t x, y, z;
+	const int lvl = map_indices(m, slot_ids[s], x, y, z);
+	if (tid == 0) {
+		corner[0] = x;
+		corner[1] = y;
+		corner[2] = z;
+		corner[3] = uint64_t(lvl);
+	}
+	__syncthreads();
+	const uint64_t len = uint64_t(1) << (m.R - lvl);
+	bool good = lvl >= 0 && uint64_t(lvl) == corner[3];
+	uint32_t l[3] = {0, 0, 0};
+	if (good) {
+		const uint64_t c[3] = {x, y, z};
+		for (int d = 0; d < 3; d++) {
+			if (corner[d] % (8 * len) != 0 || c[d] < corner[d]) good = false;
+			const uint64_t r = (c[d] - corner[d]) / len;
+			if (r > 7 || (c[d] - corner[d]) % len) good = false;
+			l[d] = uint32_t(r & 7u);
+		}
+		if (good && morton9(l[0], l[1], l[2]) != tid) good = false;
+	}
+	const bool box_good = good;
+	if (good) {
+		for (int d = 0; d < 6; d++) {
+			const int a = d >> 1;
+			const bool plus = d & 1;
+			const int32_t e = face_ell[6 * size_t(s) + d];
+			const bool boundary = plus ? l[a] == 7 : l[a] == 0;
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] = boundary ? (plus ? 0u : 7u) : (plus ? q[a] + 1 : q[a] - 1);
+			const uint32_t mq = morton9(q[0], q[1], q[2]);
+			if (!boundary) {
+				if (e != int32_t(ts + mq)) good = false;
+				continue;
+			}
+			if (e == -1) {
+				atomicOr(&no_nb[d], 1);
+				continue;
+			}
+			if (e < -1) {
+				good = false;
+				continue;
+			}
+			if (map_level(m, slot_ids[e]) != lvl || uint32_t(e) < mq) {
+				good = false;
+				continue;
+			}
+			const int32_t st = e - int32_t(mq);
+			atomicOr(&has_nb[d], 1);
+			atomicMax(&nst[d], st);  // all must agree: checked below
+		}
+	}
+	__shared__ int box_ok;
+	if (tid == 0) box_ok = 1;
+	__syncthreads();
+	if (!box_good) atomicAnd(&box_ok, 0);
+	if (!good) atomicAnd(&ok, 0);
+	__syncthreads();
+	// second pass: every boundary neighbor consistent with the agreed start
+	if (ok) {
+		for (int d = 0; d < 6; d++) {
+			const int a = d >> 1;
+			const bool plus = d & 1;
+			const bool boundary = plus ? l[a] == 7 : l[a] == 0;
+			if (!boundary) continue;
+			if (has_nb[d] && no_nb[d]) good = false;
+			const int32_t e = face_ell[6 * size_t(s) + d];
+			if (e == -1) continue;
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] = plus ? 0u : 7u;
+			if (e != nst[d] + int32_t(morton9(q[0], q[1], q[2]))) good = false;
+		}
+		if (!good) atomicAnd(&ok, 0);
+	}
+	__syncthreads();
+	if (tid == 0) {
+		treg[gt] = ok ? 1u : (box_ok ? 0x30u : 0x20u);  // reasons: 0x20 not a uniform box, 0x30 irregular side
+		for (int d = 0; d < 6; d++) tnb[6 * size_t(gt) + d] = (ok && has_nb[d]) ? nst[d] : -1;
+	}
+}
+
 }  // namespace
 
 // Tile boundaries of one run [r0, r1): greedy, each tile ends at the
@@ -267,6 +391,57 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
 	return out;
+}
+
+// Regular / irregular split of the tiles of one layout (see
+// classify_tiles_kernel): per-run lists of tile indices, and for regular
+// tiles the six neighbor-box start slots.
+void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_inner, size_t n_tiles_outer,
+                      const uint64_t* slot_ids, const int32_t* face_ell, DBuf<uint32_t>& lists, DBuf<int32_t>& tnb,
+                      DBuf<RegTileMeta>& regmeta, size_t counts[4], hipStream_t s) {
+	const size_t nt = n_tiles_inner + n_tiles_outer;
+	tnb.alloc(6 * nt + 6);
+	for (int k = 0; k < 4; k++) counts[k] = 0;
+	lists.alloc(nt + 1);
+	if (!nt) return;
+	DBuf<uint32_t> treg;
+	treg.alloc(nt);
+	classify_tiles_kernel<<<unsigned(nt), 512, 0, s>>>(m, tstart, slot_ids, face_ell, treg.p, tnb.p);
+	HIP_CHECK(hipGetLastError());
+	const std::vector<uint32_t> h = download(treg.p, nt, s);
+	// layout: [regular inner | regular outer | irregular inner | irregular outer]
+	std::vector<uint32_t> reg[2], irr[2];
+	size_t why[4] = {0, 0, 0, 0};
+	for (size_t t = 0; t < nt; t++) {
+		const int run = t < n_tiles_inner ? 0 : 1;
+		(h[t] == 1u ? reg[run] : irr[run]).push_back(uint32_t(t));
+		why[h[t] == 1u ? 0 : (h[t] >> 4)]++;
+	}
+	if (getenv("DCCRGX_DEBUG_TILES"))
+		fprintf(stderr, "[dccrgx] tiles: %zu regular, %zu not 512 slots, %zu not a uniform box, %zu irregular side\n",
+		        why[0], why[1], why[2], why[3]);
+	std::vector<uint32_t> all;
+	for (auto* v : {&reg[0], &reg[1], &irr[0], &irr[1]}) all.insert(all.end(), v->begin(), v->end());
+	counts[0] = reg[0].size();
+	counts[1] = reg[1].size();
+	counts[2] = irr[0].size();
+	counts[3] = irr[1].size();
+	HIP_CHECK(hipMemcpyAsync(lists.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, s));
+	// per regular tile, in list order: start slot + neighbor-box starts
+	const std::vector<uint32_t> hts = download(tstart, nt + 1, s);
+	const std::vector<int32_t> hnb = download(tnb.p, 6 * nt, s);
+	std::vector<RegTileMeta> meta;
+	for (int run = 0; run < 2; run++)
+		for (uint32_t t : reg[run]) {
+			RegTileMeta r{};
+			r.ts = hts[t];
+			for (int d = 0; d < 6; d++) r.nst[d] = hnb[6 * size_t(t) + d];
+			meta.push_back(r);
+		}
+	regmeta.alloc(meta.size() + 1);
+	if (!meta.empty())
+		HIP_CHECK(hipMemcpyAsync(regmeta.p, meta.data(), meta.size() * sizeof(RegTileMeta), hipMemcpyHostToDevice, s));
+	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace dccrgx

@@ -177,12 +177,15 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double
                                        double diff_threshold, uint64_t* out, size_t cap, size_t* n);
 
 /* data layout of the advection sweep (built on first use): out[0] tile size,
- * [1] tiles, [2] distinct out-of-tile face neighbors summed over tiles,
- * [3] largest per-tile count, [4] finer faces, [5] algorithmic HBM bytes of
- * one sweep over all local cells (own fields 64 B/cell + face rows 12 B/cell
- * + 4 B per out-of-tile neighbor + 8 B per finer face + 12 B per tile).
- * No reference counterpart (layout introspection for the roofline). */
-int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[6]);
+ * [1] tiles, [2] distinct out-of-tile face neighbors summed over the tiles,
+ * [3] largest per-tile count, [4] finer faces, [5] face-neighbor entries
+ * (get_face_neighbors_of summed over local cells), [6] algorithmic HBM bytes
+ * of one sweep over all local cells as SURVEY §8(d) fixes them (64 B per cell
+ * + 4 B per face entry + 4 B per row pointer), [7] the 64 B-per-cell core
+ * alone, [8] regular tiles (aligned uniform boxes swept without face rows),
+ * [9] cells in regular tiles.  No reference counterpart (roofline
+ * introspection). */
+int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[10]);
 
 /* ---- Poisson solver (tests/poisson/poisson_solve.hpp:156-1056) ----------
  * dccrgx_poisson_cache = Poisson_Solve::cache_system_info (827-971): local

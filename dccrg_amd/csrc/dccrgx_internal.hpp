@@ -230,6 +230,10 @@ struct Grid {
 	DBuf<int32_t> tnb;
 	size_t tcount[4] = {0, 0, 0, 0};
 	DBuf<RegTileMeta> tregmeta;  // per regular tile (list order): start slot + neighbor-box starts
+	// per irregular tile (list order), 8 x u32: first slot, slots, first ext,
+	// ext count, first finer face, finer faces; empty when some tile exceeds
+	// the pipelined kernel's capacities (> 1024 ext cells or > 512 finer faces)
+	DBuf<uint32_t> tmeta;
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;

@@ -390,6 +390,33 @@ static void ensure_tiles(Grid& g) {
 	g.total_ext = tb.total_ext;
 	k_classify_tiles(g.m, g.tstart.p, g.n_tiles_inner, g.n_tiles_outer, g.slot_ids.p, g.face_ell.p, g.tlists, g.tnb,
 	                 g.tregmeta, g.tcount, g.s_comp);
+	{
+		// records of the irregular tiles for the pipelined tile kernel
+		const size_t nt = g.n_tiles_inner + g.n_tiles_outer, ni = g.tcount[2] + g.tcount[3];
+		const auto ts = download(g.tstart.p, nt + 1, g.s_comp);
+		const auto ep = download(g.ext_ptr.p, nt + 1, g.s_comp);
+		const auto fb = download(g.fine_base.p, nt + 1, g.s_comp);
+		const auto li = download(g.tlists.p + g.tcount[0] + g.tcount[1], ni, g.s_comp);
+		std::vector<uint32_t> rec(8 * ni, 0u);
+		bool fits = true;
+		for (size_t i = 0; i < ni; i++) {
+			const uint32_t t = li[i];
+			// finer faces of tile t: up to the next tile's first one (fine_base is
+			// the exclusive scan at each tile's first slot)
+			const uint32_t fend = t + 1 < nt ? fb[t + 1] : uint32_t(g.n_fine_faces);
+			uint32_t* r = &rec[8 * i];
+			r[0] = ts[t];
+			r[1] = ts[t + 1] - ts[t];
+			r[2] = ep[t];
+			r[3] = ep[t + 1] - ep[t];
+			r[4] = fb[t];
+			r[5] = fend - fb[t];
+			if (r[3] > 1024u || r[5] > 512u || r[1] > 512u) fits = false;
+		}
+		g.tmeta.release();
+		if (fits && ni) upload(g.tmeta, rec, g.s_comp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	}
 	g.tiles_valid = true;
 }
 

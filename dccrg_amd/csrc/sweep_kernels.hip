@@ -868,6 +868,24 @@ struct AdvPtrs {
 	const double* p[7];  // rho, lx, ly, lz, vx, vy, vz
 };
 
+// The upwind flux through one face with the cell `c` on its minus side and
+// `n` on its plus side, along axis a (solve.hpp:136-225 for direction +a):
+// the reference's expression and operand order.  The minus-side cell adds
+// -G, the plus-side cell +G; evaluated from the plus side the reference
+// computes the same products in swapped (commutative) order, so one
+// evaluation per face is bitwise what each side would get.
+__device__ __forceinline__ double adv_face_g(int a, double cd, double clx, double cly, double clz, double cv_a,
+                                             const AdvNb& n, double dt) {
+#pragma clang fp contract(off)
+	double ca, cb, cc, na, nb, nc;
+	if (a == 0) { ca = clx; cb = cly; cc = clz; na = n.lx; nb = n.ly; nc = n.lz; }
+	else if (a == 1) { ca = cly; cb = clx; cc = clz; na = n.ly; nb = n.lx; nc = n.lz; }
+	else { ca = clz; cb = clx; cc = cly; na = n.lz; nb = n.lx; nc = n.ly; }
+	const double min_area = fmin(cb * cc, nb * nc);
+	const double v = (ca * n.v + na * cv_a) / (ca + na);
+	return (v >= 0 ? cd : n.d) * dt * v * min_area;
+}
+
 template <int MINW, int DIAG>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
@@ -875,6 +893,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 #pragma clang fp contract(off)
 	__shared__ double shd[7][512];  // rho, vx, vy, vz, lx, ly, lz of the tile's cells
 	__shared__ double she[1920];
+	__shared__ double shg[3][512];  // flux through each cell's +x, +y, +z face
 	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
 	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
 	uint32_t t = t0 + j;
@@ -926,32 +945,156 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		const bool more = tn < t1;
 		if (more) load(tn);  // the next tile's loads fly while this one is computed
 		const uint32_t ts = meta[tc].ts;
-		const double cd = shd[0][tid], cvx = shd[1][tid], cvy = shd[2][tid], cvz = shd[3][tid], clx = shd[4][tid],
-		             cly = shd[5][tid], clz = shd[6][tid];
+		const double cd = shd[0][tid], clx = shd[4][tid], cly = shd[5][tid], clz = shd[6][tid];
+		const double cva[3] = {shd[1][tid], shd[2][tid], shd[3][tid]};
+		// pass 1: the +x, +y, +z face of every cell, once per face; the -side
+		// faces on the tile boundary (their minus cell is outside) here too
+		double gm[3] = {0, 0, 0};  // flux through this cell's -a face when it is on the tile boundary
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			double g = 0;
+			if (l[a] < 7) {
+				uint32_t q[3] = {l[0], l[1], l[2]};
+				q[a] += 1;
+				const uint32_t li = m9(q[0], q[1], q[2]);
+				g = adv_face_g(a, cd, clx, cly, clz, cva[a],
+				               AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]}, dt);
+			} else if (meta[tc].nst[2 * a + 1] >= 0) {
+				const uint32_t k = uint32_t(2 * a + 1) * 320u + fi[a];
+				g = adv_face_g(a, cd, clx, cly, clz, cva[a],
+				               AdvNb{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]}, dt);
+			}
+			shg[a][tid] = g;
+			if (l[a] == 0 && meta[tc].nst[2 * a] >= 0) {
+				// minus cell = the ext cell n, plus cell = this one
+				const uint32_t k = uint32_t(2 * a) * 320u + fi[a];
+				const AdvNb n{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]};
+				const AdvNb self{cd, clx, cly, clz, cva[a]};
+				gm[a] = adv_face_g(a, n.d, n.lx, n.ly, n.lz, n.v, self, dt);
+			}
+		}
+		__syncthreads();
+		// pass 2: sum in the reference's face order -x, +x, -y, +y, -z, +z
 		double acc = 0;
 #pragma unroll
-		for (int d = 0; d < 6; d++) {
-			if (DIAG == 2) {
-				acc += shd[1 + (d >> 1)][tid ^ (1u << (d >> 1))];
-				continue;
-			}
-			const int a = d >> 1;
-			const bool plus = d & 1;
-			const bool inside = plus ? l[a] < 7 : l[a] > 0;
-			AdvNb n;
-			if (inside) {
+		for (int a = 0; a < 3; a++) {
+			if (l[a] > 0) {
 				uint32_t q[3] = {l[0], l[1], l[2]};
-				q[a] = plus ? q[a] + 1 : q[a] - 1;
-				const uint32_t li = m9(q[0], q[1], q[2]);
-				n = AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]};
-			} else {
-				if (meta[tc].nst[d] < 0) continue;  // no neighbor on this side
-				const uint32_t k = uint32_t(d) * 320u + fi[a];
-				n = AdvNb{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]};
+				q[a] -= 1;
+				acc += shg[a][m9(q[0], q[1], q[2])];
+			} else if (meta[tc].nst[2 * a] >= 0) {
+				acc += gm[a];
 			}
-			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, n, dt);
+			if (l[a] < 7 || meta[tc].nst[2 * a + 1] >= 0) acc += -shg[a][tid];
 		}
 		rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+		if (!more) break;
+		t = tn;
+	}
+}
+
+// Persistent, software-pipelined form of advection_tiles_kernel for any tile
+// (the tables of tile_build.hip): the same XCD-contiguous persistent schedule
+// as advection_regular_pp_kernel; per tile one 32-B record; while a tile is
+// computed from LDS, the next tile's own fields, face rows, ext cells (at
+// most two per thread) and finer-face index pairs are in flight into
+// registers, so the compute phase issues no global load.
+struct TileMeta {
+	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
+};
+
+template <int MINW>
+__global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
+    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
+    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
+#pragma clang fp contract(off)
+	constexpr uint32_t T = 512;
+	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
+	const uint32_t W = T + ecap;
+	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
+	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
+	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
+	uint32_t t = t0 + j;
+	if (t >= t1) return;  // block-uniform
+	const uint32_t tid = threadIdx.x;
+	const double* const rho = P.p[0];
+	const double* const lx = P.p[1];
+	const double* const ly = P.p[2];
+	const double* const lz = P.p[3];
+	const double* const vx = P.p[4];
+	const double* const vy = P.p[5];
+	const double* const vz = P.p[6];
+	// the register set of the tile being loaded (field order rho vx vy vz lx ly lz)
+	double c[7], xa[7], xb[7];
+	uint32_t row[3], fq[2];
+	auto load7 = [&](uint32_t slot, double (&v)[7]) {
+		const uint32_t o = slot << 3;
+		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
+		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+	};
+	auto load = [&](uint32_t tt) {
+		const uint32_t ts = meta[tt].ts, n = meta[tt].n, e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb,
+		               nf = meta[tt].nf;
+		if (tid < n) {
+			load7(ts + tid, c);
+			row[0] = tell[3 * (ts + tid)];
+			row[1] = tell[3 * (ts + tid) + 1];
+			row[2] = tell[3 * (ts + tid) + 2];
+		}
+		if (tid < ne) load7(ext[e0 + tid], xa);
+		if (tid + T < ne) load7(ext[e0 + tid + T], xb);
+		if (tid < nf) {
+			fq[0] = tfine[2 * (fb + tid)];
+			fq[1] = tfine[2 * (fb + tid) + 1];
+		}
+	};
+	load(t);
+	for (;;) {
+		const uint32_t n = meta[t].n, ne = meta[t].ne, nf = meta[t].nf, ts = meta[t].ts;
+		__syncthreads();  // the previous tile's faces have been read from LDS
+		if (tid < n)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
+		if (tid < ne)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + T + tid] = xa[k];
+		if (tid + T < ne)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + 2 * T + tid] = xb[k];
+		if (tid < nf) {
+			shf[2 * tid] = fq[0];
+			shf[2 * tid + 1] = fq[1];
+		}
+		const uint32_t r0 = row[0], r1 = row[1], r2 = row[2];
+		__syncthreads();
+		const uint32_t tn = t + B;
+		const bool more = tn < t1;
+		if (more) load(tn);  // the next tile's loads fly while this one is computed
+		if (tid < n) {
+			const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
+			             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
+			auto fetch = [&](uint32_t li, int d) -> AdvNb {
+				return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
+			};
+			const uint32_t rr[3] = {r0, r1, r2};
+			double acc = 0;
+#pragma unroll
+			for (int d = 0; d < 6; d++) {
+				const uint32_t code = (rr[d >> 1] >> (16 * (d & 1))) & 0xffffu;
+				if (code == 0xffffu) continue;
+				if (code & 0x8000u) {
+					const uint32_t fk = code & 0x7fffu;
+					const uint32_t q0 = shf[2 * fk], q1 = shf[2 * fk + 1];
+					const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
+#pragma unroll
+					for (int k = 0; k < 4; k++)
+						acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
+				} else {
+					acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
+				}
+			}
+			rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+		}
 		if (!more) break;
 		t = tn;
 	}
@@ -1185,6 +1328,22 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		HIP_CHECK(hipGetLastError());
 	}
 	if (!n_irr) {
+		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
+		return;
+	}
+	static const int tiles_pp = [] {  // DCCRGX_ADV_TPP=0: the non-persistent tile kernel
+		const char* e = getenv("DCCRGX_ADV_TPP");
+		return e ? atoi(e) : 1;
+	}();
+	if (tiles_pp && T == 512 && g.tmeta.n && diag == 0) {
+		const TileMeta* meta = reinterpret_cast<const TileMeta*>(g.tmeta.p) + (run == 0 ? 0 : g.tcount[2]);
+		const uint32_t ecap = uint32_t(g.max_ext);
+		const size_t lds = size_t(7) * (T + ecap) * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
+		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
+		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
+		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta,
+		                                                     uint32_t(n_irr), ecap, dt);
+		HIP_CHECK(hipGetLastError());
 		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
 		return;
 	}

@@ -196,6 +196,121 @@ __global__ __launch_bounds__(64 * G2_ROWS) void gol_structured_v2(const uint32_t
 	}
 }
 
+// v3 (nx a multiple of 256): a lane owns 4 consecutive x (16-B loads and
+// stores), a wave one 256-x segment of one y row, a block G3_ROWS
+// consecutive rows of the same segment; each wave marches a chunk of zc
+// planes with the raw loads of the next DEPTH planes in flight while the
+// current one is summed (8 B per cell-update, the y+-1 rows
+// and the segment-edge columns are re-reads served by L2).  Blocks are
+// dealt to XCDs in contiguous runs of the (x segment, y, z chunk) order, so
+// the rows shared by vertically adjacent blocks stay in one XCD's L2.
+constexpr int G3_ROWS = 4;
+
+struct G3Plane {
+	uint4 m, c, p;  // rows y-1, y, y+1 at this lane's 4 x
+	uint32_t e[3];  // lane 0: column x0-1, lane 63: column x0+256 (rows y-1, y, y+1)
+};
+
+template <int DEPTH>
+__global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t* __restrict__ st,
+                                                                 uint32_t* __restrict__ out, int nx, int ny, int nz,
+                                                                 int px, int py, int pz, int zc, unsigned nbx,
+                                                                 unsigned nby, unsigned nb) {
+	const unsigned per_xcd = gridDim.x >> 3;
+	const unsigned L = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+	if (L >= nb) return;  // block-uniform
+	const unsigned bx = L % nbx, r = L / nbx, by = r % nby, bz = r / nby;
+	const int lane = threadIdx.x & 63;
+	const int y = int(by) * G3_ROWS + (threadIdx.x >> 6);
+	if (y >= ny) return;  // wave-uniform
+	const int x0 = int(bx) * 256;
+	const int x = x0 + 4 * lane;
+	int ym = y - 1, yp = y + 1;
+	bool ymin = true, ypin = true;
+	if (ym < 0) {
+		if (py) ym += ny;
+		else ymin = false;
+	}
+	if (yp >= ny) {
+		if (py) yp -= ny;
+		else ypin = false;
+	}
+	// the edge column of lane 0 (left) / lane 63 (right), -1 when outside
+	int xe = -1;
+	if (lane == 0) xe = x0 > 0 ? x0 - 1 : (px ? nx - 1 : -1);
+	if (lane == 63) xe = x0 + 256 < nx ? x0 + 256 : (px ? 0 : -1);
+	const size_t plane = size_t(nx) * ny;
+	const size_t om = size_t(ym) * nx, oc = size_t(y) * nx, op = size_t(yp) * nx;
+	auto load = [&](int z, G3Plane& P) {
+		P.m = P.c = P.p = make_uint4(0, 0, 0, 0);
+		P.e[0] = P.e[1] = P.e[2] = 0;
+		if (z < 0 || z >= nz) {
+			if (!pz) return;
+			z = z < 0 ? z + nz : z - nz;
+		}
+		const uint32_t* p = st + size_t(z) * plane;
+		P.c = *reinterpret_cast<const uint4*>(p + oc + x);
+		if (ymin) P.m = *reinterpret_cast<const uint4*>(p + om + x);
+		if (ypin) P.p = *reinterpret_cast<const uint4*>(p + op + x);
+		if (xe >= 0) {
+			P.e[1] = p[oc + xe];
+			if (ymin) P.e[0] = p[om + xe];
+			if (ypin) P.e[2] = p[op + xe];
+		}
+	};
+	// the in-plane 3x3 sums at this lane's 4 x
+	auto psum = [&](const G3Plane& P, uint32_t s[4]) {
+		const uint32_t c0 = (P.m.x > 0) + (P.c.x > 0) + (P.p.x > 0), c1 = (P.m.y > 0) + (P.c.y > 0) + (P.p.y > 0),
+		               c2 = (P.m.z > 0) + (P.c.z > 0) + (P.p.z > 0), c3 = (P.m.w > 0) + (P.c.w > 0) + (P.p.w > 0);
+		const uint32_t ce = (P.e[0] > 0) + (P.e[1] > 0) + (P.e[2] > 0);
+		uint32_t l = __shfl_up(c3, 1, 64), rr = __shfl_down(c0, 1, 64);
+		if (lane == 0) l = ce;
+		if (lane == 63) rr = ce;
+		s[0] = l + c0 + c1;
+		s[1] = c0 + c1 + c2;
+		s[2] = c1 + c2 + c3;
+		s[3] = c2 + c3 + rr;
+	};
+	const int z0 = int(bz) * zc;
+	const int z1 = min(z0 + zc, nz);
+	// Q[i] holds the raw loads of plane z + 1 + i (DEPTH planes in flight)
+	G3Plane A, B, Q[DEPTH];
+	load(z0 - 1, A);
+	load(z0, B);
+#pragma unroll
+	for (int i = 0; i < DEPTH; i++)
+		if (z0 + 1 + i <= z1) load(z0 + 1 + i, Q[i]);
+	uint32_t sp[4], sc[4], sn[4];
+	psum(A, sp);
+	psum(B, sc);
+	uint4 cur = B.c;
+	for (int z = z0; z < z1; z++) {
+		G3Plane E = Q[DEPTH - 1];
+		if (z + 1 + DEPTH <= z1) load(z + 1 + DEPTH, E);
+		psum(Q[0], sn);
+		uint4 o;
+		uint32_t cnt;
+		cnt = sp[0] + sc[0] + sn[0] - (cur.x > 0);
+		o.x = cnt == 3 ? 1u : (cnt == 2 ? cur.x : 0u);
+		cnt = sp[1] + sc[1] + sn[1] - (cur.y > 0);
+		o.y = cnt == 3 ? 1u : (cnt == 2 ? cur.y : 0u);
+		cnt = sp[2] + sc[2] + sn[2] - (cur.z > 0);
+		o.z = cnt == 3 ? 1u : (cnt == 2 ? cur.z : 0u);
+		cnt = sp[3] + sc[3] + sn[3] - (cur.w > 0);
+		o.w = cnt == 3 ? 1u : (cnt == 2 ? cur.w : 0u);
+		*reinterpret_cast<uint4*>(out + size_t(z) * plane + oc + x) = o;
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			sp[i] = sc[i];
+			sc[i] = sn[i];
+		}
+		cur = Q[0].c;
+#pragma unroll
+		for (int i = 0; i + 1 < DEPTH; i++) Q[i] = Q[i + 1];
+		Q[DEPTH - 1] = E;
+	}
+}
+
 // ---------------------------------------------------------------------------
 // Advection (tests/advection/solve.hpp:44-279), fp64, fused flux + apply.
 // Face entry = neighbor slot * 8 + dir (0..5 = -x,+x,-y,+y,-z,+z).  The flux
@@ -886,14 +1001,19 @@ __device__ __forceinline__ double adv_face_g(int a, double cd, double clx, doubl
 	return (v >= 0 ? cd : n.d) * dt * v * min_area;
 }
 
-template <int MINW, int DIAG>
+template <int MINW>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
                                                                          uint32_t ntiles, double dt) {
 #pragma clang fp contract(off)
-	__shared__ double shd[7][512];  // rho, vx, vy, vz, lx, ly, lz of the tile's cells
-	__shared__ double she[1920];
+	// rows rho, vx, vy, vz, lx, ly, lz; columns 0..511 the tile's own cells,
+	// 512 + 64 d + (face cell) the out-of-tile neighbor across side d (only
+	// rows rho, lx, ly, lz and the velocity along d's axis are filled), so
+	// every face reads its neighbor through one LDS index, whichever side
+	constexpr uint32_t W = 512 + 6 * 64;
+	__shared__ double shd[7][W];
 	__shared__ double shg[3][512];  // flux through each cell's +x, +y, +z face
+	__shared__ double shm[3][64];   // flux through the tile's -x, -y, -z boundary faces
 	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
 	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
 	uint32_t t = t0 + j;
@@ -905,6 +1025,18 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
 	// index of this cell within a side of each axis (the two other coordinates)
 	const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
+	// LDS column of the +a neighbor of this cell (inside the tile or across side 2a+1)
+	uint32_t lp[3];
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		uint32_t q[3] = {l[0], l[1], l[2]};
+		q[a] += 1;
+		lp[a] = l[a] < 7 ? m9(q[0], q[1], q[2]) : 512u + 64u * uint32_t(2 * a + 1) + fi[a];
+	}
+	// boundary-face duty of waves 0..2: wave a evaluates the -a side face of
+	// the cell at l[a] = 0 whose face index is the lane
+	const uint32_t bu = lane & 7u, bv = lane >> 3;
+	const uint32_t bcell = w == 0 ? m9(0, bu, bv) : (w == 1 ? m9(bu, 0, bv) : m9(bu, bv, 0));
 	const double* __restrict__ rho = P.p[0];
 	const double* __restrict__ lx = P.p[1];
 	const double* __restrict__ ly = P.p[2];
@@ -912,6 +1044,8 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	const double* __restrict__ vx = P.p[4];
 	const double* __restrict__ vy = P.p[5];
 	const double* __restrict__ vz = P.p[6];
+	// LDS row of value `val` (0 rho, 1 lx, 2 ly, 3 lz, 4 velocity along a)
+	auto vrow = [](uint32_t val, uint32_t a) -> uint32_t { return val == 0 ? 0u : (val == 4 ? 1u + a : val + 3u); };
 	// one register set: the tile being loaded
 	double c[7], e[4];
 	auto load = [&](uint32_t tt) {
@@ -926,7 +1060,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			if (row >= 30u) continue;
 			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
 			const int32_t st = meta[tt].nst[d];
-			if (st < 0 || DIAG == 1) continue;
+			if (st < 0) continue;
 			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
 			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
 			e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
@@ -938,8 +1072,13 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 #pragma unroll
 		for (int k = 0; k < 7; k++) shd[k][tid] = c[k];
 #pragma unroll
-		for (int i = 0; i < 4; i++)
-			if (w + 8u * i < 30u) she[(w + 8u * i) * 64u + lane] = e[i];
+		for (int i = 0; i < 4; i++) {
+			const uint32_t row = w + 8u * uint32_t(i);
+			if (row < 30u) {
+				const uint32_t d = row / 5u, val = row - 5u * d;
+				shd[vrow(val, d >> 1)][512u + 64u * d + lane] = e[i];
+			}
+		}
 		__syncthreads();
 		const uint32_t tc = t, tn = t + B;
 		const bool more = tn < t1;
@@ -947,45 +1086,40 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		const uint32_t ts = meta[tc].ts;
 		const double cd = shd[0][tid], clx = shd[4][tid], cly = shd[5][tid], clz = shd[6][tid];
 		const double cva[3] = {shd[1][tid], shd[2][tid], shd[3][tid]};
-		// pass 1: the +x, +y, +z face of every cell, once per face; the -side
-		// faces on the tile boundary (their minus cell is outside) here too
-		double gm[3] = {0, 0, 0};  // flux through this cell's -a face when it is on the tile boundary
+		// pass 1: the +x, +y, +z face of every cell, once per face, branch-free
+		// (a missing face beyond a non-periodic boundary evaluates zeros and
+		// is masked by a select)
 #pragma unroll
 		for (int a = 0; a < 3; a++) {
-			double g = 0;
-			if (l[a] < 7) {
-				uint32_t q[3] = {l[0], l[1], l[2]};
-				q[a] += 1;
-				const uint32_t li = m9(q[0], q[1], q[2]);
-				g = adv_face_g(a, cd, clx, cly, clz, cva[a],
-				               AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]}, dt);
-			} else if (meta[tc].nst[2 * a + 1] >= 0) {
-				const uint32_t k = uint32_t(2 * a + 1) * 320u + fi[a];
-				g = adv_face_g(a, cd, clx, cly, clz, cva[a],
-				               AdvNb{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]}, dt);
-			}
-			shg[a][tid] = g;
-			if (l[a] == 0 && meta[tc].nst[2 * a] >= 0) {
-				// minus cell = the ext cell n, plus cell = this one
-				const uint32_t k = uint32_t(2 * a) * 320u + fi[a];
-				const AdvNb n{she[k], she[k + 64], she[k + 128], she[k + 192], she[k + 256]};
-				const AdvNb self{cd, clx, cly, clz, cva[a]};
-				gm[a] = adv_face_g(a, n.d, n.lx, n.ly, n.lz, n.v, self, dt);
-			}
+			const uint32_t li = lp[a];
+			const double g = adv_face_g(a, cd, clx, cly, clz, cva[a],
+			                            AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]}, dt);
+			const bool has = l[a] < 7 || meta[tc].nst[2 * a + 1] >= 0;
+			shg[a][tid] = has ? g : 0.0;
+		}
+		// the tile's -a boundary faces (minus cell outside): 192 faces on
+		// waves 0..2, wave-uniform
+		if (w < 3 && meta[tc].nst[2 * w] >= 0) {
+			const uint32_t k = 512u + 64u * (2u * w) + lane;
+			const AdvNb self{shd[0][bcell], shd[4][bcell], shd[5][bcell], shd[6][bcell], shd[1 + w][bcell]};
+			double gmv;
+			if (w == 0) gmv = adv_face_g(0, shd[0][k], shd[4][k], shd[5][k], shd[6][k], shd[1][k], self, dt);
+			else if (w == 1) gmv = adv_face_g(1, shd[0][k], shd[4][k], shd[5][k], shd[6][k], shd[2][k], self, dt);
+			else gmv = adv_face_g(2, shd[0][k], shd[4][k], shd[5][k], shd[6][k], shd[3][k], self, dt);
+			shm[w][lane] = gmv;
 		}
 		__syncthreads();
 		// pass 2: sum in the reference's face order -x, +x, -y, +y, -z, +z
 		double acc = 0;
 #pragma unroll
 		for (int a = 0; a < 3; a++) {
-			if (l[a] > 0) {
-				uint32_t q[3] = {l[0], l[1], l[2]};
-				q[a] -= 1;
-				acc += shg[a][m9(q[0], q[1], q[2])];
-			} else if (meta[tc].nst[2 * a] >= 0) {
-				acc += gm[a];
-			}
-			if (l[a] < 7 || meta[tc].nst[2 * a + 1] >= 0) acc += -shg[a][tid];
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] -= 1;
+			double gm = 0;
+			if (l[a] > 0) gm = shg[a][m9(q[0] & 7u, q[1] & 7u, q[2] & 7u)];
+			else if (meta[tc].nst[2 * a] >= 0) gm = shm[a][fi[a]];
+			acc += gm;
+			acc += -shg[a][tid];
 		}
 		rho_out[ts + tid] = cd + acc / (clx * cly * clz);
 		if (!more) break;
@@ -1182,9 +1316,34 @@ void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, con
 void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s) {
 	static const int variant = [] {
 		const char* e = getenv("DCCRGX_GOL_VARIANT");
-		return e ? atoi(e) : 2;
+		return e ? atoi(e) : 3;
 	}();
-	if (variant == 2) {
+	static const int zc3 = [] {  // DCCRGX_GOL_ZC: planes per z chunk of the v3 kernel
+		const char* e = getenv("DCCRGX_GOL_ZC");
+		return e ? atoi(e) : 64;
+	}();
+	static const int depth3 = [] {  // DCCRGX_GOL_DEPTH: planes of loads in flight per wave (v3)
+		const char* e = getenv("DCCRGX_GOL_DEPTH");
+		return e ? atoi(e) : 3;
+	}();
+	if (variant == 3 && n[0] % 256 == 0 && n[0] * n[1] * n[2] < (uint64_t(1) << 32)) {
+		const int zc = int(std::min<uint64_t>(n[2], uint64_t(zc3 > 0 ? zc3 : 32)));
+		const unsigned nbx = unsigned(n[0] / 256), nby = unsigned((n[1] + G3_ROWS - 1) / G3_ROWS),
+		               nbz = unsigned((n[2] + zc - 1) / zc);
+		const size_t nb = size_t(nbx) * nby * nbz;
+		const unsigned grid = unsigned((nb + 7) / 8 * 8);
+#define DX_GOL3(D)                                                                                                   \
+	gol_structured_v3<D><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1], \
+	                                                   per[2], zc, nbx, nby, unsigned(nb))
+		if (depth3 <= 2) DX_GOL3(2);
+		else if (depth3 == 3) DX_GOL3(3);
+		else if (depth3 == 4) DX_GOL3(4);
+		else DX_GOL3(6);
+#undef DX_GOL3
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
+	if (variant >= 2) {
 		const int zc = int(n[2] <= 64 ? n[2] : 64);
 		dim3 g2(unsigned((n[0] + G2_OUT - 1) / G2_OUT), unsigned((n[1] + G2_ROWS - 1) / G2_ROWS),
 		        unsigned((n[2] + zc - 1) / zc));
@@ -1309,14 +1468,7 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * size_t(pp_blocks), (n_reg + 7) / 8 * 8));
 		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		if (pp_blocks >= 3)
-			advection_regular_pp_kernel<6, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else if (diag == 6)
-			advection_regular_pp_kernel<4, 1><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else if (diag == 7)
-			advection_regular_pp_kernel<4, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else
-			advection_regular_pp_kernel<4, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
 		HIP_CHECK(hipGetLastError());
 	} else if (n_reg) {
 		if (diag == 5)

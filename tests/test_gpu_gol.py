@@ -37,7 +37,10 @@ def _run(g, o, steps):
 
 @pytest.mark.parametrize("length,periodic", [((16, 12, 10), (False, False, False)), ((16, 12, 10), (True, True, True)),
                                              ((70, 9, 33), (True, False, True)), ((1, 1, 1), (True, True, True)),
-                                             ((2, 3, 1), (True, True, False)), ((64, 8, 40), (False, True, False))])
+                                             ((2, 3, 1), (True, True, False)), ((64, 8, 40), (False, True, False)),
+                                             # 256-multiples of x: the 16-B-per-lane kernel
+                                             ((256, 8, 12), (False, False, False)), ((256, 6, 9), (True, True, True)),
+                                             ((512, 5, 40), (True, False, False)), ((256, 1, 1), (True, True, True))])
 def test_structured_matches_oracle(gpu, length, periodic):
     g, o = make_pair(length, 0, periodic, 1)
     got, exp = _run(g, o, 6)

@@ -263,7 +263,23 @@ def main():
     el = time.perf_counter() - t0
     kern_ms, kern_n = g.kernel_timing(0)
 
-    stats = torch.tensor([el, float(n_local), float(c["recv"]), kern_ms], dtype=torch.float64, device="cuda")
+    # halo break-out (N > 1): the same exchange alone, K times back to back
+    # (pack + grouped RCCL send/recv of the density into the halo slots)
+    halo_el = 0.0
+    if world > 1:
+        g.synchronize()
+        dist.barrier()
+        th = time.perf_counter()
+        for _ in range(a.steps):
+            g.update_copies_of_remote_neighbors()
+        g.synchronize()
+        dist.barrier()
+        halo_el = time.perf_counter() - th
+    n_send = g.get_number_of_update_send_cells()
+    n_peers = len(g.get_peers())
+
+    stats = torch.tensor([el, float(n_local), float(c["recv"]), kern_ms, halo_el, float(n_send)],
+                         dtype=torch.float64, device="cuda")
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -283,16 +299,17 @@ def main():
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
     launches_per_step = kern_n / a.steps if a.steps else 0
 
-    # HBM bytes per launch of the sweep kernel from the committed PMC passes
-    # (FETCH_SIZE x measured read correction + WRITE_SIZE, scripts/traffic.py);
-    # only valid for the same mesh, so it is dropped for any other cell count
+    # HBM bytes per step of the sweep kernels from the committed PMC passes
+    # (FETCH_SIZE x 2 + WRITE_SIZE, summed over the regular-tile and the
+    # general tile kernel, scripts/traffic.py); only valid for the same mesh,
+    # so it is dropped for any other cell count
     traffic = None
     tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
     if os.path.exists(tf):
         try:
             t = json.load(open(tf))
-            if t.get("cells") == n_local and world == 1:
-                traffic = t.get("hbm_bytes_per_dispatch")
+            if t.get("cells") == n_local and t.get("alg_bytes_per_step") == alg_bytes_step and world == 1:
+                traffic = t.get("hbm_bytes_per_step")
         except (OSError, ValueError):
             traffic = None
 
@@ -346,6 +363,21 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if world > 1:
+            # rank with the most halo traffic; xGMI: one link per peer pair,
+            # ~153 GB/s per link and direction (BASELINE north star)
+            halo_ms = float(mx[4]) / a.steps * 1e3
+            send_bytes = float(mx[5]) * 8.0
+            per_link = send_bytes / max(n_peers, 1) / (halo_ms / 1e3) / 1e9 if halo_ms > 0 else None
+            line["halo"] = {
+                "ms_per_exchange": halo_ms,
+                "frac_of_step": halo_ms / line["ms_per_step"] if line["ms_per_step"] else None,
+                "payload_bytes_per_cell": 8,
+                "send_bytes_max_rank": send_bytes,
+                "peers_rank0": n_peers,
+                "xgmi": {"achieved": per_link, "peak": 153.0, "unit": "GB/s per link per direction",
+                         "frac": per_link / 153.0 if per_link else None},
+            }
         print(json.dumps(line), flush=True)
     g.close()
     if world > 1:

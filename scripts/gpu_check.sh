@@ -25,22 +25,14 @@ rc=$?
 echo "[gpu_check] rocprof rc=$rc"
 find gpurun_out/prof_${TAG} -name '*stats*' | head
 [ $rc -eq 0 ] || exit $rc
-# HBM traffic of the sweep: FETCH_SIZE and WRITE_SIZE in separate --pmc runs
+# HBM traffic of the sweep (both advection kernels): FETCH_SIZE and
+# WRITE_SIZE in separate --pmc runs
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex advection_tiles -d gpurun_out/pmc_${TAG}_$c -o run \
-      --output-format csv -- python -u bench.py --steps 10 --warmup 1 --no-cpu-baseline > /dev/null 2> gpurun_out/pmc_${TAG}_$c.err
+  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex 'advection_(regular|tiles)' -d gpurun_out/pmc_${TAG}_$c -o run \
+      --output-format csv -- python -u bench.py --steps 10 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_${TAG}_$c.json 2> gpurun_out/pmc_${TAG}_$c.err
   rc=$?
   echo "[gpu_check] pmc $c rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-# calibration of FETCH_SIZE for this kernel's 8-B-per-lane loads: the
-# stream-only diagnostic form of the sweep reads exactly 56 B per cell
-DCCRGX_ADV_DIAG=3 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex advection_tiles \
-    -d gpurun_out/pmc_${TAG}_CALIB -o run --output-format csv -- \
-    python -u bench.py --steps 10 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_${TAG}_CALIB.json 2> gpurun_out/pmc_${TAG}_CALIB.err
-rc=$?
-echo "[gpu_check] pmc calibration rc=$rc"
-[ $rc -eq 0 ] || exit $rc
-python scripts/traffic.py advection_tiles gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE \
-    --calib-dir gpurun_out/pmc_${TAG}_CALIB --calib-json gpurun_out/pmc_${TAG}_CALIB.json \
-    > gpurun_out/traffic_${TAG}.json && cat gpurun_out/traffic_${TAG}.json
+python scripts/traffic.py 'advection_(regular|tiles)' gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE \
+    --bench-json gpurun_out/pmc_${TAG}_FETCH_SIZE.json > gpurun_out/traffic_${TAG}.json && cat gpurun_out/traffic_${TAG}.json

@@ -75,6 +75,7 @@ _SIGS = {
     "dccrgx_wait_remote_neighbor_copy_updates": (C.c_int, [vp]),
     "dccrgx_gol_step": (C.c_int, [vp, C.c_int, C.c_int]),
     "dccrgx_gol_commit": (C.c_int, [vp, C.c_int]),
+    "dccrgx_gol_amr": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int]),
     "dccrgx_advection_step": (C.c_int, [vp, P(C.c_int), C.c_double, C.c_int]),
     "dccrgx_advection_commit": (C.c_int, [vp, C.c_int]),
     "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),

@@ -332,6 +332,11 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face
 void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 
+// --- launchers implemented in gol_amr.hip ----------------------------------
+void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, uint32_t* state, uint64_t* lst,
+               const uint32_t* ptr, const uint64_t* nid, const int32_t* nslot, size_t s0, size_t s1, int* err,
+               hipStream_t s);
+
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots
 void k_po_cache(const MapCtx& m, const double l0[3], const uint64_t* slot_ids, const int32_t* cls,

@@ -1542,6 +1542,37 @@ int dccrgx_gol_commit(dccrgx_grid* gp, int sf) {
 	});
 }
 
+// get_live_neighbors of tests/game_of_life/solve.hpp:37-170, split at its
+// halo: phase 0 = the collect loop (46-110), phase 1 = spread + rule
+// (113-167); see gol_amr.hip
+int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(phase == 0 || phase == 1, "phase must be 0 (collect) or 1 (spread)");
+		Field& st = field(g, sf);
+		Field& ls = field(g, lf);
+		DX_REQUIRE(st.elem == 4, "game of life state must be a 4-byte field");
+		DX_REQUIRE(ls.elem == 64, "live level-0 neighbor list must be a 64-byte field (8 x uint64)");
+		size_t s0, s1;
+		region_range(g, region, s0, s1);
+		if (s1 <= s0) return 0;
+		ensure_csr(g);
+		DBuf<int> err;
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		k_time_begin(g);
+		k_gol_amr(phase, g.m, g.slot_ids.p, (uint32_t*)st.data.p, (uint64_t*)ls.data.p, g.nof_ptr.p, g.nof_id.p,
+		          g.nof_slot.p, s0, s1, err.p, g.s_comp);
+		k_time_end(g);
+		int h = 0;
+		HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+		DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+		return 0;
+	});
+}
+
 static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
 	for (int k = 0; k < 7; k++) {
 		Field& F = field(g, fids[k]);

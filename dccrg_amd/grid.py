@@ -42,8 +42,9 @@ class Field:
         return out
 
     def set(self, values, slot0=0):
-        a = np.ascontiguousarray(values, dtype=self.dtype)
-        check(lib().dccrgx_field_upload(self.grid.h, self.id, slot0, a.size, _ptr(a)))
+        # subarray dtypes (e.g. (uint64, 8)) take values of shape (n, 8)
+        a = np.ascontiguousarray(values, dtype=self.dtype.base)
+        check(lib().dccrgx_field_upload(self.grid.h, self.id, slot0, a.nbytes // self.dtype.itemsize, _ptr(a)))
 
     def set_transfer(self, transfer: bool):
         self.transfer = bool(transfer)
@@ -367,6 +368,22 @@ class Dccrg:
 
     def gol_commit(self, state: Field):
         check(lib().dccrgx_gol_commit(self.h, state.id))
+
+    def gol_amr_collect(self, state: Field, lst: Field, region="all"):
+        """First loop of get_live_neighbors (tests/game_of_life/solve.hpp:46-110)."""
+        check(lib().dccrgx_gol_amr(self.h, 0, state.id, lst.id, REGION[region]))
+
+    def gol_amr_spread(self, state: Field, lst: Field, region="all"):
+        """Spread among siblings + rule (tests/game_of_life/solve.hpp:113-167)."""
+        check(lib().dccrgx_gol_amr(self.h, 1, state.id, lst.id, REGION[region]))
+
+    def get_live_neighbors(self, state: Field, lst: Field):
+        """One turn of the refined game emulating the unrefined one, as
+        tests/game_of_life/solve.hpp:37-170 (collect, halo of both fields,
+        spread + rule).  `lst` is a 64-byte field (8 x uint64)."""
+        self.gol_amr_collect(state, lst)
+        self.update_copies_of_remote_neighbors()
+        self.gol_amr_spread(state, lst)
 
     @staticmethod
     def _fids(fields):

@@ -162,6 +162,18 @@ int dccrgx_wait_remote_neighbor_copy_updates(dccrgx_grid* g);
  * device pointer is swapped when dccrgx_gol_commit is called. */
 int dccrgx_gol_step(dccrgx_grid* g, int state_field, int region);
 int dccrgx_gol_commit(dccrgx_grid* g, int state_field);
+
+/* Game of life on a refined grid emulating the unrefined game:
+ * get_live_neighbors, tests/game_of_life/solve.hpp:37-170, split at its halo.
+ * phase 0 (collect, 46-110): list_field[cell] = the distinct level-0 parents
+ * of live neighbors (neighbors_of order, own parent skipped), error_cell (0)
+ * padded; phase 1 (spread + rule, 113-167): merge the lists of same-parent
+ * neighbors, count, update state in place.  Between the phases the caller
+ * runs update_copies_of_remote_neighbors (both fields transferred).
+ * list_field: 64-byte elements (8 x uint64 = Cell_Data::data[1..8]).
+ * DCCRGX_EINVAL where the reference aborts (list overflow, siblings
+ * disagreeing on their state). */
+int dccrgx_gol_amr(dccrgx_grid* g, int phase, int state_field, int list_field, int region);
 /* first-order upwind advection over face neighbors, flux + apply fused
  * (tests/advection/solve.hpp:44-279).  fields: density, vx, vy, vz, lx, ly, lz
  * (all fp64).  Writes the new density into a scratch buffer; commit swaps. */

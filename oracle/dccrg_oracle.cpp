@@ -652,6 +652,86 @@ static void gol_step(const Grid& g, std::unordered_map<uint64_t, uint32_t>& aliv
 }
 
 /* ---------------------------------------------------------------------------
+ * Game of life on a refined grid emulating the unrefined game —
+ * tests/game_of_life/solve.hpp:37-170 (get_live_neighbors), literally: the
+ * collect loop (46-110), the halo (111; one process here), the in-place
+ * spread among same-parent neighbors (113-150), the rule (152-167).  data[0]
+ * is the state, data[1..8] the list of live level-0 neighbor parents.  The
+ * reference loops in get_cells() (hash) order; ascending order here.
+ * Aborts become exceptions with the reference's messages.
+ * ------------------------------------------------------------------------- */
+using GolAmrData = std::array<uint64_t, 9>;
+
+static uint64_t level0_parent(const Mapping& m, uint64_t cell) {  // dccrg_mapping.hpp:479-493
+	const int lvl = m.level(cell);
+	if (lvl < 0 || lvl > m.R) return error_cell;
+	if (lvl == 0) return cell;
+	return m.from_indices(m.indices(cell), 0);
+}
+
+static void gol_amr_step(const Grid& g, std::unordered_map<uint64_t, GolAmrData>& data) {
+	std::vector<uint64_t> cells;
+	for (const auto& cp : g.cell_process) cells.push_back(cp.first);
+	std::sort(cells.begin(), cells.end());
+	for (const uint64_t cell : cells) {
+		GolAmrData& cd = data.at(cell);
+		for (size_t i = 1; i < cd.size(); i++) cd[i] = 0;
+		const uint64_t cp = level0_parent(g.m, cell);
+		for (const auto& ni : g.nof.at(cell)) {
+			const uint64_t nb = ni.first;
+			if (nb == error_cell) continue;
+			const uint64_t np = level0_parent(g.m, nb);
+			if (np == cp) continue;
+			const GolAmrData& nd = data.at(nb);
+			if (nd[0] == 0) {
+				for (size_t i = 1; i < cd.size(); i++)
+					if (cd[i] == np) throw std::runtime_error("Neighbor should not be alive.");
+			} else {
+				for (size_t i = 1; i < cd.size(); i++) {
+					if (cd[i] == np) break;
+					else if (cd[i] == error_cell) {
+						cd[i] = np;
+						break;
+					} else if (i == cd.size() - 1)
+						throw std::runtime_error("No more room in live neighbor list.");
+				}
+			}
+		}
+	}
+	for (const uint64_t cell : cells) {
+		const uint64_t cp = level0_parent(g.m, cell);
+		GolAmrData& cd = data.at(cell);
+		for (const auto& ni : g.nof.at(cell)) {
+			const uint64_t nb = ni.first;
+			if (nb == error_cell) continue;
+			if (cp != level0_parent(g.m, nb)) continue;
+			const GolAmrData& nd = data.at(nb);
+			for (size_t i = 1; i < nd.size(); i++) {
+				if (nd[i] == error_cell) break;
+				for (size_t j = 1; j < cd.size(); j++) {
+					if (cd[j] == error_cell) {
+						cd[j] = nd[i];
+						break;
+					} else if (cd[j] == nd[i]) break;
+					else if (j == cd.size() - 1)
+						throw std::runtime_error("No room in live neighbor list of cell");
+				}
+			}
+		}
+	}
+	for (const uint64_t cell : cells) {
+		GolAmrData& cd = data.at(cell);
+		size_t live = 0;
+		for (size_t i = 1; i < cd.size(); i++) {
+			if (cd[i] != error_cell) live++;
+			cd[i] = error_cell;
+		}
+		if (live == 3) cd[0] = 1;
+		else if (live != 2) cd[0] = 0;
+	}
+}
+
+/* ---------------------------------------------------------------------------
  * Advection — tests/advection/{initialize.hpp:36-82, solve.hpp:44-346}
  * ------------------------------------------------------------------------- */
 struct AdvCell {
@@ -1041,6 +1121,7 @@ struct OracleHandle {
 	Grid g;
 	std::unordered_map<uint64_t, AdvCell> adv;
 	std::unordered_map<uint64_t, uint32_t> gol;
+	std::unordered_map<uint64_t, GolAmrData> gola;
 	PoissonSolver po;
 	std::string err;
 };
@@ -1273,6 +1354,31 @@ int or_gol_get(void* hp, const uint64_t* ids, uint32_t* alive, size_t n) {
 	OR_TRY({
 		auto* h = static_cast<OracleHandle*>(hp);
 		for (size_t i = 0; i < n; i++) alive[i] = h->gol.at(ids[i]);
+		return 0;
+	})
+}
+
+/* ---- game of life, refined (solve.hpp) ---- */
+int or_gola_set(void* hp, const uint64_t* ids, const uint32_t* alive, size_t n) {
+	auto* h = static_cast<OracleHandle*>(hp);
+	h->gola.clear();
+	for (const auto& cp : h->g.cell_process) h->gola[cp.first] = GolAmrData{};
+	for (size_t i = 0; i < n; i++) h->gola[ids[i]][0] = alive[i];
+	return 0;
+}
+
+int or_gola_steps(void* hp, int steps) {
+	OR_TRY({
+		auto* h = static_cast<OracleHandle*>(hp);
+		for (int s = 0; s < steps; s++) gol_amr_step(h->g, h->gola);
+		return 0;
+	})
+}
+
+int or_gola_get(void* hp, const uint64_t* ids, uint32_t* alive, size_t n) {
+	OR_TRY({
+		auto* h = static_cast<OracleHandle*>(hp);
+		for (size_t i = 0; i < n; i++) alive[i] = uint32_t(h->gola.at(ids[i])[0]);
 		return 0;
 	})
 }

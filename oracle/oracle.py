@@ -65,6 +65,9 @@ def lib():
     L.or_gol_set.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
     L.or_gol_steps.argtypes = [C.c_void_p, C.c_int]
     L.or_gol_get.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
+    L.or_gola_set.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
+    L.or_gola_steps.argtypes = [C.c_void_p, C.c_int]
+    L.or_gola_get.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
     L.or_set_geometry.argtypes = [C.c_void_p, f64p, f64p]
     L.or_geometry_batch.argtypes = [C.c_void_p, u64p, C.c_size_t, f64p, f64p]
     L.or_adv_initialize.argtypes = [C.c_void_p]
@@ -239,6 +242,21 @@ class Grid:
         ids = np.ascontiguousarray(ids, np.uint64)
         out = np.empty(ids.size, np.uint32)
         self._chk(lib().or_gol_get(self.h, ids, out, ids.size))
+        return out
+
+    # -- game of life on a refined grid (tests/game_of_life/solve.hpp) ----------
+    def gola_set(self, ids, alive):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        alive = np.ascontiguousarray(alive, np.uint32)
+        lib().or_gola_set(self.h, ids, alive, ids.size)
+
+    def gola_steps(self, steps):
+        self._chk(lib().or_gola_steps(self.h, int(steps)))
+
+    def gola_get(self, ids):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        out = np.empty(ids.size, np.uint32)
+        self._chk(lib().or_gola_get(self.h, ids, out, ids.size))
         return out
 
     # -- advection ---------------------------------------------------------

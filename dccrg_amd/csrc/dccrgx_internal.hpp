@@ -234,6 +234,10 @@ struct Grid {
 	// ext count, first finer face, finer faces; empty when some tile exceeds
 	// the pipelined kernel's capacities (> 1024 ext cells or > 512 finer faces)
 	DBuf<uint32_t> tmeta;
+	// per tile (all tiles, slot order), 16 u32: ts, n, e0, ne, fb, nf,
+	// nst[6] (regular: neighbor-box starts), kind (1 regular), pad; for the
+	// fused sweep over both kinds (empty when a tile exceeds its limits)
+	DBuf<uint32_t> tfmeta;
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;

@@ -415,6 +415,29 @@ static void ensure_tiles(Grid& g) {
 		}
 		g.tmeta.release();
 		if (fits && ni) upload(g.tmeta, rec, g.s_comp);
+		// records of every tile, slot order, for the fused sweep
+		const size_t nr = g.tcount[0] + g.tcount[1];
+		const auto lr = download(g.tlists.p, nr, g.s_comp);
+		const auto nb = download(g.tnb.p, 6 * nt, g.s_comp);
+		std::vector<uint8_t> is_reg(nt, 0);
+		for (uint32_t t : lr) is_reg[t] = 1;
+		std::vector<uint32_t> fr(16 * nt, 0u);
+		bool ffits = true;
+		for (size_t t = 0; t < nt; t++) {
+			uint32_t* r = &fr[16 * t];
+			const uint32_t fend = t + 1 < nt ? fb[t + 1] : uint32_t(g.n_fine_faces);
+			r[0] = ts[t];
+			r[1] = ts[t + 1] - ts[t];
+			r[2] = ep[t];
+			r[3] = ep[t + 1] - ep[t];
+			r[4] = fb[t];
+			r[5] = fend - fb[t];
+			for (int d = 0; d < 6; d++) r[6 + d] = is_reg[t] ? uint32_t(nb[6 * t + size_t(d)]) : 0xffffffffu;
+			r[12] = is_reg[t];
+			if (!is_reg[t] && (r[3] > 1024u || r[5] > 512u || r[1] > 512u)) ffits = false;
+		}
+		g.tfmeta.release();
+		if (ffits && nt && g.tile == 512) upload(g.tfmeta, fr, g.s_comp);
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	}
 	g.tiles_valid = true;

@@ -1234,6 +1234,175 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 	}
 }
 
+// (A/B variant, off by default: see k_advection_tiles.)
+// One persistent sweep over every tile of a run in slot (= Morton) order,
+// regular and general tiles alike (FTileMeta::kind), so that a tile's face
+// neighbors - whatever their kind - were swept by the same XCD a few tiles
+// earlier and are still in its L2.  (Sweeping the two kinds in two launches
+// re-fetched the faces between them from the fabric: ~1.5x the algorithmic
+// bytes, PMC FETCH_SIZE, profiles/r01h.)  Per tile, as the two separate
+// kernels: own fields at slot ts + tid; a general tile adds its 16-bit face
+// rows, ext cells and finer-face pairs, a regular tile (aligned 8^3 box of
+// one level, Morton-local) its six 64-cell boundary faces from the same-level
+// neighbor boxes, with face codes from Morton arithmetic.  While a tile is
+// computed from LDS, the next tile's loads are in flight in registers (the
+// boundary rows of a regular tile share the general tile's ext registers).
+// Every face is evaluated from each side with the reference's expression,
+// as the general kernel does.
+struct FTileMeta {
+	uint32_t ts, n, e0, ne, fb, nf;
+	int32_t nst[6];  // regular: start slot of the same-level neighbor box per side (-1: none)
+	uint32_t kind, pad[3];
+};
+
+template <int MINW>
+__global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
+    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
+    const uint32_t* __restrict__ tfine, const FTileMeta* __restrict__ meta, uint32_t ntiles, uint32_t W, double dt) {
+#pragma clang fp contract(off)
+	constexpr uint32_t T = 512;
+	extern __shared__ double shd[];  // [7][W] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
+	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
+	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
+	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
+	uint32_t t = t0 + j;
+	if (t >= t1) return;  // block-uniform
+	const uint32_t tid = threadIdx.x;
+	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+	// Morton-local coordinates of this thread's cell in a regular tile
+	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
+	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
+	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
+	const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
+	const double* const rho = P.p[0];
+	const double* const lx = P.p[1];
+	const double* const ly = P.p[2];
+	const double* const lz = P.p[3];
+	const double* const vx = P.p[4];
+	const double* const vy = P.p[5];
+	const double* const vz = P.p[6];
+	// register set of the tile being loaded (field order rho vx vy vz lx ly lz);
+	// a regular tile's boundary values go to xa[0..3]
+	double c[7], xa[7], xb[7];
+	uint32_t row[3], fq[2];
+	auto load7 = [&](uint32_t slot, double (&v)[7]) {
+		const uint32_t o = slot << 3;
+		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
+		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+	};
+	auto load = [&](uint32_t tt) {
+		const uint32_t ts = meta[tt].ts, n = meta[tt].n;
+		if (tid < n) load7(ts + tid, c);
+		if (meta[tt].kind) {
+			// boundary rows k = (side * 5 + value) * 64 + face cell, rows w + 8 i
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const uint32_t r = w + 8u * uint32_t(i);  // wave-uniform
+				xa[i] = 0;
+				if (r >= 30u) continue;
+				const uint32_t d = r / 5u, val = r - 5u * d, a = d >> 1;
+				const int32_t st = meta[tt].nst[d];
+				if (st < 0) continue;
+				const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
+				const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
+				xa[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+			}
+		} else {
+			const uint32_t e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb, nf = meta[tt].nf;
+			if (tid < n) {
+				row[0] = tell[3 * (ts + tid)];
+				row[1] = tell[3 * (ts + tid) + 1];
+				row[2] = tell[3 * (ts + tid) + 2];
+			}
+			if (tid < ne) load7(ext[e0 + tid], xa);
+			if (tid + T < ne) load7(ext[e0 + tid + T], xb);
+			if (tid < nf) {
+				fq[0] = tfine[2 * (fb + tid)];
+				fq[1] = tfine[2 * (fb + tid) + 1];
+			}
+		}
+	};
+	// LDS row of boundary value `val` (0 rho, 1 lx, 2 ly, 3 lz, 4 velocity along a)
+	auto vrow = [](uint32_t val, uint32_t a) -> uint32_t { return val == 0 ? 0u : (val == 4 ? 1u + a : val + 3u); };
+	load(t);
+	for (;;) {
+		const uint32_t n = meta[t].n, ts = meta[t].ts, kind = meta[t].kind;
+		__syncthreads();  // the previous tile's faces have been read from LDS
+		if (tid < n)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
+		uint32_t rr[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
+		if (kind) {
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const uint32_t r = w + 8u * uint32_t(i);
+				if (r < 30u) {
+					const uint32_t d = r / 5u, val = r - 5u * d;
+					shd[vrow(val, d >> 1) * W + T + 64u * d + lane] = xa[i];
+				}
+			}
+			// face codes (same encoding as the general tile's rows): in-tile
+			// Morton index, T + 64 d + face cell across side d, 0xffff none
+#pragma unroll
+			for (int a = 0; a < 3; a++) {
+				uint32_t qm[3] = {l[0], l[1], l[2]}, qp[3] = {l[0], l[1], l[2]};
+				qm[a] -= 1;
+				qp[a] += 1;
+				const uint32_t cm = l[a] > 0 ? m9(qm[0] & 7u, qm[1] & 7u, qm[2] & 7u)
+				                             : (meta[t].nst[2 * a] >= 0 ? T + 64u * (2 * a) + fi[a] : 0xffffu);
+				const uint32_t cp = l[a] < 7 ? m9(qp[0] & 7u, qp[1] & 7u, qp[2] & 7u)
+				                             : (meta[t].nst[2 * a + 1] >= 0 ? T + 64u * (2 * a + 1) + fi[a] : 0xffffu);
+				rr[a] = cm | (cp << 16);
+			}
+		} else {
+			const uint32_t ne = meta[t].ne, nf = meta[t].nf;
+			if (tid < ne)
+#pragma unroll
+				for (int k = 0; k < 7; k++) shd[k * W + T + tid] = xa[k];
+			if (tid + T < ne)
+#pragma unroll
+				for (int k = 0; k < 7; k++) shd[k * W + 2 * T + tid] = xb[k];
+			if (tid < nf) {
+				shf[2 * tid] = fq[0];
+				shf[2 * tid + 1] = fq[1];
+			}
+			rr[0] = row[0];
+			rr[1] = row[1];
+			rr[2] = row[2];
+		}
+		__syncthreads();
+		const uint32_t tn = t + B;
+		const bool more = tn < t1;
+		if (more) load(tn);  // the next tile's loads fly while this one is computed
+		if (tid < n) {
+			const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
+			             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
+			auto fetch = [&](uint32_t li, int d) -> AdvNb {
+				return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
+			};
+			double acc = 0;
+#pragma unroll
+			for (int d = 0; d < 6; d++) {
+				const uint32_t code = (rr[d >> 1] >> (16 * (d & 1))) & 0xffffu;
+				if (code == 0xffffu) continue;
+				if (code & 0x8000u) {
+					const uint32_t fk = code & 0x7fffu;
+					const uint32_t q0 = shf[2 * fk], q1 = shf[2 * fk + 1];
+					const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
+#pragma unroll
+					for (int k = 0; k < 4; k++)
+						acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
+				} else {
+					acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
+				}
+			}
+			rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+		}
+		if (!more) break;
+		t = tn;
+	}
+}
+
 // max_time_step local part (solve.hpp:289-333): block minima
 __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __restrict__ vy,
                               const double* __restrict__ vz, const double* __restrict__ lx,
@@ -1459,6 +1628,27 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		irr = all_d.p;
 		n_irr += n_reg;
 		n_reg = 0;
+	}
+	// DCCRGX_ADV_FUSED=1: both tile kinds in one slot-order launch.  Measured
+	// on config 3 (profiles/r01i): 10% fewer fabric bytes (919 vs 1015 MB per
+	// sweep) but 10% slower (0.2195 vs 0.1988 ms), so the two-launch sweep
+	// stays the default.
+	static const int fused = [] {
+		const char* e = getenv("DCCRGX_ADV_FUSED");
+		return e ? atoi(e) : 0;
+	}();
+	if (fused && use_regular && T == 512 && g.tfmeta.n && diag == 0) {
+		const size_t ntr = run == 0 ? g.n_tiles_inner : g.n_tiles_outer;
+		if (!ntr) return;
+		const FTileMeta* meta = reinterpret_cast<const FTileMeta*>(g.tfmeta.p) + (run == 0 ? 0 : g.n_tiles_inner);
+		const uint32_t W = T + uint32_t(std::max<size_t>(g.max_ext, 384));
+		const size_t lds = size_t(7) * W * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
+		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (ntr + 7) / 8 * 8));
+		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
+		advection_fused_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta,
+		                                                  uint32_t(ntr), W, dt);
+		HIP_CHECK(hipGetLastError());
+		return;
 	}
 	static const int pp_blocks = [] {  // DCCRGX_ADV_PP=k: persistent regular kernel, k blocks per CU (0: off)
 		const char* e = getenv("DCCRGX_ADV_PP");

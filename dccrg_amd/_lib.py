@@ -63,6 +63,8 @@ _SIGS = {
     "dccrgx_pin": (C.c_int, [vp, u64, C.c_int]),
     "dccrgx_unpin": (C.c_int, [vp, u64]),
     "dccrgx_balance_load": (C.c_int, [vp]),
+    "dccrgx_balance_load_to": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_get_cell_process": (C.c_int, [vp, vp, vp, sz, P(sz)]),
     "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
     "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),
     "dccrgx_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp)]),

@@ -671,23 +671,17 @@ static std::vector<uint64_t> stop_refining_impl(Grid& g) {
 // balance_load with pins (dccrg.hpp:1024-1044, make_new_partition 8426-8518,
 // migration continue_balance_load 3899-3934): pinned cells move, the rest
 // keep their owner; payloads of moved cells travel over RCCL.
-static void balance_load_impl(Grid& g) {
-	std::vector<uint64_t> mine;
-	for (auto& kv : g.pins) {
-		mine.push_back(kv.first);
-		mine.push_back(uint64_t(kv.second));
-	}
-	std::vector<std::vector<uint64_t>> all;
-	allgather_u64(g, mine, all);
-	materialize(g);
-	std::vector<int32_t> new_owner = g.owners;
-	for (auto& v : all)
-		for (size_t i = 0; i + 1 < v.size(); i += 2) {
-			auto it = std::lower_bound(g.leaves.begin(), g.leaves.end(), v[i]);
-			if (it == g.leaves.end() || *it != v[i]) continue;
-			if (int64_t(v[i + 1]) < 0 || int64_t(v[i + 1]) >= g.size) continue;
-			new_owner[size_t(it - g.leaves.begin())] = int32_t(v[i + 1]);
-		}
+// Move every leaf to new_owner[i] (g.leaves order): migration plan in
+// ascending id per (source, destination) as make_new_partition sorts its
+// receive lists (8482-8493), payloads of every field packed in that order and
+// moved with grouped RCCL send/recv (continue_balance_load 3899-3934), then
+// the rebuild and the unpack into the new slots.  A detached view (size > 1,
+// no communicator) rebuilds its structures only; the payload of a cell it
+// receives is left to its caller (the multi-rank tests move it).
+static void migrate_to(Grid& g, const std::vector<int32_t>& new_owner) {
+	DX_REQUIRE(new_owner.size() == g.leaves.size(), "one new owner per leaf");
+	for (int32_t o : new_owner) DX_REQUIRE(o >= 0 && o < g.size, "new owner out of range");
+	const bool transport = g.size > 1 && g.comm;
 	// migration plan: ascending id per (source, destination)
 	std::map<int, std::vector<uint64_t>> out, in;
 	for (size_t i = 0; i < g.leaves.size(); i++) {
@@ -707,7 +701,7 @@ static void balance_load_impl(Grid& g) {
 		in_off[kv.first] = in_ids.size();
 		in_ids.insert(in_ids.end(), kv.second.begin(), kv.second.end());
 	}
-	if (g.size > 1) {
+	if (transport) {
 		DBuf<uint64_t> dids;
 		upload(dids, out_ids, s);
 		DBuf<int32_t> oslots, err;
@@ -738,9 +732,8 @@ static void balance_load_impl(Grid& g) {
 		HIP_CHECK(hipStreamSynchronize(s));
 	}
 	g.owners = new_owner;
-	g.pins.clear();
 	rebuild(g);
-	if (!in_ids.empty()) {
+	if (transport && !in_ids.empty()) {
 		DBuf<uint64_t> dids;
 		upload(dids, in_ids, s);
 		DBuf<int32_t> islots, err;
@@ -756,6 +749,30 @@ static void balance_load_impl(Grid& g) {
 		}
 		HIP_CHECK(hipStreamSynchronize(s));
 	}
+}
+
+// balance_load with pins (dccrg.hpp:1024-1044; update_pin_requests
+// all-gathers them, make_new_partition 8426-8518 moves every pinned cell to
+// its process): pins stay in force until unpin (5909), as the reference's
+// pin_requests do; the rest keep their owner (no third-party partitioner).
+static void balance_load_impl(Grid& g) {
+	std::vector<uint64_t> mine;
+	for (auto& kv : g.pins) {
+		mine.push_back(kv.first);
+		mine.push_back(uint64_t(kv.second));
+	}
+	std::vector<std::vector<uint64_t>> all;
+	allgather_u64(g, mine, all);
+	materialize(g);
+	std::vector<int32_t> new_owner = g.owners;
+	for (auto& v : all)
+		for (size_t i = 0; i + 1 < v.size(); i += 2) {
+			auto it = std::lower_bound(g.leaves.begin(), g.leaves.end(), v[i]);
+			if (it == g.leaves.end() || *it != v[i]) continue;
+			if (int64_t(v[i + 1]) < 0 || int64_t(v[i + 1]) >= g.size) continue;
+			new_owner[size_t(it - g.leaves.begin())] = int32_t(v[i + 1]);
+		}
+	migrate_to(g, new_owner);
 }
 
 // --------------------------------------------------------------------------- Poisson
@@ -1352,6 +1369,33 @@ int dccrgx_get_cells_to_receive(dccrgx_grid* gp, int peer, uint64_t* ids, size_t
 	});
 }
 
+int dccrgx_get_cell_process(dccrgx_grid* gp, uint64_t* ids, int32_t* owners, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		// an implicit (initial uniform) mesh stays implicit: the structured
+		// sweeps key on it
+		const bool imp = implicit_mesh(g);
+		const uint64_t total = imp ? g.m.first[1] - 1 : g.leaves.size();
+		*n = size_t(total);
+		if (!ids) return 0;
+		if (cap < total) return int(DCCRGX_ERANGE);
+		if (!imp) {
+			std::copy(g.leaves.begin(), g.leaves.end(), ids);
+			if (owners) std::copy(g.owners.begin(), g.owners.end(), owners);
+			return 0;
+		}
+		for (int p = 0; p < g.size; p++) {
+			uint64_t f, c;
+			block_range(total, uint64_t(g.size), uint64_t(p), f, c);
+			for (uint64_t i = 0; i < c; i++) {
+				ids[f - 1 + i] = f + i;
+				if (owners) owners[f - 1 + i] = p;
+			}
+		}
+		return 0;
+	});
+}
+
 int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* nr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
@@ -1424,6 +1468,18 @@ int dccrgx_unpin(dccrgx_grid* gp, uint64_t cell) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		g.pins.erase(cell);
+		return 0;
+	});
+}
+
+int dccrgx_balance_load_to(dccrgx_grid* gp, const uint64_t* ids, const int32_t* new_owner, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		materialize(g);
+		DX_REQUIRE(n == g.leaves.size(), "balance_load_to needs one owner per leaf of the grid");
+		for (size_t i = 0; i < n; i++) DX_REQUIRE(ids[i] == g.leaves[i], "leaf ids must be the grid's, ascending");
+		migrate_to(g, std::vector<int32_t>(new_owner, new_owner + n));
 		return 0;
 	});
 }

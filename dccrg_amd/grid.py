@@ -332,6 +332,24 @@ class Dccrg:
         check(lib().dccrgx_balance_load(self.h))
         return self
 
+    def balance_load_to(self, ids, new_owners):
+        """Repartition to an explicit owner per leaf (every leaf, ascending id,
+        identical on all ranks); payloads migrate."""
+        ids = np.ascontiguousarray(ids, np.uint64)
+        own = np.ascontiguousarray(new_owners, np.int32)
+        check(lib().dccrgx_balance_load_to(self.h, _ptr(ids), _ptr(own), ids.size))
+        return self
+
+    def get_cell_process(self):
+        """(ids, owners) of every leaf of the grid, ascending id
+        (get_cell_process, dccrg.hpp:6848)."""
+        n = C.c_size_t()
+        check(lib().dccrgx_get_cell_process(self.h, None, None, 0, C.byref(n)))
+        ids = np.empty(n.value, np.uint64)
+        own = np.empty(n.value, np.int32)
+        check(lib().dccrgx_get_cell_process(self.h, _ptr(ids), _ptr(own), ids.size, C.byref(n)))
+        return ids, own
+
     # ---- fields ---------------------------------------------------------------
     def add_field(self, name, dtype, transfer=True):
         fid = C.c_int()

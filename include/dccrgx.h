@@ -114,6 +114,11 @@ int64_t dccrgx_get_slot(dccrgx_grid* g, uint64_t cell);
 int dccrgx_get_peers(dccrgx_grid* g, int32_t* peers, size_t cap, size_t* n);
 int dccrgx_get_cells_to_send(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
 int dccrgx_get_cells_to_receive(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
+/* every leaf of the grid with its process, ascending id (the global
+ * cell_process map the reference keeps on every rank, get_cell_process
+ * 6848); ids == NULL: *n = count only */
+int dccrgx_get_cell_process(dccrgx_grid* g, uint64_t* ids, int32_t* owners, size_t cap, size_t* n);
+
 /* get_number_of_update_send_cells / _receive_cells 5382-5490 */
 int dccrgx_get_number_of_update_cells(dccrgx_grid* g, uint64_t* n_send, uint64_t* n_receive);
 
@@ -137,6 +142,12 @@ int dccrgx_set_cells(dccrgx_grid* g, const uint64_t* ids, const int32_t* owners,
 int dccrgx_pin(dccrgx_grid* g, uint64_t cell, int process);
 int dccrgx_unpin(dccrgx_grid* g, uint64_t cell);
 int dccrgx_balance_load(dccrgx_grid* g);
+/* balance_load to an explicit partition (SURVEY §8(b) balance_load(new_owner);
+ * stands in for a partitioner's import/export lists, make_new_partition
+ * 8349-8581): ids = every leaf of the grid ascending (as get_all_leaves),
+ * new_owner[i] its process; identical arguments on every rank.  Payloads of
+ * all fields migrate (continue_balance_load 3899-3934). */
+int dccrgx_balance_load_to(dccrgx_grid* g, const uint64_t* ids, const int32_t* new_owner, size_t n);
 
 /* ---- fields (replaces Cell_Data + get_mpi_datatype, dccrg_get_cell_datatype.hpp:40-340)
  * transfer != 0: the field is part of update_copies_of_remote_neighbors. */

@@ -82,7 +82,7 @@ def gol_main(a, dccrgx_mod, torch):
         "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                      "traffic": None, "kernel": "gol_structured_kernel", "alg_bytes_per_step": 8 * n,
                      "kernel_ms_per_step": kms / a.steps},
-        "cpu_baseline": None}), flush=True)
+        "cpu_baseline": None if a.no_cpu_baseline else gol_cpu_baseline(a.cpu_seconds)}), flush=True)
     g.close()
 
 
@@ -180,6 +180,31 @@ def build_grid(dccrg_amd, rank, size, base, R, uid):
         g.stop_refining()
     g.advection_initialize(f)
     return g, f
+
+
+def gol_cpu_baseline(seconds):
+    """The oracle's game of life (CPU restatement of the reference's loop over
+    cell.neighbors_of, one core) on a 64 x 64 x 16 sample of config 2 (same
+    26-point stencil, non-periodic, same alive(id) rule)."""
+    from oracle import oracle as O
+
+    n = (64, 64, 16)
+    o = O.Grid(n, 0, (False, False, False), 1, 1)
+    ids, _ = o.cells()
+    z = (ids ^ np.uint64(0x5DEECE66D)) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    o.gol_set(ids, (z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32))
+    o.gol_steps(1)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.gol_steps(1)
+        steps += 1
+    el = time.perf_counter() - t0
+    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
+                sample=f"oracle restatement, 64x64x16 game of life ({ids.size} cells), {steps} steps, "
+                       f"{el:.1f} s on 1 host core")
 
 
 def cpu_baseline(seconds):

@@ -641,6 +641,23 @@ __device__ __forceinline__ double ldo(const double* __restrict__ p, uint32_t off
 	return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(p) + off);
 }
 
+// own-field stream of the tile sweeps: NT bit 1 marks the loads
+// non-temporal (do not displace the face lines other tiles re-read from L2)
+template <int NT>
+__device__ __forceinline__ double ldo_own(const double* __restrict__ p, uint32_t off) {
+	const double* q = reinterpret_cast<const double*>(reinterpret_cast<const char*>(p) + off);
+	if (NT & 2) return __builtin_nontemporal_load(q);
+	return *q;
+}
+
+// density store of the tile sweeps: NT bit 0 marks it non-temporal (a
+// streaming write that should not allocate over useful L2 lines)
+template <int NT>
+__device__ __forceinline__ void st_out(double* __restrict__ p, uint32_t i, double v) {
+	if (NT & 1) __builtin_nontemporal_store(v, p + i);
+	else p[i] = v;
+}
+
 __device__ __forceinline__ AdvNb adv_gather(const double* __restrict__ rho, const double* __restrict__ lx,
                                             const double* __restrict__ ly, const double* __restrict__ lz,
                                             const double* __restrict__ vdir, size_t n) {
@@ -1001,7 +1018,7 @@ __device__ __forceinline__ double adv_face_g(int a, double cd, double clx, doubl
 	return (v >= 0 ? cd : n.d) * dt * v * min_area;
 }
 
-template <int MINW>
+template <int MINW, int NT>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
                                                                          uint32_t ntiles, double dt) {
@@ -1051,8 +1068,8 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	auto load = [&](uint32_t tt) {
 		const uint32_t ts = meta[tt].ts;
 		const uint32_t o = (ts + tid) << 3;
-		c[0] = ldo(rho, o); c[1] = ldo(vx, o); c[2] = ldo(vy, o); c[3] = ldo(vz, o);
-		c[4] = ldo(lx, o); c[5] = ldo(ly, o); c[6] = ldo(lz, o);
+		c[0] = ldo_own<NT>(rho, o); c[1] = ldo_own<NT>(vx, o); c[2] = ldo_own<NT>(vy, o); c[3] = ldo_own<NT>(vz, o);
+		c[4] = ldo_own<NT>(lx, o); c[5] = ldo_own<NT>(ly, o); c[6] = ldo_own<NT>(lz, o);
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
@@ -1121,7 +1138,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			acc += gm;
 			acc += -shg[a][tid];
 		}
-		rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+		st_out<NT>(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 		if (!more) break;
 		t = tn;
 	}
@@ -1137,7 +1154,7 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW>
+template <int MINW, int NT>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
     const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
@@ -1166,11 +1183,16 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
 		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
 	};
+	auto load7own = [&](uint32_t slot, double (&v)[7]) {
+		const uint32_t o = slot << 3;
+		v[0] = ldo_own<NT>(rho, o); v[1] = ldo_own<NT>(vx, o); v[2] = ldo_own<NT>(vy, o); v[3] = ldo_own<NT>(vz, o);
+		v[4] = ldo_own<NT>(lx, o); v[5] = ldo_own<NT>(ly, o); v[6] = ldo_own<NT>(lz, o);
+	};
 	auto load = [&](uint32_t tt) {
 		const uint32_t ts = meta[tt].ts, n = meta[tt].n, e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb,
 		               nf = meta[tt].nf;
 		if (tid < n) {
-			load7(ts + tid, c);
+			load7own(ts + tid, c);
 			row[0] = tell[3 * (ts + tid)];
 			row[1] = tell[3 * (ts + tid) + 1];
 			row[2] = tell[3 * (ts + tid) + 2];
@@ -1227,7 +1249,7 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 					acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
 				}
 			}
-			rho_out[ts + tid] = cd + acc / (clx * cly * clz);
+			st_out<NT>(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 		}
 		if (!more) break;
 		t = tn;
@@ -1527,6 +1549,19 @@ void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 	HIP_CHECK(hipGetLastError());
 }
 
+// DCCRGX_ADV_NT: non-temporal hints of the tile sweeps (bit 0 density
+// store, bit 1 own-field loads).  Measured on config 3: the store hint
+// 0.1960 -> 0.1945 ms (default on); the load hint 0.2185 ms, because the
+// own-field lines are the face lines neighboring tiles re-read from L2;
+// non-temporal face/ext loads from tiles swept earlier: no gain (0.199 ms).
+static int adv_nt() {
+	static const int v = [] {
+		const char* e = getenv("DCCRGX_ADV_NT");
+		return e ? atoi(e) : 1;
+	}();
+	return v;
+}
+
 int adv_variant() {
 	static int v = [] {
 		const char* e = getenv("DCCRGX_ADV_VARIANT");
@@ -1658,7 +1693,10 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * size_t(pp_blocks), (n_reg + 7) / 8 * 8));
 		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		if (adv_nt() == 1) advection_regular_pp_kernel<4, 1><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else if (adv_nt() == 2) advection_regular_pp_kernel<4, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else if (adv_nt() == 3) advection_regular_pp_kernel<4, 3><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		else advection_regular_pp_kernel<4, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
 		HIP_CHECK(hipGetLastError());
 	} else if (n_reg) {
 		if (diag == 5)
@@ -1683,8 +1721,14 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		const size_t lds = size_t(7) * (T + ecap) * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
 		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta,
-		                                                     uint32_t(n_irr), ecap, dt);
+#define DX_TPP(NTV)                                                                                          \
+	advection_tiles_pp_kernel<4, NTV><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta, \
+	                                                         uint32_t(n_irr), ecap, dt)
+		if (adv_nt() == 1) DX_TPP(1);
+		else if (adv_nt() == 2) DX_TPP(2);
+		else if (adv_nt() == 3) DX_TPP(3);
+		else DX_TPP(0);
+#undef DX_TPP
 		HIP_CHECK(hipGetLastError());
 		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
 		return;

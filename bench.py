@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--workload", choices=["advection", "gol", "poisson"], default="advection",
+    p.add_argument("--workload", choices=["advection", "gol", "gol_amr", "poisson"], default="advection",
                    help="advection = BASELINE metric (default); gol = config 2 game of life line; "
                         "poisson = config 4 BiCG line")
     return p.parse_args()
@@ -84,6 +84,95 @@ def gol_main(a, dccrgx_mod, torch):
                      "kernel_ms_per_step": kms / a.steps},
         "cpu_baseline": None if a.no_cpu_baseline else gol_cpu_baseline(a.cpu_seconds)}), flush=True)
     g.close()
+
+
+def gol_amr_main(a, dccrgx_mod, torch):
+    """the refined game emulating the level-0 game
+    (tests/game_of_life/solve.hpp get_live_neighbors, as unrefined2d.cpp
+    plays it) on a 2048 x 2048 x 1 level-0 grid, max refinement level 1, a
+    seeded quarter of the level-0 cells refined (children inherit the state),
+    p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
+    halo between them is a no-op).  Algorithmic bytes per leaf and step, both
+    phases: slot id 8 B twice, row pointer 2 x 4 B, per neighbor entry id 8 B
+    + slot 4 B twice, the neighbor's state 4 B (collect), the list 64 B
+    written and read back, a same-parent neighbor's list 64 B (spread),
+    state 4 B written."""
+    n = 2048
+    g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
+    g.set_maximum_refinement_level(1).initialize()
+    rng = np.random.default_rng(7)
+    lvl0 = np.arange(1, n * n + 1, dtype=np.uint64)
+    live0 = rng.random(n * n) < 0.3
+    t_setup = time.perf_counter()
+    for c in rng.choice(lvl0, size=n * n // 4, replace=False):
+        g.refine_completely(int(c))
+    g.stop_refining()
+    setup_s = time.perf_counter() - t_setup
+    st = g.add_field("is_alive", np.uint32)
+    ls = g.add_field("gol_list", np.dtype((np.uint64, 8)))
+    slots = g.slot_ids()[: g.n_local]
+    lvl = (slots > np.uint64(n * n)).astype(np.int64)
+    # level-0 parent of a level-1 leaf (2 x 2 x 2 children per parent, x fastest)
+    c1 = slots.astype(np.int64) - 1 - n * n
+    x1, y1 = c1 % (2 * n), (c1 // (2 * n)) % (2 * n)
+    par = np.where(lvl == 0, slots.astype(np.int64) - 1, (y1 // 2) * n + x1 // 2)
+    st.set(live0[par].astype(np.uint32))
+    for _ in range(a.warmup):
+        g.get_live_neighbors(st, ls)
+    g.synchronize()
+    torch.cuda.synchronize()
+    g.kernel_timing(1)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.get_live_neighbors(st, ls)
+    g.synchronize()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms, kn = g.kernel_timing(0)
+    nl = g.n_local
+    kbar = g.neighbor_entries("of") / nl
+    sib = float(np.mean(np.where(lvl == 1, 7.0, 0.0)))  # same-parent neighbors per leaf
+    per_cell = 2 * 8 + 2 * 4 + kbar * (2 * 12 + 4) + 64 + 64 + sib * 64 + 4
+    ach = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
+    print(json.dumps({
+        "metric": "cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
+        "value": nl * a.steps / el, "unit": "cell-updates/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32/u64", "data": "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
+        "config": {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
+                   "leaves": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s},
+        "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                     "kernel": "gol_amr_collect_kernel + gol_amr_spread_kernel", "alg_bytes_per_cell": per_cell,
+                     "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps},
+        "cpu_baseline": None if a.no_cpu_baseline else gol_amr_cpu_baseline(a.cpu_seconds)}), flush=True)
+    g.close()
+
+
+def gol_amr_cpu_baseline(seconds):
+    """The oracle's get_live_neighbors (one core) on a 128 x 128 x 1 sample of
+    the same workload."""
+    from oracle import oracle as O
+
+    n = 128
+    o = O.Grid((n, n, 1), 1, (False, False, False), 1, 1)
+    rng = np.random.default_rng(7)
+    ids0, _ = o.cells()
+    live0 = rng.random(n * n) < 0.3
+    for c in rng.choice(ids0, size=n * n // 4, replace=False):
+        o.refine_completely(int(c))
+    o.stop_refining()
+    ids, _ = o.cells()
+    par = o.mapping.batch(ids)["level0_parent"].astype(np.int64) - 1
+    o.gola_set(ids, live0[par].astype(np.uint32))
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.gola_steps(1)
+        steps += 1
+    el = time.perf_counter() - t0
+    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
+                sample=f"oracle restatement, 128x128x1 level-0, quarter refined ({ids.size} leaves), {steps} steps, "
+                       f"{el:.1f} s on 1 host core")
 
 
 def poisson_main(a, dccrgx_mod, torch, rank, world, uid):
@@ -161,7 +250,8 @@ def poisson_main(a, dccrgx_mod, torch, rank, world, uid):
                          "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
                          "kernel": "po_phase_a + po_phase_b + po_phase_c", "alg_bytes_per_cell_iteration": per_cell,
                          "kernel_ms_per_step": kms / it, "launches_per_step": kn / it, "residual_min": res},
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": None if (a.no_cpu_baseline or world > 1) else poisson_cpu_baseline(a.cpu_seconds)}),
+            flush=True)
     g.close()
 
 
@@ -180,6 +270,41 @@ def build_grid(dccrg_amd, rank, size, base, R, uid):
         g.stop_refining()
     g.advection_initialize(f)
     return g, f
+
+
+def poisson_cpu_baseline(seconds):
+    """The oracle's Poisson_Solve (one core) on a 32^3 sample of config 4
+    (same cell lengths, periodic, refined twice at the center, same rhs):
+    batches of 20 iterations (min = max) until ~`seconds`."""
+    import math
+
+    from oracle import oracle as O
+
+    n = 32
+    L0 = (2 * math.pi / n, math.pi / n, 8 * math.pi / n)
+    o = O.Grid((n, n, n), 2, (True, True, True), 0, 1)
+    o.set_geometry((0, 0, 0), L0)
+    for _ in range(2):  # poisson3d.cpp:174-192
+        ids, _ = o.cells()
+        c, L = o.geometry(ids)
+        mn, mx = c - L / 2, c + L / 2
+        sel = ((mn[:, 0] < 1.01 * math.pi) & (mx[:, 0] > 0.99 * math.pi) & (mn[:, 1] < 0.51 * math.pi)
+               & (mx[:, 1] > 0.49 * math.pi) & (mn[:, 2] < 4.01 * math.pi) & (mx[:, 2] > 3.99 * math.pi))
+        for cell in ids[sel]:
+            o.refine_completely(int(cell))
+        o.stop_refining()
+    ids, _ = o.cells()
+    c, _ = o.geometry(ids)
+    rhs = -(81.0 / 16.0) * np.sin(c[:, 0]) * np.cos(2 * c[:, 1]) * np.sin(c[:, 2] / 4)
+    its, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.po_set(ids, rhs, np.zeros(ids.size), np.zeros(ids.size, np.int32))
+        it, _ = o.po_solve(20, 20)
+        its += it
+    el = time.perf_counter() - t0
+    return dict(value=ids.size * its / el, unit="cell-updates/s", cores=1, kind="port",
+                sample=f"oracle restatement, 32^3 base refined twice at the center ({ids.size} cells), "
+                       f"{its} BiCG iterations incl. setup, {el:.1f} s on 1 host core")
 
 
 def gol_cpu_baseline(seconds):
@@ -245,6 +370,8 @@ def main():
 
     if a.workload == "gol":
         return gol_main(a, dccrg_amd, torch)
+    if a.workload == "gol_amr":
+        return gol_amr_main(a, dccrg_amd, torch)
     uid = None
     if world > 1:
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]

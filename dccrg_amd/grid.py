@@ -244,6 +244,15 @@ class Dccrg:
         check(rc)
         return [(int(ids[i]), int(dirs[i])) for i in range(n.value)]
 
+    def neighbor_entries(self, kind="of"):
+        """Number of entries of a local CSR (no download of the entries)."""
+        n = C.c_size_t()
+        ptr = np.empty(self.n_local + 1, np.uint32)
+        rc = lib().dccrgx_download_csr(self.h, CSR_KIND[kind], _ptr(ptr), None, None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        return int(n.value)
+
     def csr(self, kind="of"):
         """Bulk download (ptr, ids, aux) of a local CSR in slot order."""
         k = CSR_KIND[kind]

@@ -92,10 +92,12 @@ def gol_amr_main(a, dccrgx_mod, torch):
     plays it) on a 2048 x 2048 x 1 level-0 grid, max refinement level 1, a
     seeded quarter of the level-0 cells refined (children inherit the state),
     p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
-    halo between them is a no-op).  Algorithmic bytes per leaf and step, both
-    phases: slot id 8 B twice, row pointer 2 x 4 B, per neighbor entry id 8 B
-    + slot 4 B twice, the neighbor's state 4 B (collect), the list 64 B
-    written and read back, a same-parent neighbor's list 64 B (spread),
+    halo between them is a no-op).  Algorithmic bytes per leaf and step:
+    level-0 parent per slot decoded per phase (2 x (8 B id read + 8 B
+    written)); collect: own parent 8 B, row pointers 8 B, per neighbor entry
+    slot 4 B + parent 8 B + state 4 B, list 64 B written; spread: own parent
+    and id 16 B, row pointers 8 B, own list 64 B, and for a level-1 leaf per
+    neighbor entry slot 4 B + parent 8 B and its 7 siblings' lists 7 x 64 B,
     state 4 B written."""
     n = 2048
     g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
@@ -131,8 +133,8 @@ def gol_amr_main(a, dccrgx_mod, torch):
     kms, kn = g.kernel_timing(0)
     nl = g.n_local
     kbar = g.neighbor_entries("of") / nl
-    sib = float(np.mean(np.where(lvl == 1, 7.0, 0.0)))  # same-parent neighbors per leaf
-    per_cell = 2 * 8 + 2 * 4 + kbar * (2 * 12 + 4) + 64 + 64 + sib * 64 + 4
+    f1 = float(np.mean(lvl == 1))  # fraction of level-1 leaves
+    per_cell = (2 * 16) + (8 + 8 + kbar * 16 + 64) + (16 + 8 + 64 + f1 * (kbar * 12 + 7 * 64) + 4)
     ach = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     print(json.dumps({
         "metric": "cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",

@@ -238,6 +238,7 @@ struct Grid {
 	// nst[6] (regular: neighbor-box starts), kind (1 regular), pad; for the
 	// fused sweep over both kinds (empty when a tile exceeds its limits)
 	DBuf<uint32_t> tfmeta;
+	DBuf<uint64_t> gol_l0p;  // refined game of life: level-0 parent per slot (scratch)
 	// halo
 	DBuf<int32_t> send_slots;
 	DBuf<uint8_t> sendbuf;
@@ -337,8 +338,8 @@ void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 
 // --- launchers implemented in gol_amr.hip ----------------------------------
-void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, uint32_t* state, uint64_t* lst,
-               const uint32_t* ptr, const uint64_t* nid, const int32_t* nslot, size_t s0, size_t s1, int* err,
+void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, uint64_t* l0p, uint32_t* state,
+               uint64_t* lst, const uint32_t* ptr, const int32_t* nslot, size_t s0, size_t s1, int* err,
                hipStream_t s);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------

@@ -24,8 +24,9 @@
 // neighbor list over 8 entries (solve.hpp:98-101, 139-146) and a dead
 // neighbor whose level-0 parent was recorded alive through a sibling
 // (solve.hpp:81-90, the siblings disagree).  One thread per leaf; the
-// neighbor rows are the device neighbors_of CSR (ids + slots).  Integer
-// work, latency bound (one dependent id decode per neighbor entry).
+// neighbor rows are the device neighbors_of CSR (slots); the level-0 parent
+// of every slot is decoded once per call.  Integer work, latency bound
+// (a dependent gather per neighbor entry).
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -46,24 +47,30 @@ __device__ __forceinline__ bool list_insert(uint64_t (&l)[kList], int& n, uint64
 	return true;
 }
 
-__global__ void gol_amr_collect_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids,
-                                       const uint32_t* __restrict__ state, uint64_t* __restrict__ lst,
-                                       const uint32_t* __restrict__ ptr, const uint64_t* __restrict__ nid,
+__global__ void level0_parent_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, size_t n,
+                                     uint64_t* __restrict__ l0p) {
+	const size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+	if (s < n) l0p[s] = map_level0_parent(m, slot_ids[s]);
+}
+
+// l0p: level-0 parent per slot (local and remote copies), computed once per
+// call so the neighbor walks do no id decoding
+__global__ void gol_amr_collect_kernel(const uint64_t* __restrict__ l0p, const uint32_t* __restrict__ state,
+                                       uint64_t* __restrict__ lst, const uint32_t* __restrict__ ptr,
                                        const int32_t* __restrict__ nslot, size_t s0, size_t s1,
                                        int* __restrict__ err) {
 	const size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x;
 	if (s >= s1) return;
-	const uint64_t parent = map_level0_parent(m, slot_ids[s]);
+	const uint64_t parent = l0p[s];
 	uint64_t l[kList];
 #pragma unroll
 	for (int i = 0; i < kList; i++) l[i] = error_cell;
 	int n = 0;
 	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
-		const uint64_t id = nid[j];
-		if (id == error_cell) continue;
-		const uint64_t q = map_level0_parent(m, id);
+		const int32_t ns = nslot[j];
+		const uint64_t q = l0p[ns];
 		if (q == parent) continue;
-		if (state[nslot[j]] == 0) {
+		if (state[ns] == 0) {
 			bool seen = false;
 #pragma unroll
 			for (int i = 0; i < kList; i++) seen |= (i < n && l[i] == q);
@@ -77,13 +84,13 @@ __global__ void gol_amr_collect_kernel(MapCtx m, const uint64_t* __restrict__ sl
 	for (int i = 0; i < kList; i++) o[i] = l[i];
 }
 
-__global__ void gol_amr_spread_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, uint32_t* __restrict__ state,
-                                      const uint64_t* __restrict__ lst, const uint32_t* __restrict__ ptr,
-                                      const uint64_t* __restrict__ nid, const int32_t* __restrict__ nslot,
+__global__ void gol_amr_spread_kernel(const uint64_t* __restrict__ slot_ids, const uint64_t* __restrict__ l0p,
+                                      uint32_t* __restrict__ state, const uint64_t* __restrict__ lst,
+                                      const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nslot,
                                       size_t s0, size_t s1, int* __restrict__ err) {
 	const size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x;
 	if (s >= s1) return;
-	const uint64_t parent = map_level0_parent(m, slot_ids[s]);
+	const uint64_t parent = l0p[s];
 	uint64_t l[kList];
 	int n = 0;
 #pragma unroll
@@ -91,14 +98,17 @@ __global__ void gol_amr_spread_kernel(MapCtx m, const uint64_t* __restrict__ slo
 		l[i] = lst[s * kList + i];
 		n += l[i] != error_cell;
 	}
-	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
-		const uint64_t id = nid[j];
-		if (id == error_cell || map_level0_parent(m, id) != parent) continue;
-		const uint64_t* nl = lst + size_t(nslot[j]) * kList;
-		for (int i = 0; i < kList; i++) {
-			const uint64_t v = nl[i];
-			if (v == error_cell) break;
-			if (!list_insert(l, n, v)) atomicOr(err, 1);
+	// a level-0 leaf is its own level-0 parent: no neighbor shares it
+	if (parent != slot_ids[s]) {
+		for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
+			const int32_t ns = nslot[j];
+			if (l0p[ns] != parent) continue;
+			const uint64_t* nl = lst + size_t(ns) * kList;
+			for (int i = 0; i < kList; i++) {
+				const uint64_t v = nl[i];
+				if (v == error_cell) break;
+				if (!list_insert(l, n, v)) atomicOr(err, 1);
+			}
 		}
 	}
 	if (n == 3) state[s] = 1;
@@ -109,16 +119,16 @@ inline unsigned blocks_for(size_t n, unsigned b) { return unsigned((n + b - 1) /
 
 }  // namespace
 
-void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, uint32_t* state, uint64_t* lst,
-               const uint32_t* ptr, const uint64_t* nid, const int32_t* nslot, size_t s0, size_t s1, int* err,
+void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, uint64_t* l0p, uint32_t* state,
+               uint64_t* lst, const uint32_t* ptr, const int32_t* nslot, size_t s0, size_t s1, int* err,
                hipStream_t s) {
 	if (s1 <= s0) return;
+	level0_parent_kernel<<<blocks_for(n_slots, 256), 256, 0, s>>>(m, slot_ids, n_slots, l0p);
 	if (phase == 0)
-		gol_amr_collect_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(m, slot_ids, state, lst, ptr, nid, nslot, s0,
-		                                                                 s1, err);
+		gol_amr_collect_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
 	else
-		gol_amr_spread_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(m, slot_ids, state, lst, ptr, nid, nslot, s0,
-		                                                                s1, err);
+		gol_amr_spread_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1,
+		                                                                err);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -134,3 +134,39 @@ def test_single_rank_balance(gpu):
     with pytest.raises(dccrg_amd.DccrgError, match="out of range"):
         g.balance_load_to(ids, owners + 1)
     g.close()
+
+
+def test_iterators_test1_invariants_over_random_partitions(gpu):
+    """tests/iterators/test1.cpp: a 1000 x 1 x 1 grid, neighborhood length 3,
+    five rounds of random load balancing; after each, every rank's inner
+    cells are exactly its local cells whose neighbors_of and neighbors_to are
+    all local, outer cells the rest, and every remote cell on the process
+    boundary is a non-local neighbor of a local cell.  The random partition
+    is the test's (RANDOM partitioner, here a seeded owner per cell through
+    balance_load_to), the invariants are the reference's."""
+    P = 3
+    gs = []
+    for r in range(P):
+        g = dccrg_amd.Dccrg(r, P, 0).set_initial_length((1000, 1, 1)).set_neighborhood_length(3)
+        g.set_maximum_refinement_level(0).initialize()
+        gs.append(g)
+    rng = np.random.default_rng(21)
+    for _ in range(5):
+        ids, _ = gs[0].get_cell_process()
+        new = rng.integers(0, P, size=ids.size).astype(np.int32)
+        for g in gs:
+            g.balance_load_to(ids, new)
+        for r, g in enumerate(gs):
+            inner_ref, outer_ref, remote_ref = set(), set(), set()
+            for c in g.local_cells().tolist():
+                assert g.is_local(c)
+                nb = [i for i, _ in g.get_neighbors_of(c)] + [i for i, _ in g.get_neighbors_to(c)]
+                nonlocal_nb = [i for i in nb if not g.is_local(i)]
+                (outer_ref if nonlocal_nb else inner_ref).add(c)
+                remote_ref.update(nonlocal_nb)
+            assert set(g.inner_cells().tolist()) == inner_ref
+            assert set(g.outer_cells().tolist()) == outer_ref
+            assert set(g.remote_cells().tolist()) == remote_ref
+            assert np.all(new[np.searchsorted(ids, g.local_cells())] == r)
+    for g in gs:
+        g.close()

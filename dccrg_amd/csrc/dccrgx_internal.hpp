@@ -220,6 +220,7 @@ struct Grid {
 	DBuf<uint32_t> tell;       // 3 x u32 per local slot (6 x u16)
 	DBuf<uint32_t> ext_ptr;    // n_tiles + 1
 	DBuf<uint32_t> ext;        // total_ext slots
+	DBuf<uint32_t> ext_pk;     // ext slots | axis mask << 29 (axes through which a face reaches the cell)
 	DBuf<uint32_t> fine_base;  // n_tiles: index of the tile's first finer face
 	DBuf<uint32_t> tfine;      // 2 x u32 per finer face (4 x u16)
 	// regular tiles (aligned uniform 8x8x8 boxes, see tile_build.hip) are swept
@@ -312,7 +313,7 @@ struct TileBuild {
 };
 TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& m,
                         bool morton, size_t n_inner, size_t n_local, int tile, DBuf<uint32_t>& tstart,
-                        DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
+                        DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext, DBuf<uint32_t>& ext_pk,
                         DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s);
 
 void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_inner, size_t n_tiles_outer,

@@ -382,7 +382,7 @@ static void ensure_tiles(Grid& g) {
 	const int T = tile_size_setting();
 	if (g.tiles_valid && g.tile == T) return;
 	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.slot_ids.p, g.m, g.morton_slots, g.n_inner,
-	                                   g.n_local, T, g.tstart, g.tell, g.ext_ptr, g.ext, g.fine_base, g.tfine, g.s_comp);
+	                                   g.n_local, T, g.tstart, g.tell, g.ext_ptr, g.ext, g.ext_pk, g.fine_base, g.tfine, g.s_comp);
 	g.tile = T;
 	g.n_tiles_inner = tb.n_tiles_inner;
 	g.n_tiles_outer = tb.n_tiles_outer;

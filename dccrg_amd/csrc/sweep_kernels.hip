@@ -1154,7 +1154,7 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW, int NT>
+template <int MINW, int NT, int EXT5>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
     const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
@@ -1197,8 +1197,22 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			row[1] = tell[3 * (ts + tid) + 1];
 			row[2] = tell[3 * (ts + tid) + 2];
 		}
-		if (tid < ne) load7(ext[e0 + tid], xa);
-		if (tid + T < ne) load7(ext[e0 + tid + T], xb);
+		if (EXT5) {
+			// ext = slot | axis mask << 29: density and lengths, and only the
+			// velocity components along the axes its faces cross
+			auto load5 = [&](uint32_t q, double (&v)[7]) {
+				const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
+				v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+				v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
+				v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
+				v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
+			};
+			if (tid < ne) load5(ext[e0 + tid], xa);
+			if (tid + T < ne) load5(ext[e0 + tid + T], xb);
+		} else {
+			if (tid < ne) load7(ext[e0 + tid], xa);
+			if (tid + T < ne) load7(ext[e0 + tid + T], xb);
+		}
 		if (tid < nf) {
 			fq[0] = tfine[2 * (fb + tid)];
 			fq[1] = tfine[2 * (fb + tid) + 1];
@@ -1721,13 +1735,20 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		const size_t lds = size_t(7) * (T + ecap) * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
 		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-#define DX_TPP(NTV)                                                                                          \
-	advection_tiles_pp_kernel<4, NTV><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta, \
-	                                                         uint32_t(n_irr), ecap, dt)
-		if (adv_nt() == 1) DX_TPP(1);
-		else if (adv_nt() == 2) DX_TPP(2);
-		else if (adv_nt() == 3) DX_TPP(3);
-		else DX_TPP(0);
+		// DCCRGX_ADV_EXT5=0: every ext cell loads all seven fields (A/B)
+		static const int ext5 = [] {
+			const char* e = getenv("DCCRGX_ADV_EXT5");
+			return e ? atoi(e) : 1;
+		}();
+#define DX_TPP(NTV, E5)                                                                                    \
+	advection_tiles_pp_kernel<4, NTV, E5><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, E5 ? g.ext_pk.p : g.ext.p, \
+	                                                             g.tfine.p, meta, uint32_t(n_irr), ecap, dt)
+		if (ext5 && adv_nt() == 1) DX_TPP(1, 1);
+		else if (ext5 && adv_nt() == 0) DX_TPP(0, 1);
+		else if (adv_nt() == 1) DX_TPP(1, 0);
+		else if (adv_nt() == 2) DX_TPP(2, 0);
+		else if (adv_nt() == 3) DX_TPP(3, 0);
+		else DX_TPP(0, 0);
 #undef DX_TPP
 		HIP_CHECK(hipGetLastError());
 		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));

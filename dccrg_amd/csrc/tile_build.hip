@@ -130,7 +130,8 @@ __device__ uint32_t local_index(uint32_t n, uint32_t ts, uint32_t te, uint32_t T
 __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
                                 const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext,
                                 const uint32_t* __restrict__ fine_idx, const uint32_t* __restrict__ fine_base,
-                                uint32_t* __restrict__ tell, uint32_t* __restrict__ tfine, int* err) {
+                                uint32_t* __restrict__ tell, uint32_t* __restrict__ tfine, uint32_t* __restrict__ ext_ax,
+                                int* err) {
 	for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < tg.n_local; r += gridDim.x * blockDim.x) {
 		uint32_t gt, ts, te;
 		tg.of(r, gt, ts, te);
@@ -143,11 +144,18 @@ __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restr
 			const int d = ent[e] & 7;
 			uint32_t k = e + 1;
 			while (k < eend && (ent[k] & 7) == d) k++;
+			// axes through which each ext cell is reached (its velocity
+			// component along them is the only one a face reads)
+			const uint32_t axbit = 1u << (d >> 1);
 			if (k - e == 1) {
 				code[d] = local_index(uint32_t(ent[e] >> 3), ts, te, T, ext, e0, e1, err);
+				if (code[d] >= T) atomicOr(&ext_ax[e0 + code[d] - T], axbit);
 			} else {
 				uint32_t li[4];
-				for (int i = 0; i < 4; i++) li[i] = local_index(uint32_t(ent[e + i] >> 3), ts, te, T, ext, e0, e1, err);
+				for (int i = 0; i < 4; i++) {
+					li[i] = local_index(uint32_t(ent[e + i] >> 3), ts, te, T, ext, e0, e1, err);
+					if (li[i] >= T) atomicOr(&ext_ax[e0 + li[i] - T], axbit);
+				}
 				tfine[2 * size_t(fk)] = li[0] | (li[1] << 16);
 				tfine[2 * size_t(fk) + 1] = li[2] | (li[3] << 16);
 				code[d] = 0x8000u | (fk - fine_base[gt]);
@@ -307,12 +315,18 @@ static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, ui
 	}
 }
 
+__global__ void pack_ext_kernel(const uint32_t* __restrict__ ext, const uint32_t* __restrict__ ax, size_t m,
+                                uint32_t* __restrict__ out) {
+	for (size_t k = blockIdx.x * size_t(blockDim.x) + threadIdx.x; k < m; k += size_t(gridDim.x) * blockDim.x)
+		out[k] = ext[k] | (ax[k] << 29);
+}
+
 TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& mc,
                         bool morton, size_t n_inner, size_t n_local, int tile, DBuf<uint32_t>& tstart,
-                        DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext,
+                        DBuf<uint32_t>& tell, DBuf<uint32_t>& ext_ptr, DBuf<uint32_t>& ext, DBuf<uint32_t>& ext_pk,
                         DBuf<uint32_t>& fine_base, DBuf<uint32_t>& tfine, hipStream_t s) {
 	DX_REQUIRE(tile > 0 && tile <= 4096, "tile size out of range");
-	DX_REQUIRE(n_local < (size_t(1) << 31), "too many local cells for 32-bit slots");
+	DX_REQUIRE(n_local < (size_t(1) << 29), "too many local cells for 29-bit tile slots");
 	TileBuild out{};
 	const uint32_t T = uint32_t(tile);
 	std::vector<uint8_t> al;
@@ -340,6 +354,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		HIP_CHECK(hipMemsetAsync(ext_ptr.p, 0, 4, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		ext.alloc(1);
+		ext_pk.alloc(1);
 		tfine.alloc(2);
 		return out;
 	}
@@ -383,8 +398,15 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	DBuf<int> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	DBuf<uint32_t> ext_ax;
+	ext_ax.alloc(m + 1);
+	HIP_CHECK(hipMemsetAsync(ext_ax.p, 0, (m + 1) * 4, s));
 	tile_ell_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(tg, T, face_ptr, face_ent, ext_ptr.p, ext.p, fine_idx.p,
-	                                                       fine_base.p, tell.p, tfine.p, err.p);
+	                                                       fine_base.p, tell.p, tfine.p, ext_ax.p, err.p);
+	HIP_CHECK(hipGetLastError());
+	// ext slots with their axis mask in bits 29..31 (slots < 2^29)
+	ext_pk.alloc(m + 1);
+	pack_ext_kernel<<<grid_for(m, 256), 256, 0, s>>>(ext.p, ext_ax.p, m, ext_pk.p);
 	HIP_CHECK(hipGetLastError());
 	int herr = 0;
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));

@@ -64,6 +64,11 @@ _SIGS = {
     "dccrgx_unpin": (C.c_int, [vp, u64]),
     "dccrgx_balance_load": (C.c_int, [vp]),
     "dccrgx_balance_load_to": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_add_neighborhood": (C.c_int, [vp, C.c_int, vp, sz]),
+    "dccrgx_remove_neighborhood": (C.c_int, [vp, C.c_int]),
+    "dccrgx_get_user_neighbors": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_int, vp, vp, sz, P(sz)]),
+    "dccrgx_get_user_update_list": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, sz, P(sz)]),
+    "dccrgx_update_copies_of_remote_neighbors_hood": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_cell_process": (C.c_int, [vp, vp, vp, sz, P(sz)]),
     "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
     "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),

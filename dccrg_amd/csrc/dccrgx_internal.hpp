@@ -153,6 +153,25 @@ struct RegTileMeta {
 	uint32_t pad;
 };
 
+// A user neighborhood (add_neighborhood, dccrg.hpp:6383-6520): its offsets,
+// neighbors_of / neighbors_to CSR of the local cells (built lazily after
+// every structural change, update_user_neighbors 8974-8980) and its
+// per-peer send / receive lists (recalculate_neighbor_update_send_receive_lists
+// for the id, 8590-8752), with their slots for the halo over this hood only.
+struct UserHood {
+	std::vector<int32_t> of, to;  // 3 per item; to = -of
+	DBuf<int32_t> d_of, d_to;
+	bool valid = false;
+	DBuf<uint32_t> nof_ptr, nto_ptr;
+	DBuf<uint64_t> nof_id, nto_id;
+	DBuf<int32_t> nof_off;
+	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
+	std::map<int, size_t> send_off, recv_off;
+	size_t n_send = 0, n_recv = 0;
+	DBuf<int32_t> send_slots, recv_slots;
+	DBuf<uint8_t> sendbuf, recvbuf;
+};
+
 struct Grid {
 	// communicator
 	int rank = 0, size = 1, device = 0;
@@ -239,6 +258,7 @@ struct Grid {
 	// nst[6] (regular: neighbor-box starts), kind (1 regular), pad; for the
 	// fused sweep over both kinds (empty when a tile exceeds its limits)
 	DBuf<uint32_t> tfmeta;
+	std::map<int, UserHood> uhoods;  // add_neighborhood ids
 	DBuf<uint64_t> gol_l0p;  // refined game of life: level-0 parent per slot (scratch)
 	// halo
 	DBuf<int32_t> send_slots;

@@ -305,6 +305,7 @@ static void rebuild(Grid& g) {
 	g.tiles_valid = false;
 	g.slot_ids_h_valid = false;
 	g.po.valid = false;
+	for (auto& kv : g.uhoods) kv.second.valid = false;
 }
 
 // full neighbors_of / neighbors_to / iterator CSR for all local rows
@@ -560,6 +561,152 @@ static void halo_wait(Grid& g) {
 	if (!g.halo_in_flight) return;
 	HIP_CHECK(hipStreamWaitEvent(g.s_comp, g.ev_halo, 0));
 	g.halo_in_flight = false;
+}
+
+// --------------------------------------------------------------------------- user neighborhoods
+// neighbors of / to every local cell for hood id (find_neighbors_of /
+// find_neighbors_to with user_hood_of / user_hood_to, 8974-8980), then the
+// send / receive lists of the id: receive from p = the cells of p in the
+// neighbors_of of local cells, send to p = the local cells in whose
+// neighbors_to a cell of p appears, both ascending (the wire order)
+static UserHood& ensure_uhood(Grid& g, int id) {
+	auto it = g.uhoods.find(id);
+	DX_REQUIRE(it != g.uhoods.end(), "no such neighborhood id");
+	UserHood& h = it->second;
+	if (h.valid) return h;
+	hipStream_t s = g.s_comp;
+	const int nh = int(h.of.size() / 3);
+	const size_t nl = g.n_local;
+	DBuf<uint32_t> c_of, c_to;
+	c_of.alloc(nl + 1);
+	c_to.alloc(nl + 1);
+	h.nof_ptr.alloc(nl + 1);
+	h.nto_ptr.alloc(nl + 1);
+	k_count_rows(g.m, h.d_of.p, h.d_to.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, c_of.p, c_to.p, s);
+	const size_t t_of = scan_exclusive_u32(c_of.p, h.nof_ptr.p, nl, s);
+	const size_t t_to = scan_exclusive_u32(c_to.p, h.nto_ptr.p, nl, s);
+	h.nof_id.alloc(t_of + 1);
+	h.nof_off.alloc(3 * t_of + 3);
+	h.nto_id.alloc(t_to + 1);
+	k_fill_neighbors_of(g.m, h.d_of.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, h.nof_ptr.p, h.nof_id.p, h.nof_off.p,
+	                    s);
+	k_fill_neighbors_to(g.m, h.d_to.p, nh, g.owner_by_id.p, g.slot_ids.p, 0, nl, h.nto_ptr.p, h.nto_id.p, s);
+	h.send_ids.clear();
+	h.recv_ids.clear();
+	if (g.size > 1) {
+		const auto pof = download(h.nof_ptr.p, nl + 1, s);
+		const auto pto = download(h.nto_ptr.p, nl + 1, s);
+		const auto iof = download(h.nof_id.p, t_of, s);
+		const auto ito = download(h.nto_id.p, t_to, s);
+		const auto& sid = slot_ids_host(g);
+		std::map<int, std::vector<uint64_t>> snd, rcv;
+		for (size_t r = 0; r < nl; r++) {
+			for (uint32_t j = pof[r]; j < pof[r + 1]; j++) {
+				const int o = host_owner(g, iof[j]);
+				if (o >= 0 && o != g.rank) rcv[o].push_back(iof[j]);
+			}
+			for (uint32_t j = pto[r]; j < pto[r + 1]; j++) {
+				const int o = host_owner(g, ito[j]);
+				if (o >= 0 && o != g.rank) snd[o].push_back(sid[r]);
+			}
+		}
+		auto uniq = [](std::map<int, std::vector<uint64_t>>& mp) {
+			for (auto& kv : mp) {
+				std::sort(kv.second.begin(), kv.second.end());
+				kv.second.erase(std::unique(kv.second.begin(), kv.second.end()), kv.second.end());
+			}
+		};
+		uniq(snd);
+		uniq(rcv);
+		h.send_ids = snd;
+		h.recv_ids = rcv;
+	}
+	std::vector<uint64_t> sall, rall;
+	h.send_off.clear();
+	h.recv_off.clear();
+	for (auto& kv : h.send_ids) {
+		h.send_off[kv.first] = sall.size();
+		sall.insert(sall.end(), kv.second.begin(), kv.second.end());
+	}
+	for (auto& kv : h.recv_ids) {
+		h.recv_off[kv.first] = rall.size();
+		rall.insert(rall.end(), kv.second.begin(), kv.second.end());
+	}
+	h.n_send = sall.size();
+	h.n_recv = rall.size();
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	h.send_slots.alloc(h.n_send + 1);
+	h.recv_slots.alloc(h.n_recv + 1);
+	if (h.n_send) {
+		DBuf<uint64_t> d;
+		upload(d, sall, s);
+		k_lookup_slots(d.p, h.n_send, g.slot_by_id.p, h.send_slots.p, err.p, s);
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	if (h.n_recv) {
+		DBuf<uint64_t> d;
+		upload(d, rall, s);
+		k_lookup_slots(d.p, h.n_recv, g.slot_by_id.p, h.recv_slots.p, err.p, s);
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	int herr = 0;
+	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(herr == 0, "user neighborhood references a cell without a local slot or remote copy");
+	h.valid = true;
+	return h;
+}
+
+// update_copies_of_remote_neighbors(id) (966-1000 with a user id): every
+// transferred field's payload of the id's send lists, packed in wire order,
+// grouped RCCL send / recv per peer, unpacked into the halo slots of the
+// id's receive lists; the compute stream waits for it
+static void uhood_halo(Grid& g, int id) {
+	UserHood& h = ensure_uhood(g, id);
+	if (g.size == 1 || (h.send_ids.empty() && h.recv_ids.empty())) return;
+	DX_REQUIRE(g.comm, "halo exchange needs a communicator (grid created without an RCCL id)");
+	DX_REQUIRE(!g.halo_in_flight, "remote neighbor update already in flight");
+	std::vector<Field*> tf;
+	size_t bpc = 0;
+	for (auto& f : g.fields)
+		if (f.transfer) {
+			tf.push_back(&f);
+			bpc += f.elem;
+		}
+	if (tf.empty()) return;
+	if (h.sendbuf.n < h.n_send * bpc + 1) h.sendbuf.alloc(h.n_send * bpc + 1);
+	if (h.recvbuf.n < h.n_recv * bpc + 1) h.recvbuf.alloc(h.n_recv * bpc + 1);
+	HIP_CHECK(hipEventRecord(g.ev_comp, g.s_comp));
+	HIP_CHECK(hipStreamWaitEvent(g.s_comm, g.ev_comp, 0));
+	std::vector<size_t> so, ro;
+	size_t a = 0, b = 0;
+	for (Field* f : tf) {
+		so.push_back(a);
+		ro.push_back(b);
+		k_pack(f->data.p, f->elem, h.send_slots.p, h.n_send, h.sendbuf.p + a, g.s_comm);
+		a += h.n_send * f->elem;
+		b += h.n_recv * f->elem;
+	}
+	NCCL_CHECK(ncclGroupStart());
+	for (size_t k = 0; k < tf.size(); k++) {
+		const size_t e = tf[k]->elem;
+		for (auto& kv : h.send_ids)
+			NCCL_CHECK(ncclSend(h.sendbuf.p + so[k] + h.send_off[kv.first] * e, kv.second.size() * e, ncclUint8,
+			                    kv.first, g.comm, g.s_comm));
+		for (auto& kv : h.recv_ids)
+			NCCL_CHECK(ncclRecv(h.recvbuf.p + ro[k] + h.recv_off[kv.first] * e, kv.second.size() * e, ncclUint8,
+			                    kv.first, g.comm, g.s_comm));
+	}
+	NCCL_CHECK(ncclGroupEnd());
+	for (size_t k = 0; k < tf.size(); k++) {
+		unpack_kernel<<<grid_for(h.n_recv * tf[k]->elem, 256), 256, 0, g.s_comm>>>(
+		    h.recvbuf.p + ro[k], tf[k]->elem, h.recv_slots.p, h.n_recv, tf[k]->data.p);
+		HIP_CHECK(hipGetLastError());
+	}
+	HIP_CHECK(hipEventRecord(g.ev_halo, g.s_comm));
+	HIP_CHECK(hipStreamWaitEvent(g.s_comp, g.ev_halo, 0));
 }
 
 // --------------------------------------------------------------------------- collectives
@@ -1468,6 +1615,97 @@ int dccrgx_unpin(dccrgx_grid* gp, uint64_t cell) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		g.pins.erase(cell);
+		return 0;
+	});
+}
+
+int dccrgx_add_neighborhood(dccrgx_grid* gp, int id, const int32_t* offsets, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		// add_neighborhood 6383-6520: the reference returns false for these
+		DX_REQUIRE(id != DCCRGX_DEFAULT_HOOD, "neighborhood id is the default id");
+		DX_REQUIRE(!g.uhoods.count(id), "neighborhood id already exists");
+		for (size_t i = 0; i < n; i++) {
+			const int32_t* o = offsets + 3 * i;
+			if (g.hood_len > 0) {
+				for (int d = 0; d < 3; d++)
+					DX_REQUIRE(unsigned(std::abs(o[d])) <= g.hood_len, "offset outside the default neighborhood");
+				DX_REQUIRE(o[0] || o[1] || o[2], "offset (0, 0, 0)");
+			} else {
+				int zeros = 0;
+				for (int d = 0; d < 3; d++) {
+					zeros += o[d] == 0;
+					DX_REQUIRE(std::abs(o[d]) <= 1, "offset outside the face neighborhood");
+				}
+				DX_REQUIRE(zeros == 2, "face neighborhood offsets must be unit face offsets");
+			}
+		}
+		UserHood& h = g.uhoods[id];
+		h.of.assign(offsets, offsets + 3 * n);
+		h.to.resize(h.of.size());
+		for (size_t i = 0; i < h.of.size(); i++) h.to[i] = -h.of[i];
+		upload(h.d_of, h.of, g.s_comp);
+		upload(h.d_to, h.to, g.s_comp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		ensure_uhood(g, id);
+		return 0;
+	});
+}
+
+int dccrgx_remove_neighborhood(dccrgx_grid* gp, int id) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.uhoods.erase(id);
+		return 0;
+	});
+}
+
+int dccrgx_get_user_neighbors(dccrgx_grid* gp, int id, uint64_t cell, int kind, uint64_t* ids, int32_t* offs,
+                              size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (!g.uhoods.count(id)) return DCCRGX_ENOTFOUND;
+		const int64_t s = slot_of(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		UserHood& h = ensure_uhood(g, id);
+		const DBuf<uint32_t>& ptr = kind == 0 ? h.nof_ptr : h.nto_ptr;
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) {
+			HIP_CHECK(hipMemcpy(ids, (kind == 0 ? h.nof_id.p : h.nto_id.p) + be[0], k * 8, hipMemcpyDeviceToHost));
+			if (offs && kind == 0)
+				HIP_CHECK(hipMemcpy(offs, h.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_get_user_update_list(dccrgx_grid* gp, int id, int peer, int receive, uint64_t* ids, size_t cap,
+                                size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (!g.uhoods.count(id)) return DCCRGX_ENOTFOUND;
+		UserHood& h = ensure_uhood(g, id);
+		const auto& mp = receive ? h.recv_ids : h.send_ids;
+		auto it = mp.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == mp.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* gp, int id) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (id == DCCRGX_DEFAULT_HOOD) {
+			halo_start(g);
+			halo_wait(g);
+		} else {
+			uhood_halo(g, id);
+		}
 		return 0;
 	});
 }

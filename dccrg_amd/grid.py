@@ -12,9 +12,10 @@ import os
 
 import numpy as np
 
-from ._lib import ENOTFOUND, ERANGE, DccrgError, check, lib
+from ._lib import EINVAL, ENOTFOUND, ERANGE, DccrgError, check, lib
 
 REGION = {"all": 0, "inner": 1, "outer": 2}
+DEFAULT_HOOD = -0xDCC  # default_neighborhood_id (dccrg.hpp:93)
 CELLS = {"local": 0, "inner": 1, "outer": 2, "remote": 3, "all": 4}
 CSR_KIND = {"of": 0, "to": 1, "face": 2, "iterator": 3}
 
@@ -210,9 +211,12 @@ class Dccrg:
     def slot_ids(self):
         return self._u64_query(lib().dccrgx_get_slot_ids)
 
-    def get_neighbors_of(self, cell):
+    def get_neighbors_of(self, cell, hood=None):
         """[(id, (x, y, z)), ...] in stencil order (get_neighbors_of, 819), or
-        None for a cell that is not local (the reference returns nullptr)."""
+        None for a cell that is not local or an unknown neighborhood id (the
+        reference returns nullptr).  hood: a user neighborhood id."""
+        if hood is not None and hood != DEFAULT_HOOD:
+            return self._user_neighbors(cell, hood, 0)
         n = C.c_size_t()
         cap = 4096
         ids = np.empty(cap, np.uint64)
@@ -224,7 +228,9 @@ class Dccrg:
         k = n.value
         return [(int(ids[i]), tuple(int(v) for v in offs[3 * i: 3 * i + 3])) for i in range(k)]
 
-    def get_neighbors_to(self, cell):
+    def get_neighbors_to(self, cell, hood=None):
+        if hood is not None and hood != DEFAULT_HOOD:
+            return self._user_neighbors(cell, hood, 1)
         n = C.c_size_t()
         cap = 8192
         ids = np.empty(cap, np.uint64)
@@ -233,6 +239,48 @@ class Dccrg:
             return None
         check(rc)
         return [(int(i), (0, 0, 0)) for i in ids[: n.value]]
+
+    def _user_neighbors(self, cell, hood, kind):
+        n = C.c_size_t()
+        rc = lib().dccrgx_get_user_neighbors(self.h, int(hood), int(cell), kind, None, None, 0, C.byref(n))
+        if rc == ENOTFOUND:
+            return None
+        if rc not in (0, ERANGE):
+            check(rc)
+        k = n.value
+        ids = np.empty(max(k, 1), np.uint64)
+        offs = np.empty(3 * max(k, 1), np.int32)
+        check(lib().dccrgx_get_user_neighbors(self.h, int(hood), int(cell), kind, _ptr(ids), _ptr(offs), k,
+                                              C.byref(n)))
+        if kind == 1:
+            return [(int(i), (0, 0, 0)) for i in ids[:k]]
+        return [(int(ids[i]), tuple(int(v) for v in offs[3 * i: 3 * i + 3])) for i in range(k)]
+
+    # ---- user neighborhoods (add_neighborhood, dccrg.hpp:6383) -----------------------
+    def add_neighborhood(self, hood, offsets):
+        """True if the neighborhood was added; False where the reference
+        returns false (default / existing id, offset outside the default
+        neighborhood or (0,0,0))."""
+        o = np.ascontiguousarray(np.asarray(offsets, np.int32).reshape(-1, 3))
+        rc = lib().dccrgx_add_neighborhood(self.h, int(hood), _ptr(o), o.shape[0])
+        if rc == EINVAL:
+            return False
+        check(rc)
+        return True
+
+    def remove_neighborhood(self, hood):
+        check(lib().dccrgx_remove_neighborhood(self.h, int(hood)))
+        return self
+
+    def _user_list(self, hood, peer, receive):
+        n = C.c_size_t()
+        rc = lib().dccrgx_get_user_update_list(self.h, int(hood), int(peer), int(receive), None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        out = np.empty(max(n.value, 1), np.uint64)
+        check(lib().dccrgx_get_user_update_list(self.h, int(hood), int(peer), int(receive), _ptr(out), n.value,
+                                                C.byref(n)))
+        return out[: n.value].copy()
 
     def get_face_neighbors_of(self, cell):
         n = C.c_size_t()
@@ -288,10 +336,14 @@ class Dccrg:
         check(lib().dccrgx_get_peers(self.h, _ptr(buf), buf.size, C.byref(n)))
         return [int(x) for x in buf[: n.value]]
 
-    def get_cells_to_send(self, peer):
+    def get_cells_to_send(self, peer, hood=None):
+        if hood is not None and hood != DEFAULT_HOOD:
+            return self._user_list(hood, peer, 0)
         return self._u64_query(lib().dccrgx_get_cells_to_send, int(peer))
 
-    def get_cells_to_receive(self, peer):
+    def get_cells_to_receive(self, peer, hood=None):
+        if hood is not None and hood != DEFAULT_HOOD:
+            return self._user_list(hood, peer, 1)
         return self._u64_query(lib().dccrgx_get_cells_to_receive, int(peer))
 
     def get_number_of_update_send_cells(self):
@@ -369,7 +421,10 @@ class Dccrg:
         return f
 
     # ---- halo -------------------------------------------------------------------
-    def update_copies_of_remote_neighbors(self):
+    def update_copies_of_remote_neighbors(self, hood=None):
+        if hood is not None and hood != DEFAULT_HOOD:
+            check(lib().dccrgx_update_copies_of_remote_neighbors_hood(self.h, int(hood)))
+            return True
         check(lib().dccrgx_update_copies_of_remote_neighbors(self.h))
         return True
 

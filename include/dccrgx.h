@@ -135,6 +135,21 @@ int dccrgx_get_new_cells(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t
  * an external partitioner); payloads of cells that stay local are kept. */
 int dccrgx_set_cells(dccrgx_grid* g, const uint64_t* ids, const int32_t* owners, size_t n);
 
+/* ---- user neighborhoods (add_neighborhood 6383-6520, remove_neighborhood
+ * 6530-6570, get_neighbors_of/_to(cell, id) 819/883, the id's
+ * cells_to_send / _receive, update_copies_of_remote_neighbors(id) 966).
+ * Offsets: 3 x int32 per item, within the default neighborhood (face
+ * offsets when its length is 0), never (0,0,0); a rejected set returns
+ * DCCRGX_EINVAL where the reference returns false.  Identical calls on every
+ * rank.  kind 0 = neighbors_of (offsets filled), 1 = neighbors_to. */
+#define DCCRGX_DEFAULT_HOOD -0xDCC  /* default_neighborhood_id (dccrg.hpp:93) */
+int dccrgx_add_neighborhood(dccrgx_grid* g, int id, const int32_t* offsets, size_t n);
+int dccrgx_remove_neighborhood(dccrgx_grid* g, int id);
+int dccrgx_get_user_neighbors(dccrgx_grid* g, int id, uint64_t cell, int kind, uint64_t* ids, int32_t* offsets,
+                              size_t cap, size_t* n);
+int dccrgx_get_user_update_list(dccrgx_grid* g, int id, int peer, int receive, uint64_t* ids, size_t cap, size_t* n);
+int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* g, int id);
+
 /* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024) ------------
  * balance_load applies the pinned owners (no third-party partitioner:
  * Zoltan is out of scope), migrates every field of moved cells over RCCL and

@@ -505,7 +505,7 @@ def main():
                 "unit": "GB/s",
                 "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
                 "traffic": traffic,
-                "kernel": "advection_regular_kernel + advection_tiles_kernel" if variant == 11
+                "kernel": "advection_regular_pp_kernel + advection_tiles_pp_kernel" if variant == 11
                           else f"advection_kernel variant {variant}",
                 "layout": layout,
                 "alg_bytes_per_step": alg_bytes_step,

@@ -49,84 +49,6 @@ __global__ void gol_csr_kernel(const uint32_t* __restrict__ state, uint32_t* __r
 	}
 }
 
-// Game of life, uniform grid (R = 0), one rank, neighborhood length 1: slot ==
-// id - 1 == x + nx*(y + ny*z).  A workgroup owns a TX x TY column tile and
-// marches up a z chunk; each plane is staged once into LDS with a one-cell
-// ring, the 3x3 in-plane sums of three consecutive planes stay in registers,
-// and count(z) = S(z-1) + S(z) + S(z+1) - state(z).
-constexpr int GTX = 64, GTY = 8, GZC = 32;
-
-__global__ __launch_bounds__(GTX* GTY) void gol_structured_kernel(const uint32_t* __restrict__ st,
-                                                                   uint32_t* __restrict__ out, int nx, int ny, int nz,
-                                                                   int px, int py, int pz) {
-	__shared__ uint32_t tile[GTY + 2][GTX + 2];
-	const int tx = threadIdx.x % GTX, ty = threadIdx.x / GTX;
-	const int x0 = blockIdx.x * GTX, y0 = blockIdx.y * GTY, z0 = blockIdx.z * GZC;
-	const int x = x0 + tx, y = y0 + ty;
-	const int z1 = min(z0 + GZC, nz);
-	const size_t plane = size_t(nx) * ny;
-
-	auto load_plane = [&](int z) -> void {
-		// returns via LDS; z may be outside [0, nz)
-		bool zin = true;
-		int zz = z;
-		if (zz < 0 || zz >= nz) {
-			if (pz) zz = (zz + nz) % nz;
-			else zin = false;
-		}
-		for (int i = threadIdx.x; i < (GTX + 2) * (GTY + 2); i += GTX * GTY) {
-			const int ly = i / (GTX + 2), lx = i % (GTX + 2);
-			int gx = x0 + lx - 1, gy = y0 + ly - 1;
-			bool in = zin;
-			if (gx < 0 || gx >= nx) {
-				if (px) gx = (gx + nx) % nx;
-				else in = false;
-			}
-			if (gy < 0 || gy >= ny) {
-				if (py) gy = (gy + ny) % ny;
-				else in = false;
-			}
-			tile[ly][lx] = in ? (st[size_t(zz) * plane + size_t(gy) * nx + gx] > 0 ? 1u : 0u) : 0u;
-		}
-	};
-	auto sum9 = [&]() -> uint32_t {
-		uint32_t s = 0;
-#pragma unroll
-		for (int dy = 0; dy < 3; dy++)
-#pragma unroll
-			for (int dx = 0; dx < 3; dx++) s += tile[ty + dy][tx + dx];
-		return s;
-	};
-
-	uint32_t s_prev, s_cur, c_cur;
-	load_plane(z0 - 1);
-	__syncthreads();
-	s_prev = sum9();
-	__syncthreads();
-	load_plane(z0);
-	__syncthreads();
-	s_cur = sum9();
-	c_cur = tile[ty + 1][tx + 1];
-	__syncthreads();
-	const bool active = x < nx && y < ny;
-	for (int z = z0; z < z1; z++) {
-		load_plane(z + 1);
-		__syncthreads();
-		const uint32_t s_next = sum9();
-		const uint32_t c_next = tile[ty + 1][tx + 1];
-		__syncthreads();
-		if (active) {
-			const uint32_t cnt = s_prev + s_cur + s_next - c_cur;
-			const size_t idx = size_t(z) * plane + size_t(y) * nx + x;
-			const uint32_t cur = st[idx];
-			out[idx] = cnt == 3 ? 1u : (cnt == 2 ? cur : 0u);
-		}
-		s_prev = s_cur;
-		s_cur = s_next;
-		c_cur = c_next;
-	}
-}
-
 // Barrier-free variant: a wavefront owns one x-run of 64 lanes (62 outputs,
 // lanes 0 and 63 only feed their neighbors) on one y row and marches up z.
 // Per plane each lane loads its column (y-1, y, y+1: three coalesced row
@@ -361,255 +283,6 @@ __global__ void advection_kernel(const double* __restrict__ rho, const double* _
 	}
 }
 
-// Same face flux, one thread per cell, no grid-stride: a workgroup maps to a
-// contiguous run of slots, and the runs are dealt so that the 8 XCDs each
-// sweep one contiguous eighth of the slot range (blocks b and b+8 share an
-// XCD: logical block = (b % 8) * (nb / 8) + b / 8), keeping the z-neighbor
-// planes of a chunk in that XCD's L2.  Faces are processed in batches of 4
-// with all their gathers issued before any flux is evaluated, so a thread
-// has up to 20 independent loads in flight instead of a dependent chain.
-constexpr int ADV_BLOCK = 256;
-constexpr int ADV_BATCH = 4;
-
-__global__ __launch_bounds__(ADV_BLOCK) void advection_kernel_v1(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ ptr,
-    const int32_t* __restrict__ ent, size_t s0, size_t s1, double dt, unsigned nb_real) {
-#pragma clang fp contract(off)
-	const unsigned nb = gridDim.x;  // multiple of 8
-	const unsigned b = blockIdx.x;
-	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (lb >= nb_real) return;
-	const size_t s = s0 + size_t(lb) * ADV_BLOCK + threadIdx.x;
-	if (s >= s1) return;
-	const double cd = rho[s];
-	const double clx = lx[s], cly = ly[s], clz = lz[s];
-	const double cvx = vx[s], cvy = vy[s], cvz = vz[s];
-	const double cv = clx * cly * clz;
-	double acc = 0;
-	const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
-	for (uint32_t e = e0; e < e1; e += ADV_BATCH) {
-		int32_t en[ADV_BATCH];
-		double nd[ADV_BATCH], nlx[ADV_BATCH], nly[ADV_BATCH], nlz[ADV_BATCH], nv[ADV_BATCH];
-#pragma unroll
-		for (int k = 0; k < ADV_BATCH; k++) en[k] = (e + k < e1) ? ent[e + k] : -1;
-#pragma unroll
-		for (int k = 0; k < ADV_BATCH; k++) {
-			if (en[k] < 0) continue;
-			const int32_t n = en[k] >> 3;
-			const int dir = en[k] & 7;
-			nd[k] = rho[n];
-			nlx[k] = lx[n];
-			nly[k] = ly[n];
-			nlz[k] = lz[n];
-			nv[k] = dir < 2 ? vx[n] : (dir < 4 ? vy[n] : vz[n]);
-		}
-#pragma unroll
-		for (int k = 0; k < ADV_BATCH; k++) {
-			if (en[k] < 0) continue;
-			const int dir = en[k] & 7;
-			double min_area, v;
-			if (dir < 2) {
-				min_area = fmin(cly * clz, nly[k] * nlz[k]);
-				v = (clx * nv[k] + nlx[k] * cvx) / (clx + nlx[k]);
-			} else if (dir < 4) {
-				min_area = fmin(clx * clz, nlx[k] * nlz[k]);
-				v = (cly * nv[k] + nly[k] * cvy) / (cly + nly[k]);
-			} else {
-				min_area = fmin(clx * cly, nlx[k] * nly[k]);
-				v = (clz * nv[k] + nlz[k] * cvz) / (clz + nlz[k]);
-			}
-			double flux;
-			if (dir & 1) {
-				flux = (v >= 0 ? cd : nd[k]) * dt * v * min_area;
-				acc -= flux / cv;
-			} else {
-				flux = (v >= 0 ? nd[k] : cd) * dt * v * min_area;
-				acc += flux / cv;
-			}
-		}
-	}
-	rho_out[s] = cd + acc;
-}
-
-// Fixed-width face table (6 int32 per cell, see face_ell_kernel): the whole
-// row is known after one load, so the 30 gathers of a cell's six regular
-// faces are all issued before the first flux is evaluated (a missing face
-// gathers the cell itself and is skipped).  Finer faces (4 cells) take a
-// second dependent step through the overflow table.  Faces are accumulated
-// in the reference's face order (dir -x,+x,-y,+y,-z,+z; the 4 finer cells in
-// get_face_neighbors_of order), bitwise equal to advection_kernel.
-__device__ __forceinline__ double adv_face(int dir, double cd, double clx, double cly, double clz, double cvx,
-                                           double cvy, double cvz, double cv, double nd, double nlx, double nly,
-                                           double nlz, double nv, double dt) {
-#pragma clang fp contract(off)
-	double min_area, v;
-	if (dir < 2) {
-		min_area = fmin(cly * clz, nly * nlz);
-		v = (clx * nv + nlx * cvx) / (clx + nlx);
-	} else if (dir < 4) {
-		min_area = fmin(clx * clz, nlx * nlz);
-		v = (cly * nv + nly * cvy) / (cly + nly);
-	} else {
-		min_area = fmin(clx * cly, nlx * nly);
-		v = (clz * nv + nlz * cvz) / (clz + nlz);
-	}
-	if (dir & 1) return -(((v >= 0 ? cd : nd) * dt * v * min_area) / cv);
-	return ((v >= 0 ? nd : cd) * dt * v * min_area) / cv;
-}
-
-__global__ __launch_bounds__(ADV_BLOCK) void advection_kernel_v2(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
-    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt, unsigned nb_real) {
-#pragma clang fp contract(off)
-	const unsigned nb = gridDim.x;
-	const unsigned b = blockIdx.x;
-	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (lb >= nb_real) return;
-	const size_t s = s0 + size_t(lb) * ADV_BLOCK + threadIdx.x;
-	if (s >= s1) return;
-	int32_t row[6];
-	{
-		const int2* r2 = reinterpret_cast<const int2*>(ell + 6 * s);
-		const int2 a = r2[0], bb = r2[1], c = r2[2];
-		row[0] = a.x; row[1] = a.y; row[2] = bb.x; row[3] = bb.y; row[4] = c.x; row[5] = c.y;
-	}
-	const double cd = rho[s];
-	const double clx = lx[s], cly = ly[s], clz = lz[s];
-	const double cvx = vx[s], cvy = vy[s], cvz = vz[s];
-	const double cv = clx * cly * clz;
-	double nd[6], nlx[6], nly[6], nlz[6], nv[6];
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		const size_t n = row[d] >= 0 ? size_t(row[d]) : s;
-		nd[d] = rho[n];
-		nlx[d] = lx[n];
-		nly[d] = ly[n];
-		nlz[d] = lz[n];
-		nv[d] = d < 2 ? vx[n] : (d < 4 ? vy[n] : vz[n]);
-	}
-	double acc = 0;
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		if (row[d] >= 0) {
-			acc += adv_face(d, cd, clx, cly, clz, cvx, cvy, cvz, cv, nd[d], nlx[d], nly[d], nlz[d], nv[d], dt);
-		} else if (row[d] <= -2) {
-			const int4 q = reinterpret_cast<const int4*>(fine)[-2 - row[d]];
-			const int32_t fs[4] = {q.x, q.y, q.z, q.w};
-			double fd[4], fx[4], fy[4], fz[4], fv[4];
-#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				fd[k] = rho[fs[k]];
-				fx[k] = lx[fs[k]];
-				fy[k] = ly[fs[k]];
-				fz[k] = lz[fs[k]];
-				fv[k] = d < 2 ? vx[fs[k]] : (d < 4 ? vy[fs[k]] : vz[fs[k]]);
-			}
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				acc += adv_face(d, cd, clx, cly, clz, cvx, cvy, cvz, cv, fd[k], fx[k], fy[k], fz[k], fv[k], dt);
-		}
-	}
-	rho_out[s] = cd + acc;
-}
-
-// LDS-staged variant: a workgroup sweeps ADV_TILE consecutive slots (a
-// compact region of space: slots follow the Morton curve on refined grids)
-// and first stages those cells' seven fields into LDS with coalesced loads
-// (they are the cells' own reads, so no extra HBM traffic).  A face whose
-// neighbor lies inside the tile is then served from LDS; only faces that
-// leave the tile gather from L2/HBM.
-template <int TILE, class F>
-__device__ __forceinline__ void adv_fetch(size_t n, size_t base, size_t s1, const double (*sh)[TILE],
-                                          const double* rho, const double* lx, const double* ly, const double* lz,
-                                          const double* vdir, int dirv, double& nd, double& nlx, double& nly,
-                                          double& nlz, double& nv, F) {
-	const size_t k = n - base;
-	if (k < size_t(TILE) && n < s1) {
-		nd = sh[0][k];
-		nlx = sh[4][k];
-		nly = sh[5][k];
-		nlz = sh[6][k];
-		nv = sh[1 + dirv][k];
-	} else {
-		nd = rho[n];
-		nlx = lx[n];
-		nly = ly[n];
-		nlz = lz[n];
-		nv = vdir[n];
-	}
-}
-
-template <int TILE, int MINW>
-__global__ __launch_bounds__(TILE, MINW) void advection_kernel_v3(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
-    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt, unsigned nb_real) {
-#pragma clang fp contract(off)
-	__shared__ double sh[7][TILE];
-	const unsigned nb = gridDim.x;
-	const unsigned b = blockIdx.x;
-	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (lb >= nb_real) return;  // block-uniform
-	const size_t base = s0 + size_t(lb) * TILE;
-	const size_t s = base + threadIdx.x;
-	const bool valid = s < s1;
-	double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
-	int32_t row[6] = {-1, -1, -1, -1, -1, -1};
-	if (valid) {
-		const int2* r2 = reinterpret_cast<const int2*>(ell + 6 * s);
-		const int2 a = r2[0], bb = r2[1], c = r2[2];
-		row[0] = a.x; row[1] = a.y; row[2] = bb.x; row[3] = bb.y; row[4] = c.x; row[5] = c.y;
-		cd = rho[s];
-		cvx = vx[s];
-		cvy = vy[s];
-		cvz = vz[s];
-		clx = lx[s];
-		cly = ly[s];
-		clz = lz[s];
-	}
-	sh[0][threadIdx.x] = cd;
-	sh[1][threadIdx.x] = cvx;
-	sh[2][threadIdx.x] = cvy;
-	sh[3][threadIdx.x] = cvz;
-	sh[4][threadIdx.x] = clx;
-	sh[5][threadIdx.x] = cly;
-	sh[6][threadIdx.x] = clz;
-	__syncthreads();
-	if (!valid) return;
-	const double cv = clx * cly * clz;
-	const double* vd[3] = {vx, vy, vz};
-	double nd[6], nlx[6], nly[6], nlz[6], nv[6];
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		const size_t n = row[d] >= 0 ? size_t(row[d]) : s;
-		adv_fetch(n, base, s1, sh, rho, lx, ly, lz, vd[d >> 1], d >> 1, nd[d], nlx[d], nly[d], nlz[d], nv[d], 0);
-	}
-	double acc = 0;
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		if (row[d] >= 0) {
-			acc += adv_face(d, cd, clx, cly, clz, cvx, cvy, cvz, cv, nd[d], nlx[d], nly[d], nlz[d], nv[d], dt);
-		} else if (row[d] <= -2) {
-			const int4 q = reinterpret_cast<const int4*>(fine)[-2 - row[d]];
-			const int32_t fs[4] = {q.x, q.y, q.z, q.w};
-			double fd[4], fx[4], fy[4], fz[4], fv[4];
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				adv_fetch(size_t(fs[k]), base, s1, sh, rho, lx, ly, lz, vd[d >> 1], d >> 1, fd[k], fx[k], fy[k], fz[k],
-				          fv[k], 0);
-#pragma unroll
-			for (int k = 0; k < 4; k++)
-				acc += adv_face(d, cd, clx, cly, clz, cvx, cvy, cvz, cv, fd[k], fx[k], fy[k], fz[k], fv[k], dt);
-		}
-	}
-	rho_out[s] = cd + acc;
-}
-
 // Face flux without the division by the cell volume (applied once per cell):
 // the face velocity and the upwind flux keep the reference's expression
 // (solve.hpp:169-225), so only the per-cell rounding of the sum differs.
@@ -656,75 +329,6 @@ template <int NT>
 __device__ __forceinline__ void st_out(double* __restrict__ p, uint32_t i, double v) {
 	if (NT & 1) __builtin_nontemporal_store(v, p + i);
 	else p[i] = v;
-}
-
-__device__ __forceinline__ AdvNb adv_gather(const double* __restrict__ rho, const double* __restrict__ lx,
-                                            const double* __restrict__ ly, const double* __restrict__ lz,
-                                            const double* __restrict__ vdir, size_t n) {
-	const uint32_t o = uint32_t(n) << 3;
-	return AdvNb{ldo(rho, o), ldo(lx, o), ldo(ly, o), ldo(lz, o), ldo(vdir, o)};
-}
-
-// v3 with one division by the cell volume per cell instead of one per face
-template <int TILE, int MINW>
-__global__ __launch_bounds__(TILE, MINW) void advection_kernel_v6(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
-    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt, unsigned nb_real) {
-#pragma clang fp contract(off)
-	__shared__ double sh[7][TILE];
-	const unsigned nb = gridDim.x;
-	const unsigned b = blockIdx.x;
-	const unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (lb >= nb_real) return;  // block-uniform
-	const size_t base = s0 + size_t(lb) * TILE;
-	const size_t s = base + threadIdx.x;
-	const bool valid = s < s1;
-	double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
-	int32_t row[6] = {-1, -1, -1, -1, -1, -1};
-	if (valid) {
-		const int2* r2 = reinterpret_cast<const int2*>(ell + 6 * s);
-		const int2 a = r2[0], bb = r2[1], c = r2[2];
-		row[0] = a.x; row[1] = a.y; row[2] = bb.x; row[3] = bb.y; row[4] = c.x; row[5] = c.y;
-		cd = rho[s]; cvx = vx[s]; cvy = vy[s]; cvz = vz[s]; clx = lx[s]; cly = ly[s]; clz = lz[s];
-	}
-	sh[0][threadIdx.x] = cd;
-	sh[1][threadIdx.x] = cvx;
-	sh[2][threadIdx.x] = cvy;
-	sh[3][threadIdx.x] = cvz;
-	sh[4][threadIdx.x] = clx;
-	sh[5][threadIdx.x] = cly;
-	sh[6][threadIdx.x] = clz;
-	__syncthreads();
-	if (!valid) return;
-	AdvNb nb6[6];
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		const size_t n = row[d] >= 0 ? size_t(row[d]) : s;
-		const size_t k = n - base;
-		if (k < size_t(TILE) && n < s1)
-			nb6[d] = AdvNb{sh[0][k], sh[4][k], sh[5][k], sh[6][k], sh[1 + (d >> 1)][k]};
-		else
-			nb6[d] = adv_gather(rho, lx, ly, lz, d < 2 ? vx : (d < 4 ? vy : vz), n);
-	}
-	double acc = 0;
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		if (row[d] >= 0) {
-			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, nb6[d], dt);
-		} else if (row[d] <= -2) {
-			const int4 q = reinterpret_cast<const int4*>(fine)[-2 - row[d]];
-			const int32_t fs[4] = {q.x, q.y, q.z, q.w};
-			const double* vdir = d < 2 ? vx : (d < 4 ? vy : vz);
-#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				const AdvNb f = adv_gather(rho, lx, ly, lz, vdir, size_t(fs[k]));
-				acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, f, dt);
-			}
-		}
-	}
-	rho_out[s] = cd + acc / (clx * cly * clz);
 }
 
 // Tiled sweep (tables: tile_build.hip).  One workgroup per tile of at most
@@ -1557,10 +1161,7 @@ void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 		HIP_CHECK(hipGetLastError());
 		return;
 	}
-	dim3 grid(unsigned((n[0] + GTX - 1) / GTX), unsigned((n[1] + GTY - 1) / GTY), unsigned((n[2] + GZC - 1) / GZC));
-	gol_structured_kernel<<<grid, GTX * GTY, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1],
-	                                                  per[2]);
-	HIP_CHECK(hipGetLastError());
+	throw Error(DCCRGX_EINVAL, "DCCRGX_GOL_VARIANT must be 2 or 3");
 }
 
 // DCCRGX_ADV_NT: non-temporal hints of the tile sweeps (bit 0 density
@@ -1586,51 +1187,11 @@ int adv_variant() {
 
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s) {
+	// the untiled gather over the face CSR (DCCRGX_ADV_VARIANT=0; the tiled
+	// sweep is variant 11, the default)
 	if (s1 <= s0) return;
-	if (adv_variant() == 9 || adv_variant() == 10) {
-		constexpr int T = 256;
-		const size_t nb_real = (s1 - s0 + T - 1) / T;
-		const size_t nb = (nb_real + 7) / 8 * 8;
-		if (adv_variant() == 9)
-			advection_kernel_v6<T, 6><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-			                                                    face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
-		else
-			advection_kernel_v6<T, 8><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-			                                                    face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
-	} else if (adv_variant() == 6) {
-		constexpr int T = 512;
-		const size_t nb_real = (s1 - s0 + T - 1) / T;
-		const size_t nb = (nb_real + 7) / 8 * 8;
-		advection_kernel_v6<T, 4><<<unsigned(nb), T, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, face_ell,
-		                                                 face_fine, s0, s1, dt, unsigned(nb_real));
-	} else if (adv_variant() >= 3) {
-		const int tile = adv_variant() == 4 ? 256 : 512;
-		const size_t nb_real = (s1 - s0 + tile - 1) / tile;
-		const size_t nb = (nb_real + 7) / 8 * 8;
-		if (adv_variant() == 3)
-			advection_kernel_v3<512, 4><<<unsigned(nb), 512, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-			                                                           face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
-		else if (adv_variant() == 4)
-			advection_kernel_v3<256, 4><<<unsigned(nb), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-			                                                           face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
-		else
-			advection_kernel_v3<1024, 4><<<unsigned((( (s1 - s0 + 1023) / 1024) + 7) / 8 * 8), 1024, 0, s>>>(
-			    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, face_ell, face_fine, s0, s1, dt,
-			    unsigned((s1 - s0 + 1023) / 1024));
-	} else if (adv_variant() == 2) {
-		const size_t nb_real = (s1 - s0 + ADV_BLOCK - 1) / ADV_BLOCK;
-		const size_t nb = (nb_real + 7) / 8 * 8;
-		advection_kernel_v2<<<unsigned(nb), ADV_BLOCK, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-		                                                       face_ell, face_fine, s0, s1, dt, unsigned(nb_real));
-	} else if (adv_variant() == 0) {
-		advection_kernel<<<grid_for(s1 - s0, 256), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-		                                                        face_ptr, face_ent, s0, s1, dt);
-	} else {
-		const size_t nb_real = (s1 - s0 + ADV_BLOCK - 1) / ADV_BLOCK;
-		const size_t nb = (nb_real + 7) / 8 * 8;
-		advection_kernel_v1<<<unsigned(nb), ADV_BLOCK, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out,
-		                                                       face_ptr, face_ent, s0, s1, dt, unsigned(nb_real));
-	}
+	advection_kernel<<<grid_for(s1 - s0, 256), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, face_ptr,
+	                                                        face_ent, s0, s1, dt);
 	HIP_CHECK(hipGetLastError());
 }
 

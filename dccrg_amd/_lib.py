@@ -64,6 +64,8 @@ _SIGS = {
     "dccrgx_unpin": (C.c_int, [vp, u64]),
     "dccrgx_balance_load": (C.c_int, [vp]),
     "dccrgx_balance_load_to": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_save_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, vp, sz]),
+    "dccrgx_load_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, sz]),
     "dccrgx_add_neighborhood": (C.c_int, [vp, C.c_int, vp, sz]),
     "dccrgx_remove_neighborhood": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_user_neighbors": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_int, vp, vp, sz, P(sz)]),

@@ -10,6 +10,11 @@
 #include <set>
 #include <unordered_set>
 
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstring>
+
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -1245,22 +1250,26 @@ int dccrgx_set_neighborhood_length(dccrgx_grid* gp, unsigned length) {
 	});
 }
 
+static void init_impl(Grid& g) {
+	DX_REQUIRE(!g.initialized, "already initialized");
+	map_init(g.m, g.len, g.R, g.per);
+	std::vector<int32_t> h(3 * 2000);
+	const int nh = default_hood(g.hood_len, h.data());
+	g.hood.assign(h.begin(), h.begin() + 3 * nh);
+	g.hood_to.resize(g.hood.size());
+	for (size_t i = 0; i < g.hood.size(); i++) g.hood_to[i] = -g.hood[i];
+	upload(g.d_hood, g.hood, g.s_comp);
+	upload(g.d_hood_to, g.hood_to, g.s_comp);
+	g.leaves.clear();
+	g.owners.clear();
+	rebuild(g);
+	g.initialized = true;
+}
+
 int dccrgx_initialize(dccrgx_grid* gp) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		DX_REQUIRE(!g.initialized, "already initialized");
-		map_init(g.m, g.len, g.R, g.per);
-		std::vector<int32_t> h(3 * 2000);
-		const int nh = default_hood(g.hood_len, h.data());
-		g.hood.assign(h.begin(), h.begin() + 3 * nh);
-		g.hood_to.resize(g.hood.size());
-		for (size_t i = 0; i < g.hood.size(); i++) g.hood_to[i] = -g.hood[i];
-		upload(g.d_hood, g.hood, g.s_comp);
-		upload(g.d_hood_to, g.hood_to, g.s_comp);
-		g.leaves.clear();
-		g.owners.clear();
-		rebuild(g);
-		g.initialized = true;
+		init_impl(g);
 		return 0;
 	});
 }
@@ -1727,6 +1736,240 @@ int dccrgx_balance_load(dccrgx_grid* gp) {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
 		balance_load_impl(g);
+		return 0;
+	});
+}
+
+// --------------------------------------------------------------------------- grid files
+// save_grid_data / load_grid_data (dccrg.hpp:1089-1740, 1742-2425), file
+// layout 1104-1120: `offset` bytes left alone, the caller's header, uint64
+// 0x1234567890abcdef, the grid block (Mapping::write dccrg_mapping.hpp:576 =
+// 3 x uint64 length + int max_ref_lvl; the neighborhood length as unsigned;
+// Grid_Topology::write dccrg_topology.hpp:144 = 3 x uint8 periodic;
+// Cartesian_Geometry::write dccrg_cartesian_geometry.hpp:618 = int id 1 +
+// 3 x double start + 3 x double level-0 length), uint64 total cells, per
+// cell (uint64 id, uint64 absolute byte offset of its data) rank by rank,
+// then the cell data in the same order.  A cell's data = the payload of
+// every transferred field, in field order (the reference writes what
+// get_mpi_datatype describes at save time).  Cells of a rank in ascending id
+// (the reference: get_cells() order).  Every rank writes its own records with
+// pwrite at offsets it derives from the global leaf/owner knowledge, so no
+// collective is needed.
+static constexpr uint64_t kEndianCheck = 0x1234567890abcdefULL;
+static constexpr int kCartesianGeometryId = 1;
+
+static std::vector<uint8_t> grid_block(const Grid& g) {
+	std::vector<uint8_t> b;
+	auto put = [&b](const void* p, size_t n) {
+		const uint8_t* q = static_cast<const uint8_t*>(p);
+		b.insert(b.end(), q, q + n);
+	};
+	put(g.len, 24);
+	const int32_t R = g.R;
+	put(&R, 4);
+	const uint32_t hood = g.hood_len;
+	put(&hood, 4);
+	const uint8_t per[3] = {uint8_t(g.per[0] != 0), uint8_t(g.per[1] != 0), uint8_t(g.per[2] != 0)};
+	put(per, 3);
+	const int32_t gid = kCartesianGeometryId;
+	put(&gid, 4);
+	put(g.start, 24);
+	put(g.l0, 24);
+	return b;
+}
+
+static void pwrite_all(int fd, const void* p, size_t n, uint64_t off) {
+	const uint8_t* q = static_cast<const uint8_t*>(p);
+	while (n) {
+		const ssize_t w = ::pwrite(fd, q, n, off_t(off));
+		DX_REQUIRE(w > 0, "grid file write failed");
+		q += w;
+		n -= size_t(w);
+		off += uint64_t(w);
+	}
+}
+
+static void pread_all(int fd, void* p, size_t n, uint64_t off) {
+	uint8_t* q = static_cast<uint8_t*>(p);
+	while (n) {
+		const ssize_t r = ::pread(fd, q, n, off_t(off));
+		DX_REQUIRE(r > 0, "grid file truncated");
+		q += r;
+		n -= size_t(r);
+		off += uint64_t(r);
+	}
+}
+
+// cells per rank (global leaf knowledge, like cell_process)
+static std::vector<uint64_t> rank_counts(Grid& g) {
+	std::vector<uint64_t> c(size_t(g.size), 0);
+	if (implicit_mesh(g)) {
+		const uint64_t total = g.m.first[1] - 1;
+		for (int p = 0; p < g.size; p++) {
+			uint64_t f, n;
+			block_range(total, uint64_t(g.size), uint64_t(p), f, n);
+			c[size_t(p)] = n;
+		}
+	} else {
+		for (int32_t o : g.owners) c[size_t(o)]++;
+	}
+	return c;
+}
+
+int dccrgx_save_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, const void* header,
+                          size_t header_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		std::vector<Field*> tf;
+		size_t bpc = 0;
+		for (auto& f : g.fields)
+			if (f.transfer) {
+				tf.push_back(&f);
+				bpc += f.elem;
+			}
+		const int fd = ::open(path, O_CREAT | O_WRONLY, 0644);
+		DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
+		struct Closer {
+			int fd;
+			~Closer() { ::close(fd); }
+		} closer{fd};
+		uint64_t off = offset;
+		if (g.rank == 0 && header_bytes) pwrite_all(fd, header, header_bytes, off);
+		off += header_bytes;
+		if (g.rank == 0) pwrite_all(fd, &kEndianCheck, 8, off);
+		off += 8;
+		const std::vector<uint8_t> block = grid_block(g);
+		if (g.rank == 0) pwrite_all(fd, block.data(), block.size(), off);
+		off += block.size();
+		const std::vector<uint64_t> cnt = rank_counts(g);
+		uint64_t total = 0, before = 0;
+		for (int p = 0; p < g.size; p++) {
+			if (p < g.rank) before += cnt[size_t(p)];
+			total += cnt[size_t(p)];
+		}
+		if (g.rank == 0) pwrite_all(fd, &total, 8, off);
+		off += 8;
+		const uint64_t list0 = off, data0 = off + 16 * total;
+		// local cells ascending, with their slots
+		const size_t nl = g.n_local;
+		const auto& sid = slot_ids_host(g);
+		std::vector<uint32_t> order(nl);
+		for (size_t i = 0; i < nl; i++) order[i] = uint32_t(i);
+		std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sid[a] < sid[b]; });
+		std::vector<uint64_t> list(2 * nl);
+		for (size_t i = 0; i < nl; i++) {
+			list[2 * i] = sid[order[i]];
+			list[2 * i + 1] = data0 + bpc * (before + i);
+		}
+		if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
+		if (nl && bpc) {
+			std::vector<uint8_t> data(nl * bpc);
+			size_t fo = 0;
+			for (Field* f : tf) {
+				const std::vector<uint8_t> h = download(f->data.p, nl * f->elem, g.s_comp);
+				for (size_t i = 0; i < nl; i++)
+					std::memcpy(&data[i * bpc + fo], &h[size_t(order[i]) * f->elem], f->elem);
+				fo += f->elem;
+			}
+			pwrite_all(fd, data.data(), data.size(), data0 + bpc * before);
+		}
+		return 0;
+	});
+}
+
+int dccrgx_load_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, size_t header_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "load_grid_data initializes the grid: call it instead of initialize");
+		const int fd = ::open(path, O_RDONLY);
+		DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
+		struct Closer {
+			int fd;
+			~Closer() { ::close(fd); }
+		} closer{fd};
+		uint64_t off = offset + header_bytes, endian = 0;
+		pread_all(fd, &endian, 8, off);
+		DX_REQUIRE(endian == kEndianCheck, "grid file endianness check failed");
+		off += 8;
+		uint8_t blk[87];
+		pread_all(fd, blk, sizeof(blk), off);
+		off += sizeof(blk);
+		uint64_t len[3];
+		int32_t R, gid;
+		uint32_t hood;
+		double start[3], l0[3];
+		std::memcpy(len, blk, 24);
+		std::memcpy(&R, blk + 24, 4);
+		std::memcpy(&hood, blk + 28, 4);
+		std::memcpy(&gid, blk + 35, 4);
+		std::memcpy(start, blk + 39, 24);
+		std::memcpy(l0, blk + 63, 24);
+		DX_REQUIRE(gid == kCartesianGeometryId, "grid file geometry is not Cartesian_Geometry");
+		for (int d = 0; d < 3; d++) {
+			g.len[d] = len[d];
+			g.per[d] = blk[32 + d] != 0;
+			g.start[d] = start[d];
+			g.l0[d] = l0[d];
+		}
+		g.R = R;
+		g.hood_len = hood;
+		init_impl(g);
+		uint64_t total = 0;
+		pread_all(fd, &total, 8, off);
+		off += 8;
+		std::vector<uint64_t> list(2 * total);
+		if (total) pread_all(fd, list.data(), 16 * total, off);
+		std::vector<std::pair<uint64_t, uint64_t>> cells(total);
+		for (size_t i = 0; i < total; i++) cells[i] = {list[2 * i], list[2 * i + 1]};
+		std::sort(cells.begin(), cells.end());
+		// owners as load_cells (3647) produces them: the level-0 block
+		// partition (create_level_0_cells), refined cells inherit it
+		const uint64_t n0 = g.m.first[1] - 1;
+		std::vector<uint64_t> ids(total);
+		std::vector<int32_t> own(total);
+		for (size_t i = 0; i < total; i++) {
+			ids[i] = cells[i].first;
+			const uint64_t l0p = map_level0_parent(g.m, ids[i]);
+			DX_REQUIRE(l0p != error_cell, "grid file lists an invalid cell");
+			for (int p = 0; p < g.size; p++) {
+				uint64_t f, c;
+				block_range(n0, uint64_t(g.size), uint64_t(p), f, c);
+				if (l0p >= f && l0p < f + c) own[i] = p;
+			}
+		}
+		g.leaves = ids;
+		g.owners = own;
+		rebuild(g);
+		// payloads of the local cells
+		std::vector<Field*> tf;
+		size_t bpc = 0;
+		for (auto& f : g.fields)
+			if (f.transfer) {
+				tf.push_back(&f);
+				bpc += f.elem;
+			}
+		const size_t nl = g.n_local;
+		if (!nl || !bpc) return 0;
+		const auto& sid = slot_ids_host(g);
+		std::vector<uint64_t> where(nl);
+		uint64_t lo = ~uint64_t(0), hi = 0;
+		for (size_t i = 0; i < nl; i++) {
+			auto it = std::lower_bound(cells.begin(), cells.end(), std::make_pair(sid[i], uint64_t(0)));
+			DX_REQUIRE(it != cells.end() && it->first == sid[i], "local cell missing from grid file");
+			where[i] = it->second;
+			lo = std::min(lo, where[i]);
+			hi = std::max(hi, where[i] + bpc);
+		}
+		std::vector<uint8_t> raw(hi - lo);
+		pread_all(fd, raw.data(), raw.size(), lo);
+		size_t fo = 0;
+		for (Field* f : tf) {
+			std::vector<uint8_t> h(nl * f->elem);
+			for (size_t i = 0; i < nl; i++) std::memcpy(&h[i * f->elem], &raw[where[i] - lo + fo], f->elem);
+			HIP_CHECK(hipMemcpy(f->data.p, h.data(), h.size(), hipMemcpyHostToDevice));
+			fo += f->elem;
+		}
 		return 0;
 	});
 }

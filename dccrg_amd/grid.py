@@ -411,6 +411,19 @@ class Dccrg:
         check(lib().dccrgx_get_cell_process(self.h, _ptr(ids), _ptr(own), ids.size, C.byref(n)))
         return ids, own
 
+    # ---- grid files (save_grid_data 1089, load_grid_data 1742) ---------------------
+    def save_grid_data(self, path, offset=0, header=b""):
+        hb = bytes(header)
+        buf = C.create_string_buffer(hb, len(hb)) if hb else None
+        check(lib().dccrgx_save_grid_data(self.h, str(path).encode(), int(offset), buf, len(hb)))
+        return True
+
+    def load_grid_data(self, path, offset=0, header_bytes=0):
+        """Initializes this grid from a file written by save_grid_data (call
+        instead of initialize, after registering the same transferred fields)."""
+        check(lib().dccrgx_load_grid_data(self.h, str(path).encode(), int(offset), int(header_bytes)))
+        return self
+
     # ---- fields ---------------------------------------------------------------
     def add_field(self, name, dtype, transfer=True):
         fid = C.c_int()

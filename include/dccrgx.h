@@ -150,6 +150,18 @@ int dccrgx_get_user_neighbors(dccrgx_grid* g, int id, uint64_t cell, int kind, u
 int dccrgx_get_user_update_list(dccrgx_grid* g, int id, int peer, int receive, uint64_t* ids, size_t cap, size_t* n);
 int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* g, int id);
 
+/* ---- grid files (save_grid_data 1089-1740, load_grid_data 1742-2425;
+ * layout 1104-1120).  save: every rank calls it with the same arguments;
+ * rank 0 writes the header bytes at `offset`, every rank its cells' records
+ * and data (the payloads of the transferred fields, in field order).  load:
+ * on a created, not yet initialized grid whose transferred fields are
+ * registered as at save time; initializes the grid from the file (length,
+ * refinement level, neighborhood length, periodicity, geometry), creates the
+ * file's cells with the level-0 block partition inherited by children, and
+ * reads the local cells' payloads. */
+int dccrgx_save_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, const void* header, size_t header_bytes);
+int dccrgx_load_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, size_t header_bytes);
+
 /* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024) ------------
  * balance_load applies the pinned owners (no third-party partitioner:
  * Zoltan is out of scope), migrates every field of moved cells over RCCL and

@@ -314,3 +314,36 @@ class Grid:
         out = np.empty(16 * ids.size)
         self._chk(lib().or_po_get(self.h, ids, ids.size, out))
         return out.reshape(-1, 16)
+
+
+# -- grid files (save_grid_data, dccrg.hpp:1089-1740; layout 1104-1120) -------
+def grid_block_bytes(length, R, hood, periodic, start, l0):
+    """The internal grid data block: Mapping::write (dccrg_mapping.hpp:576:
+    3 x uint64 length, int max_ref_lvl), the neighborhood length (unsigned,
+    dccrg.hpp:1216-1231), Grid_Topology::write (dccrg_topology.hpp:144:
+    3 x uint8), Cartesian_Geometry::write (dccrg_cartesian_geometry.hpp:618:
+    int geometry id 1, 3 x double start, 3 x double level-0 length)."""
+    import struct
+
+    return (struct.pack("<3Qi", *[int(v) for v in length], int(R)) + struct.pack("<I", int(hood))
+            + struct.pack("<3B", *[1 if p else 0 for p in periodic])
+            + struct.pack("<i3d3d", 1, *[float(v) for v in start], *[float(v) for v in l0]))
+
+
+def grid_file_bytes(block, header, offset, cells_by_rank, data_of):
+    """A whole grid file as save_grid_data lays it out: `offset` zero bytes
+    (untouched by the writer), the user header, uint64 0x1234567890abcdef,
+    the block, uint64 total cells, (id, data offset) per cell rank by rank,
+    then the cells' data in the same order.  data_of(id) -> bytes."""
+    import struct
+
+    head = bytes(offset) + bytes(header) + struct.pack("<Q", 0x1234567890ABCDEF) + bytes(block)
+    cells = [int(c) for r in cells_by_rank for c in r]
+    head += struct.pack("<Q", len(cells))
+    data = [bytes(data_of(c)) for c in cells]
+    pos = len(head) + 16 * len(cells)
+    lst = b""
+    for c, d in zip(cells, data):
+        lst += struct.pack("<QQ", c, pos)
+        pos += len(d)
+    return head + lst + b"".join(data)

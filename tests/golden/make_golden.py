@@ -227,6 +227,33 @@ def gol_fixture():
     return dict(game_of_life_test=kat, simple_game_of_life=blinker)
 
 
+WRITE_PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_write_probe")
+
+GRID_FILE_CASES = [
+    # length, R, hood, periodic, start, level-0 cell length
+    ([4, 3, 2], 2, 1, [1, 0, 1], [0.5, -1.0, 2.0], [0.25, 0.125, 1.5]),
+    ([128, 128, 128], 2, 0, [1, 1, 0], [0.0, 0.0, 0.0], [1 / 128, 1 / 128, 1 / 128]),
+    ([10, 10, 10], 0, 2, [1, 1, 1], [-3.0, 0.0, 7.5], [0.1, 0.2, 0.3]),
+]
+
+
+def grid_file_fixture():
+    """The internal-grid-data block of save_grid_data (dccrg.hpp:1196-1258)
+    written by the reference's own Mapping / Topology / Cartesian_Geometry
+    writers (oracle/ref_write_probe.cpp)."""
+    out = []
+    for length, R, hood, per, start, l0 in GRID_FILE_CASES:
+        path = os.path.join("/tmp", f"dccrgx_probe_{os.getpid()}.bin")
+        line = " ".join(str(v) for v in [*length, R, hood, *per] + [repr(float(v)) for v in [*start, *l0]] + [path])
+        sizes = subprocess.run([WRITE_PROBE], input=line + "\n", capture_output=True, text=True,
+                               check=True).stdout.split()
+        data = open(path, "rb").read()
+        os.remove(path)
+        out.append(dict(length=length, R=R, hood=hood, periodic=per, start=start, l0=l0,
+                        sizes=[int(v) for v in sizes], block_hex=data.hex()))
+    return out
+
+
 def main():
     if not os.path.exists(PROBE):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
@@ -240,6 +267,8 @@ def main():
         json.dump(hood_count_fixture(), f, indent=0)
     with open(os.path.join(HERE, "kat_gol.json"), "w") as f:
         json.dump(gol_fixture(), f, indent=0)
+    with open(os.path.join(HERE, "grid_file_ref.json"), "w") as f:
+        json.dump(grid_file_fixture(), f, indent=0)
     print("golden fixtures written to", HERE)
 
 

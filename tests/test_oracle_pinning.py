@@ -137,3 +137,13 @@ def test_blinker_kat(golden_dir):
             assert bool(st[pos[c]]) == even
         for c in k["dead_after_even_turn"]:
             assert bool(st[pos[c]]) != even
+
+
+def test_grid_file_block_matches_reference_writers(golden_dir):
+    """save_grid_data's internal grid block as the reference's own Mapping /
+    Grid_Topology / Cartesian_Geometry writers produce it
+    (oracle/ref_write_probe.cpp -> tests/golden/grid_file_ref.json)."""
+    for c in _load(golden_dir, "grid_file_ref.json"):
+        b = O.grid_block_bytes(c["length"], c["R"], c["hood"], c["periodic"], c["start"], c["l0"])
+        assert b.hex() == c["block_hex"]
+        assert len(b) == c["sizes"][3]

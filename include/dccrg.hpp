@@ -156,6 +156,16 @@ public:
 		for (auto i : ids) r.push_back({i, {{0, 0, 0}}});
 		return r;
 	}
+	// get_neighbors_of / _to (819 / 883) for a user neighborhood id
+	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_of(uint64_t cell, int neighborhood_id,
+	                                                                      bool* found = nullptr) const {
+		if (neighborhood_id == DCCRGX_DEFAULT_HOOD) return get_neighbors_of(cell, found);
+		return user_neighbors(cell, neighborhood_id, 0, found);
+	}
+	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_to(uint64_t cell, int neighborhood_id) const {
+		if (neighborhood_id == DCCRGX_DEFAULT_HOOD) return get_neighbors_to(cell);
+		return user_neighbors(cell, neighborhood_id, 1, nullptr);
+	}
 	std::vector<std::pair<uint64_t, int>> get_face_neighbors_of(uint64_t cell) const {  // 2806
 		std::vector<std::pair<uint64_t, int>> r;
 		uint64_t ids[64];
@@ -168,6 +178,33 @@ public:
 		return r;
 	}
 	bool is_local(uint64_t cell) const { return dccrgx_is_local(g_, cell) == 1; }  // 3270
+	// the update lists of a neighborhood id (get_cells_to_send / _receive
+	// 6900-6914 per id)
+	std::vector<uint64_t> get_cells_to_send(int peer, int neighborhood_id = DCCRGX_DEFAULT_HOOD) const {
+		if (neighborhood_id == DCCRGX_DEFAULT_HOOD)
+			return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells_to_send(g_, peer, o, c, n); });
+		return fetch([&](uint64_t* o, size_t c, size_t* n) {
+			return dccrgx_get_user_update_list(g_, neighborhood_id, peer, 0, o, c, n);
+		});
+	}
+	std::vector<uint64_t> get_cells_to_receive(int peer, int neighborhood_id = DCCRGX_DEFAULT_HOOD) const {
+		if (neighborhood_id == DCCRGX_DEFAULT_HOOD)
+			return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells_to_receive(g_, peer, o, c, n); });
+		return fetch([&](uint64_t* o, size_t c, size_t* n) {
+			return dccrgx_get_user_update_list(g_, neighborhood_id, peer, 1, o, c, n);
+		});
+	}
+
+	// ---- user neighborhoods (add_neighborhood 6383, remove_neighborhood 6530) ----
+	bool add_neighborhood(int neighborhood_id, const std::vector<std::array<int, 3>>& items) {
+		std::vector<int32_t> o;
+		for (const auto& it : items) o.insert(o.end(), it.begin(), it.end());
+		return dccrgx_add_neighborhood(g_, neighborhood_id, o.data(), items.size()) == DCCRGX_OK;
+	}
+	Dccrg& remove_neighborhood(int neighborhood_id) {
+		detail::check(dccrgx_remove_neighborhood(g_, neighborhood_id));
+		return *this;
+	}
 	int get_process(uint64_t cell) const { return dccrgx_get_process(g_, cell); }   // 5807
 
 	// ---- refinement / partition ----------------------------------------------
@@ -182,6 +219,29 @@ public:
 	Dccrg& balance_load(bool /*use_zoltan*/ = true) {
 		detail::check(dccrgx_balance_load(g_));
 		return *this;
+	}
+	// balance_load to an explicit partition: one owner per leaf, leaves ascending
+	Dccrg& balance_load(const std::vector<uint64_t>& leaves, const std::vector<int32_t>& owners) {
+		detail::check(dccrgx_balance_load_to(g_, leaves.data(), owners.data(), leaves.size()));
+		return *this;
+	}
+
+	// ---- grid files (save_grid_data 1089, load_grid_data 1742) ------------------
+	// the header is raw bytes (the reference takes (void*, count, MPI_Datatype))
+	bool save_grid_data(const std::string& name, uint64_t offset, const void* header = nullptr,
+	                    size_t header_bytes = 0) {
+		upload();
+		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
+	}
+	// replaces initialize(): every setting comes from the file
+	bool load_grid_data(const std::string& name, uint64_t offset, size_t header_bytes, int rank = 0, int size = 1,
+	                    int device = 0, const void* rccl_id = nullptr) {
+		detail::check(dccrgx_create(rank, size, device, rccl_id, &g_));
+		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
+		rank_ = rank;
+		if (dccrgx_load_grid_data(g_, name.c_str(), offset, header_bytes) != DCCRGX_OK) return false;
+		download();
+		return true;
 	}
 
 	// ---- Cell_Data payload (host staging) -----------------------------------
@@ -212,6 +272,9 @@ public:
 		return dccrgx_wait_remote_neighbor_copy_update_sends(g_) == DCCRGX_OK;
 	}
 	bool wait_remote_neighbor_copy_updates() { return dccrgx_wait_remote_neighbor_copy_updates(g_) == DCCRGX_OK; }
+	bool update_copies_of_remote_neighbors(int neighborhood_id) {  // 966 with an id
+		return dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) == DCCRGX_OK;
+	}
 
 	// ---- device SoA fields ------------------------------------------------------
 	template <class T>
@@ -231,6 +294,22 @@ private:
 		std::vector<uint64_t> v(n);
 		if (n) detail::check(f(v.data(), n, &n));
 		return v;
+	}
+	std::vector<std::pair<uint64_t, std::array<int, 3>>> user_neighbors(uint64_t cell, int id, int kind,
+	                                                                    bool* found) const {
+		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
+		size_t n = 0;
+		int rc = dccrgx_get_user_neighbors(g_, id, cell, kind, nullptr, nullptr, 0, &n);
+		if (found) *found = rc != DCCRGX_ENOTFOUND;
+		if (rc == DCCRGX_ENOTFOUND) return r;
+		if (rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> ids(n);
+		std::vector<int32_t> off(3 * n);
+		detail::check(dccrgx_get_user_neighbors(g_, id, cell, kind, ids.data(), off.data(), n, &n));
+		for (size_t i = 0; i < n; i++)
+			r.push_back({ids[i], kind == 0 ? std::array<int, 3>{{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}
+			                               : std::array<int, 3>{{0, 0, 0}}});
+		return r;
 	}
 	void set_geometry_impl(const No_Geometry::Parameters&) {}
 	void set_geometry_impl(const Cartesian_Geometry::Parameters& p) {

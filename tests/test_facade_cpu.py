@@ -30,3 +30,20 @@ def test_c_header_is_plain_c(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert subprocess.run([str(tmp_path / "t")]).returncode == 0
+
+
+def test_facade_every_member_instantiates(tmp_path):
+    """Explicit instantiation compiles every member of dccrg::Dccrg (an
+    unused member of a class template is otherwise never checked)."""
+    from dccrg_amd import build as B
+
+    B.build()
+    src = tmp_path / "inst.cpp"
+    src.write_text('#include "dccrg.hpp"\nstruct Cell { unsigned is_alive; double x; };\n'
+                   "template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry>;\n"
+                   "template class dccrg::Dccrg<Cell>;\nint main() { return 0; }\n")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src),
+                        "-L", os.path.join(ROOT, "dccrg_amd"), "-ldccrgx",
+                        f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}", "-o", str(tmp_path / "inst")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

@@ -432,6 +432,19 @@ def main():
     n_send = g.get_number_of_update_send_cells()
     n_peers = len(g.get_peers())
 
+    # device neighbor build (find_neighbors_of / _to for every
+    # local cell, initialize_neighbors): the full neighbors_of / neighbors_to /
+    # iterator CSR of the frozen mesh, built once here (the sweep itself
+    # uses the face tables); output bytes = 8 B id + 12 B offset + 4 B slot per
+    # neighbors_of entry, 8 B per neighbors_to entry, 4 B per iterator entry
+    g.synchronize()
+    tb = time.perf_counter()
+    n_of = g.neighbor_entries("of")
+    g.synchronize()
+    build_s = time.perf_counter() - tb
+    n_to = g.neighbor_entries("to")
+    n_it = g.neighbor_entries("iterator")
+
     stats = torch.tensor([el, float(n_local), float(c["recv"]), kern_ms, halo_el, float(n_send)],
                          dtype=torch.float64, device="cuda")
     if world > 1:
@@ -516,6 +529,12 @@ def main():
                 "launches_per_step": launches_per_step,
             },
             "cpu_baseline": cpu,
+            "neighbor_build": {
+                "what": "neighbors_of + neighbors_to + iterator CSR of all local cells (device kernels)",
+                "seconds": build_s, "cells_per_s": n_local / build_s if build_s > 0 else None,
+                "entries_of": n_of, "entries_to": n_to,
+                "output_GB_per_s": (24 * n_of + 8 * n_to + 4 * n_it) / build_s / 1e9 if build_s > 0 else None,
+            },
         }
         if world > 1:
             # rank with the most halo traffic; xGMI: one link per peer pair,

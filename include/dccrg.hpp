@@ -17,8 +17,10 @@
 #ifndef DCCRG_AMD_DCCRG_HPP
 #define DCCRG_AMD_DCCRG_HPP
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
+#include <tuple>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -30,7 +32,7 @@ namespace dccrg {
 
 static const uint64_t error_cell = 0;                     // dccrg_mapping.hpp:37
 static const uint64_t error_index = 0xFFFFFFFFFFFFFFFFull;  // dccrg_mapping.hpp:40
-static const int default_neighborhood_id = -0xDCC;        // dccrg.hpp:112 (value irrelevant here)
+static const int default_neighborhood_id = -0xDCC;        // dccrg.hpp:93
 
 // dccrg_no_geometry.hpp / dccrg_cartesian_geometry.hpp parameter stand-ins
 struct No_Geometry {
@@ -47,6 +49,24 @@ inline void check(int rc) {
 	if (rc != DCCRGX_OK) throw std::runtime_error(std::string("dccrgx: ") + dccrgx_last_error());
 }
 }  // namespace detail
+
+// Items of the iteration ranges (Neighbors_Item 7288-7340, Cells_Item
+// 7364-7402): ids with data pointers into the host staging copy, so that a
+// reference-style loop `for (const auto& cell: grid.local_cells_items())`
+// `for (const auto& n: cell.neighbors_of) n.data->...` reads the payload
+// downloaded last (the facade refreshes the items on download()).
+template <class Cell_Data>
+struct Neighbors_Item {
+	uint64_t id;
+	Cell_Data* data;
+	int x, y, z;  // offset of the neighbor's min corner in index units
+};
+template <class Cell_Data>
+struct Cells_Item {
+	uint64_t id;
+	Cell_Data* data;
+	std::vector<Neighbors_Item<Cell_Data>> neighbors_of;  // sorted by (id, offset), no duplicates (11451-11500)
+};
 
 template <class Cell_Data, class Geometry = No_Geometry>
 class Dccrg {
@@ -261,6 +281,50 @@ public:
 		if (s < 0 || size_t(s) >= host_.size()) return nullptr;
 		return &host_[size_t(s)];
 	}
+
+	// ---- iteration (inner_cells / outer_cells / local_cells 7478-7602) ------------
+	// items of a selection, ascending id, each with its iterator neighbors_of;
+	// data pointers are valid until the next download() or structural change
+	std::vector<Cells_Item<Cell_Data>> cells_items(int which = DCCRGX_CELLS_LOCAL) {
+		if (host_.empty()) download();
+		size_t nl = 0, ns = 0;
+		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
+		{
+			size_t ni = 0, no = 0;
+			detail::check(dccrgx_get_counts(g_, &ni, &no, nullptr, nullptr));
+			nl = ni + no;
+		}
+		std::vector<uint32_t> ptr(nl + 1);
+		size_t ne = 0;
+		int rc = dccrgx_download_csr(g_, 0, ptr.data(), nullptr, nullptr, 0, &ne);
+		if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> nid(ne + 1);
+		std::vector<int32_t> off(3 * ne + 3);
+		detail::check(dccrgx_download_csr(g_, 0, ptr.data(), nid.data(), off.data(), ne, &ne));
+		std::vector<Cells_Item<Cell_Data>> out;
+		for (uint64_t id : get_cells(which)) {
+			const int64_t s = dccrgx_get_slot(g_, id);
+			Cells_Item<Cell_Data> it{id, &host_[size_t(s)], {}};
+			for (uint32_t j = ptr[size_t(s)]; j < ptr[size_t(s) + 1]; j++) {
+				const int64_t ns2 = dccrgx_get_slot(g_, nid[j]);
+				it.neighbors_of.push_back({nid[j], ns2 >= 0 ? &host_[size_t(ns2)] : nullptr, off[3 * j], off[3 * j + 1],
+				                           off[3 * j + 2]});
+			}
+			std::sort(it.neighbors_of.begin(), it.neighbors_of.end(), [](const auto& a, const auto& b) {
+				return std::tie(a.id, a.x, a.y, a.z) < std::tie(b.id, b.x, b.y, b.z);
+			});
+			it.neighbors_of.erase(std::unique(it.neighbors_of.begin(), it.neighbors_of.end(),
+			                                  [](const auto& a, const auto& b) {
+				                                  return a.id == b.id && a.x == b.x && a.y == b.y && a.z == b.z;
+			                                  }),
+			                      it.neighbors_of.end());
+			out.push_back(std::move(it));
+		}
+		return out;
+	}
+	std::vector<Cells_Item<Cell_Data>> local_cells_items() { return cells_items(DCCRGX_CELLS_LOCAL); }
+	std::vector<Cells_Item<Cell_Data>> inner_cells_items() { return cells_items(DCCRGX_CELLS_INNER); }
+	std::vector<Cells_Item<Cell_Data>> outer_cells_items() { return cells_items(DCCRGX_CELLS_OUTER); }
 
 	// ---- halo (966, 5010-5367) -------------------------------------------------
 	bool update_copies_of_remote_neighbors() { return dccrgx_update_copies_of_remote_neighbors(g_) == DCCRGX_OK; }

@@ -258,6 +258,15 @@ struct Grid {
 	// nst[6] (regular: neighbor-box starts), kind (1 regular), pad; for the
 	// fused sweep over both kinds (empty when a tile exceeds its limits)
 	DBuf<uint32_t> tfmeta;
+	// work tickets of the persistent advection kernels: [kernel (0 regular,
+	// 1 general)][set][XCD][32] (one 128-B line per counter); a launch draws
+	// from set adv_par[kernel] and
+	// zeroes the other set for the next launch of that kernel
+	DBuf<uint32_t> adv_ctr;
+	uint32_t adv_par[2] = {0, 0};
+	// second compute stream: the general-tile sweep runs beside the regular one
+	hipStream_t s_adv2 = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	std::map<int, UserHood> uhoods;  // add_neighborhood ids
 	DBuf<uint64_t> gol_l0p;  // refined game of life: level-0 parent per slot (scratch)
 	// halo
@@ -349,7 +358,7 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
                  const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
 // tiled advection sweep over the regular and the irregular tiles of one run
 // (run 0 inner, 1 outer: tiles never straddle the two)
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, int run, double dt, hipStream_t s);
+void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
 int adv_variant();  // DCCRGX_ADV_VARIANT (11 = tiled, the default)
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,

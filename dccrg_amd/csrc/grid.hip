@@ -1184,6 +1184,9 @@ int dccrgx_destroy(dccrgx_grid* gp) {
 		if (g.comm) ncclCommDestroy(g.comm);
 		if (g.ev_comp) (void)hipEventDestroy(g.ev_comp);
 		if (g.ev_halo) (void)hipEventDestroy(g.ev_halo);
+		if (g.ev_fork) (void)hipEventDestroy(g.ev_fork);
+		if (g.ev_join) (void)hipEventDestroy(g.ev_join);
+		if (g.s_adv2) (void)hipStreamDestroy(g.s_adv2);
 		if (g.s_comp) (void)hipStreamDestroy(g.s_comp);
 		if (g.s_comm) (void)hipStreamDestroy(g.s_comm);
 		delete gp;

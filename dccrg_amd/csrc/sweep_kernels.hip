@@ -622,10 +622,63 @@ __device__ __forceinline__ double adv_face_g(int a, double cd, double clx, doubl
 	return (v >= 0 ? cd : n.d) * dt * v * min_area;
 }
 
-template <int MINW, int NT>
+// Work tickets of the persistent sweeps.  Static: block j of XCD x takes
+// tiles j, j + B, j + 2B, ... of the x-th eighth of the list.  Dynamic: the
+// blocks of XCD x draw the tiles of that eighth in order from counter x
+// (tiles differ in cost, and a block that starts late - beside the other
+// sweep on the second stream - takes fewer).  Each ticket is drawn one tile
+// ahead of its use, so the atomic's latency hides behind the tile in flight.
+// Counters sit 128 B apart (one cache line each).
+// A launch draws from counter set `par` and zeroes the other set, which the
+// next launch of the same kernel (ordered after this one) draws from.
+template <bool DYN>
+struct Tickets {
+	uint32_t* ctr;
+	uint32_t x, B, t0, t1, pend = 0, slot = 0;
+	uint32_t* s_tk;  // 2 LDS words
+	// the first tile of this block (or >= t1: none); block-uniform
+	__device__ __forceinline__ uint32_t first() {
+		if (!DYN) return t0 + (blockIdx.x >> 3);
+		if (threadIdx.x == 0) s_tk[0] = atomicAdd(ctr + 32u * x, 1u);
+		__syncthreads();
+		const uint32_t t = t0 + s_tk[0];
+		if (threadIdx.x == 0 && t < t1) pend = atomicAdd(ctr + 32u * x, 1u);
+		return t;
+	}
+	// before the barrier that precedes next(): publish the drawn ticket, draw one more
+	__device__ __forceinline__ void draw() {
+		if (DYN && threadIdx.x == 0) {
+			s_tk[slot] = pend;
+			pend = atomicAdd(ctr + 32u * x, 1u);
+		}
+	}
+	// after that barrier: the tile after t
+	__device__ __forceinline__ uint32_t next(uint32_t t) {
+		if (!DYN) return t + B;
+		const uint32_t tn = t0 + s_tk[slot];
+		slot ^= 1u;
+		return tn;
+	}
+};
+
+template <bool DYN>
+__device__ __forceinline__ Tickets<DYN> make_tickets(uint32_t* ctr, uint32_t par, uint32_t ntiles, uint32_t* s_tk) {
+	Tickets<DYN> k;
+	k.x = blockIdx.x & 7u;
+	k.B = gridDim.x >> 3;
+	k.t0 = uint32_t((uint64_t(k.x) * ntiles) >> 3);
+	k.t1 = uint32_t((uint64_t(k.x + 1) * ntiles) >> 3);
+	k.s_tk = s_tk;
+	k.ctr = ctr + 256u * par;
+	if (DYN && blockIdx.x == 0 && threadIdx.x < 8) ctr[256u * (par ^ 1u) + 32u * threadIdx.x] = 0;
+	return k;
+}
+
+template <int MINW, int NT, bool DYN, int DEPTH = 1>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
-                                                                         uint32_t ntiles, double dt) {
+                                                                         uint32_t ntiles, double dt, uint32_t* ctr,
+                                                                         uint32_t par) {
 #pragma clang fp contract(off)
 	// rows rho, vx, vy, vz, lx, ly, lz; columns 0..511 the tile's own cells,
 	// 512 + 64 d + (face cell) the out-of-tile neighbor across side d (only
@@ -635,9 +688,10 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	__shared__ double shd[7][W];
 	__shared__ double shg[3][512];  // flux through each cell's +x, +y, +z face
 	__shared__ double shm[3][64];   // flux through the tile's -x, -y, -z boundary faces
-	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
-	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
-	uint32_t t = t0 + j;
+	__shared__ uint32_t s_tk[2];
+	Tickets<DYN> tk = make_tickets<DYN>(ctr, par, ntiles, s_tk);
+	const uint32_t t1 = tk.t1;
+	uint32_t t = tk.first();
 	if (t >= t1) return;  // block-uniform
 	const uint32_t tid = threadIdx.x;
 	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
@@ -667,43 +721,44 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	const double* __restrict__ vz = P.p[6];
 	// LDS row of value `val` (0 rho, 1 lx, 2 ly, 3 lz, 4 velocity along a)
 	auto vrow = [](uint32_t val, uint32_t a) -> uint32_t { return val == 0 ? 0u : (val == 4 ? 1u + a : val + 3u); };
-	// one register set: the tile being loaded
-	double c[7], e[4];
-	auto load = [&](uint32_t tt) {
+	// a register set: a tile being loaded
+	struct RegSet {
+		double c[7], e[4];
+	};
+	auto load = [&](uint32_t tt, RegSet& r) {
 		const uint32_t ts = meta[tt].ts;
 		const uint32_t o = (ts + tid) << 3;
-		c[0] = ldo_own<NT>(rho, o); c[1] = ldo_own<NT>(vx, o); c[2] = ldo_own<NT>(vy, o); c[3] = ldo_own<NT>(vz, o);
-		c[4] = ldo_own<NT>(lx, o); c[5] = ldo_own<NT>(ly, o); c[6] = ldo_own<NT>(lz, o);
+		r.c[0] = ldo_own<NT>(rho, o); r.c[1] = ldo_own<NT>(vx, o); r.c[2] = ldo_own<NT>(vy, o);
+		r.c[3] = ldo_own<NT>(vz, o); r.c[4] = ldo_own<NT>(lx, o); r.c[5] = ldo_own<NT>(ly, o);
+		r.c[6] = ldo_own<NT>(lz, o);
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
-			e[i] = 0;
+			r.e[i] = 0;
 			if (row >= 30u) continue;
 			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
 			const int32_t st = meta[tt].nst[d];
 			if (st < 0) continue;
 			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
 			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
-			e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+			r.e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
 		}
 	};
-	load(t);
-	for (;;) {
-		__syncthreads();  // the previous tile's faces have been read from LDS
+	// a loaded tile into LDS (after the barrier that ends the previous tile's reads)
+	auto stage = [&](const RegSet& r) {
 #pragma unroll
-		for (int k = 0; k < 7; k++) shd[k][tid] = c[k];
+		for (int k = 0; k < 7; k++) shd[k][tid] = r.c[k];
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);
 			if (row < 30u) {
 				const uint32_t d = row / 5u, val = row - 5u * d;
-				shd[vrow(val, d >> 1)][512u + 64u * d + lane] = e[i];
+				shd[vrow(val, d >> 1)][512u + 64u * d + lane] = r.e[i];
 			}
 		}
-		__syncthreads();
-		const uint32_t tc = t, tn = t + B;
-		const bool more = tn < t1;
-		if (more) load(tn);  // the next tile's loads fly while this one is computed
+	};
+	// the staged tile tc from LDS
+	auto compute = [&](uint32_t tc) {
 		const uint32_t ts = meta[tc].ts;
 		const double cd = shd[0][tid], clx = shd[4][tid], cly = shd[5][tid], clz = shd[6][tid];
 		const double cva[3] = {shd[1][tid], shd[2][tid], shd[3][tid]};
@@ -743,8 +798,47 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			acc += -shg[a][tid];
 		}
 		st_out<NT>(rho_out, ts + tid, cd + acc / (clx * cly * clz));
-		if (!more) break;
-		t = tn;
+	};
+	RegSet ra;
+	load(t, ra);
+	if constexpr (DEPTH == 2) {
+		// two tiles of loads in flight (static schedule): while tile t is
+		// computed, tile t + B is in flight in one register set and tile
+		// t + 2B is issued into the other as soon as that set is staged
+		const uint32_t B = tk.B;
+		RegSet rb;
+		uint32_t tn = t + B;
+		if (tn < t1) load(tn, rb);
+		auto step = [&](RegSet& r, uint32_t tc, uint32_t tl) {
+			__syncthreads();  // the previous tile's faces have been read from LDS
+			stage(r);
+			__syncthreads();
+			if (tl < t1) load(tl, r);
+			compute(tc);
+		};
+		for (;;) {
+			step(ra, t, tn + B);
+			if (tn >= t1) break;
+			t = tn;
+			tn = t + B;
+			step(rb, t, tn + B);
+			if (tn >= t1) break;
+			t = tn;
+			tn = t + B;
+		}
+	} else {
+		for (;;) {
+			tk.draw();
+			__syncthreads();  // the previous tile's faces have been read from LDS
+			stage(ra);
+			__syncthreads();
+			const uint32_t tc = t, tn = tk.next(t);
+			const bool more = tn < t1;
+			if (more) load(tn, ra);  // the next tile's loads fly while this one is computed
+			compute(tc);
+			if (!more) break;
+			t = tn;
+		}
 	}
 }
 
@@ -758,18 +852,20 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW, int NT, int EXT5>
+template <int MINW, int NT, int EXT5, bool DYN>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
+    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt,
+    uint32_t* ctr, uint32_t par) {
 #pragma clang fp contract(off)
 	constexpr uint32_t T = 512;
 	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
 	const uint32_t W = T + ecap;
 	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
-	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
-	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
-	uint32_t t = t0 + j;
+	__shared__ uint32_t s_tk[2];
+	Tickets<DYN> tk = make_tickets<DYN>(ctr, par, ntiles, s_tk);
+	const uint32_t t1 = tk.t1;
+	uint32_t t = tk.first();
 	if (t >= t1) return;  // block-uniform
 	const uint32_t tid = threadIdx.x;
 	const double* const rho = P.p[0];
@@ -825,6 +921,7 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 	load(t);
 	for (;;) {
 		const uint32_t n = meta[t].n, ne = meta[t].ne, nf = meta[t].nf, ts = meta[t].ts;
+		tk.draw();
 		__syncthreads();  // the previous tile's faces have been read from LDS
 		if (tid < n)
 #pragma unroll
@@ -841,7 +938,7 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		}
 		const uint32_t r0 = row[0], r1 = row[1], r2 = row[2];
 		__syncthreads();
-		const uint32_t tn = t + B;
+		const uint32_t tn = tk.next(t);
 		const bool more = tn < t1;
 		if (more) load(tn);  // the next tile's loads fly while this one is computed
 		if (tid < n) {
@@ -1206,7 +1303,28 @@ static uint32_t tile_ecap(int T, size_t max_ext) {
 	return uint32_t(std::min(cap, max_ext));
 }
 
-void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g, int run, double dt, hipStream_t s) {
+void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s) {
+	// DCCRGX_ADV_DYN=1: tiles drawn from per-XCD counters instead of the static
+	// schedule (A/B: equal on config 3 once the counters sit on separate lines)
+	static const int dyn = [] {
+		const char* e = getenv("DCCRGX_ADV_DYN");
+		return e ? atoi(e) : 0;
+	}();
+	// DCCRGX_ADV_DEPTH=1: one tile of loads in flight in the regular sweep
+	// instead of two (A/B: 2 is 0.7-0.9% faster on config 3)
+	static const int depth = [] {
+		const char* e = getenv("DCCRGX_ADV_DEPTH");
+		return e ? atoi(e) : 2;
+	}();
+	// DCCRGX_ADV_2S=1: the general-tile sweep on a second stream beside the regular one
+	static const int two_streams = [] {
+		const char* e = getenv("DCCRGX_ADV_2S");
+		return e ? atoi(e) : 0;
+	}();
+	if (dyn && g.adv_ctr.n < 1024) {
+		g.adv_ctr.alloc(1024);
+		HIP_CHECK(hipMemsetAsync(g.adv_ctr.p, 0, 1024 * sizeof(uint32_t), s));
+	}
 	static const int diag = [] {
 		const char* e = getenv("DCCRGX_ADV_DIAG");
 		return e ? atoi(e) : 0;
@@ -1264,14 +1382,41 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		const char* e = getenv("DCCRGX_ADV_PP");
 		return e ? atoi(e) : 2;
 	}();
+	static const int tiles_pp = [] {  // DCCRGX_ADV_TPP=0: the non-persistent tile kernel
+		const char* e = getenv("DCCRGX_ADV_TPP");
+		return e ? atoi(e) : 1;
+	}();
+	// the general sweep beside the regular one on a second stream: forked
+	// after everything queued on s, joined before whatever s runs next
+	const bool fork =
+	    two_streams && n_reg && pp_blocks > 0 && n_irr && tiles_pp && T == 512 && g.tmeta.n && diag == 0;
+	if (fork) {
+		if (!g.s_adv2) {
+			HIP_CHECK(hipStreamCreateWithFlags(&g.s_adv2, hipStreamNonBlocking));
+			HIP_CHECK(hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming));
+			HIP_CHECK(hipEventCreateWithFlags(&g.ev_join, hipEventDisableTiming));
+		}
+		HIP_CHECK(hipEventRecord(g.ev_fork, s));
+		HIP_CHECK(hipStreamWaitEvent(g.s_adv2, g.ev_fork, 0));
+	}
 	if (n_reg && pp_blocks > 0) {
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * size_t(pp_blocks), (n_reg + 7) / 8 * 8));
 		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		if (adv_nt() == 1) advection_regular_pp_kernel<4, 1><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else if (adv_nt() == 2) advection_regular_pp_kernel<4, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else if (adv_nt() == 3) advection_regular_pp_kernel<4, 3><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
-		else advection_regular_pp_kernel<4, 0><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		uint32_t* ctr = g.adv_ctr.p;
+		const uint32_t par = g.adv_par[0];
+		g.adv_par[0] ^= 1u;
+#define DX_REG(NTV, DY) \
+	advection_regular_pp_kernel<4, NTV, DY><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par)
+		if (depth == 2 && !dyn && adv_nt() == 0)
+			advection_regular_pp_kernel<4, 0, false, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par);
+		else if (dyn && adv_nt() == 0) DX_REG(0, true);
+		else if (dyn && adv_nt() == 1) DX_REG(1, true);
+		else if (adv_nt() == 1) DX_REG(1, false);
+		else if (adv_nt() == 2) DX_REG(2, false);
+		else if (adv_nt() == 3) DX_REG(3, false);
+		else DX_REG(0, false);
+#undef DX_REG
 		HIP_CHECK(hipGetLastError());
 	} else if (n_reg) {
 		if (diag == 5)
@@ -1286,10 +1431,6 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
 		return;
 	}
-	static const int tiles_pp = [] {  // DCCRGX_ADV_TPP=0: the non-persistent tile kernel
-		const char* e = getenv("DCCRGX_ADV_TPP");
-		return e ? atoi(e) : 1;
-	}();
 	if (tiles_pp && T == 512 && g.tmeta.n && diag == 0) {
 		const TileMeta* meta = reinterpret_cast<const TileMeta*>(g.tmeta.p) + (run == 0 ? 0 : g.tcount[2]);
 		const uint32_t ecap = uint32_t(g.max_ext);
@@ -1301,17 +1442,27 @@ void k_advection_tiles(const double* const f[7], double* rho_out, const Grid& g,
 			const char* e = getenv("DCCRGX_ADV_EXT5");
 			return e ? atoi(e) : 1;
 		}();
-#define DX_TPP(NTV, E5)                                                                                    \
-	advection_tiles_pp_kernel<4, NTV, E5><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, E5 ? g.ext_pk.p : g.ext.p, \
-	                                                             g.tfine.p, meta, uint32_t(n_irr), ecap, dt)
-		if (ext5 && adv_nt() == 1) DX_TPP(1, 1);
-		else if (ext5 && adv_nt() == 0) DX_TPP(0, 1);
-		else if (adv_nt() == 1) DX_TPP(1, 0);
-		else if (adv_nt() == 2) DX_TPP(2, 0);
-		else if (adv_nt() == 3) DX_TPP(3, 0);
-		else DX_TPP(0, 0);
+		hipStream_t st = fork ? g.s_adv2 : s;
+		uint32_t* ctr = g.adv_ctr.p ? g.adv_ctr.p + 512 : nullptr;
+		const uint32_t par = g.adv_par[1];
+		g.adv_par[1] ^= 1u;
+#define DX_TPP(NTV, E5, DY)                                                                                     \
+	advection_tiles_pp_kernel<4, NTV, E5, DY><<<nblk, 512, lds, st>>>(P, rho_out, g.tell.p, E5 ? g.ext_pk.p : g.ext.p, \
+	                                                                  g.tfine.p, meta, uint32_t(n_irr), ecap, dt, ctr, par)
+		if (dyn && ext5 && adv_nt() == 0) DX_TPP(0, 1, true);
+		else if (dyn && ext5 && adv_nt() == 1) DX_TPP(1, 1, true);
+		else if (ext5 && adv_nt() == 1) DX_TPP(1, 1, false);
+		else if (ext5 && adv_nt() == 0) DX_TPP(0, 1, false);
+		else if (adv_nt() == 1) DX_TPP(1, 0, false);
+		else if (adv_nt() == 2) DX_TPP(2, 0, false);
+		else if (adv_nt() == 3) DX_TPP(3, 0, false);
+		else DX_TPP(0, 0, false);
 #undef DX_TPP
 		HIP_CHECK(hipGetLastError());
+		if (fork) {
+			HIP_CHECK(hipEventRecord(g.ev_join, st));
+			HIP_CHECK(hipStreamWaitEvent(s, g.ev_join, 0));
+		}
 		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
 		return;
 	}

@@ -110,3 +110,43 @@ def test_inner_outer_split_equals_all(gpu):
     b = f[0].get(0, g.n_local)
     assert np.array_equal(a, b)
     g.close()
+
+
+def _variant_rho(base=(64, 64, 16), R=2, steps=10):
+    """Density after `steps` sweeps of the large refined case (regular and
+    general tiles both present) under the current DCCRGX_ADV_* schedule."""
+    g, f = gpu_grid(base, R)
+    prerefine(g, f, R)
+    dt = g.advection_max_time_step(f)
+    for _ in range(steps):
+        g.advection_step(f, 0.5 * dt)
+        g.advection_commit(f[0])
+    rho = f[0].get(0, g.n_local)
+    g.close()
+    return rho
+
+
+@pytest.mark.parametrize("env", ["DCCRGX_ADV_DEPTH=1", "DCCRGX_ADV_DYN=1", "DCCRGX_ADV_DYN=1 DCCRGX_ADV_2S=1"])
+def test_schedule_variants_bitwise(gpu, tmp_path, env):
+    """The A/B schedules of the persistent tile sweeps (one tile of loads in
+    flight instead of two, per-XCD tile tickets, the general sweep on a second
+    stream) change only which block sweeps which tile and when: every cell's
+    result is bitwise the default's.  The knobs are read once per process, so
+    the variant runs in a child process."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "rho.npy"
+    code = ("import sys, numpy as np, torch; sys.path[:0] = [%r, %r]; "
+            "from test_gpu_advection import _variant_rho; np.save(%r, _variant_rho())"
+            % (root, os.path.join(root, "tests"), str(out)))
+    child_env = dict(os.environ)
+    for kv in env.split():
+        k, v = kv.split("=")
+        child_env[k] = v
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=child_env, capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert np.array_equal(np.load(str(out)), _variant_rho())

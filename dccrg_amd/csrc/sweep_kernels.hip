@@ -1310,11 +1310,11 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 		const char* e = getenv("DCCRGX_ADV_DYN");
 		return e ? atoi(e) : 0;
 	}();
-	// DCCRGX_ADV_DEPTH=1: one tile of loads in flight in the regular sweep
-	// instead of two (A/B: 2 is 0.7-0.9% faster on config 3)
+	// DCCRGX_ADV_DEPTH=2: two tiles of loads in flight in the regular sweep
+	// instead of one (A/B on config 3: equal, 0.1896 vs 0.1894 ms)
 	static const int depth = [] {
 		const char* e = getenv("DCCRGX_ADV_DEPTH");
-		return e ? atoi(e) : 2;
+		return e ? atoi(e) : 1;
 	}();
 	// DCCRGX_ADV_2S=1: the general-tile sweep on a second stream beside the regular one
 	static const int two_streams = [] {
@@ -1408,7 +1408,9 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 		g.adv_par[0] ^= 1u;
 #define DX_REG(NTV, DY) \
 	advection_regular_pp_kernel<4, NTV, DY><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par)
-		if (depth == 2 && !dyn && adv_nt() == 0)
+		if (depth == 2 && !dyn && adv_nt() == 1)
+			advection_regular_pp_kernel<4, 1, false, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par);
+		else if (depth == 2 && !dyn && adv_nt() == 0)
 			advection_regular_pp_kernel<4, 0, false, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par);
 		else if (dyn && adv_nt() == 0) DX_REG(0, true);
 		else if (dyn && adv_nt() == 1) DX_REG(1, true);

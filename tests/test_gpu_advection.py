@@ -126,10 +126,10 @@ def _variant_rho(base=(64, 64, 16), R=2, steps=10):
     return rho
 
 
-@pytest.mark.parametrize("env", ["DCCRGX_ADV_DEPTH=1", "DCCRGX_ADV_DYN=1", "DCCRGX_ADV_DYN=1 DCCRGX_ADV_2S=1"])
+@pytest.mark.parametrize("env", ["DCCRGX_ADV_DEPTH=2", "DCCRGX_ADV_DYN=1", "DCCRGX_ADV_DYN=1 DCCRGX_ADV_2S=1"])
 def test_schedule_variants_bitwise(gpu, tmp_path, env):
-    """The A/B schedules of the persistent tile sweeps (one tile of loads in
-    flight instead of two, per-XCD tile tickets, the general sweep on a second
+    """The A/B schedules of the persistent tile sweeps (two tiles of loads in
+    flight instead of one, per-XCD tile tickets, the general sweep on a second
     stream) change only which block sweeps which tile and when: every cell's
     result is bitwise the default's.  The knobs are read once per process, so
     the variant runs in a child process."""

@@ -297,14 +297,24 @@ __global__ __launch_bounds__(512) void classify_tiles_kernel(MapCtx m, const uin
 // (the latest one on ties), so that on
 // Morton-ordered slots tiles coincide with aligned boxes wherever the mesh
 // allows (fewer distinct out-of-tile neighbors than arbitrary cuts).
+// DCCRGX_TILE_LO=k: the earliest allowed cut is k/8 of T (default 2: T/4)
+static uint32_t tile_lo(uint32_t T) {
+	static const int k = [] {
+		const char* e = getenv("DCCRGX_TILE_LO");
+		return e ? atoi(e) : 2;
+	}();
+	return std::max<uint32_t>(1u, uint32_t(uint64_t(T) * uint32_t(std::min(std::max(k, 1), 8)) / 8u));
+}
+
 static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, uint32_t T, std::vector<uint32_t>& out) {
 	uint32_t a = r0;
+	const uint32_t lo = tile_lo(T);
 	while (a < r1) {
 		out.push_back(a);
 		if (r1 - a <= T) break;
 		uint32_t best = a + T;
 		int best_al = -1;
-		for (uint32_t b = a + T; b >= a + T / 4 && b > a; b--) {
+		for (uint32_t b = a + T; b >= a + lo && b > a; b--) {
 			const int v = al.empty() ? 0 : int(al[b]);
 			if (v > best_al) {
 				best_al = v;

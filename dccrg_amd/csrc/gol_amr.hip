@@ -27,6 +27,8 @@
 // neighbor rows are the device neighbors_of CSR (slots); the level-0 parent
 // of every slot is decoded once per call.  Integer work, latency bound
 // (a dependent gather per neighbor entry).
+#include <cstdlib>
+
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -55,6 +57,10 @@ __global__ void level0_parent_kernel(MapCtx m, const uint64_t* __restrict__ slot
 
 // l0p: level-0 parent per slot (local and remote copies), computed once per
 // call so the neighbor walks do no id decoding
+// The neighbor walks gather K rows ahead (slots, then their level-0 parents
+// and states) before consuming them in row order, so K independent gathers
+// are in flight per thread instead of one dependent chain.
+template <int K>
 __global__ void gol_amr_collect_kernel(const uint64_t* __restrict__ l0p, const uint32_t* __restrict__ state,
                                        uint64_t* __restrict__ lst, const uint32_t* __restrict__ ptr,
                                        const int32_t* __restrict__ nslot, size_t s0, size_t s1,
@@ -66,24 +72,37 @@ __global__ void gol_amr_collect_kernel(const uint64_t* __restrict__ l0p, const u
 #pragma unroll
 	for (int i = 0; i < kList; i++) l[i] = error_cell;
 	int n = 0;
-	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
-		const int32_t ns = nslot[j];
-		const uint64_t q = l0p[ns];
-		if (q == parent) continue;
-		if (state[ns] == 0) {
-			bool seen = false;
+	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j += K) {
+		int32_t nsk[K];
+		uint64_t qk[K];
+		uint32_t stk[K];
 #pragma unroll
-			for (int i = 0; i < kList; i++) seen |= (i < n && l[i] == q);
-			if (seen) atomicOr(err, 2);
-			continue;
+		for (int k = 0; k < K; k++) nsk[k] = j + k < e ? nslot[j + k] : -1;
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			qk[k] = nsk[k] >= 0 ? l0p[nsk[k]] : parent;
+			stk[k] = nsk[k] >= 0 ? state[nsk[k]] : 0u;
 		}
-		if (!list_insert(l, n, q)) atomicOr(err, 1);
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const uint64_t q = qk[k];
+			if (q == parent) continue;  // also the padding past the row
+			if (stk[k] == 0) {
+				bool seen = false;
+#pragma unroll
+				for (int i = 0; i < kList; i++) seen |= (i < n && l[i] == q);
+				if (seen) atomicOr(err, 2);
+				continue;
+			}
+			if (!list_insert(l, n, q)) atomicOr(err, 1);
+		}
 	}
 	uint64_t* o = lst + s * kList;
 #pragma unroll
 	for (int i = 0; i < kList; i++) o[i] = l[i];
 }
 
+template <int K>
 __global__ void gol_amr_spread_kernel(const uint64_t* __restrict__ slot_ids, const uint64_t* __restrict__ l0p,
                                       uint32_t* __restrict__ state, const uint64_t* __restrict__ lst,
                                       const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nslot,
@@ -100,14 +119,22 @@ __global__ void gol_amr_spread_kernel(const uint64_t* __restrict__ slot_ids, con
 	}
 	// a level-0 leaf is its own level-0 parent: no neighbor shares it
 	if (parent != slot_ids[s]) {
-		for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
-			const int32_t ns = nslot[j];
-			if (l0p[ns] != parent) continue;
-			const uint64_t* nl = lst + size_t(ns) * kList;
-			for (int i = 0; i < kList; i++) {
-				const uint64_t v = nl[i];
-				if (v == error_cell) break;
-				if (!list_insert(l, n, v)) atomicOr(err, 1);
+		for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j += K) {
+			int32_t nsk[K];
+			bool sib[K];
+#pragma unroll
+			for (int k = 0; k < K; k++) nsk[k] = j + k < e ? nslot[j + k] : -1;
+#pragma unroll
+			for (int k = 0; k < K; k++) sib[k] = nsk[k] >= 0 && l0p[nsk[k]] == parent;
+#pragma unroll
+			for (int k = 0; k < K; k++) {
+				if (!sib[k]) continue;
+				const uint64_t* nl = lst + size_t(nsk[k]) * kList;
+				for (int i = 0; i < kList; i++) {
+					const uint64_t v = nl[i];
+					if (v == error_cell) break;
+					if (!list_insert(l, n, v)) atomicOr(err, 1);
+				}
 			}
 		}
 	}
@@ -124,11 +151,22 @@ void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, size_t n_sl
                hipStream_t s) {
 	if (s1 <= s0) return;
 	level0_parent_kernel<<<blocks_for(n_slots, 256), 256, 0, s>>>(m, slot_ids, n_slots, l0p);
-	if (phase == 0)
-		gol_amr_collect_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
-	else
-		gol_amr_spread_kernel<<<blocks_for(s1 - s0, 256), 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1,
-		                                                                err);
+	// DCCRGX_GOL_AMR_K=1 / 4: one / four neighbor rows ahead instead of eight
+	// (A/B on the bench's 11.5 M leaves: 3.02 / 2.25 / 2.20 ms per step)
+	static const int kk = [] {
+		const char* e = getenv("DCCRGX_GOL_AMR_K");
+		return e ? atoi(e) : 8;
+	}();
+	const unsigned nb = blocks_for(s1 - s0, 256);
+	if (phase == 0) {
+		if (kk == 1) gol_amr_collect_kernel<1><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
+		else if (kk == 4) gol_amr_collect_kernel<4><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
+		else gol_amr_collect_kernel<8><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
+	} else {
+		if (kk == 1) gol_amr_spread_kernel<1><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
+		else if (kk == 4) gol_amr_spread_kernel<4><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
+		else gol_amr_spread_kernel<8><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
+	}
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -144,13 +144,25 @@ __global__ void po_cache_kernel(MapCtx m, double l0x, double l0y, double l0z, co
 template <bool SUBTRACT>
 __device__ __forceinline__ double po_apply_row(const PoArrays& a, size_t s, double acc, const double* __restrict__ x) {
 #pragma clang fp contract(off)
+	// the six face entries, their factors and the same-size / coarser
+	// neighbors' values are gathered together before the ordered sum
+	int32_t ev[6];
+	double fv[6], xv[6];
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) ev[dir] = a.ell[6 * s + dir];
+#pragma unroll
 	for (int dir = 0; dir < 6; dir++) {
-		const int32_t e = a.ell[6 * s + dir];
+		fv[dir] = ev[dir] != -1 ? a.f[dir][s] : 0.0;
+		xv[dir] = ev[dir] >= 0 ? x[ev[dir]] : 0.0;
+	}
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) {
+		const int32_t e = ev[dir];
 		if (e == -1) continue;
-		double mul = a.f[dir][s];
+		double mul = fv[dir];
 		if (e >= 0) {
-			if (SUBTRACT) acc -= mul * x[e];
-			else acc += mul * x[e];
+			if (SUBTRACT) acc -= mul * xv[dir];
+			else acc += mul * xv[dir];
 		} else {
 			mul /= 4.0;
 			const size_t k = size_t(-2 - e);

@@ -10,12 +10,15 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# DCCRGX_LIB selects another build of the same library (kernel A/B runs);
-# default: the in-tree build
-LIB_PATH = os.environ.get("DCCRGX_LIB") or os.path.join(HERE, "libdccrgx.so")
+LIB_PATH = os.path.join(HERE, "libdccrgx.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "dccrgx.h")
 
 _lib = None
+
+# int (*)(void* ctx, const void* const* send, const size_t* send_bytes,
+#         void* const* recv, const size_t* recv_bytes)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                          C.POINTER(C.c_size_t))
 
 u64 = C.c_uint64
 i64 = C.c_int64
@@ -29,6 +32,7 @@ _SIGS = {
     "dccrgx_abi_version": (C.c_int, []),
     "dccrgx_get_unique_id": (C.c_int, [vp]),
     "dccrgx_create": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, P(vp)]),
+    "dccrgx_create_with_exchange": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, P(vp)]),
     "dccrgx_destroy": (C.c_int, [vp]),
     "dccrgx_set_initial_length": (C.c_int, [vp, P(u64)]),
     "dccrgx_set_maximum_refinement_level": (C.c_int, [vp, C.c_int]),
@@ -64,6 +68,15 @@ _SIGS = {
     "dccrgx_unpin": (C.c_int, [vp, u64]),
     "dccrgx_balance_load": (C.c_int, [vp]),
     "dccrgx_balance_load_to": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_initialize_balance_load": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_continue_balance_load": (C.c_int, [vp]),
+    "dccrgx_finish_balance_load": (C.c_int, [vp]),
+    "dccrgx_migration_message_size": (C.c_int, [vp, C.c_int, P(sz), P(sz)]),
+    "dccrgx_migration_pack": (C.c_int, [vp, C.c_int, vp, sz]),
+    "dccrgx_migration_place": (C.c_int, [vp, C.c_int, vp, sz]),
+    "dccrgx_halo_message_size": (C.c_int, [vp, C.c_int, C.c_int, P(sz), P(sz)]),
+    "dccrgx_halo_pack": (C.c_int, [vp, C.c_int, C.c_int, vp, sz]),
+    "dccrgx_halo_place": (C.c_int, [vp, C.c_int, C.c_int, vp, sz]),
     "dccrgx_save_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, vp, sz]),
     "dccrgx_load_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, sz]),
     "dccrgx_add_neighborhood": (C.c_int, [vp, C.c_int, vp, sz]),
@@ -74,6 +87,7 @@ _SIGS = {
     "dccrgx_get_cell_process": (C.c_int, [vp, vp, vp, sz, P(sz)]),
     "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
     "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),
+    "dccrgx_set_field_window": (C.c_int, [vp, C.c_int, sz, sz]),
     "dccrgx_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp)]),
     "dccrgx_field_upload": (C.c_int, [vp, C.c_int, sz, sz, vp]),
     "dccrgx_field_download": (C.c_int, [vp, C.c_int, sz, sz, vp]),

@@ -1,0 +1,1614 @@
+// dccrgx C ABI (include/dccrgx.h): every entry point wraps the host driver
+// in an exception guard and returns a status code.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <numeric>
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include "dccrgx_grid.hpp"
+
+namespace dccrgx {
+
+static thread_local std::string g_last_error;
+
+template <class F>
+static int guard(F&& f) {
+	try {
+		return f();
+	} catch (const Error& e) {
+		g_last_error = e.what();
+		return e.code;
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return DCCRGX_EINVAL;
+	}
+}
+
+static int copy_out_u64(const std::vector<uint64_t>& v, uint64_t* out, size_t cap, size_t* n) {
+	if (n) *n = v.size();
+	if (v.size() > cap || (!out && !v.empty())) return DCCRGX_ERANGE;
+	if (!v.empty()) std::memcpy(out, v.data(), v.size() * 8);
+	return DCCRGX_OK;
+}
+
+// dccrg_mapping.hpp:316-329: the largest level whose ids fit in 64 bits
+static int max_possible_level(const uint64_t len[3]) {
+	const double gl = double(len[0]) * double(len[1]) * double(len[2]);
+	int lvl = 0;
+	double cur = 0;
+	while (cur <= double(~uint64_t(0))) {
+		cur += gl * std::pow(8.0, double(lvl));
+		lvl++;
+	}
+	return lvl - 2;
+}
+
+// the largest neighborhood length whose neighbors_to dedupe fits in LDS
+static unsigned max_hood_length() {
+	unsigned L = 0;
+	while (true) {
+		const unsigned n = (2 * (L + 1) + 1) * (2 * (L + 1) + 1) * (2 * (L + 1) + 1) - 1;
+		if (int(n) > max_hood_items()) return L;
+		L++;
+	}
+}
+
+static void init_impl(Grid& g) {
+	DX_REQUIRE(!g.initialized, "already initialized");
+	map_init(g.m, g.len, g.R, g.per);
+	const unsigned L = g.hood_len;
+	const size_t cube = size_t(2 * L + 1) * (2 * L + 1) * (2 * L + 1);
+	std::vector<int32_t> h(3 * std::max<size_t>(cube, 6));
+	const int nh = default_hood(g.hood_len, h.data());
+	g.hood.assign(h.begin(), h.begin() + 3 * nh);
+	g.hood_to.resize(g.hood.size());
+	for (size_t i = 0; i < g.hood.size(); i++) g.hood_to[i] = -g.hood[i];
+	upload(g.d_hood, g.hood, g.s_comp);
+	upload(g.d_hood_to, g.hood_to, g.s_comp);
+	Mesh nm;
+	nm.implicit = true;
+	nm.bp.init(g.m.first[1] - 1, uint64_t(g.size));
+	rebuild(g, nm);
+	g.initialized = true;
+}
+
+// --------------------------------------------------------------------------- Poisson
+// Poisson_Solve (tests/poisson/poisson_solve.hpp:156-1056) over device fields.
+
+// halo update of exactly the given fields (the reference's
+// Poisson_Cell::transfer_switch, 92-140)
+static void halo_only(Grid& g, const std::vector<int>& fids) {
+	if (g.size == 1 || g.peers.empty()) return;
+	std::vector<char> saved(g.fields.size());
+	for (size_t i = 0; i < g.fields.size(); i++) {
+		saved[i] = g.fields[i].transfer;
+		g.fields[i].transfer = false;
+	}
+	for (int f : fids) field(g, f).transfer = true;
+	try {
+		halo_start(g);
+	} catch (...) {
+		for (size_t i = 0; i < g.fields.size(); i++) g.fields[i].transfer = saved[i];
+		throw;
+	}
+	for (size_t i = 0; i < g.fields.size(); i++) g.fields[i].transfer = saved[i];
+	halo_wait(g);
+}
+
+__global__ void po_classify_kernel(int32_t* cls, DevMesh M, const uint64_t* ids, size_t n, size_t n_local,
+                                   int32_t value) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const int32_t sl = dm_slot(M, ids[i]);
+		if (sl >= 0 && size_t(sl) < n_local) cls[sl] = value;  // only local cells (is_local, 839-878)
+	}
+}
+
+static int po_field(Grid& g, const char* name, size_t elem) {
+	Field f;
+	f.name = name;
+	f.elem = elem;
+	f.win_len = elem;
+	f.transfer = false;
+	g.fields.push_back(std::move(f));
+	Field& nf = g.fields.back();
+	nf.data.alloc(g.n_slots * elem);
+	if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+	return int(g.fields.size() - 1);
+}
+
+static void po_ensure_fields(Grid& g) {
+	PoissonState& P = g.po;
+	if (P.type >= 0) return;
+	P.type = po_field(g, "poisson.type", 4);
+	P.p0 = po_field(g, "poisson.p0", 8);
+	P.p1 = po_field(g, "poisson.p1", 8);
+	P.r0 = po_field(g, "poisson.r0", 8);
+	P.r1 = po_field(g, "poisson.r1", 8);
+	P.ap0 = po_field(g, "poisson.A_dot_p0", 8);
+	P.best = po_field(g, "poisson.best_solution", 8);
+	P.sf = po_field(g, "poisson.scaling_factor", 8);
+	static const char* fn[6] = {"poisson.f_x_neg", "poisson.f_x_pos", "poisson.f_y_neg",
+	                            "poisson.f_y_pos", "poisson.f_z_neg", "poisson.f_z_pos"};
+	for (int k = 0; k < 6; k++) P.f[k] = po_field(g, fn[k], 8);
+}
+
+static PoArrays po_arrays(Grid& g) {
+	PoissonState& P = g.po;
+	auto d = [&](int f) { return (double*)field(g, f).data.p; };
+	PoArrays a{};
+	a.ell = P.ell.p;
+	a.fine = P.fine.p;
+	a.type = (const int32_t*)field(g, P.type).data.p;
+	a.rhs = d(P.rhs);
+	a.sol = d(P.sol);
+	a.best = d(P.best);
+	a.p0 = d(P.p0);
+	a.p1 = d(P.p1);
+	a.r0 = d(P.r0);
+	a.r1 = d(P.r1);
+	a.ap0 = d(P.ap0);
+	a.sf = d(P.sf);
+	for (int k = 0; k < 6; k++) a.f[k] = d(P.f[k]);
+	return a;
+}
+
+// cache_system_info 827-971
+static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns, const uint64_t* skip, size_t nk) {
+	DX_REQUIRE(field(g, rhs).elem == 8 && field(g, sol).elem == 8, "rhs and solution must be fp64 fields");
+	po_ensure_fields(g);
+	PoissonState& P = g.po;
+	P.rhs = rhs;
+	P.sol = sol;
+	ensure_face(g);
+	hipStream_t s = g.s_comp;
+	const size_t nl = g.n_local;
+	int32_t* type = (int32_t*)field(g, P.type).data.p;
+	// classify: local cells boundary, then skip, then solve (836-878)
+	k_fill_i32(type, nl, 1, s);
+	for (int pass = 0; pass < 2; pass++) {
+		const uint64_t* ids = pass == 0 ? skip : solve;
+		const size_t n = pass == 0 ? nk : ns;
+		if (!n) continue;
+		DBuf<uint64_t> d;
+		d.alloc(n);
+		HIP_CHECK(hipMemcpyAsync(d.p, ids, n * 8, hipMemcpyHostToDevice, s));
+		po_classify_kernel<<<grid_for(n, 256), 256, 0, s>>>(type, g.dm(), d.p, n, nl, pass == 0 ? 2 : 0);
+		HIP_CHECK(hipGetLastError());
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	halo_only(g, {P.type});  // TYPE (880-881)
+	DBuf<int32_t> cls;
+	cls.alloc(g.n_slots + 1);
+	if (g.n_slots) HIP_CHECK(hipMemcpyAsync(cls.p, type, g.n_slots * 4, hipMemcpyDeviceToDevice, s));
+	P.ell.alloc(6 * nl + 6);
+	P.fine.alloc(g.face_fine.n);
+	const PoArrays a = po_arrays(g);
+	k_po_cache(g.m, g.l0, g.slot_ids.p, cls.p, g.face_ell.p, g.face_fine.p, nl, P.ell.p, P.fine.p, type, a, s);
+	HIP_CHECK(hipStreamSynchronize(s));
+	std::vector<int> geo{P.sf};  // GEOMETRY (969-970)
+	for (int k = 0; k < 6; k++) geo.push_back(P.f[k]);
+	halo_only(g, geo);
+	HIP_CHECK(hipStreamSynchronize(s));
+	P.valid = true;
+}
+
+// sums of the last phase -> (all ranks) -> scalar control flow
+static void po_reduce(Grid& g, int k, unsigned nb, const PoParams& prm, int stage) {
+	PoissonState& P = g.po;
+	const bool one = g.size == 1;
+	k_po_reduce(k, P.part.p, nb, P.red.p, P.st.p, prm, stage, one, g.s_comp);
+	if (one) return;
+	comm_require(g, "Poisson solve");
+	if (g.nccl && !g.xfn) {
+		NCCL_CHECK(ncclAllReduce(P.red.p, P.red.p, size_t(k), ncclFloat64, ncclSum, g.nccl, g.s_comp));
+	} else {
+		double h[2] = {0, 0};
+		HIP_CHECK(hipMemcpyAsync(h, P.red.p, size_t(k) * 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		comm_allreduce_f64(g, h, k, 0);
+		HIP_CHECK(hipMemcpyAsync(P.red.p, h, size_t(k) * 8, hipMemcpyHostToDevice, g.s_comp));
+	}
+	k_po_scalar(P.red.p, P.st.p, prm, stage, g.s_comp);
+}
+
+static PoScalars po_read_scalars(Grid& g) {
+	PoScalars h{};
+	HIP_CHECK(hipMemcpyAsync(&h, g.po.st.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	return h;
+}
+
+// solve 251-522 / solve_failsafe 531-634 after po_cache; the host only
+// enqueues kernels and polls the device's `done` flag every few iterations.
+// Timed (dccrgx_kernel_timing): from the first phase of an iteration to its
+// last, the reductions included, the halo excluded.
+static PoScalars po_solve(Grid& g, const PoParams& prm, bool failsafe) {
+	PoissonState& P = g.po;
+	DX_REQUIRE(P.valid, "Poisson system not cached for the current mesh");
+	hipStream_t s = g.s_comp;
+	const size_t n = g.n_local;
+	const unsigned nb = k_po_blocks(n);
+	if (P.part.n < 2 * size_t(nb)) P.part.alloc(2 * size_t(nb));
+	P.red.alloc(2);
+	P.st.alloc(1);
+	const PoArrays a = po_arrays(g);
+	const int poll = 8;
+	if (!failsafe) {
+		halo_only(g, {P.sol});  // INIT (983-984)
+		k_po_phase(PO_PHASE_INIT, a, n, prm, P.st.p, P.part.p, s);
+		po_reduce(g, 1, nb, prm, PO_STAGE_INIT);
+		for (unsigned it = 0; it < prm.max_it; it++) {
+			halo_only(g, {P.p0, P.p1});  // SOLVING (283-284)
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_A, a, n, prm, P.st.p, P.part.p, s);
+			po_reduce(g, 2, nb, prm, PO_STAGE_A);
+			k_po_phase(PO_PHASE_B, a, n, prm, P.st.p, P.part.p, s);
+			po_reduce(g, 1, nb, prm, PO_STAGE_B);
+			k_po_phase(PO_PHASE_C, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			if ((it + 1) % poll == 0 && po_read_scalars(g).done) break;
+		}
+		k_po_phase(PO_PHASE_FINISH, a, n, prm, P.st.p, P.part.p, s);
+	} else {
+		k_po_reduce(1, P.part.p, 0, P.red.p, P.st.p, prm, PO_STAGE_JACOBI_INIT, true, s);
+		for (unsigned it = 0; it < prm.max_it; it++) {
+			halo_only(g, {P.sol});  // INIT (545, 551)
+			k_time_begin(g);
+			k_po_phase(PO_PHASE_JACOBI, a, n, prm, P.st.p, P.part.p, s);
+			po_reduce(g, 1, nb, prm, PO_STAGE_JACOBI);
+			k_po_phase(PO_PHASE_JACOBI_COPY, a, n, prm, P.st.p, P.part.p, s);
+			k_time_end(g);
+			if ((it + 1) % poll == 0 && po_read_scalars(g).done) break;
+		}
+	}
+	return po_read_scalars(g);
+}
+
+// --------------------------------------------------------------------------- grid files
+// save_grid_data / load_grid_data (dccrg.hpp:1089-1740, 1742-2425), file
+// layout 1104-1120: `offset` bytes left alone, the caller's header, uint64
+// 0x1234567890abcdef, the grid block (Mapping::write dccrg_mapping.hpp:576 =
+// 3 x uint64 length + int max_ref_lvl; the neighborhood length as unsigned;
+// Grid_Topology::write dccrg_topology.hpp:144 = 3 x uint8 periodic;
+// Cartesian_Geometry::write dccrg_cartesian_geometry.hpp:618 = int id 1 +
+// 3 x double start + 3 x double level-0 length), uint64 total cells, per
+// cell (uint64 id, uint64 absolute byte offset of its data) rank by rank,
+// then the cell data in the same order.  A cell's data = the payload of
+// every transferred field, in field order (the reference writes what
+// get_mpi_datatype describes at save time).  Cells of a rank in ascending id
+// (the reference: get_cells() order).  Every rank writes its own records with
+// pwrite at offsets derived from the all-gathered per-rank cell counts.
+static constexpr uint64_t kEndianCheck = 0x1234567890abcdefULL;
+static constexpr int kCartesianGeometryId = 1;
+
+static std::vector<uint8_t> grid_block(const Grid& g) {
+	std::vector<uint8_t> b;
+	auto put = [&b](const void* p, size_t n) {
+		const uint8_t* q = static_cast<const uint8_t*>(p);
+		b.insert(b.end(), q, q + n);
+	};
+	put(g.len, 24);
+	const int32_t R = g.R;
+	put(&R, 4);
+	const uint32_t hood = g.hood_len;
+	put(&hood, 4);
+	const uint8_t per[3] = {uint8_t(g.per[0] != 0), uint8_t(g.per[1] != 0), uint8_t(g.per[2] != 0)};
+	put(per, 3);
+	const int32_t gid = kCartesianGeometryId;
+	put(&gid, 4);
+	put(g.start, 24);
+	put(g.l0, 24);
+	return b;
+}
+
+static void pwrite_all(int fd, const void* p, size_t n, uint64_t off) {
+	const uint8_t* q = static_cast<const uint8_t*>(p);
+	while (n) {
+		const ssize_t w = ::pwrite(fd, q, n, off_t(off));
+		DX_REQUIRE(w > 0, "grid file write failed");
+		q += w;
+		n -= size_t(w);
+		off += uint64_t(w);
+	}
+}
+
+static void pread_all(int fd, void* p, size_t n, uint64_t off) {
+	uint8_t* q = static_cast<uint8_t*>(p);
+	while (n) {
+		const ssize_t r = ::pread(fd, q, n, off_t(off));
+		DX_REQUIRE(r > 0, "grid file truncated");
+		q += r;
+		n -= size_t(r);
+		off += uint64_t(r);
+	}
+}
+
+struct Closer {
+	int fd;
+	~Closer() { ::close(fd); }
+};
+
+static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const void* header, size_t header_bytes) {
+	DX_REQUIRE(g.initialized, "not initialized");
+	const std::vector<Field*> tf = transfer_fields(g);
+	size_t bpc = 0;
+	for (Field* f : tf) bpc += f->elem;
+	const auto cnt = comm_allgather_u64(g, {uint64_t(g.n_local)});
+	uint64_t total = 0, before = 0;
+	for (int p = 0; p < g.size; p++) {
+		const uint64_t c = cnt[size_t(p)].empty() ? 0 : cnt[size_t(p)][0];
+		if (p < g.rank) before += c;
+		total += c;
+	}
+	const int fd = ::open(path, O_CREAT | O_WRONLY, 0644);
+	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
+	Closer closer{fd};
+	uint64_t off = offset;
+	if (g.rank == 0 && header_bytes) pwrite_all(fd, header, header_bytes, off);
+	off += header_bytes;
+	if (g.rank == 0) pwrite_all(fd, &kEndianCheck, 8, off);
+	off += 8;
+	const std::vector<uint8_t> block = grid_block(g);
+	if (g.rank == 0) pwrite_all(fd, block.data(), block.size(), off);
+	off += block.size();
+	if (g.rank == 0) pwrite_all(fd, &total, 8, off);
+	off += 8;
+	const uint64_t list0 = off, data0 = off + 16 * total;
+	// local cells ascending, with their slots
+	const size_t nl = g.n_local;
+	const auto& sid = slot_ids_host(g);
+	std::vector<uint32_t> order(nl);
+	std::iota(order.begin(), order.end(), 0u);
+	std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sid[a] < sid[b]; });
+	std::vector<uint64_t> list(2 * nl);
+	for (size_t i = 0; i < nl; i++) {
+		list[2 * i] = sid[order[i]];
+		list[2 * i + 1] = data0 + bpc * (before + i);
+	}
+	if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
+	if (nl && bpc) {
+		std::vector<uint8_t> data(nl * bpc);
+		size_t fo = 0;
+		for (Field* f : tf) {
+			const std::vector<uint8_t> h = download(f->data.p, nl * f->elem, g.s_comp);
+			for (size_t i = 0; i < nl; i++) std::memcpy(&data[i * bpc + fo], &h[size_t(order[i]) * f->elem], f->elem);
+			fo += f->elem;
+		}
+		pwrite_all(fd, data.data(), data.size(), data0 + bpc * before);
+	}
+}
+
+static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t header_bytes) {
+	DX_REQUIRE(!g.initialized, "load_grid_data initializes the grid: call it instead of initialize");
+	const int fd = ::open(path, O_RDONLY);
+	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
+	Closer closer{fd};
+	uint64_t off = offset + header_bytes, endian = 0;
+	pread_all(fd, &endian, 8, off);
+	DX_REQUIRE(endian == kEndianCheck, "grid file endianness check failed");
+	off += 8;
+	uint8_t blk[87];
+	pread_all(fd, blk, sizeof(blk), off);
+	off += sizeof(blk);
+	uint64_t len[3];
+	int32_t R, gid;
+	uint32_t hood;
+	double start[3], l0[3];
+	std::memcpy(len, blk, 24);
+	std::memcpy(&R, blk + 24, 4);
+	std::memcpy(&hood, blk + 28, 4);
+	std::memcpy(&gid, blk + 35, 4);
+	std::memcpy(start, blk + 39, 24);
+	std::memcpy(l0, blk + 63, 24);
+	DX_REQUIRE(gid == kCartesianGeometryId, "grid file geometry is not Cartesian_Geometry");
+	// the same checks as the setters (a foreign or corrupt file must not
+	// reach the builders)
+	for (int d = 0; d < 3; d++) DX_REQUIRE(len[d] > 0, "grid file: grid length must be > 0");
+	DX_REQUIRE(R >= 0 && R <= max_possible_level(len) && R < kMaxLevels, "grid file: invalid refinement level");
+	DX_REQUIRE(hood <= max_hood_length(), "grid file: neighborhood length not supported");
+	for (int d = 0; d < 3; d++) DX_REQUIRE(l0[d] > 0, "grid file: cell length must be > 0");
+	for (int d = 0; d < 3; d++) {
+		g.len[d] = len[d];
+		g.per[d] = blk[32 + d] != 0;
+		g.start[d] = start[d];
+		g.l0[d] = l0[d];
+	}
+	g.R = R;
+	g.hood_len = hood;
+	init_impl(g);
+	uint64_t total = 0;
+	pread_all(fd, &total, 8, off);
+	off += 8;
+	std::vector<uint64_t> list(2 * total);
+	if (total) pread_all(fd, list.data(), 16 * total, off);
+	std::vector<std::pair<uint64_t, uint64_t>> cells(total);
+	for (size_t i = 0; i < total; i++) cells[i] = {list[2 * i], list[2 * i + 1]};
+	std::sort(cells.begin(), cells.end());
+	// owners as load_cells (3647) produces them: the level-0 block
+	// partition (create_level_0_cells), refined cells inherit it
+	std::vector<uint64_t> ids(total);
+	std::vector<int32_t> own(total);
+	for (size_t i = 0; i < total; i++) {
+		ids[i] = cells[i].first;
+		DX_REQUIRE(i == 0 || ids[i] > ids[i - 1], "grid file lists a cell twice");
+		const uint64_t l0p = map_level0_parent(g.m, ids[i]);
+		DX_REQUIRE(l0p != error_cell, "grid file lists an invalid cell");
+		own[i] = g.mesh.bp.owner(l0p);
+	}
+	Mesh nm;
+	mesh_from_global(g, nm, ids, own);
+	rebuild(g, nm);
+	// payloads of the local cells
+	const std::vector<Field*> tf = transfer_fields(g);
+	size_t bpc = 0;
+	for (Field* f : tf) bpc += f->elem;
+	const size_t nl = g.n_local;
+	if (!nl || !bpc) return;
+	const auto& sid = slot_ids_host(g);
+	std::vector<uint64_t> where(nl);
+	uint64_t lo = ~uint64_t(0), hi = 0;
+	for (size_t i = 0; i < nl; i++) {
+		auto it = std::lower_bound(cells.begin(), cells.end(), std::make_pair(sid[i], uint64_t(0)));
+		DX_REQUIRE(it != cells.end() && it->first == sid[i], "local cell missing from grid file");
+		where[i] = it->second;
+		lo = std::min(lo, where[i]);
+		hi = std::max(hi, where[i] + bpc);
+	}
+	std::vector<uint8_t> raw(hi - lo);
+	pread_all(fd, raw.data(), raw.size(), lo);
+	size_t fo = 0;
+	for (Field* f : tf) {
+		std::vector<uint8_t> h(nl * f->elem);
+		for (size_t i = 0; i < nl; i++) std::memcpy(&h[i * f->elem], &raw[where[i] - lo + fo], f->elem);
+		HIP_CHECK(hipMemcpy(f->data.p, h.data(), h.size(), hipMemcpyHostToDevice));
+		fo += f->elem;
+	}
+}
+
+static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
+	for (int k = 0; k < 7; k++) {
+		Field& F = field(g, fids[k]);
+		DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+		f[k] = (const double*)F.data.p;
+	}
+}
+
+static void gol_step_impl(Grid& g, Field& f, int region) {
+	size_t s0, s1;
+	region_range(g, region, s0, s1);
+	if (s1 <= s0) return;
+	if (!g.gol_plan_valid) {
+		g.gol_plan_ok = gol_slab_plan(g, g.gol_inner, g.gol_outer);
+		g.gol_plan_valid = true;
+	}
+	const uint32_t* st = (const uint32_t*)f.data.p;
+	uint32_t* out = (uint32_t*)f.scratch.p;
+	k_time_begin(g);
+	bool done = false;
+	if (g.gol_plan_ok) {
+		done = true;
+		const uint64_t plane = g.len[0] * g.len[1];
+		for (int r = 0; r < 2 && done; r++) {
+			if (r == 0 && region == DCCRGX_REGION_OUTER) continue;
+			if (r == 1 && region == DCCRGX_REGION_INNER) continue;
+			for (const GolBox& b : r == 0 ? g.gol_inner : g.gol_outer) {
+				const uint64_t n[3] = {g.len[0], g.len[1], b.nz};
+				const int per[3] = {g.per[0], g.per[1], b.lo == -3 ? g.per[2] : 0};
+				const uint32_t* lo = b.lo >= 0 ? st + uint64_t(b.lo) : nullptr;
+				const uint32_t* hi = b.hi >= 0 ? st + uint64_t(b.hi) : nullptr;
+				(void)plane;
+				if (!k_gol_structured(st + b.slot0, out + b.slot0, n, per, lo, hi, g.s_comp)) {
+					done = false;
+					break;
+				}
+			}
+		}
+	}
+	if (!done) {
+		ensure_csr(g);
+		k_gol_csr(st, out, g.it_ptr.p, g.it_slot.p, s0, s1, g.s_comp);
+	}
+	k_time_end(g);
+}
+
+}  // namespace dccrgx
+
+// ============================================================================
+// C ABI
+// ============================================================================
+using namespace dccrgx;
+
+struct dccrgx_grid {
+	Grid g;
+};
+
+#define GRID_OR_FAIL(gp) \
+	if (!(gp)) throw Error(DCCRGX_EINVAL, "null grid"); \
+	Grid& g = (gp)->g
+
+static dccrgx_grid* new_grid(int rank, int size, int device) {
+	DX_REQUIRE(size >= 1 && rank >= 0 && rank < size, "invalid rank/size");
+	HIP_CHECK(hipSetDevice(device));
+	auto* h = new dccrgx_grid();
+	Grid& g = h->g;
+	g.rank = rank;
+	g.size = size;
+	g.device = device;
+	HIP_CHECK(hipStreamCreateWithFlags(&g.s_comp, hipStreamNonBlocking));
+	HIP_CHECK(hipStreamCreateWithFlags(&g.s_comm, hipStreamNonBlocking));
+	HIP_CHECK(hipEventCreateWithFlags(&g.ev_comp, hipEventDisableTiming));
+	HIP_CHECK(hipEventCreateWithFlags(&g.ev_halo, hipEventDisableTiming));
+	mesh_init_implicit(g);
+	return h;
+}
+
+extern "C" {
+
+const char* dccrgx_last_error(void) { return g_last_error.c_str(); }
+int dccrgx_abi_version(void) { return DCCRGX_ABI_VERSION; }
+
+int dccrgx_get_unique_id(void* out) {
+	return guard([&] {
+		ncclUniqueId id;
+		NCCL_CHECK(ncclGetUniqueId(&id));
+		std::memcpy(out, &id, sizeof(id));
+		return 0;
+	});
+}
+
+int dccrgx_create(int rank, int size, int device, const void* nccl_id, dccrgx_grid** out) {
+	return guard([&] {
+		DX_REQUIRE(out, "null output");
+		dccrgx_grid* h = new_grid(rank, size, device);
+		if (size > 1 && nccl_id) {  // without an id: a detached view of one rank (no transport)
+			ncclUniqueId id;
+			std::memcpy(&id, nccl_id, sizeof(id));
+			const ncclResult_t r = ncclCommInitRank(&h->g.nccl, size, id, rank);
+			if (r != ncclSuccess) {
+				delete h;
+				throw Error(DCCRGX_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+			}
+		}
+		*out = h;
+		return 0;
+	});
+}
+
+int dccrgx_create_with_exchange(int rank, int size, int device, dccrgx_exchange_fn fn, void* ctx, dccrgx_grid** out) {
+	return guard([&] {
+		DX_REQUIRE(out && fn, "null output or exchange function");
+		dccrgx_grid* h = new_grid(rank, size, device);
+		h->g.xfn = fn;
+		h->g.xctx = ctx;
+		*out = h;
+		return 0;
+	});
+}
+
+int dccrgx_destroy(dccrgx_grid* gp) {
+	return guard([&] {
+		if (!gp) return 0;
+		Grid& g = gp->g;
+		(void)hipDeviceSynchronize();
+		drain_timing(g);
+		if (g.nccl) ncclCommDestroy(g.nccl);
+		if (g.ev_comp) (void)hipEventDestroy(g.ev_comp);
+		if (g.ev_halo) (void)hipEventDestroy(g.ev_halo);
+		if (g.s_comp) (void)hipStreamDestroy(g.s_comp);
+		if (g.s_comm) (void)hipStreamDestroy(g.s_comm);
+		delete gp;
+		return 0;
+	});
+}
+
+int dccrgx_set_initial_length(dccrgx_grid* gp, const uint64_t length[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_initial_length after initialize");
+		for (int d = 0; d < 3; d++) DX_REQUIRE(length[d] > 0, "grid length must be > 0");
+		for (int d = 0; d < 3; d++) g.len[d] = length[d];
+		return 0;
+	});
+}
+
+int dccrgx_set_maximum_refinement_level(dccrgx_grid* gp, int level) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_maximum_refinement_level after initialize");
+		const int maxpos = max_possible_level(g.len);
+		if (level < 0) level = maxpos;
+		DX_REQUIRE(level <= maxpos && level < kMaxLevels, "refinement level too large for the grid");
+		g.R = level;
+		return 0;
+	});
+}
+
+int dccrgx_get_maximum_refinement_level(dccrgx_grid* gp, int* level) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		*level = g.R;
+		return 0;
+	});
+}
+
+int dccrgx_set_periodic(dccrgx_grid* gp, int x, int y, int z) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_periodic after initialize");
+		g.per[0] = x != 0;
+		g.per[1] = y != 0;
+		g.per[2] = z != 0;
+		return 0;
+	});
+}
+
+int dccrgx_set_neighborhood_length(dccrgx_grid* gp, unsigned length) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(!g.initialized, "set_neighborhood_length after initialize");
+		DX_REQUIRE(length <= max_hood_length(),
+		           "neighborhood length > " + std::to_string(max_hood_length()) + " not supported");
+		g.hood_len = length;
+		return 0;
+	});
+}
+
+int dccrgx_initialize(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		init_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_set_geometry(dccrgx_grid* gp, const double start[3], const double l0[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		for (int d = 0; d < 3; d++) DX_REQUIRE(l0[d] > 0, "cell length must be > 0");
+		for (int d = 0; d < 3; d++) {
+			g.start[d] = start[d];
+			g.l0[d] = l0[d];
+		}
+		return 0;
+	});
+}
+
+int dccrgx_geometry_batch(dccrgx_grid* gp, const uint64_t* ids, size_t n, double* center, double* length) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(ids || !n, "null ids");
+		MapCtx m;
+		map_init(m, g.len, g.R, g.per);
+		const double nan = std::numeric_limits<double>::quiet_NaN();
+		for (size_t i = 0; i < n; i++) {
+			uint64_t ind[3];
+			const int lvl = map_indices(m, ids[i], ind[0], ind[1], ind[2]);
+			for (int d = 0; d < 3; d++) {
+				double L = nan, c = nan;
+				if (lvl >= 0) {  // dccrg_cartesian_geometry.hpp:299-303, 334-359
+					L = g.l0[d] * (1.0 / double(uint64_t(1) << lvl));
+					c = g.start[d] + double(ind[d]) * g.l0[d] / double(uint64_t(1) << g.R) + L / 2;
+				}
+				if (length) length[3 * i + d] = L;
+				if (center) center[3 * i + d] = c;
+			}
+		}
+		return 0;
+	});
+}
+
+uint64_t dccrgx_get_cell_from_indices(dccrgx_grid* gp, const uint64_t ind[3], int level) {
+	if (!gp) return error_cell;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return map_from_indices(m, ind[0], ind[1], ind[2], level);
+}
+
+int dccrgx_get_indices(dccrgx_grid* gp, uint64_t cell, uint64_t ind[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		MapCtx m;
+		map_init(m, g.len, g.R, g.per);
+		const int l = map_indices(m, cell, ind[0], ind[1], ind[2]);
+		return l < 0 ? DCCRGX_ENOTFOUND : 0;
+	});
+}
+
+int dccrgx_get_refinement_level(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return map_level(m, cell);
+}
+
+uint64_t dccrgx_get_last_cell(dccrgx_grid* gp) {
+	if (!gp) return 0;
+	MapCtx m;
+	map_init(m, gp->g.len, gp->g.R, gp->g.per);
+	return m.last;
+}
+
+int dccrgx_get_counts(dccrgx_grid* gp, size_t* ni, size_t* no, size_t* nr, size_t* ns) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (ni) *ni = g.n_inner;
+		if (no) *no = g.n_outer;
+		if (nr) *nr = g.n_recv;
+		if (ns) *ns = g.n_slots;
+		return 0;
+	});
+}
+
+int dccrgx_get_cells(dccrgx_grid* gp, int which, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		const auto& ids = slot_ids_host(g);
+		std::vector<uint64_t> v;
+		switch (which) {
+		case DCCRGX_CELLS_LOCAL: v.assign(ids.begin(), ids.begin() + ptrdiff_t(g.n_local)); break;
+		case DCCRGX_CELLS_INNER: v.assign(ids.begin(), ids.begin() + ptrdiff_t(g.n_inner)); break;
+		case DCCRGX_CELLS_OUTER: v.assign(ids.begin() + ptrdiff_t(g.n_inner), ids.begin() + ptrdiff_t(g.n_local)); break;
+		case DCCRGX_CELLS_REMOTE: v.assign(ids.begin() + ptrdiff_t(g.n_local), ids.end()); break;
+		case DCCRGX_CELLS_ALL: v = ids; break;
+		default: throw Error(DCCRGX_EINVAL, "invalid selection");
+		}
+		std::sort(v.begin(), v.end());
+		return copy_out_u64(v, out, cap, n);
+	});
+}
+
+int dccrgx_get_slot_ids(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		return copy_out_u64(slot_ids_host(g), out, cap, n);
+	});
+}
+
+int dccrgx_get_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32_t* offs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = lookup_slot(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_csr(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.nof_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) {
+			HIP_CHECK(hipMemcpy(ids, g.nof_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
+			if (offs) HIP_CHECK(hipMemcpy(offs, g.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_get_neighbors_to(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = lookup_slot(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_csr(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.nto_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) HIP_CHECK(hipMemcpy(ids, g.nto_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32_t* dirs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const int64_t s = lookup_slot(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		ensure_face(g);
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, g.face_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		std::vector<int32_t> ent(k);
+		if (k) HIP_CHECK(hipMemcpy(ent.data(), g.face_ent.p + be[0], k * 4, hipMemcpyDeviceToHost));
+		const auto& sid = slot_ids_host(g);
+		static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
+		for (size_t i = 0; i < k; i++) {
+			ids[i] = sid[size_t(ent[i] >> 3)];
+			if (dirs) dirs[i] = dmap[ent[i] & 7];
+		}
+		return 0;
+	});
+}
+
+int dccrgx_download_csr(dccrgx_grid* gp, int kind, uint32_t* ptr, uint64_t* ids, int32_t* aux, size_t cap,
+                        size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(kind >= 0 && kind <= 3, "invalid CSR kind");
+		const size_t nl = g.n_local;
+		const uint32_t* dptr = nullptr;
+		if (kind == 2) {
+			ensure_face(g);
+			dptr = g.face_ptr.p;
+		} else {
+			ensure_csr(g);
+			dptr = kind == 0 ? g.nof_ptr.p : kind == 1 ? g.nto_ptr.p : g.it_ptr.p;
+		}
+		std::vector<uint32_t> hp = download(dptr, nl + 1, g.s_comp);
+		const size_t tot = hp[nl];
+		if (n) *n = tot;
+		if (tot > cap) return DCCRGX_ERANGE;
+		std::memcpy(ptr, hp.data(), (nl + 1) * 4);
+		if (!tot) return 0;
+		const auto& sid = slot_ids_host(g);
+		if (kind == 0) {
+			HIP_CHECK(hipMemcpy(ids, g.nof_id.p, tot * 8, hipMemcpyDeviceToHost));
+			if (aux) HIP_CHECK(hipMemcpy(aux, g.nof_off.p, tot * 12, hipMemcpyDeviceToHost));
+		} else if (kind == 1) {
+			HIP_CHECK(hipMemcpy(ids, g.nto_id.p, tot * 8, hipMemcpyDeviceToHost));
+		} else if (kind == 2) {
+			std::vector<int32_t> ent = download(g.face_ent.p, tot, g.s_comp);
+			static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
+			for (size_t i = 0; i < tot; i++) {
+				ids[i] = sid[size_t(ent[i] >> 3)];
+				if (aux) aux[i] = dmap[ent[i] & 7];
+			}
+		} else {
+			std::vector<int32_t> sl = download(g.it_slot.p, tot, g.s_comp);
+			for (size_t i = 0; i < tot; i++) ids[i] = sid[size_t(sl[i])];
+			if (aux) HIP_CHECK(hipMemcpy(aux, g.it_off.p, tot * 12, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_is_local(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return 0;
+	try {
+		return is_local_cell(gp->g, cell) ? 1 : 0;
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return 0;
+	}
+}
+
+int dccrgx_get_process(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	try {
+		return lookup_owner(gp->g, cell);
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return -1;
+	}
+}
+
+int64_t dccrgx_get_slot(dccrgx_grid* gp, uint64_t cell) {
+	if (!gp) return -1;
+	try {
+		return lookup_slot(gp->g, cell);
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return -1;
+	}
+}
+
+int dccrgx_get_peers(dccrgx_grid* gp, int32_t* peers, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (n) *n = g.peers.size();
+		if (g.peers.size() > cap) return DCCRGX_ERANGE;
+		for (size_t i = 0; i < g.peers.size(); i++) peers[i] = g.peers[i];
+		return 0;
+	});
+}
+
+int dccrgx_get_cells_to_send(dccrgx_grid* gp, int peer, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		auto it = g.halo.send_ids.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == g.halo.send_ids.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_get_cells_to_receive(dccrgx_grid* gp, int peer, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		auto it = g.halo.recv_ids.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == g.halo.recv_ids.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_get_cell_process(dccrgx_grid* gp, uint64_t* ids, int32_t* owners, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		std::vector<uint64_t> k;
+		std::vector<int32_t> o;
+		known_leaves(g, k, o);
+		if (n) *n = k.size();
+		if (!ids) return 0;
+		if (cap < k.size()) return int(DCCRGX_ERANGE);
+		std::copy(k.begin(), k.end(), ids);
+		if (owners) std::copy(o.begin(), o.end(), owners);
+		return 0;
+	});
+}
+
+int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* nr) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (ns) *ns = g.halo.n_send;
+		if (nr) *nr = g.halo.n_recv;
+		return 0;
+	});
+}
+
+int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 2449-2459: only local cells
+		if (map_level(g.m, cell) >= g.R) return 0;                      // 2474-2477: no-op at max level
+		g.refine_requests.push_back(cell);
+		return 0;
+	});
+}
+
+int dccrgx_stop_refining(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		g.last_new_cells = stop_refining_impl(g);
+		if (!out) {
+			if (n) *n = g.last_new_cells.size();
+			return 0;
+		}
+		return copy_out_u64(g.last_new_cells, out, cap, n);
+	});
+}
+
+int dccrgx_get_new_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		return copy_out_u64(g.last_new_cells, out, cap, n);
+	});
+}
+
+int dccrgx_set_cells(dccrgx_grid* gp, const uint64_t* ids, const int32_t* owners, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		DX_REQUIRE(!g.mig.active, "balance_load in progress");
+		std::vector<uint64_t> L(ids, ids + n);
+		std::vector<int32_t> O(owners, owners + n);
+		for (size_t i = 0; i < n; i++) {
+			DX_REQUIRE(L[i] != error_cell && L[i] <= g.m.last, "invalid cell id");
+			DX_REQUIRE(i == 0 || L[i] > L[i - 1], "cell ids must be strictly ascending");
+			DX_REQUIRE(O[i] >= 0 && O[i] < g.size, "invalid owner");
+		}
+		Mesh nm;
+		mesh_from_global(g, nm, L, O);
+		rebuild(g, nm);
+		g.pins.clear();
+		return 0;
+	});
+}
+
+int dccrgx_pin(dccrgx_grid* gp, uint64_t cell, int process) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(process >= 0 && process < g.size, "invalid process");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 5877-5887: local leaves only
+		g.pins[cell] = process;
+		return 0;
+	});
+}
+
+int dccrgx_unpin(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.pins.erase(cell);
+		return 0;
+	});
+}
+
+int dccrgx_add_neighborhood(dccrgx_grid* gp, int id, const int32_t* offsets, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		// add_neighborhood 6383-6520: the reference returns false for these
+		DX_REQUIRE(id != DCCRGX_DEFAULT_HOOD, "neighborhood id is the default id");
+		DX_REQUIRE(!g.uhoods.count(id), "neighborhood id already exists");
+		for (size_t i = 0; i < n; i++) {
+			const int32_t* o = offsets + 3 * i;
+			if (g.hood_len > 0) {
+				for (int d = 0; d < 3; d++)
+					DX_REQUIRE(unsigned(std::abs(o[d])) <= g.hood_len, "offset outside the default neighborhood");
+				DX_REQUIRE(o[0] || o[1] || o[2], "offset (0, 0, 0)");
+			} else {
+				int zeros = 0;
+				for (int d = 0; d < 3; d++) {
+					zeros += o[d] == 0;
+					DX_REQUIRE(std::abs(o[d]) <= 1, "offset outside the face neighborhood");
+				}
+				DX_REQUIRE(zeros == 2, "face neighborhood offsets must be unit face offsets");
+			}
+		}
+		UserHood& h = g.uhoods[id];
+		h.of.assign(offsets, offsets + 3 * n);
+		h.to.resize(h.of.size());
+		for (size_t i = 0; i < h.of.size(); i++) h.to[i] = -h.of[i];
+		upload(h.d_of, h.of, g.s_comp);
+		upload(h.d_to, h.to, g.s_comp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		ensure_uhood(g, id);
+		return 0;
+	});
+}
+
+int dccrgx_remove_neighborhood(dccrgx_grid* gp, int id) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.uhoods.erase(id);
+		return 0;
+	});
+}
+
+int dccrgx_get_user_neighbors(dccrgx_grid* gp, int id, uint64_t cell, int kind, uint64_t* ids, int32_t* offs,
+                              size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (!g.uhoods.count(id)) return DCCRGX_ENOTFOUND;
+		const int64_t s = lookup_slot(g, cell);
+		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		UserHood& h = ensure_uhood(g, id);
+		const DBuf<uint32_t>& ptr = kind == 0 ? h.nof_ptr : h.nto_ptr;
+		uint32_t be[2];
+		HIP_CHECK(hipMemcpy(be, ptr.p + s, 8, hipMemcpyDeviceToHost));
+		const size_t k = be[1] - be[0];
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		if (k) {
+			HIP_CHECK(hipMemcpy(ids, (kind == 0 ? h.nof_id.p : h.nto_id.p) + be[0], k * 8, hipMemcpyDeviceToHost));
+			if (offs && kind == 0)
+				HIP_CHECK(hipMemcpy(offs, h.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_get_user_update_list(dccrgx_grid* gp, int id, int peer, int receive, uint64_t* ids, size_t cap,
+                                size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (!g.uhoods.count(id)) return DCCRGX_ENOTFOUND;
+		UserHood& h = ensure_uhood(g, id);
+		const auto& mp = receive ? h.plan.recv_ids : h.plan.send_ids;
+		auto it = mp.find(peer);
+		static const std::vector<uint64_t> empty;
+		return copy_out_u64(it == mp.end() ? empty : it->second, ids, cap, n);
+	});
+}
+
+int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* gp, int id) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (id == DCCRGX_DEFAULT_HOOD) {
+			halo_start(g);
+			halo_wait(g);
+		} else {
+			uhood_halo(g, id);
+		}
+		return 0;
+	});
+}
+
+int dccrgx_halo_message_size(dccrgx_grid* gp, int hood, int peer, size_t* sb, size_t* rb) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		size_t a = 0, b = 0;
+		halo_message_size(g, hood, peer, a, b);
+		if (sb) *sb = a;
+		if (rb) *rb = b;
+		return 0;
+	});
+}
+
+int dccrgx_halo_pack(dccrgx_grid* gp, int hood, int peer, void* buf, size_t cap) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_pack_peer(g, hood, peer, static_cast<uint8_t*>(buf), cap);
+		return 0;
+	});
+}
+
+int dccrgx_halo_place(dccrgx_grid* gp, int hood, int peer, const void* buf, size_t bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_place_peer(g, hood, peer, static_cast<const uint8_t*>(buf), bytes);
+		return 0;
+	});
+}
+
+int dccrgx_balance_load(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (g.size == 1) return 0;
+		initialize_balance_load_impl(g, nullptr, nullptr, 0);
+		continue_balance_load_impl(g);
+		finish_balance_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_balance_load_to(dccrgx_grid* gp, const uint64_t* cells, const int32_t* procs, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		DX_REQUIRE((cells && procs) || !n, "null export list");
+		if (g.size == 1) {
+			for (size_t i = 0; i < n; i++) DX_REQUIRE(procs[i] == 0, "new process out of range");
+			return 0;
+		}
+		initialize_balance_load_impl(g, cells, procs, n);
+		continue_balance_load_impl(g);
+		finish_balance_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_initialize_balance_load(dccrgx_grid* gp, const uint64_t* cells, const int32_t* procs, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE((cells && procs) || !n, "null export list");
+		initialize_balance_load_impl(g, cells, procs, n);
+		return 0;
+	});
+}
+
+int dccrgx_continue_balance_load(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		continue_balance_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_finish_balance_load(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		finish_balance_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_migration_message_size(dccrgx_grid* gp, int peer, size_t* sb, size_t* rb) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		size_t a = 0, b = 0;
+		migration_message_size(g, peer, a, b);
+		if (sb) *sb = a;
+		if (rb) *rb = b;
+		return 0;
+	});
+}
+
+int dccrgx_migration_pack(dccrgx_grid* gp, int peer, void* buf, size_t cap) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		migration_pack_peer(g, peer, static_cast<uint8_t*>(buf), cap);
+		return 0;
+	});
+}
+
+int dccrgx_migration_place(dccrgx_grid* gp, int peer, const void* buf, size_t bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		migration_place_peer(g, peer, static_cast<const uint8_t*>(buf), bytes);
+		return 0;
+	});
+}
+
+int dccrgx_save_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, const void* header,
+                          size_t header_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		save_grid_impl(g, path, offset, header, header_bytes);
+		return 0;
+	});
+}
+
+int dccrgx_load_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, size_t header_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		load_grid_impl(g, path, offset, header_bytes);
+		return 0;
+	});
+}
+
+int dccrgx_add_field(dccrgx_grid* gp, const char* name, size_t elem, int transfer, int* fid) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(elem > 0, "element size must be > 0");
+		Field f;
+		f.name = name ? name : "";
+		f.elem = elem;
+		f.win_len = elem;
+		f.transfer = transfer != 0;
+		g.fields.push_back(std::move(f));
+		Field& nf = g.fields.back();
+		if (g.initialized) {
+			nf.data.alloc(g.n_slots * elem);
+			if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+		}
+		*fid = int(g.fields.size() - 1);
+		return 0;
+	});
+}
+
+int dccrgx_set_field_transfer(dccrgx_grid* gp, int fid, int transfer) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		field(g, fid).transfer = transfer != 0;
+		return 0;
+	});
+}
+
+int dccrgx_set_field_window(dccrgx_grid* gp, int fid, size_t offset, size_t bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(offset + bytes <= f.elem && bytes > 0, "window outside the element");
+		f.win_off = offset;
+		f.win_len = bytes;
+		return 0;
+	});
+}
+
+int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		*ptr = field(g, fid).data.p;
+		return 0;
+	});
+}
+
+int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const void* host) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		if (n) HIP_CHECK(hipMemcpy(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice));
+		return 0;
+	});
+}
+
+int dccrgx_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_t n, void* host) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		if (n) HIP_CHECK(hipMemcpy(host, f.data.p + slot0 * f.elem, n * f.elem, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_update_copies_of_remote_neighbors(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_start(g);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_start_remote_neighbor_copy_updates(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_start(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_update_receives(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_update_sends(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_wait_remote_neighbor_copy_updates(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		halo_wait(g);
+		return 0;
+	});
+}
+
+int dccrgx_gol_step(dccrgx_grid* gp, int sf, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, sf);
+		DX_REQUIRE(f.elem == 4, "game of life state must be a 4-byte field");
+		ensure_scratch(g, f);
+		gol_step_impl(g, f, region);
+		return 0;
+	});
+}
+
+int dccrgx_gol_commit(dccrgx_grid* gp, int sf) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		commit(g, field(g, sf));
+		return 0;
+	});
+}
+
+// get_live_neighbors of tests/game_of_life/solve.hpp:37-170, split at its
+// halo: phase 0 = the collect loop (46-110), phase 1 = spread + rule
+// (113-167); see gol_amr.hip
+int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(phase == 0 || phase == 1, "phase must be 0 (collect) or 1 (spread)");
+		Field& st = field(g, sf);
+		Field& ls = field(g, lf);
+		DX_REQUIRE(st.elem == 4, "game of life state must be a 4-byte field");
+		DX_REQUIRE(ls.elem == 64, "live level-0 neighbor list must be a 64-byte field (8 x uint64)");
+		size_t s0, s1;
+		region_range(g, region, s0, s1);
+		if (s1 <= s0) return 0;
+		ensure_csr(g);
+		DBuf<int> err;
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		k_time_begin(g);
+		if (g.gol_l0p.n < g.n_slots) g.gol_l0p.alloc(g.n_slots);
+		k_gol_amr(phase, g.m, g.slot_ids.p, g.n_slots, g.gol_l0p.p, (uint32_t*)st.data.p, (uint64_t*)ls.data.p,
+		          g.nof_ptr.p, g.nof_slot.p, s0, s1, err.p, g.s_comp);
+		k_time_end(g);
+		int h = 0;
+		HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+		DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+		return 0;
+	});
+}
+
+int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int region) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const double* f[7];
+		adv_fields(g, fids, f);
+		Field& rho = field(g, fids[0]);
+		ensure_scratch(g, rho);
+		size_t s0, s1;
+		region_range(g, region, s0, s1);
+		if (s1 <= s0) return 0;
+		ensure_tiles(g);
+		k_time_begin(g);
+		// tiles never straddle the inner / outer runs
+		if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
+		if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
+		k_time_end(g);
+		return 0;
+	});
+}
+
+int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[10]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(out, "null output");
+		ensure_tiles(g);
+		const uint64_t nt = g.n_tiles_inner + g.n_tiles_outer;
+		uint32_t entries = 0;
+		HIP_CHECK(hipMemcpy(&entries, g.face_ptr.p + g.n_local, 4, hipMemcpyDeviceToHost));
+		const uint64_t n = g.n_local;
+		out[0] = uint64_t(g.tile);
+		out[1] = nt;
+		out[2] = g.total_ext;
+		out[3] = g.max_ext;
+		out[4] = g.n_fine_faces;
+		out[5] = entries;
+		// 64 B per cell (7 fp64 fields read, density written) +
+		// the face CSR (4 B per entry + 4 B row pointer)
+		out[6] = 64 * n + 4 * (n + 1) + 4 * uint64_t(entries);
+		out[7] = 64 * n;
+		out[8] = g.tcount[0] + g.tcount[1];
+		out[9] = 512 * (g.tcount[0] + g.tcount[1]);
+		return 0;
+	});
+}
+
+int dccrgx_advection_commit(dccrgx_grid* gp, int df) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		commit(g, field(g, df));
+		return 0;
+	});
+}
+
+// tests/advection/initialize.hpp:36-82 + Cartesian_Geometry get_center /
+// get_length (dccrg_cartesian_geometry.hpp:282-362), evaluated on the host
+// with the reference's expression order so the initial state is bitwise the
+// reference's.
+int dccrgx_advection_initialize(dccrgx_grid* gp, const int fids[7]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		// local cells and remote copies alike: the analytic initial state of a
+		// remote copy is what initialize() + update_copies_of_remote_neighbors()
+		// with transfer_all_data = true would deliver (initialize.hpp:80)
+		const auto& ids = slot_ids_host(g);
+		const size_t n = g.n_slots;
+		std::vector<double> a[7];
+		for (auto& v : a) v.resize(n);
+		for (size_t i = 0; i < n; i++) {
+			uint64_t ind[3];
+			const int lvl = map_indices(g.m, ids[i], ind[0], ind[1], ind[2]);
+			const double sf = 1.0 / double(uint64_t(1) << lvl);
+			double L[3], c[3];
+			for (int d = 0; d < 3; d++) L[d] = g.l0[d] * sf;
+			for (int d = 0; d < 3; d++)
+				c[d] = g.start[d] + double(ind[d]) * g.l0[d] / double(uint64_t(1) << g.R) + L[d] / 2;
+			const double radius = 0.15;
+			const double hr = std::min(std::sqrt(std::pow(c[0] - 0.25, 2.0) + std::pow(c[1] - 0.5, 2.0)), radius) / radius;
+			a[0][i] = 0.25 * (1 + std::cos(M_PI * hr));
+			a[1][i] = -c[1] + 0.5;
+			a[2][i] = +c[0] - 0.5;
+			a[3][i] = 0;
+			a[4][i] = L[0];
+			a[5][i] = L[1];
+			a[6][i] = L[2];
+		}
+		for (int k = 0; k < 7; k++) {
+			Field& F = field(g, fids[k]);
+			DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+			if (n) HIP_CHECK(hipMemcpy(F.data.p, a[k].data(), n * 8, hipMemcpyHostToDevice));
+		}
+		return 0;
+	});
+}
+
+int dccrgx_advection_max_time_step(dccrgx_grid* gp, const int fids[7], double* out) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		const double* f[7];
+		adv_fields(g, fids, f);
+		const size_t nb = 512;
+		DBuf<double> part;
+		part.alloc(nb);
+		k_adv_dt(f, g.n_local, part.p, nb, g.s_comp);
+		auto h = download(part.p, nb, g.s_comp);
+		*out = *std::min_element(h.begin(), h.end());
+		return 0;
+	});
+}
+
+int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_increase, double diff_threshold,
+                                       uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		ensure_face(g);
+		Field& F = field(g, df);
+		DBuf<uint64_t> d;
+		d.alloc(g.n_local + 1);
+		const size_t k = k_adv_candidates(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p,
+		                                  g.n_local, diff_increase, diff_threshold, d.p, g.s_comp);
+		auto v = download(d.p, k, g.s_comp);
+		std::sort(v.begin(), v.end());
+		return copy_out_u64(v, out, cap, n);
+	});
+}
+
+int dccrgx_allreduce_f64(dccrgx_grid* gp, double* v, int count, int op) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		comm_allreduce_f64(g, v, count, op);
+		return 0;
+	});
+}
+
+int dccrgx_barrier(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		double z = 0;
+		comm_allreduce_f64(g, &z, 1, 0);
+		return 0;
+	});
+}
+
+int dccrgx_synchronize(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		HIP_CHECK(hipStreamSynchronize(g.s_comm));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		return 0;
+	});
+}
+
+void* dccrgx_compute_stream(dccrgx_grid* gp) { return gp ? (void*)gp->g.s_comp : nullptr; }
+
+int dccrgx_kernel_timing(dccrgx_grid* gp, int enable, double* total_ms, int64_t* count) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		drain_timing(g);
+		if (total_ms) *total_ms = g.timed_ms;
+		if (count) *count = g.timed_count;
+		if (enable == 1) {
+			g.timing = true;
+			g.timed_ms = 0;
+			g.timed_count = 0;
+		} else if (enable == 0) {
+			g.timing = false;
+		}
+		return 0;
+	});
+}
+
+// ---- Poisson (tests/poisson/poisson_solve.hpp) ----------------------------
+int dccrgx_poisson_cache(dccrgx_grid* gp, int rhs_field, int solution_field, const uint64_t* solve_cells,
+                         size_t n_solve, const uint64_t* skip_cells, size_t n_skip) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "grid not initialized");
+		DX_REQUIRE((solve_cells || !n_solve) && (skip_cells || !n_skip), "null cell list");
+		po_cache(g, rhs_field, solution_field, solve_cells, n_solve, skip_cells, n_skip);
+		return 0;
+	});
+}
+
+int dccrgx_poisson_solve(dccrgx_grid* gp, unsigned max_iterations, unsigned min_iterations, double stop_residual,
+                         double p_of_norm, double stop_after_residual_increase, int failsafe, unsigned* iterations,
+                         double* residual) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(p_of_norm > 0, "p_of_norm must be > 0");
+		// solve() is a do-while (279-506): at least one iteration
+		const unsigned max_it = failsafe ? max_iterations : std::max(1u, max_iterations);
+		const PoParams prm{max_it, min_iterations, stop_residual, p_of_norm, stop_after_residual_increase};
+		const PoScalars st = po_solve(g, prm, failsafe != 0);
+		if (iterations) *iterations = st.iteration;
+		if (residual) *residual = failsafe ? st.norm : st.residual_min;
+		return 0;
+	});
+}
+
+int dccrgx_poisson_field(dccrgx_grid* gp, const char* name, int* fid) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(name && fid, "null argument");
+		DX_REQUIRE(g.po.type >= 0, "Poisson system not cached yet");
+		const std::string want = std::string("poisson.") + name;
+		for (size_t i = 0; i < g.fields.size(); i++)
+			if (g.fields[i].name == want) {
+				*fid = int(i);
+				return 0;
+			}
+		throw Error(DCCRGX_ENOTFOUND, "no Poisson field " + std::string(name));
+	});
+}
+
+}  // extern "C"

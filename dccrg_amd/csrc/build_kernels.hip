@@ -3,14 +3,16 @@
 // initialize_neighbors 8240-8289, find_neighbors_of 4339-4680,
 // find_neighbors_to 4708-4861, update_remote_neighbor_info 8992-9270,
 // recalculate_neighbor_update_send_receive_lists 8590-8752,
-// get_face_neighbors_of 2806-2933).
+// get_face_neighbors_of 2806-2933, update_cell_pointers 11314-11628) and of
+// the rank's leaf knowledge (dccrgx_mesh.hpp: hash table, ghost region,
+// refinement closure induce_refines 9591-9720, execute_refines 10104-10554).
 //
 // Layout: one wavefront (64 lanes) per cell; lanes own stencil items (or
 // neighbors_to candidates); per-cell output positions come from a wave
 // prefix scan (shuffle) / ballot + popcount compaction, so every row is
-// written in the reference's order without atomics.  Existence of a leaf is
-// one load from a dense id-indexed owner table (HBM is 288 GB; the table is
-// 4 B per possible id).
+// written in the reference's order without atomics.  Existence / owner /
+// slot of a leaf is one 16-byte probe sequence in the rank's hash table (or
+// the block-partition formula on the initial level-0 grid).
 #include <hipcub/hipcub.hpp>
 
 #include "dccrgx_internal.hpp"
@@ -20,12 +22,7 @@ namespace dccrgx {
 namespace {
 
 constexpr int WAVE = 64;
-
-struct DevExists {
-	const int32_t* owner;
-	uint64_t last;
-	__device__ bool operator()(uint64_t id) const { return id != 0 && id <= last && owner[id] >= 0; }
-};
+constexpr int kMaxNtoLds = 8192;  // u64 entries of the neighbors_to dedupe (64 KB of LDS)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
@@ -48,13 +45,6 @@ __device__ __forceinline__ int wave_sum(int v) {
 	return v;
 }
 
-inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u) {
-	size_t g = (n + per_block - 1) / per_block;
-	if (g > cap) g = cap;
-	if (g == 0) g = 1;
-	return unsigned(g);
-}
-
 __device__ void cell_coords(const MapCtx& m, uint64_t id, uint64_t c[3], int& lvl) {
 	lvl = map_indices(m, id, c[0], c[1], c[2]);
 }
@@ -65,23 +55,64 @@ __global__ void fill_i32_kernel(int32_t* p, size_t n, int32_t v) {
 		p[i] = v;
 }
 
-__global__ void scatter_owner_kernel(int32_t* owner_by_id, const uint64_t* ids, const int32_t* owners, size_t n) {
+__global__ void iota_u64_kernel(uint64_t* out, uint64_t first, size_t n) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		owner_by_id[ids[i]] = owners[i];
+		out[i] = first + i;
 }
 
-__global__ void scatter_slots_kernel(int32_t* slot_by_id, const uint64_t* slot_ids, size_t n) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		slot_by_id[slot_ids[i]] = int32_t(i);
+// insert (id, owner, slot = -1); keys are unique
+__global__ void hash_insert_kernel(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids,
+                                   const int32_t* owners, int32_t owner_const, size_t n) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[i];
+		uint64_t h = hash_home(id, shift);
+		for (;;) {
+			unsigned long long* kp = reinterpret_cast<unsigned long long*>(&tab[h].key);
+			const unsigned long long prev = atomicCAS(kp, 0ull, (unsigned long long)id);
+			if (prev == 0ull || prev == id) {
+				tab[h].owner = owners ? owners[i] : owner_const;
+				tab[h].slot = -1;
+				break;
+			}
+			h = (h + 1) & mask;
+		}
+	}
+}
+
+__global__ void hash_set_slots_kernel(DevMesh M, const uint64_t* slot_ids, size_t n, int32_t* err) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = slot_ids[i];
+		uint64_t h = hash_home(id, M.shift);
+		HashEntry* tab = const_cast<HashEntry*>(M.tab);
+		for (;;) {
+			const uint64_t k = tab[h].key;
+			if (k == id) {
+				tab[h].slot = int32_t(i);
+				break;
+			}
+			if (k == 0) {
+				atomicExch(err, 1);
+				break;
+			}
+			h = (h + 1) & M.mask;
+		}
+	}
+}
+
+__global__ void lookup_kernel(DevMesh M, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[i];
+		if (owner) owner[i] = dm_owner(M, id);
+		if (slot) slot[i] = dm_slot(M, id);
+	}
 }
 
 // --------------------------------------------------------------------------
 // Pass 1: does a local cell have any remote neighbors_of / neighbors_to?
 // (update_remote_neighbor_info 8992-9095).  One wave per cell.
-__global__ void remote_flags_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh,
-                                    const int32_t* owner_by_id, int rank, const uint64_t* cells, size_t n,
-                                    uint32_t* flag) {
-	const DevExists ex{owner_by_id, m.last};
+__global__ void remote_flags_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M, int rank,
+                                    const uint64_t* cells, size_t n, uint32_t* flag) {
+	const DevExists ex{M};
 	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
 	for (size_t w = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; w < n; w += waves) {
 		uint64_t c[3];
@@ -92,14 +123,13 @@ __global__ void remote_flags_kernel(MapCtx m, const int32_t* hood, const int32_t
 			ItemOut o;
 			nof_item(m, c, lvl, hood + 3 * k, ex, o);
 			for (int i = 0; i < o.n; i++) {
-				if (o.id[i] == error_cell) continue;
-				const int32_t ow = (o.id[i] <= m.last) ? owner_by_id[o.id[i]] : -1;
+				const int32_t ow = dm_owner(M, o.id[i]);
 				if (ow >= 0 && ow != rank) remote = true;
 			}
 		}
 		for (int k = lane_id(); k < 10 * nh; k += WAVE) {
 			const uint64_t f = nto_candidate(m, c, lvl, hood_to, nh, k, ex);
-			if (f != error_cell && owner_by_id[f] != rank) remote = true;
+			if (f != error_cell && dm_owner(M, f) != rank) remote = true;
 		}
 		const bool any = __any(remote);
 		if (lane_id() == 0) flag[w] = any ? 1u : 0u;
@@ -137,7 +167,7 @@ __device__ int nto_row(const MapCtx& m, const int32_t* hood_to, int nh, const De
 			cnt += __popcll(mask);
 		}
 	}
-	if (cnt > cap) cnt = cap;  // cap = 10*nh rounded up: never reached
+	if (cnt > cap) cnt = cap;  // cap >= 10*nh (max_hood_items): never reached
 	int P = 1;
 	while (P < cnt) P <<= 1;
 	for (int i = cnt + lane_id(); i < P; i += WAVE) lds[i] = ~0ull;
@@ -171,11 +201,11 @@ __device__ int nto_row(const MapCtx& m, const int32_t* hood_to, int nh, const De
 }
 
 // per-row counts in slot order (one wave = one block per row)
-__global__ void count_rows_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh,
-                                  const int32_t* owner_by_id, const uint64_t* slot_ids, size_t row0, size_t nrows,
-                                  uint32_t* nof_cnt, uint32_t* nto_cnt, int cap) {
+__global__ void count_rows_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M,
+                                  const uint64_t* slot_ids, size_t row0, size_t nrows, uint32_t* nof_cnt,
+                                  uint32_t* nto_cnt, int cap) {
 	extern __shared__ uint64_t lds[];
-	const DevExists ex{owner_by_id, m.last};
+	const DevExists ex{M};
 	for (size_t r = blockIdx.x; r < nrows; r += gridDim.x) {
 		uint64_t c[3];
 		int lvl;
@@ -196,10 +226,9 @@ __global__ void count_rows_kernel(MapCtx m, const int32_t* hood, const int32_t* 
 }
 
 // neighbors_of rows in stencil order (4339-4680 semantics, see dccrgx_neighbors.hpp)
-__global__ void fill_nof_kernel(MapCtx m, const int32_t* hood, int nh, const int32_t* owner_by_id,
-                                const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr,
-                                uint64_t* ids, int32_t* offs) {
-	const DevExists ex{owner_by_id, m.last};
+__global__ void fill_nof_kernel(MapCtx m, const int32_t* hood, int nh, DevMesh M, const uint64_t* slot_ids, size_t row0,
+                                size_t nrows, const uint32_t* ptr, uint64_t* ids, int32_t* offs) {
+	const DevExists ex{M};
 	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
 	for (size_t r = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; r < nrows; r += waves) {
 		uint64_t c[3];
@@ -224,11 +253,10 @@ __global__ void fill_nof_kernel(MapCtx m, const int32_t* hood, int nh, const int
 	}
 }
 
-__global__ void fill_nto_kernel(MapCtx m, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
-                                const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr,
-                                uint64_t* ids, int cap) {
+__global__ void fill_nto_kernel(MapCtx m, const int32_t* hood_to, int nh, DevMesh M, const uint64_t* slot_ids,
+                                size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids, int cap) {
 	extern __shared__ uint64_t lds[];
-	const DevExists ex{owner_by_id, m.last};
+	const DevExists ex{M};
 	for (size_t r = blockIdx.x; r < nrows; r += gridDim.x) {
 		uint64_t c[3];
 		int lvl;
@@ -238,64 +266,105 @@ __global__ void fill_nto_kernel(MapCtx m, const int32_t* hood_to, int nh, const 
 }
 
 // --------------------------------------------------------------------------
-__global__ void extract_remote_kernel(const uint64_t* ids, size_t n, const int32_t* owner_by_id, int rank,
-                                      uint64_t stride, uint64_t* keys, unsigned long long* counter) {
+__global__ void extract_remote_kernel(const uint64_t* ids, size_t n, DevMesh M, int rank, uint64_t stride,
+                                      uint64_t* keys, unsigned long long* counter) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = ids[i];
 		if (id == error_cell) continue;
-		const int32_t o = owner_by_id[id];
+		const int32_t o = dm_owner(M, id);
 		if (o >= 0 && o != rank) keys[atomicAdd(counter, 1ull)] = uint64_t(o) * stride + id;
 	}
 }
 
 __global__ void extract_send_kernel(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids,
-                                    size_t row0, size_t nrows, const int32_t* owner_by_id, int rank, uint64_t stride,
-                                    uint64_t* keys, unsigned long long* counter) {
+                                    size_t row0, size_t nrows, DevMesh M, int rank, uint64_t stride, uint64_t* keys,
+                                    unsigned long long* counter) {
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t self = slot_ids[row0 + r];
 		for (uint32_t e = nto_ptr[r]; e < nto_ptr[r + 1]; e++) {
-			const int32_t o = owner_by_id[nto_id[e]];
+			const int32_t o = dm_owner(M, nto_id[e]);
 			if (o >= 0 && o != rank) keys[atomicAdd(counter, 1ull)] = uint64_t(o) * stride + self;
 		}
 	}
 }
 
-__global__ void lookup_slots_kernel(const uint64_t* ids, size_t n, const int32_t* slot_by_id, int32_t* out,
-                                    int32_t* err) {
+__global__ void lookup_slots_kernel(const uint64_t* ids, size_t n, DevMesh M, int32_t* out, int32_t* err) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
-		const int32_t s = slot_by_id[ids[i]];
+		const int32_t s = dm_slot(M, ids[i]);
 		out[i] = s;
 		if (s < 0) atomicExch(err, 1);
 	}
 }
 
-// iterator neighbor list (update_cell_pointers 11451-11500): the row's
-// (id, offset) pairs without duplicates.  One thread per row.
+// (id, offset) order of std::set<pair<uint64_t, array<int, 3>>>
+__device__ __forceinline__ bool key_less(uint64_t ia, const int32_t* oa, uint64_t ib, const int32_t* ob) {
+	if (ia != ib) return ia < ib;
+	if (oa[0] != ob[0]) return oa[0] < ob[0];
+	if (oa[1] != ob[1]) return oa[1] < ob[1];
+	return oa[2] < ob[2];
+}
+
+// iterator neighbor range cell.neighbors_of (update_cell_pointers
+// 11451-11500): the distinct (id, offset) pairs of the row, the ones whose id
+// is not in the row's neighbors_to first ("only_of"), then the ones whose id
+// is ("both"), each class in (id, offset) order.  One thread per row; the
+// position of an entry is its rank within its class.
 __global__ void iterator_lists_kernel(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
-                                      const int32_t* nof_slot, size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr,
-                                      int32_t* it_slot, int pass) {
+                                      const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id,
+                                      size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot,
+                                      int32_t* it_off, int pass) {
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		const uint32_t b = nof_ptr[r], e = nof_ptr[r + 1];
-		uint32_t k = 0;
-		for (uint32_t j = b; j < e; j++) {
-			bool dup = false;
-			for (uint32_t i = b; i < j && !dup; i++) {
-				dup = nof_id[i] == nof_id[j] && nof_off[3 * i] == nof_off[3 * j] &&
-				      nof_off[3 * i + 1] == nof_off[3 * j + 1] && nof_off[3 * i + 2] == nof_off[3 * j + 2];
+		const uint32_t tb = nto_ptr[r], te = nto_ptr[r + 1];
+		auto is_dup = [&](uint32_t j) {
+			for (uint32_t i = b; i < j; i++)
+				if (nof_id[i] == nof_id[j] && nof_off[3 * i] == nof_off[3 * j] && nof_off[3 * i + 1] == nof_off[3 * j + 1] &&
+				    nof_off[3 * i + 2] == nof_off[3 * j + 2])
+					return true;
+			return false;
+		};
+		auto both = [&](uint64_t id) {
+			uint32_t lo = tb, hi = te;
+			while (lo < hi) {
+				const uint32_t mid = (lo + hi) >> 1;
+				if (nto_id[mid] < id) lo = mid + 1;
+				else hi = mid;
 			}
-			if (dup) continue;
-			if (pass == 1) it_slot[it_ptr[r] + k] = nof_slot[j];
-			k++;
+			return lo < te && nto_id[lo] == id;
+		};
+		uint32_t n_only = 0, n_all = 0;
+		for (uint32_t j = b; j < e; j++) {
+			if (is_dup(j)) continue;
+			n_all++;
+			if (!both(nof_id[j])) n_only++;
 		}
-		if (pass == 0) it_cnt[r] = k;
+		if (pass == 0) {
+			it_cnt[r] = n_all;
+			continue;
+		}
+		for (uint32_t j = b; j < e; j++) {
+			if (is_dup(j)) continue;
+			const bool bj = both(nof_id[j]);
+			uint32_t rank = 0;
+			for (uint32_t i = b; i < e; i++) {
+				if (i == j || is_dup(i) || both(nof_id[i]) != bj) continue;
+				if (key_less(nof_id[i], nof_off + 3 * i, nof_id[j], nof_off + 3 * j)) rank++;
+			}
+			const uint32_t pos = it_ptr[r] + (bj ? n_only : 0u) + rank;
+			it_slot[pos] = nof_slot[j];
+			if (it_off) {
+				it_off[3 * pos] = nof_off[3 * j];
+				it_off[3 * pos + 1] = nof_off[3 * j + 1];
+				it_off[3 * pos + 2] = nof_off[3 * j + 2];
+			}
+		}
 	}
 }
 
 // face lists (get_face_neighbors_of semantics), one thread per local slot
-__global__ void face_lists_kernel(MapCtx m, const int32_t* owner_by_id, const int32_t* slot_by_id,
-                                  const uint64_t* slot_ids, size_t nrows, uint32_t* cnt, const uint32_t* ptr,
-                                  int32_t* ent, int32_t* err, int pass) {
-	const DevExists ex{owner_by_id, m.last};
+__global__ void face_lists_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
+                                  const uint32_t* ptr, int32_t* ent, int32_t* err, int pass) {
+	const DevExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		uint64_t c[3];
 		int lvl;
@@ -306,7 +375,7 @@ __global__ void face_lists_kernel(MapCtx m, const int32_t* owner_by_id, const in
 			const int nf = face_dir(m, c, lvl, dir, ex, out);
 			for (int i = 0; i < nf; i++) {
 				if (pass == 1) {
-					const int32_t s = slot_by_id[out[i]];
+					const int32_t s = dm_slot(M, out[i]);
 					if (s < 0) atomicExch(err, 1);
 					ent[ptr[r] + k] = s * 8 + dir;
 				}
@@ -317,25 +386,23 @@ __global__ void face_lists_kernel(MapCtx m, const int32_t* owner_by_id, const in
 	}
 }
 
-__global__ void remap_field_kernel(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old,
-                                   const int32_t* new_slot_by_id, uint64_t last, uint8_t* new_data, size_t elem) {
+__global__ void remap_field_kernel(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, DevMesh newM,
+                                   uint8_t* new_data, size_t elem) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n_old; i += size_t(gridDim.x) * blockDim.x) {
-		const uint64_t id = old_ids[i];
-		if (id == 0 || id > last) continue;
-		const int32_t s = new_slot_by_id[id];
+		const int32_t s = dm_slot(newM, old_ids[i]);
 		if (s < 0) continue;
 		for (size_t b = 0; b < elem; b++) new_data[size_t(s) * elem + b] = old_data[i * elem + b];
 	}
 }
 
-__global__ void parent_fill_kernel(uint8_t* data, const uint64_t* slot_ids, size_t n, MapCtx m,
-                                   const uint8_t* old_data, const int32_t* old_slot_by_id, size_t elem) {
+__global__ void parent_fill_kernel(uint8_t* data, const uint64_t* slot_ids, size_t n, MapCtx m, const uint8_t* old_data,
+                                   DevMesh oldM, size_t elem) {
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = slot_ids[s];
-		if (old_slot_by_id[id] >= 0) continue;
+		if (dm_slot(oldM, id) >= 0) continue;
 		const uint64_t p = map_parent(m, id);
 		if (p == error_cell || p == id) continue;
-		const int32_t ps = old_slot_by_id[p];
+		const int32_t ps = dm_slot(oldM, p);
 		if (ps < 0) continue;
 		for (size_t b = 0; b < elem; b++) data[s * elem + b] = old_data[size_t(ps) * elem + b];
 	}
@@ -385,37 +452,194 @@ __global__ void face_ell_kernel(const uint32_t* ptr, const int32_t* ent, size_t 
 	}
 }
 
-int nto_cap(int nh) {
-	int P = 1;
-	while (P < 10 * nh) P <<= 1;
-	return P;
+// ---- ghost region ---------------------------------------------------------------
+// (level-0 parent, volume in finest-level cells) of every local cell
+__global__ void l0_volume_kernel(MapCtx m, const uint64_t* ids, size_t n, uint64_t* l0, uint64_t* vol) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const int lvl = map_level(m, ids[i]);
+		l0[i] = map_level0_parent(m, ids[i]);
+		vol[i] = uint64_t(1) << (3 * (m.R - lvl));
+	}
+}
+
+__device__ __forceinline__ bool sorted_has(const uint64_t* a, size_t n, uint64_t v) {
+	size_t lo = 0, hi = n;
+	while (lo < hi) {
+		const size_t mid = (lo + hi) >> 1;
+		if (a[mid] < v) lo = mid + 1;
+		else hi = mid;
+	}
+	return lo < n && a[lo] == v;
+}
+
+// keys-only hash set (wholly local level-0 cells): same probing as the mesh table
+__global__ void keyset_insert_kernel(uint64_t* tab, uint64_t mask, uint32_t shift, const uint64_t* keys,
+                                     const uint64_t* vals, uint64_t want, size_t n) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		if (vals && vals[i] != want) continue;
+		const uint64_t id = keys[i];
+		uint64_t h = hash_home(id, shift);
+		for (;;) {
+			const unsigned long long prev =
+			    atomicCAS(reinterpret_cast<unsigned long long*>(tab + h), 0ull, (unsigned long long)id);
+			if (prev == 0ull || prev == id) break;
+			h = (h + 1) & mask;
+		}
+	}
+}
+
+struct KeySet {
+	const uint64_t* tab;
+	uint64_t mask;
+	uint32_t shift;
+	__device__ __forceinline__ bool has(uint64_t id) const {
+		if (!tab) return false;
+		uint64_t h = hash_home(id, shift);
+		for (;;) {
+			const uint64_t k = tab[h];
+			if (k == id) return true;
+			if (k == 0) return false;
+			h = (h + 1) & mask;
+		}
+	}
+};
+
+// per distinct level-0 parent p of local cells: every level-0 cell q within
+// Chebyshev distance `radius` (periodic wrap) that is not wholly local
+// (full[] sorted; implicit grids: the block partition decides) is emitted
+__global__ void ghost_l0_kernel(MapCtx m, DevMesh M, int rank, const uint64_t* par, size_t n, KeySet full,
+                                int radius, uint64_t* out, unsigned long long* counter, unsigned long long cap) {
+	MapCtx m0 = m;  // level-0 index space
+	const int side = 2 * radius + 1;
+	const int cube = side * side * side;
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t x, y, z;
+		map_indices(m, par[i], x, y, z);
+		const int64_t len0 = int64_t(1) << m.R;
+		const int64_t b[3] = {int64_t(x), int64_t(y), int64_t(z)};
+		for (int k = 0; k < cube; k++) {
+			const int dx = k % side - radius, dy = (k / side) % side - radius, dz = k / (side * side) - radius;
+			uint64_t w[3];
+			if (!map_wrap(m0, 0, b[0] + dx * len0, w[0]) || !map_wrap(m0, 1, b[1] + dy * len0, w[1]) ||
+			    !map_wrap(m0, 2, b[2] + dz * len0, w[2]))
+				continue;
+			const uint64_t q = map_from_indices(m, w[0], w[1], w[2], 0);
+			bool local_full;
+			if (M.implicit) local_full = M.bp.owner(q) == rank;
+			else local_full = full.has(q);
+			if (local_full) continue;
+			const unsigned long long pos = atomicAdd(counter, 1ull);
+			if (pos < cap) out[pos] = q;
+		}
+	}
+}
+
+__global__ void cells_under_kernel(MapCtx m, const uint64_t* ids, size_t n, const uint64_t* l0, size_t nl0,
+                                   uint64_t* out, unsigned long long* counter) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		if (sorted_has(l0, nl0, map_level0_parent(m, ids[i]))) out[atomicAdd(counter, 1ull)] = ids[i];
+	}
+}
+
+// ---- refinement -------------------------------------------------------------------
+// induce_refines (9591-9720): for a requested local cell r, every existing
+// neighbors_of / neighbors_to entry coarser than r must be refined as well
+__global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M, int rank,
+                               const uint64_t* req, size_t n, uint64_t* out, unsigned long long* counter,
+                               unsigned long long cap) {
+	const DevExists ex{M};
+	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
+	for (size_t w = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; w < n; w += waves) {
+		const uint64_t r = req[w];
+		if (dm_owner(M, r) != rank) continue;  // wave-uniform
+		uint64_t c[3];
+		int lvl;
+		cell_coords(m, r, c, lvl);
+		auto emit = [&](uint64_t q) {
+			if (q == error_cell || !ex(q) || map_level(m, q) >= lvl) return;
+			const unsigned long long pos = atomicAdd(counter, 1ull);
+			if (pos < cap) out[pos] = q;
+		};
+		for (int k = lane_id(); k < nh; k += WAVE) {
+			ItemOut o;
+			nof_item(m, c, lvl, hood + 3 * k, ex, o);
+			for (int i = 0; i < o.n; i++) emit(o.id[i]);
+		}
+		for (int k = lane_id(); k < 10 * nh; k += WAVE) emit(nto_candidate(m, c, lvl, hood_to, nh, k, ex));
+	}
+}
+
+// execute_refines (10104-10554): children replace refined leaves and inherit
+// the owner (10228-10237)
+__global__ void refine_count_kernel(const uint64_t* kid, size_t n, const uint64_t* S, size_t nS, uint32_t* cnt) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		cnt[i] = sorted_has(S, nS, kid[i]) ? 8u : 1u;
+}
+
+__global__ void refine_fill_kernel(MapCtx m, const uint64_t* kid, const int32_t* kown, size_t n, const uint32_t* pos,
+                                   const uint32_t* cnt, uint64_t* oid, int32_t* oown) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t p = pos[i];
+		if (cnt[i] == 1u) {
+			oid[p] = kid[i];
+			oown[p] = kown[i];
+		} else {
+			uint64_t ch[8];
+			map_all_children(m, kid[i], ch);
+			for (int k = 0; k < 8; k++) {
+				oid[p + k] = ch[k];
+				oown[p + k] = kown[i];
+			}
+		}
+	}
 }
 
 }  // namespace
 
 // ============================================================================
+int max_hood_items() { return kMaxNtoLds / 10; }
+
+static int nto_cap(int nh) {
+	int P = 1;
+	while (P < 10 * nh) P <<= 1;
+	return P;
+}
+
 void k_fill_i32(int32_t* p, size_t n, int32_t v, hipStream_t s) {
 	if (!n) return;
 	fill_i32_kernel<<<grid_for(n, 256), 256, 0, s>>>(p, n, v);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_scatter_owner(int32_t* owner_by_id, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s) {
+void k_iota_u64(uint64_t* out, uint64_t first, size_t n, hipStream_t s) {
 	if (!n) return;
-	scatter_owner_kernel<<<grid_for(n, 256), 256, 0, s>>>(owner_by_id, ids, owners, n);
+	iota_u64_kernel<<<grid_for(n, 256), 256, 0, s>>>(out, first, n);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_scatter_slots(int32_t* slot_by_id, const uint64_t* slot_ids, size_t n, hipStream_t s) {
+void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids, const int32_t* owners,
+                   int32_t owner_const, size_t n, hipStream_t s) {
 	if (!n) return;
-	scatter_slots_kernel<<<grid_for(n, 256), 256, 0, s>>>(slot_by_id, slot_ids, n);
+	hash_insert_kernel<<<grid_for(n, 256), 256, 0, s>>>(tab, mask, shift, ids, owners, owner_const, n);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
-                    int rank, const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s) {
+void k_hash_set_slots(const DevMesh& M, const uint64_t* slot_ids, size_t n, int32_t* err, hipStream_t s) {
 	if (!n) return;
-	remote_flags_kernel<<<grid_for(n, 4), 256, 0, s>>>(m, hood, hood_to, nh, owner_by_id, rank, cells, n, flag);
+	hash_set_slots_kernel<<<grid_for(n, 256), 256, 0, s>>>(M, slot_ids, n, err);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_lookup(const DevMesh& M, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot, hipStream_t s) {
+	if (!n) return;
+	lookup_kernel<<<grid_for(n, 256), 256, 0, s>>>(M, ids, n, owner, slot);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M, int rank,
+                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s) {
+	if (!n) return;
+	remote_flags_kernel<<<grid_for(n, 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, cells, n, flag);
 	HIP_CHECK(hipGetLastError());
 }
 
@@ -426,135 +650,169 @@ void k_assign_slots2(const uint32_t* flag, const uint32_t* scan_outer, size_t n,
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
+void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M,
                   const uint64_t* slot_ids, size_t row0, size_t nrows, uint32_t* nof_cnt, uint32_t* nto_cnt,
                   hipStream_t s) {
 	if (!nrows) return;
 	const int cap = nto_cap(nh);
-	count_rows_kernel<<<grid_for(nrows, 1, 256u * 64u), WAVE, size_t(cap) * 8, s>>>(
-	    m, hood, hood_to, nh, owner_by_id, slot_ids, row0, nrows, nof_cnt, nto_cnt, cap);
+	DX_REQUIRE(cap <= kMaxNtoLds, "neighborhood too large for the neighbors_to build");
+	count_rows_kernel<<<grid_for(nrows, 1, 256u * 64u), WAVE, size_t(cap) * 8, s>>>(m, hood, hood_to, nh, M, slot_ids,
+	                                                                                  row0, nrows, nof_cnt, nto_cnt, cap);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_fill_neighbors_of(const MapCtx& m, const int32_t* hood, int nh, const int32_t* owner_by_id,
-                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
-                         int32_t* offs, hipStream_t s) {
+void k_fill_neighbors_of(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M, const uint64_t* slot_ids,
+                         size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids, int32_t* offs, hipStream_t s) {
 	if (!nrows) return;
-	fill_nof_kernel<<<grid_for(nrows, 4), 256, 0, s>>>(m, hood, nh, owner_by_id, slot_ids, row0, nrows, ptr, ids,
-	                                                    offs);
+	fill_nof_kernel<<<grid_for(nrows, 4), 256, 0, s>>>(m, hood, nh, M, slot_ids, row0, nrows, ptr, ids, offs);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
-                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
-                         hipStream_t s) {
+void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const DevMesh& M, const uint64_t* slot_ids,
+                         size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids, hipStream_t s) {
 	if (!nrows) return;
 	const int cap = nto_cap(nh);
-	fill_nto_kernel<<<grid_for(nrows, 1, 256u * 64u), WAVE, size_t(cap) * 8, s>>>(m, hood_to, nh, owner_by_id,
-	                                                                                slot_ids, row0, nrows, ptr, ids, cap);
+	DX_REQUIRE(cap <= kMaxNtoLds, "neighborhood too large for the neighbors_to build");
+	fill_nto_kernel<<<grid_for(nrows, 1, 256u * 64u), WAVE, size_t(cap) * 8, s>>>(m, hood_to, nh, M, slot_ids, row0,
+	                                                                                nrows, ptr, ids, cap);
 	HIP_CHECK(hipGetLastError());
 }
 
-size_t k_extract_remote(const uint64_t* ids, size_t n, const int32_t* owner_by_id, int rank, uint64_t stride,
-                        uint64_t* keys_out, hipStream_t s) {
-	if (!n) return 0;
-	DBuf<unsigned long long> ctr;
-	ctr.alloc(1);
-	HIP_CHECK(hipMemsetAsync(ctr.p, 0, sizeof(unsigned long long), s));
-	extract_remote_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, owner_by_id, rank, stride, keys_out, ctr.p);
-	HIP_CHECK(hipGetLastError());
+static size_t read_counter(const DBuf<unsigned long long>& ctr, hipStream_t s) {
 	unsigned long long h = 0;
 	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, sizeof(h), hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	return size_t(h);
+}
+
+static void zero_counter(DBuf<unsigned long long>& ctr, hipStream_t s) {
+	ctr.alloc(1);
+	HIP_CHECK(hipMemsetAsync(ctr.p, 0, sizeof(unsigned long long), s));
+}
+
+size_t k_extract_remote(const uint64_t* ids, size_t n, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out,
+                        hipStream_t s) {
+	if (!n) return 0;
+	DBuf<unsigned long long> ctr;
+	zero_counter(ctr, s);
+	extract_remote_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, rank, stride, keys_out, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	return read_counter(ctr, s);
 }
 
 size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
-                      size_t nrows, const int32_t* owner_by_id, int rank, uint64_t stride, uint64_t* keys_out,
-                      hipStream_t s) {
+                      size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s) {
 	if (!nrows) return 0;
 	DBuf<unsigned long long> ctr;
-	ctr.alloc(1);
-	HIP_CHECK(hipMemsetAsync(ctr.p, 0, sizeof(unsigned long long), s));
-	extract_send_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nto_id, nto_ptr, slot_ids, row0, nrows, owner_by_id, rank,
-	                                                         stride, keys_out, ctr.p);
+	zero_counter(ctr, s);
+	extract_send_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nto_id, nto_ptr, slot_ids, row0, nrows, M, rank, stride,
+	                                                         keys_out, ctr.p);
 	HIP_CHECK(hipGetLastError());
-	unsigned long long h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, sizeof(h), hipMemcpyDeviceToHost, s));
+	return read_counter(ctr, s);
+}
+
+__global__ void iota_i32_kernel(int32_t* out, size_t n) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		out[i] = int32_t(i);
+}
+
+void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
+                         hipStream_t s) {
+	ids.clear();
+	slots.clear();
+	if (!n) return;
+	DBuf<uint64_t> k2;
+	DBuf<int32_t> v1, v2;
+	k2.alloc(n);
+	v1.alloc(n);
+	v2.alloc(n);
+	iota_i32_kernel<<<grid_for(n, 256), 256, 0, s>>>(v1.p, n);
+	HIP_CHECK(hipGetLastError());
+	size_t bytes = 0;
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, slot_ids, k2.p, v1.p, v2.p, n, 0, 64, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(bytes);
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, slot_ids, k2.p, v1.p, v2.p, n, 0, 64, s));
+	ids = download(k2.p, n, s);
+	slots = download(v2.p, n, s);
+}
+
+void sort_u64(uint64_t* keys, size_t n, hipStream_t s) {
+	if (n < 2) return;
+	DBuf<uint64_t> tmp;
+	tmp.alloc(n);
+	size_t b1 = 0;
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, 64, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(b1);
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipMemcpyAsync(keys, tmp.p, n * 8, hipMemcpyDeviceToDevice, s));
 	HIP_CHECK(hipStreamSynchronize(s));
-	return size_t(h);
 }
 
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s) {
 	if (n == 0) return 0;
 	DBuf<uint64_t> tmp;
 	tmp.alloc(n);
-	DBuf<unsigned int> nsel;
+	DBuf<unsigned long long> nsel;
 	nsel.alloc(1);
 	size_t b1 = 0, b2 = 0;
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, int(n), 0, 64, s));
-	HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, b2, tmp.p, keys, nsel.p, int(n), s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, b2, tmp.p, keys, nsel.p, n, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(std::max(b1, b2));
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, int(n), 0, 64, s));
-	HIP_CHECK(hipcub::DeviceSelect::Unique(temp.p, b2, tmp.p, keys, nsel.p, int(n), s));
-	unsigned int h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, nsel.p, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
-	return size_t(h);
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceSelect::Unique(temp.p, b2, tmp.p, keys, nsel.p, n, s));
+	return read_counter(nsel, s);
 }
 
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {
 	// scans n + 1 entries: out[n] = sum(in[0..n))
 	size_t bytes = 0;
-	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, int(n + 1), s));
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n + 1, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(bytes);
-	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in, out, int(n + 1), s));
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in, out, n + 1, s));
 	uint32_t h = 0;
 	HIP_CHECK(hipMemcpyAsync(&h, out + n, sizeof(h), hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	return h;
 }
 
-void k_lookup_slots(const uint64_t* ids, size_t n, const int32_t* slot_by_id, int32_t* out, int32_t* err_flag,
-                    hipStream_t s) {
+void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s) {
 	if (!n) return;
-	lookup_slots_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, slot_by_id, out, err_flag);
+	lookup_slots_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, out, err_flag);
 	HIP_CHECK(hipGetLastError());
 }
 
 void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
-                      const int32_t* nof_slot, size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr,
-                      int32_t* it_slot, int pass, hipStream_t s) {
+                      const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
+                      uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off, int pass,
+                      hipStream_t s) {
 	if (!nrows) return;
-	iterator_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nof_ptr, nof_id, nof_off, nof_slot, nrows, it_cnt,
-	                                                           it_ptr, it_slot, pass);
+	iterator_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nof_ptr, nof_id, nof_off, nof_slot, nto_ptr, nto_id,
+	                                                           nrows, it_cnt, it_ptr, it_slot, it_off, pass);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_face_lists(const MapCtx& m, const int32_t* owner_by_id, const int32_t* slot_by_id, const uint64_t* slot_ids,
-                  size_t nrows, uint32_t* cnt, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass,
-                  hipStream_t s) {
+void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
+                  const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s) {
 	if (!nrows) return;
-	face_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, owner_by_id, slot_by_id, slot_ids, nrows, cnt, ptr, ent,
-	                                                       err_flag, pass);
+	face_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, cnt, ptr, ent, err_flag, pass);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_remap_field2(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const int32_t* new_slot_by_id,
-                    uint64_t last, uint8_t* new_data, size_t elem, hipStream_t s) {
+void k_remap_field(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const DevMesh& newM,
+                   uint8_t* new_data, size_t elem, hipStream_t s) {
 	if (!n_old) return;
-	remap_field_kernel<<<grid_for(n_old, 256), 256, 0, s>>>(old_data, old_ids, n_old, new_slot_by_id, last, new_data,
-	                                                        elem);
+	remap_field_kernel<<<grid_for(n_old, 256), 256, 0, s>>>(old_data, old_ids, n_old, newM, new_data, elem);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int32_t* slot_by_id, const MapCtx& m,
-                   const uint8_t* old_data, const int32_t* old_slot_by_id, size_t elem, hipStream_t s) {
-	(void)slot_by_id;
+void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const MapCtx& m, const uint8_t* old_data,
+                   const DevMesh& oldM, size_t elem, hipStream_t s) {
 	if (!n) return;
-	parent_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(data, slot_ids, n, m, old_data, old_slot_by_id, elem);
+	parent_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(data, slot_ids, n, m, old_data, oldM, elem);
 	HIP_CHECK(hipGetLastError());
 }
 
@@ -582,11 +840,131 @@ void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s) {
 	morton_keys_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, ids, n, keys.p);
 	HIP_CHECK(hipGetLastError());
 	size_t bytes = 0;
-	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys.p, keys2.p, ids, ids2.p, int(n), 0, 63, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, 63, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(bytes);
-	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, keys.p, keys2.p, ids, ids2.p, int(n), 0, 63, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, 63, s));
 	HIP_CHECK(hipMemcpyAsync(ids, ids2.p, n * 8, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ---- ghost region ---------------------------------------------------------------
+std::vector<uint64_t> k_ghost_level0(const MapCtx& m, const DevMesh& M, int rank, const uint64_t* local, size_t n,
+                                     int radius, hipStream_t s) {
+	if (!n) return {};
+	// distinct level-0 parents of the local cells; the wholly local ones
+	// (leaf volume 8^R) in a keys-only hash set.  Implicit grids: every local
+	// cell is a level-0 cell and the block partition tells what is local.
+	DBuf<uint64_t> uk, uv, set;
+	const uint64_t* par = local;
+	size_t np = n;
+	KeySet ks{nullptr, 0, 63};
+	if (!M.implicit) {
+		DBuf<uint64_t> l0, vol, l0s, vols;
+		l0.alloc(n);
+		vol.alloc(n);
+		l0s.alloc(n);
+		vols.alloc(n);
+		uk.alloc(n);
+		uv.alloc(n);
+		l0_volume_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, local, n, l0.p, vol.p);
+		HIP_CHECK(hipGetLastError());
+		DBuf<unsigned long long> nu;
+		nu.alloc(1);
+		size_t b1 = 0, b2 = 0;
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, l0.p, l0s.p, vol.p, vols.p, n, 0, 64, s));
+		HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(nullptr, b2, l0s.p, uk.p, vols.p, uv.p, nu.p, hipcub::Sum(), n, s));
+		DBuf<uint8_t> temp;
+		temp.alloc(std::max(b1, b2));
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, b1, l0.p, l0s.p, vol.p, vols.p, n, 0, 64, s));
+		HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(temp.p, b2, l0s.p, uk.p, vols.p, uv.p, nu.p, hipcub::Sum(), n, s));
+		np = read_counter(nu, s);
+		par = uk.p;
+		uint32_t bits = 4;
+		while ((uint64_t(1) << bits) < 2 * np) bits++;
+		set.alloc(size_t(1) << bits);
+		HIP_CHECK(hipMemsetAsync(set.p, 0, set.n * 8, s));
+		ks = KeySet{set.p, set.n - 1, 64u - bits};
+		keyset_insert_kernel<<<grid_for(np, 256), 256, 0, s>>>(set.p, ks.mask, ks.shift, uk.p, uv.p,
+		                                                       uint64_t(1) << (3 * m.R), np);
+		HIP_CHECK(hipGetLastError());
+	}
+	unsigned long long cap = 1ull << 22;
+	for (;;) {
+		DBuf<uint64_t> out;
+		out.alloc(size_t(cap));
+		DBuf<unsigned long long> ctr;
+		zero_counter(ctr, s);
+		ghost_l0_kernel<<<grid_for(np, 256), 256, 0, s>>>(m, M, rank, par, np, ks, radius, out.p, ctr.p, cap);
+		HIP_CHECK(hipGetLastError());
+		const size_t k = read_counter(ctr, s);
+		if (k > cap) {
+			cap = k;
+			continue;
+		}
+		const size_t u = sort_unique_u64(out.p, k, s);
+		return download(out.p, u, s);
+	}
+}
+
+std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size_t n, const std::vector<uint64_t>& l0,
+                                    hipStream_t s) {
+	if (!n || l0.empty()) return {};
+	DBuf<uint64_t> dl0, out;
+	upload(dl0, l0, s);
+	out.alloc(n);
+	DBuf<unsigned long long> ctr;
+	zero_counter(ctr, s);
+	cells_under_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, local, n, dl0.p, l0.size(), out.p, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t k = read_counter(ctr, s);
+	sort_u64(out.p, k, s);
+	return download(out.p, k, s);
+}
+
+std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
+                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s) {
+	if (req.empty()) return {};
+	DBuf<uint64_t> dreq;
+	upload(dreq, req, s);
+	unsigned long long cap = req.size() * 16 + 1024;
+	for (;;) {
+		DBuf<uint64_t> out;
+		out.alloc(size_t(cap));
+		DBuf<unsigned long long> ctr;
+		zero_counter(ctr, s);
+		induced_kernel<<<grid_for(req.size(), 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p,
+		                                                       ctr.p, cap);
+		HIP_CHECK(hipGetLastError());
+		const size_t k = read_counter(ctr, s);
+		if (k > cap) {
+			cap = k;
+			continue;
+		}
+		const size_t u = sort_unique_u64(out.p, k, s);
+		return download(out.p, u, s);
+	}
+}
+
+void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
+                     DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out, hipStream_t s) {
+	DBuf<uint64_t> dS;
+	upload(dS, S, s);
+	DBuf<uint32_t> cnt, pos;
+	cnt.alloc(n + 1);
+	pos.alloc(n + 1);
+	HIP_CHECK(hipMemsetAsync(cnt.p, 0, (n + 1) * 4, s));
+	if (n) {
+		refine_count_kernel<<<grid_for(n, 256), 256, 0, s>>>(kid, n, dS.p, S.size(), cnt.p);
+		HIP_CHECK(hipGetLastError());
+	}
+	n_out = scan_exclusive_u32(cnt.p, pos.p, n, s);
+	out_id.alloc(n_out + 1);
+	out_own.alloc(n_out + 1);
+	if (n) {
+		refine_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, kown, n, pos.p, cnt.p, out_id.p, out_own.p);
+		HIP_CHECK(hipGetLastError());
+	}
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 

@@ -1,0 +1,36 @@
+// Host driver functions shared by grid.hip (halo, refinement, migration,
+// sweeps) and api.hip (the C ABI).
+#pragma once
+
+#include "dccrgx_internal.hpp"
+
+namespace dccrgx {
+
+std::vector<Field*> transfer_fields(Grid& g);
+Field& field(Grid& g, int fid);
+void ensure_scratch(Grid& g, Field& f);
+void commit(Grid& g, Field& f);
+void region_range(const Grid& g, int region, size_t& s0, size_t& s1);
+void drain_timing(Grid& g);
+
+void halo_start(Grid& g);
+void halo_wait(Grid& g);
+UserHood& ensure_uhood(Grid& g, int id);
+HaloPlan& plan_of(Grid& g, int hood);
+void uhood_halo(Grid& g, int id);
+size_t halo_pack_peer(Grid& g, int hood, int peer, uint8_t* buf, size_t cap);
+void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t bytes);
+void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb);
+
+std::vector<uint64_t> stop_refining_impl(Grid& g);
+
+void initialize_balance_load_impl(Grid& g, const uint64_t* cells, const int32_t* procs, size_t n);
+void continue_balance_load_impl(Grid& g);
+void finish_balance_load_impl(Grid& g);
+void migration_message_size(Grid& g, int peer, size_t& sb, size_t& rb);
+void migration_pack_peer(Grid& g, int peer, uint8_t* buf, size_t cap);
+void migration_place_peer(Grid& g, int peer, const uint8_t* buf, size_t bytes);
+
+bool gol_slab_plan(Grid& g, std::vector<GolBox>& inner, std::vector<GolBox>& outer);
+
+}  // namespace dccrgx

@@ -13,6 +13,7 @@
 
 #include "../../include/dccrgx.h"
 #include "dccrgx_mapping.hpp"
+#include "dccrgx_mesh.hpp"
 #include "dccrgx_neighbors.hpp"
 
 namespace dccrgx {
@@ -77,6 +78,10 @@ struct DBuf {
 		if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
 		n = count;
 	}
+	// grow-only (keeps the allocation when it is large enough)
+	void reserve(size_t count) {
+		if (count > n) alloc(count);
+	}
 	void swap(DBuf& o) {
 		std::swap(p, o.p);
 		std::swap(n, o.n);
@@ -99,12 +104,25 @@ inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
 	return h;
 }
 
+inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u) {
+	size_t g = (n + per_block - 1) / per_block;
+	if (g > cap) g = cap;
+	if (g == 0) g = 1;
+	return unsigned(g);
+}
+
+// A field: one SoA array over all slots.  The halo carries bytes
+// [win_off, win_off + win_len) of every element (the part a Cell_Data's
+// get_mpi_datatype describes, dccrg_get_cell_datatype.hpp:40-340); the whole
+// element by default.
 struct Field {
 	std::string name;
 	size_t elem = 0;
 	bool transfer = false;
+	size_t win_off = 0, win_len = 0;
 	DBuf<uint8_t> data;     // n_slots * elem
 	DBuf<uint8_t> scratch;  // double buffer for sweeps (allocated on demand)
+	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
 // ---- Poisson BiCG (tests/poisson/poisson_solve.hpp) ------------------------
@@ -153,11 +171,23 @@ struct RegTileMeta {
 	uint32_t pad;
 };
 
+// Send / receive lists of one neighborhood (recalculate_neighbor_update_
+// send_receive_lists 8590-8752): per peer the ids in ascending order (= the
+// wire order of update_copies_of_remote_neighbors), their slots flattened
+// peer by peer, and staging buffers.  For the default neighborhood the
+// receive slots of a peer are one contiguous run of halo slots.
+struct HaloPlan {
+	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
+	std::map<int, size_t> send_off, recv_off;  // cell offsets into send_slots / recv_slots
+	size_t n_send = 0, n_recv = 0;
+	DBuf<int32_t> send_slots, recv_slots;
+	DBuf<uint8_t> sendbuf, recvbuf;
+	std::vector<int> peers() const;
+};
+
 // A user neighborhood (add_neighborhood, dccrg.hpp:6383-6520): its offsets,
 // neighbors_of / neighbors_to CSR of the local cells (built lazily after
-// every structural change, update_user_neighbors 8974-8980) and its
-// per-peer send / receive lists (recalculate_neighbor_update_send_receive_lists
-// for the id, 8590-8752), with their slots for the halo over this hood only.
+// every structural change, update_user_neighbors 8974-8980) and its halo plan.
 struct UserHood {
 	std::vector<int32_t> of, to;  // 3 per item; to = -of
 	DBuf<int32_t> d_of, d_to;
@@ -165,17 +195,60 @@ struct UserHood {
 	DBuf<uint32_t> nof_ptr, nto_ptr;
 	DBuf<uint64_t> nof_id, nto_id;
 	DBuf<int32_t> nof_off;
-	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
-	std::map<int, size_t> send_off, recv_off;
-	size_t n_send = 0, n_recv = 0;
-	DBuf<int32_t> send_slots, recv_slots;
+	HaloPlan plan;
+};
+
+// The leaves this rank knows (dccrgx_mesh.hpp): implicit (initial level-0
+// grid, block partition) or an explicit list of own + ghost leaves.
+struct Mesh {
+	bool implicit = true;
+	DBuf<uint64_t> kid;   // explicit: known leaves, any order
+	DBuf<int32_t> kown;   // their owners
+	size_t n_known = 0;
+	DBuf<HashEntry> tab;
+	uint64_t mask = 0;
+	uint32_t shift = 63;
+	BlockPart bp;
+	DevMesh dev(uint64_t last) const {
+		DevMesh d{};
+		d.tab = tab.p;
+		d.mask = mask;
+		d.shift = shift;
+		d.implicit = implicit ? 1 : 0;
+		d.bp = bp;
+		d.last = last;
+		return d;
+	}
+};
+
+// A balance_load in progress (initialize_balance_load 3746 / continue 3899 /
+// finish 3942): per peer the cells leaving / arriving (ascending id), the
+// payloads of every field packed peer by peer (per peer: field 0 of every
+// cell, field 1 of every cell, ...).
+struct Migration {
+	bool active = false, transferred = false;
+	std::map<int, std::vector<uint64_t>> out, in;
+	std::map<int, size_t> out_off, in_off;  // byte offsets into the buffers
+	std::vector<uint64_t> in_pinned;        // arriving cells that stay pinned here
 	DBuf<uint8_t> sendbuf, recvbuf;
+	size_t bytes_per_cell = 0;
+};
+
+// a box of whole z-planes of the uniform grid in slot order (slot0 first
+// slot, nz planes) and the slots of its z-1 / z+1 planes (-2: outside the
+// grid, -3: the box wraps onto itself periodically)
+struct GolBox {
+	uint64_t slot0, nz;
+	int64_t lo, hi;
 };
 
 struct Grid {
-	// communicator
+	// communicator: RCCL (nccl != nullptr), a caller-provided host exchange
+	// (xfn), or none (a detached view: structures only, no collectives)
 	int rank = 0, size = 1, device = 0;
-	ncclComm_t comm = nullptr;
+	ncclComm_t nccl = nullptr;
+	dccrgx_exchange_fn xfn = nullptr;
+	void* xctx = nullptr;
 	hipStream_t s_comp = nullptr, s_comm = nullptr;
 	hipEvent_t ev_comp = nullptr, ev_halo = nullptr;
 	bool halo_in_flight = false;
@@ -191,34 +264,32 @@ struct Grid {
 	std::vector<int32_t> hood_to;  // neighborhood_to (negated)
 	double start[3] = {0, 0, 0}, l0[3] = {1, 1, 1};
 
-	// global leaves (like cell_process, dccrg.hpp:7197): sorted ids + owners
-	std::vector<uint64_t> leaves;
-	std::vector<int32_t> owners;
-	std::unordered_map<uint64_t, int> pins;
+	Mesh mesh;
+	std::unordered_map<uint64_t, int> pins;  // local cells pinned to a process (pin 5832-5909)
 	std::vector<uint64_t> refine_requests;
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
+	Migration mig;
 
 	// local layout
 	size_t n_inner = 0, n_outer = 0, n_local = 0, n_recv = 0, n_slots = 0;
-	std::vector<int> peers;                                     // union of send/recv peers, ascending
-	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;    // ascending ids per peer
-	std::map<int, size_t> recv_slot0;                           // first halo slot per peer
-	std::map<int, size_t> send_off;                             // offset into send_slots per peer
-	size_t n_send_total = 0;
-	std::vector<uint64_t> extra_remote;                         // remote neighbors_to-only cells
-	std::vector<uint64_t> slot_ids_h;                           // host mirror of slot -> id
+	std::vector<int> peers;           // union of send/recv peers, ascending
+	HaloPlan halo;                    // default neighborhood
+	std::vector<uint64_t> extra_remote;  // remote neighbors_to-only cells
+	std::vector<uint64_t> slot_ids_h;    // host mirror of slot -> id
 	bool slot_ids_h_valid = false;
+	// host index of the slotted ids (ascending) and their slots, for per-cell
+	// queries (is_local, operator[], refine_completely) without a device trip
+	std::vector<uint64_t> index_ids_h;
+	std::vector<int32_t> index_slots_h;
+	bool index_h_valid = false;
 
-	// device structures
-	DBuf<int32_t> owner_by_id;  // last_cell + 1 entries, -1 = not a leaf
-	DBuf<int32_t> slot_by_id;   // last_cell + 1 entries, -1 = no slot on this rank
-	DBuf<uint64_t> slot_ids;    // n_slots
+	DBuf<uint64_t> slot_ids;  // n_slots
 	DBuf<int32_t> d_hood, d_hood_to;
 	// full CSR (built lazily): neighbors_of (stencil order), neighbors_to (ascending)
 	bool csr_valid = false;
 	DBuf<uint32_t> nof_ptr, nto_ptr, it_ptr;
 	DBuf<uint64_t> nof_id, nto_id;
-	DBuf<int32_t> nof_off, nof_slot, it_slot;
+	DBuf<int32_t> nof_off, nof_slot, it_slot, it_off;
 	// face CSR (built lazily): entry = slot * 8 + dir (dir 0..5 = -x,+x,-y,+y,-z,+z)
 	bool face_valid = false;
 	DBuf<uint32_t> face_ptr;
@@ -233,7 +304,7 @@ struct Grid {
 	// tile + k: ext[k] of the tile, 0x8000 | j: finer face j of the tile whose
 	// four tile-local indices are in `tfine`, 0xffff: no face neighbor)
 	bool tiles_valid = false;
-	int tile = 0;
+	int tile = 512;
 	size_t n_tiles_inner = 0, n_tiles_outer = 0, max_ext = 0, total_ext = 0;
 	DBuf<uint32_t> tstart;     // n_tiles + 1
 	DBuf<uint32_t> tell;       // 3 x u32 per local slot (6 x u16)
@@ -252,26 +323,14 @@ struct Grid {
 	DBuf<RegTileMeta> tregmeta;  // per regular tile (list order): start slot + neighbor-box starts
 	// per irregular tile (list order), 8 x u32: first slot, slots, first ext,
 	// ext count, first finer face, finer faces; empty when some tile exceeds
-	// the pipelined kernel's capacities (> 1024 ext cells or > 512 finer faces)
+	// the pipelined kernel's capacities (> 1024 ext cells or > 512 finer
+	// faces): the run is then swept by the untiled face-CSR kernel
 	DBuf<uint32_t> tmeta;
-	// per tile (all tiles, slot order), 16 u32: ts, n, e0, ne, fb, nf,
-	// nst[6] (regular: neighbor-box starts), kind (1 regular), pad; for the
-	// fused sweep over both kinds (empty when a tile exceeds its limits)
-	DBuf<uint32_t> tfmeta;
-	// work tickets of the persistent advection kernels: [kernel (0 regular,
-	// 1 general)][set][XCD][32] (one 128-B line per counter); a launch draws
-	// from set adv_par[kernel] and
-	// zeroes the other set for the next launch of that kernel
-	DBuf<uint32_t> adv_ctr;
-	uint32_t adv_par[2] = {0, 0};
-	// second compute stream: the general-tile sweep runs beside the regular one
-	hipStream_t s_adv2 = nullptr;
-	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	std::map<int, UserHood> uhoods;  // add_neighborhood ids
 	DBuf<uint64_t> gol_l0p;  // refined game of life: level-0 parent per slot (scratch)
-	// halo
-	DBuf<int32_t> send_slots;
-	DBuf<uint8_t> sendbuf;
+	// uniform game of life: the regions as plane boxes (gol_slab_plan), built lazily
+	bool gol_plan_valid = false, gol_plan_ok = false;
+	std::vector<GolBox> gol_inner, gol_outer;
 
 	std::vector<Field> fields;
 
@@ -289,52 +348,118 @@ struct Grid {
 
 	PoissonState po;
 
+	DevMesh dm() const { return mesh.dev(m.last); }
 	bool uniform() const { return R == 0; }
+	bool has_collectives() const { return size == 1 || nccl != nullptr || xfn != nullptr; }
 };
+
+// --- comm.hip: collectives and point-to-point transfers -----------------------
+// Every rank calls these in the same order (as the reference's MPI calls).
+// exchange: send[p] to rank p, receive what rank p sends (any sizes)
+std::vector<std::vector<uint8_t>> comm_exchange(Grid& g, const std::vector<std::vector<uint8_t>>& send);
+std::vector<std::vector<uint64_t>> comm_allgather_u64(Grid& g, const std::vector<uint64_t>& mine);
+std::vector<std::vector<uint64_t>> comm_alltoall_u64(Grid& g, const std::vector<std::vector<uint64_t>>& send);
+void comm_allreduce_f64(Grid& g, double* v, int count, int op);  // 0 sum, 1 min, 2 max
+uint64_t comm_allreduce_max_u64(Grid& g, uint64_t v);
+// device payloads: per peer one message of known size each way
+struct DevMsg {
+	int peer;
+	const uint8_t* send;
+	size_t send_bytes;
+	uint8_t* recv;
+	size_t recv_bytes;
+};
+void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s);
+void comm_require(const Grid& g, const char* what);
+
+// --- mesh.hip: knowledge, hash table, structures --------------------------------
+void mesh_init_implicit(Grid& g);
+// from a global leaf list (every leaf, ascending, owners): keep own + ghost
+void mesh_from_global(Grid& g, Mesh& out, const std::vector<uint64_t>& ids, const std::vector<int32_t>& owners);
+// explicit own + ghost list of the current mesh (materializes an implicit mesh)
+void mesh_materialize(Grid& g, Mesh& out);
+// after a repartition: own leaves known, ghosts fetched from their owners
+void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n_local);
+void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s);
+void rebuild(Grid& g, Mesh& new_mesh);  // new_mesh is moved into g.mesh
+void ensure_csr(Grid& g);
+void ensure_face(Grid& g);
+void ensure_tiles(Grid& g);
+const std::vector<uint64_t>& slot_ids_host(Grid& g);
+// batch lookups of known leaves: owner (-1 unknown) and slot (-1 none)
+void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot);
+int32_t lookup_owner(Grid& g, uint64_t id);
+bool is_local_cell(Grid& g, uint64_t id);
+int64_t lookup_slot(Grid& g, uint64_t id);
+// all known leaves (own + ghost) ascending
+void known_leaves(Grid& g, std::vector<uint64_t>& ids, std::vector<int32_t>& owners);
+// local leaf ids on the device (slot order)
+inline const uint64_t* local_ids_dev(const Grid& g) { return g.slot_ids.p; }
 
 // --- launchers implemented in build_kernels.hip -----------------------------
 void k_fill_i32(int32_t* p, size_t n, int32_t v, hipStream_t s);
-void k_scatter_owner(int32_t* owner_by_id, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s);
-void k_scatter_slots(int32_t* slot_by_id, const uint64_t* slot_ids, size_t n, hipStream_t s);
+void k_iota_u64(uint64_t* out, uint64_t first, size_t n, hipStream_t s);
+void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids, const int32_t* owners,
+                   int32_t owner_const, size_t n, hipStream_t s);
+void k_hash_set_slots(const DevMesh& M, const uint64_t* slot_ids, size_t n, int32_t* err, hipStream_t s);
+void k_lookup(const DevMesh& M, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot, hipStream_t s);
 // flag local cells that have a remote neighbors_of / neighbors_to entry
-void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
-                    int rank, const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s);
-// local ids -> slots: inner first, outer second, both ascending
+void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M, int rank,
+                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s);
+// local ids -> slots: inner first, outer second, both in the input order
 void k_assign_slots2(const uint32_t* flag, const uint32_t* scan_outer, size_t n, size_t n_inner, const uint64_t* cells,
                      uint64_t* slot_ids, hipStream_t s);
-void k_fill_neighbors_of(const MapCtx& m, const int32_t* hood, int nh, const int32_t* owner_by_id,
-                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
-                         int32_t* offs, hipStream_t s);
-void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
-                         const uint64_t* slot_ids, size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids,
-                         hipStream_t s);
-void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const int32_t* owner_by_id,
+void k_fill_neighbors_of(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M, const uint64_t* slot_ids,
+                         size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids, int32_t* offs, hipStream_t s);
+void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const DevMesh& M, const uint64_t* slot_ids,
+                         size_t row0, size_t nrows, const uint32_t* ptr, uint64_t* ids, hipStream_t s);
+void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M,
                   const uint64_t* slot_ids, size_t row0, size_t nrows, uint32_t* nof_cnt, uint32_t* nto_cnt,
                   hipStream_t s);
+int max_hood_items();  // largest stencil the neighbors_to dedupe can hold in LDS
 // remote (owner != rank) entries of an id array as composite keys owner*(last+1)+id
-size_t k_extract_remote(const uint64_t* ids, size_t n, const int32_t* owner_by_id, int rank, uint64_t stride,
+size_t k_extract_remote(const uint64_t* ids, size_t n, const DevMesh& M, int rank, uint64_t stride,
                         uint64_t* keys_out, hipStream_t s);
 // keys for the send side: for each neighbors_to entry with a remote owner,
 // owner*(last+1) + the row's own id
 size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
-                      size_t nrows, const int32_t* owner_by_id, int rank, uint64_t stride, uint64_t* keys_out,
-                      hipStream_t s);
+                      size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s);
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s);  // in place
+void sort_u64(uint64_t* keys, size_t n, hipStream_t s);           // in place
+// (id, slot) of every slot sorted by id
+void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
+                         hipStream_t s);
 void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
 size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
-void k_lookup_slots(const uint64_t* ids, size_t n, const int32_t* slot_by_id, int32_t* out, int32_t* err_flag,
-                    hipStream_t s);
+void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s);
+// iterator ranges cell.neighbors_of (update_cell_pointers 11451-11500): pass
+// 0 counts, pass 1 fills slots (+ offsets when it_off != nullptr)
 void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
-                      const int32_t* nof_slot, size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr,
-                      int32_t* it_slot, int pass, hipStream_t s);
-void k_face_lists(const MapCtx& m, const int32_t* owner_by_id, const int32_t* slot_by_id, const uint64_t* slot_ids,
-                  size_t nrows, uint32_t* cnt, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass,
-                  hipStream_t s);
-void k_remap_field2(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const int32_t* new_slot_by_id,
-                    uint64_t last, uint8_t* new_data, size_t elem, hipStream_t s);
-void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const int32_t* slot_by_id, const MapCtx& m,
-                   const uint8_t* old_data, const int32_t* old_slot_by_id, size_t elem, hipStream_t s);
+                      const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
+                      uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off, int pass,
+                      hipStream_t s);
+void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
+                  const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s);
+void k_remap_field(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const DevMesh& newM,
+                   uint8_t* new_data, size_t elem, hipStream_t s);
+void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const MapCtx& m, const uint8_t* old_data,
+                   const DevMesh& oldM, size_t elem, hipStream_t s);
+// ghost region: the level-0 cells within `radius` of the level-0 parent of a
+// local cell that are not wholly owned here (sorted, unique)
+std::vector<uint64_t> k_ghost_level0(const MapCtx& m, const DevMesh& M, int rank, const uint64_t* local, size_t n,
+                                     int radius, hipStream_t s);
+// local cells whose level-0 parent is in `l0` (sorted)
+std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size_t n, const std::vector<uint64_t>& l0,
+                                    hipStream_t s);
+// refinement closure (induce_refines 9591-9720): coarser neighbors_of /
+// neighbors_to entries of the requested local cells
+std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
+                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s);
+// known list after refining the sorted set S: every known leaf in S is
+// replaced by its 8 children (same owner)
+void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
+                     DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out, hipStream_t s);
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {
@@ -350,16 +475,23 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
                       DBuf<RegTileMeta>& regmeta, size_t counts[4], hipStream_t s);
 
 // --- launchers implemented in sweep_kernels.hip -----------------------------
-void k_pack(const uint8_t* field, size_t elem, const int32_t* slots, size_t n, uint8_t* out, hipStream_t s);
+// gather bytes [off, off + len) of the elements at `slots` into `out`
+void k_pack(const uint8_t* field, size_t elem, size_t off, size_t len, const int32_t* slots, size_t n, uint8_t* out,
+            hipStream_t s);
+// scatter: inverse of k_pack
+void k_place(const uint8_t* in, size_t elem, size_t off, size_t len, const int32_t* slots, size_t n, uint8_t* field,
+             hipStream_t s);
 void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
                size_t s1, hipStream_t s);
-void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s);
+// uniform 26-point game of life on a box of nx x ny x nz cells stored in
+// raster order; planes z = -1 and z = nz come from lo / hi (nullptr: outside)
+bool k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], const uint32_t* lo,
+                      const uint32_t* hi, hipStream_t s);
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
-                 const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s);
+                 size_t s0, size_t s1, double dt, hipStream_t s);
 // tiled advection sweep over the regular and the irregular tiles of one run
 // (run 0 inner, 1 outer: tiles never straddle the two)
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
-int adv_variant();  // DCCRGX_ADV_VARIANT (11 = tiled, the default)
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                         const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,

@@ -151,22 +151,11 @@ void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, size_t n_sl
                hipStream_t s) {
 	if (s1 <= s0) return;
 	level0_parent_kernel<<<blocks_for(n_slots, 256), 256, 0, s>>>(m, slot_ids, n_slots, l0p);
-	// DCCRGX_GOL_AMR_K=1 / 4: one / four neighbor rows ahead instead of eight
-	// (A/B on the bench's 11.5 M leaves: 3.02 / 2.25 / 2.20 ms per step)
-	static const int kk = [] {
-		const char* e = getenv("DCCRGX_GOL_AMR_K");
-		return e ? atoi(e) : 8;
-	}();
+	// eight neighbor rows gathered ahead (measured on the bench's 11.5 M
+	// leaves: 3.02 / 2.25 / 2.20 ms per step with one / four / eight)
 	const unsigned nb = blocks_for(s1 - s0, 256);
-	if (phase == 0) {
-		if (kk == 1) gol_amr_collect_kernel<1><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
-		else if (kk == 4) gol_amr_collect_kernel<4><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
-		else gol_amr_collect_kernel<8><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
-	} else {
-		if (kk == 1) gol_amr_spread_kernel<1><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
-		else if (kk == 4) gol_amr_spread_kernel<4><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
-		else gol_amr_spread_kernel<8><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
-	}
+	if (phase == 0) gol_amr_collect_kernel<8><<<nb, 256, 0, s>>>(l0p, state, lst, ptr, nslot, s0, s1, err);
+	else gol_amr_spread_kernel<8><<<nb, 256, 0, s>>>(slot_ids, l0p, state, lst, ptr, nslot, s0, s1, err);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,556 @@
+// The rank's leaf knowledge (dccrgx_mesh.hpp) and the local structures built
+// from it: slots, inner / outer classification, send / receive lists
+// (update_remote_neighbor_info dccrg.hpp:8992-9095,
+// recalculate_neighbor_update_send_receive_lists 8590-8752), the neighbor
+// CSRs (initialize_neighbors 8240-8289), face tables and advection tiles.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+#include "dccrgx_internal.hpp"
+
+namespace dccrgx {
+
+namespace {
+
+__global__ void select_owner_kernel(const uint64_t* ids, const int32_t* own, size_t n, int rank, uint64_t* out,
+                                    unsigned long long* counter) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		if (own[i] == rank) out[atomicAdd(counter, 1ull)] = ids[i];
+}
+
+__global__ void fill_owner_kernel(int32_t* own, size_t n, int32_t v) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) own[i] = v;
+}
+
+}  // namespace
+
+std::vector<int> HaloPlan::peers() const {
+	std::vector<int> p;
+	for (auto& kv : send_ids) p.push_back(kv.first);
+	for (auto& kv : recv_ids) p.push_back(kv.first);
+	std::sort(p.begin(), p.end());
+	p.erase(std::unique(p.begin(), p.end()), p.end());
+	return p;
+}
+
+static int ghost_radius(const Grid& g) { return std::max(1, int(g.hood_len)); }
+
+void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s) {
+	uint32_t bits = 4;
+	while ((uint64_t(1) << bits) < 2 * uint64_t(n)) bits++;
+	M.tab.alloc(size_t(1) << bits);
+	HIP_CHECK(hipMemsetAsync(M.tab.p, 0, M.tab.n * sizeof(HashEntry), s));
+	M.mask = (uint64_t(1) << bits) - 1;
+	M.shift = 64u - bits;
+	k_hash_insert(M.tab.p, M.mask, M.shift, ids, owners, -2, n, s);
+}
+
+void mesh_init_implicit(Grid& g) {
+	g.mesh = Mesh{};
+	g.mesh.implicit = true;
+	g.mesh.bp.init(g.m.first[1] - 1, uint64_t(g.size));
+}
+
+// keep the own leaves and the ghost leaves (level-0 parent within the ghost
+// radius of an own leaf's level-0 parent) of a global list
+void mesh_from_global(Grid& g, Mesh& out, const std::vector<uint64_t>& ids, const std::vector<int32_t>& owners) {
+	const MapCtx& m = g.m;
+	std::vector<uint64_t> lp;
+	for (size_t i = 0; i < ids.size(); i++)
+		if (owners[i] == g.rank) lp.push_back(map_level0_parent(m, ids[i]));
+	std::sort(lp.begin(), lp.end());
+	lp.erase(std::unique(lp.begin(), lp.end()), lp.end());
+	const int r = ghost_radius(g);
+	const int side = 2 * r + 1;
+	MapCtx m0;
+	{
+		const int per[3] = {m.periodic[0], m.periodic[1], m.periodic[2]};
+		map_init(m0, m.len, 0, per);
+	}
+	std::vector<uint64_t> need;
+	for (uint64_t p : lp) {
+		uint64_t x, y, z;
+		map_indices(m0, p, x, y, z);
+		for (int k = 0; k < side * side * side; k++) {
+			const int dx = k % side - r, dy = (k / side) % side - r, dz = k / (side * side) - r;
+			uint64_t w[3];
+			if (!map_wrap(m0, 0, int64_t(x) + dx, w[0]) || !map_wrap(m0, 1, int64_t(y) + dy, w[1]) ||
+			    !map_wrap(m0, 2, int64_t(z) + dz, w[2]))
+				continue;
+			need.push_back(map_from_indices(m0, w[0], w[1], w[2], 0));
+		}
+	}
+	std::sort(need.begin(), need.end());
+	need.erase(std::unique(need.begin(), need.end()), need.end());
+	std::vector<uint64_t> kid;
+	std::vector<int32_t> kown;
+	for (size_t i = 0; i < ids.size(); i++) {
+		if (owners[i] == g.rank || std::binary_search(need.begin(), need.end(), map_level0_parent(m, ids[i]))) {
+			kid.push_back(ids[i]);
+			kown.push_back(owners[i]);
+		}
+	}
+	out = Mesh{};
+	out.implicit = false;
+	out.bp.init(m.first[1] - 1, uint64_t(g.size));
+	upload(out.kid, kid, g.s_comp);
+	upload(out.kown, kown, g.s_comp);
+	out.n_known = kid.size();
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+}
+
+// explicit own + ghost list of the current mesh
+void mesh_materialize(Grid& g, Mesh& out) {
+	hipStream_t s = g.s_comp;
+	out = Mesh{};
+	out.implicit = false;
+	out.bp = g.mesh.bp;
+	if (!g.mesh.implicit) {
+		out.kid.alloc(g.mesh.n_known + 1);
+		out.kown.alloc(g.mesh.n_known + 1);
+		out.n_known = g.mesh.n_known;
+		if (out.n_known) {
+			HIP_CHECK(hipMemcpyAsync(out.kid.p, g.mesh.kid.p, out.n_known * 8, hipMemcpyDeviceToDevice, s));
+			HIP_CHECK(hipMemcpyAsync(out.kown.p, g.mesh.kown.p, out.n_known * 4, hipMemcpyDeviceToDevice, s));
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+		return;
+	}
+	// implicit: the block of own level-0 cells + the ring of level-0 cells
+	// around it (owners by the block partition)
+	uint64_t f, c;
+	g.mesh.bp.range(uint64_t(g.rank), f, c);
+	DBuf<uint64_t> local;
+	local.alloc(c + 1);
+	k_iota_u64(local.p, f, c, s);
+	const std::vector<uint64_t> ring = k_ghost_level0(g.m, g.dm(), g.rank, local.p, c, ghost_radius(g), s);
+	std::vector<int32_t> rown(ring.size());
+	for (size_t i = 0; i < ring.size(); i++) rown[i] = g.mesh.bp.owner(ring[i]);
+	out.n_known = c + ring.size();
+	out.kid.alloc(out.n_known + 1);
+	out.kown.alloc(out.n_known + 1);
+	if (c) {
+		HIP_CHECK(hipMemcpyAsync(out.kid.p, local.p, c * 8, hipMemcpyDeviceToDevice, s));
+		fill_owner_kernel<<<grid_for(c, 256), 256, 0, s>>>(out.kown.p, c, g.rank);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (!ring.empty()) {
+		HIP_CHECK(hipMemcpyAsync(out.kid.p + c, ring.data(), ring.size() * 8, hipMemcpyHostToDevice, s));
+		HIP_CHECK(hipMemcpyAsync(out.kown.p + c, rown.data(), ring.size() * 4, hipMemcpyHostToDevice, s));
+	}
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// Own leaves `local` (device, n) after a repartition; the ghost leaves are
+// asked from whoever owns them: every rank sends every other rank the
+// level-0 cells of its ghost region, and gets back the leaves it owns under
+// them (finish_balance_load 3942-4147 all-gathers every added cell instead).
+void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n) {
+	hipStream_t s = g.s_comp;
+	DevMesh probe{};
+	probe.implicit = 0;
+	probe.last = g.m.last;
+	const std::vector<uint64_t> need = k_ghost_level0(g.m, probe, g.rank, local.p, n, ghost_radius(g), s);
+	const auto reqs = comm_allgather_u64(g, need);
+	std::vector<std::vector<uint64_t>> replies(size_t(g.size));
+	for (int p = 0; p < g.size; p++)
+		if (p != g.rank) replies[size_t(p)] = k_cells_under(g.m, local.p, n, reqs[size_t(p)], s);
+	const auto ghosts = comm_alltoall_u64(g, replies);
+	std::vector<uint64_t> gid;
+	std::vector<int32_t> gown;
+	for (int p = 0; p < g.size; p++) {
+		if (p == g.rank) continue;
+		gid.insert(gid.end(), ghosts[size_t(p)].begin(), ghosts[size_t(p)].end());
+		gown.insert(gown.end(), ghosts[size_t(p)].size(), p);
+	}
+	out = Mesh{};
+	out.implicit = false;
+	out.bp.init(g.m.first[1] - 1, uint64_t(g.size));
+	out.n_known = n + gid.size();
+	out.kid.alloc(out.n_known + 1);
+	out.kown.alloc(out.n_known + 1);
+	if (n) {
+		HIP_CHECK(hipMemcpyAsync(out.kid.p, local.p, n * 8, hipMemcpyDeviceToDevice, s));
+		fill_owner_kernel<<<grid_for(n, 256), 256, 0, s>>>(out.kown.p, n, g.rank);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (!gid.empty()) {
+		HIP_CHECK(hipMemcpyAsync(out.kid.p + n, gid.data(), gid.size() * 8, hipMemcpyHostToDevice, s));
+		HIP_CHECK(hipMemcpyAsync(out.kown.p + n, gown.data(), gid.size() * 4, hipMemcpyHostToDevice, s));
+	}
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+static void decode_keys(const std::vector<uint64_t>& keys, uint64_t stride, std::map<int, std::vector<uint64_t>>& out) {
+	out.clear();
+	for (uint64_t k : keys) out[int(k / stride)].push_back(k % stride);
+}
+
+// ---------------------------------------------------------------------------
+// (Re)build every local structure from `nm`.  Field payloads of cells that
+// stay on this rank are carried over (old slot -> new slot); freshly created
+// children inherit their parent's payload.
+void rebuild(Grid& g, Mesh& nm) {
+	hipStream_t s = g.s_comp;
+	const MapCtx& m = g.m;
+	const int nh = int(g.hood.size() / 3);
+
+	DBuf<uint64_t> old_slot_ids;
+	old_slot_ids.swap(g.slot_ids);
+	Mesh old = std::move(g.mesh);
+	const size_t old_n_local = g.n_local;
+	g.mesh = std::move(nm);
+	Mesh& M = g.mesh;
+	M.tab.release();
+
+	// 1. own leaves, ascending
+	DBuf<uint64_t> d_local;
+	if (M.implicit) {
+		uint64_t f, c;
+		M.bp.range(uint64_t(g.rank), f, c);
+		d_local.alloc(c + 1);
+		k_iota_u64(d_local.p, f, c, s);
+		g.n_local = c;
+	} else {
+		mesh_build_hash(M, M.kid.p, M.kown.p, M.n_known, s);
+		d_local.alloc(M.n_known + 1);
+		DBuf<unsigned long long> ctr;
+		ctr.alloc(1);
+		HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
+		if (M.n_known) {
+			select_owner_kernel<<<grid_for(M.n_known, 256), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank, d_local.p,
+			                                                              ctr.p);
+			HIP_CHECK(hipGetLastError());
+		}
+		unsigned long long hn = 0;
+		HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		g.n_local = size_t(hn);
+		sort_u64(d_local.p, g.n_local, s);
+	}
+	const size_t nl = g.n_local;
+	DevMesh dm = g.dm();  // implicit: no table yet (owners by formula)
+
+	// 2. inner / outer classification (update_remote_neighbor_info 8992-9095)
+	DBuf<uint32_t> flag, scan;
+	flag.alloc(nl + 1);
+	scan.alloc(nl + 1);
+	HIP_CHECK(hipMemsetAsync(flag.p, 0, (nl + 1) * sizeof(uint32_t), s));
+	if (g.size > 1) k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.rank, d_local.p, nl, flag.p, s);
+	g.n_outer = scan_exclusive_u32(flag.p, scan.p, nl, s);
+	g.n_inner = nl - g.n_outer;
+	DBuf<uint64_t> local_slots;
+	local_slots.alloc(nl + 1);
+	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
+	d_local.release();
+	int order = g.slot_order;
+	if (order < 0) order = g.R > 0 ? 1 : 0;
+	bool fits = true;
+	for (int d = 0; d < 3; d++) fits = fits && m.glen[d] <= (uint64_t(1) << 21);
+	g.morton_slots = order == 1 && fits;
+	if (g.morton_slots) {
+		k_morton_sort(m, local_slots.p, g.n_inner, s);
+		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
+	}
+
+	// 3. neighbor lists of outer cells -> send / receive lists (8590-8752)
+	HaloPlan& H = g.halo;
+	H.send_ids.clear();
+	H.recv_ids.clear();
+	g.extra_remote.clear();
+	DX_REQUIRE(uint64_t(g.size) <= ~uint64_t(0) / (m.last + 1), "cell ids too large for the list keys");
+	const uint64_t stride = m.last + 1;
+	if (g.n_outer > 0) {
+		const size_t no = g.n_outer;
+		DBuf<uint32_t> c_of, c_to, p_of, p_to;
+		c_of.alloc(no + 1);
+		c_to.alloc(no + 1);
+		p_of.alloc(no + 1);
+		p_to.alloc(no + 1);
+		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, c_of.p, c_to.p, s);
+		const size_t t_of = scan_exclusive_u32(c_of.p, p_of.p, no, s);
+		const size_t t_to = scan_exclusive_u32(c_to.p, p_to.p, no, s);
+		DBuf<uint64_t> of_id, to_id, keys;
+		DBuf<int32_t> of_off;
+		of_id.alloc(t_of + 1);
+		of_off.alloc(3 * t_of + 3);
+		to_id.alloc(t_to + 1);
+		keys.alloc(std::max(t_of, t_to) + 1);
+		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, local_slots.p, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
+		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, p_to.p, to_id.p, s);
+		size_t nk = k_extract_remote(of_id.p, t_of, dm, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		decode_keys(download(keys.p, nk, s), stride, H.recv_ids);
+		nk = k_extract_send(to_id.p, p_to.p, local_slots.p, g.n_inner, no, dm, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		decode_keys(download(keys.p, nk, s), stride, H.send_ids);
+		nk = k_extract_remote(to_id.p, t_to, dm, g.rank, stride, keys.p, s);
+		nk = sort_unique_u64(keys.p, nk, s);
+		std::map<int, std::vector<uint64_t>> rem_to;
+		decode_keys(download(keys.p, nk, s), stride, rem_to);
+		std::vector<uint64_t> extra;
+		for (auto& kv : rem_to) {
+			const auto it = H.recv_ids.find(kv.first);
+			for (uint64_t id : kv.second)
+				if (it == H.recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id))
+					extra.push_back(id);
+		}
+		std::sort(extra.begin(), extra.end());
+		g.extra_remote = extra;
+	}
+	g.peers = H.peers();
+
+	// 4. slots: local | halo (per peer, ascending) | remote neighbors_to-only
+	std::vector<uint64_t> halo;
+	H.recv_off.clear();
+	for (auto& kv : H.recv_ids) {
+		H.recv_off[kv.first] = halo.size();
+		halo.insert(halo.end(), kv.second.begin(), kv.second.end());
+	}
+	H.n_recv = halo.size();
+	g.n_recv = H.n_recv;
+	halo.insert(halo.end(), g.extra_remote.begin(), g.extra_remote.end());
+	g.n_slots = nl + halo.size();
+	g.slot_ids.alloc(g.n_slots + 1);
+	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, local_slots.p, nl * 8, hipMemcpyDeviceToDevice, s));
+	if (!halo.empty())
+		HIP_CHECK(hipMemcpyAsync(g.slot_ids.p + nl, halo.data(), halo.size() * 8, hipMemcpyHostToDevice, s));
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	if (M.implicit) mesh_build_hash(M, g.slot_ids.p, nullptr, g.n_slots, s);
+	dm = g.dm();
+	k_hash_set_slots(dm, g.slot_ids.p, g.n_slots, err.p, s);
+	{
+		std::vector<int32_t> rs(H.n_recv);
+		std::iota(rs.begin(), rs.end(), int32_t(nl));
+		upload(H.recv_slots, rs, s);
+	}
+
+	// 5. send slots (ascending id per peer = wire order)
+	std::vector<uint64_t> sids;
+	H.send_off.clear();
+	for (auto& kv : H.send_ids) {
+		H.send_off[kv.first] = sids.size();
+		sids.insert(sids.end(), kv.second.begin(), kv.second.end());
+	}
+	H.n_send = sids.size();
+	{
+		DBuf<uint64_t> d;
+		upload(d, sids, s);
+		H.send_slots.alloc(sids.size() + 1);
+		k_lookup_slots(d.p, sids.size(), dm, H.send_slots.p, err.p, s);
+		int32_t herr = 0;
+		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		DX_REQUIRE(herr == 0, "internal error: slot of a local, halo or send cell missing from the mesh table");
+	}
+
+	// 6. carry field payloads over
+	const DevMesh odm = old.dev(m.last);
+	for (auto& f : g.fields) {
+		DBuf<uint8_t> nd;
+		nd.alloc(g.n_slots * f.elem);
+		if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
+		if (f.data.p && old_slot_ids.p) {
+			k_remap_field(f.data.p, old_slot_ids.p, old_n_local, dm, nd.p, f.elem, s);
+			k_parent_fill(nd.p, g.slot_ids.p, nl, m, f.data.p, odm, f.elem, s);
+		}
+		f.data.swap(nd);
+		f.scratch.release();
+	}
+	HIP_CHECK(hipStreamSynchronize(s));
+	g.csr_valid = false;
+	g.face_valid = false;
+	g.tiles_valid = false;
+	g.slot_ids_h_valid = false;
+	g.index_h_valid = false;
+	g.po.valid = false;
+	g.gol_plan_valid = false;
+	for (auto& kv : g.uhoods) kv.second.valid = false;
+}
+
+// full neighbors_of / neighbors_to / iterator CSR for all local rows
+void ensure_csr(Grid& g) {
+	if (g.csr_valid) return;
+	hipStream_t s = g.s_comp;
+	const int nh = int(g.hood.size() / 3);
+	const size_t nl = g.n_local;
+	const DevMesh dm = g.dm();
+	DBuf<uint32_t> c_of, c_to;
+	c_of.alloc(nl + 1);
+	c_to.alloc(nl + 1);
+	g.nof_ptr.alloc(nl + 1);
+	g.nto_ptr.alloc(nl + 1);
+	g.it_ptr.alloc(nl + 1);
+	k_count_rows(g.m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.slot_ids.p, 0, nl, c_of.p, c_to.p, s);
+	const size_t t_of = scan_exclusive_u32(c_of.p, g.nof_ptr.p, nl, s);
+	const size_t t_to = scan_exclusive_u32(c_to.p, g.nto_ptr.p, nl, s);
+	g.nof_id.alloc(t_of + 1);
+	g.nof_off.alloc(3 * t_of + 3);
+	g.nof_slot.alloc(t_of + 1);
+	g.nto_id.alloc(t_to + 1);
+	k_fill_neighbors_of(g.m, g.d_hood.p, nh, dm, g.slot_ids.p, 0, nl, g.nof_ptr.p, g.nof_id.p, g.nof_off.p, s);
+	k_fill_neighbors_to(g.m, g.d_hood_to.p, nh, dm, g.slot_ids.p, 0, nl, g.nto_ptr.p, g.nto_id.p, s);
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	k_lookup_slots(g.nof_id.p, t_of, dm, g.nof_slot.p, err.p, s);
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, c_of.p, nullptr,
+	                 nullptr, nullptr, 0, s);
+	const size_t t_it = scan_exclusive_u32(c_of.p, g.it_ptr.p, nl, s);
+	g.it_slot.alloc(t_it + 1);
+	g.it_off.alloc(3 * t_it + 3);
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, nullptr,
+	                 g.it_ptr.p, g.it_slot.p, g.it_off.p, 1, s);
+	int32_t herr = 0;
+	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(herr == 0, "neighbor list references a cell unknown to this rank (unbalanced mesh?)");
+	g.csr_valid = true;
+}
+
+void ensure_face(Grid& g) {
+	if (g.face_valid) return;
+	hipStream_t s = g.s_comp;
+	const size_t nl = g.n_local;
+	const DevMesh dm = g.dm();
+	DBuf<uint32_t> cnt;
+	cnt.alloc(nl + 1);
+	g.face_ptr.alloc(nl + 1);
+	DBuf<int32_t> err;
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, nullptr, nullptr, err.p, 0, s);
+	const size_t t = scan_exclusive_u32(cnt.p, g.face_ptr.p, nl, s);
+	g.face_ent.alloc(t + 1);
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, g.face_ptr.p, g.face_ent.p, err.p, 1, s);
+	int32_t herr = 0;
+	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
+	g.face_ell.alloc(6 * nl + 6);
+	g.face_fine.alloc(t / 4 + 4);
+	g.n_fine_faces = k_face_ell(g.face_ptr.p, g.face_ent.p, nl, g.face_ell.p, g.face_fine.p, s);
+	g.face_valid = true;
+}
+
+void ensure_tiles(Grid& g) {
+	ensure_face(g);
+	if (g.tiles_valid) return;
+	const int T = g.tile;
+	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.slot_ids.p, g.m, g.morton_slots, g.n_inner,
+	                                   g.n_local, T, g.tstart, g.tell, g.ext_ptr, g.ext, g.ext_pk, g.fine_base, g.tfine,
+	                                   g.s_comp);
+	g.n_tiles_inner = tb.n_tiles_inner;
+	g.n_tiles_outer = tb.n_tiles_outer;
+	g.max_ext = tb.max_ext;
+	g.total_ext = tb.total_ext;
+	k_classify_tiles(g.m, g.tstart.p, g.n_tiles_inner, g.n_tiles_outer, g.slot_ids.p, g.face_ell.p, g.tlists, g.tnb,
+	                 g.tregmeta, g.tcount, g.s_comp);
+	// records of the irregular tiles for the pipelined tile kernel
+	const size_t nt = g.n_tiles_inner + g.n_tiles_outer, ni = g.tcount[2] + g.tcount[3];
+	const auto ts = download(g.tstart.p, nt + 1, g.s_comp);
+	const auto ep = download(g.ext_ptr.p, nt + 1, g.s_comp);
+	const auto fb = download(g.fine_base.p, nt + 1, g.s_comp);
+	const auto li = download(g.tlists.p + g.tcount[0] + g.tcount[1], ni, g.s_comp);
+	std::vector<uint32_t> rec(8 * ni, 0u);
+	bool fits = true;
+	for (size_t i = 0; i < ni; i++) {
+		const uint32_t t = li[i];
+		// finer faces of tile t: up to the next tile's first one (fine_base is
+		// the exclusive scan at each tile's first slot)
+		const uint32_t fend = t + 1 < nt ? fb[t + 1] : uint32_t(g.n_fine_faces);
+		uint32_t* r = &rec[8 * i];
+		r[0] = ts[t];
+		r[1] = ts[t + 1] - ts[t];
+		r[2] = ep[t];
+		r[3] = ep[t + 1] - ep[t];
+		r[4] = fb[t];
+		r[5] = fend - fb[t];
+		if (r[3] > 1024u || r[5] > 512u || r[1] > 512u) fits = false;
+	}
+	g.tmeta.release();
+	if (fits && ni) upload(g.tmeta, rec, g.s_comp);
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	g.tiles_valid = true;
+}
+
+const std::vector<uint64_t>& slot_ids_host(Grid& g) {
+	if (!g.slot_ids_h_valid) {
+		g.slot_ids_h = download(g.slot_ids.p, g.n_slots, g.s_comp);
+		g.slot_ids_h_valid = true;
+	}
+	return g.slot_ids_h;
+}
+
+void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot) {
+	if (!n) return;
+	hipStream_t s = g.s_comp;
+	DBuf<uint64_t> d;
+	d.alloc(n);
+	HIP_CHECK(hipMemcpyAsync(d.p, ids, n * 8, hipMemcpyHostToDevice, s));
+	DBuf<int32_t> o, sl;
+	o.alloc(n);
+	sl.alloc(n);
+	k_lookup(g.dm(), d.p, n, o.p, sl.p, s);
+	if (owner) HIP_CHECK(hipMemcpyAsync(owner, o.p, n * 4, hipMemcpyDeviceToHost, s));
+	if (slot) HIP_CHECK(hipMemcpyAsync(slot, sl.p, n * 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// slot of a slotted id from the host index, -1 if it has no slot
+static int64_t host_slot(Grid& g, uint64_t id) {
+	if (!g.index_h_valid) {
+		k_sorted_slot_index(g.slot_ids.p, g.n_slots, g.index_ids_h, g.index_slots_h, g.s_comp);
+		g.index_h_valid = true;
+	}
+	auto it = std::lower_bound(g.index_ids_h.begin(), g.index_ids_h.end(), id);
+	if (it == g.index_ids_h.end() || *it != id) return -1;
+	return g.index_slots_h[size_t(it - g.index_ids_h.begin())];
+}
+
+bool is_local_cell(Grid& g, uint64_t id) {
+	if (!g.initialized || id == error_cell || id > g.m.last) return false;
+	if (g.mesh.implicit) return id <= g.mesh.bp.n0 && g.mesh.bp.owner(id) == g.rank;
+	const int64_t s = host_slot(g, id);
+	return s >= 0 && size_t(s) < g.n_local;
+}
+
+int32_t lookup_owner(Grid& g, uint64_t id) {
+	if (!g.initialized || id == error_cell || id > g.m.last) return -1;
+	if (g.mesh.implicit) return id <= g.mesh.bp.n0 ? g.mesh.bp.owner(id) : -1;
+	const int64_t s = host_slot(g, id);
+	if (s >= 0 && size_t(s) < g.n_local) return g.rank;
+	int32_t o = -1;  // a ghost leaf (or none): the device table knows
+	lookup_batch(g, &id, 1, &o, nullptr);
+	return o;
+}
+
+int64_t lookup_slot(Grid& g, uint64_t id) {
+	if (!g.initialized || id == error_cell || id > g.m.last) return -1;
+	return host_slot(g, id);
+}
+
+void known_leaves(Grid& g, std::vector<uint64_t>& ids, std::vector<int32_t>& owners) {
+	const Mesh* src = &g.mesh;
+	Mesh tmp;
+	if (g.mesh.implicit) {
+		mesh_materialize(g, tmp);
+		src = &tmp;
+	}
+	std::vector<uint64_t> k = download(src->kid.p, src->n_known, g.s_comp);
+	std::vector<int32_t> o = download(src->kown.p, src->n_known, g.s_comp);
+	std::vector<size_t> idx(k.size());
+	std::iota(idx.begin(), idx.end(), size_t(0));
+	std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return k[a] < k[b]; });
+	ids.resize(k.size());
+	owners.resize(k.size());
+	for (size_t i = 0; i < idx.size(); i++) {
+		ids[i] = k[idx[i]];
+		owners[i] = o[idx[i]];
+	}
+}
+
+}  // namespace dccrgx

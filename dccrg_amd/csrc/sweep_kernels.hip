@@ -15,25 +15,33 @@ namespace dccrgx {
 
 namespace {
 
-inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 64u) {
-	size_t g = (n + per_block - 1) / per_block;
-	if (g > cap) g = cap;
-	if (g == 0) g = 1;
-	return unsigned(g);
-}
-
 // ---------------------------------------------------------------------------
+// halo pack / place: bytes [off, off + len) of the elements at `slots`
 template <class T>
 __global__ void pack_kernel(const T* __restrict__ f, const int32_t* __restrict__ slots, size_t n, T* __restrict__ out) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
 		out[i] = f[slots[i]];
 }
 
-__global__ void pack_bytes_kernel(const uint8_t* __restrict__ f, size_t elem, const int32_t* __restrict__ slots,
-                                  size_t n, uint8_t* __restrict__ out) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * elem; i += size_t(gridDim.x) * blockDim.x) {
-		const size_t k = i / elem, b = i - k * elem;
-		out[i] = f[size_t(slots[k]) * elem + b];
+template <class T>
+__global__ void place_kernel(const T* __restrict__ in, const int32_t* __restrict__ slots, size_t n, T* __restrict__ f) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		f[slots[i]] = in[i];
+}
+
+__global__ void pack_bytes_kernel(const uint8_t* __restrict__ f, size_t elem, size_t off, size_t len,
+                                  const int32_t* __restrict__ slots, size_t n, uint8_t* __restrict__ out) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * len; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t k = i / len, b = i - k * len;
+		out[i] = f[size_t(slots[k]) * elem + off + b];
+	}
+}
+
+__global__ void place_bytes_kernel(const uint8_t* __restrict__ in, size_t elem, size_t off, size_t len,
+                                   const int32_t* __restrict__ slots, size_t n, uint8_t* __restrict__ f) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * len; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t k = i / len, b = i - k * len;
+		f[size_t(slots[k]) * elem + off + b] = in[i];
 	}
 }
 
@@ -49,76 +57,7 @@ __global__ void gol_csr_kernel(const uint32_t* __restrict__ state, uint32_t* __r
 	}
 }
 
-// Barrier-free variant: a wavefront owns one x-run of 64 lanes (62 outputs,
-// lanes 0 and 63 only feed their neighbors) on one y row and marches up z.
-// Per plane each lane loads its column (y-1, y, y+1: three coalesced row
-// loads, the outer two served from L1/L2 since neighboring waves load them
-// as their own middle rows), the x-direction 3-sum comes from two lane
-// shuffles, and the three in-plane sums of z-1, z, z+1 stay in registers.
-constexpr int G2_OUT = 62, G2_ROWS = 4;
-
-__global__ __launch_bounds__(64 * G2_ROWS) void gol_structured_v2(const uint32_t* __restrict__ st,
-                                                                 uint32_t* __restrict__ out, int nx, int ny, int nz,
-                                                                 int px, int py, int pz, int zc) {
-	const int lane = threadIdx.x & 63;
-	const int y = blockIdx.y * G2_ROWS + (threadIdx.x >> 6);
-	if (y >= ny) return;  // wave-uniform
-	const int x0 = blockIdx.x * G2_OUT;
-	int x = x0 + lane - 1;
-	bool xin = true;
-	if (x < 0 || x >= nx) {
-		if (px) x = ((x % nx) + nx) % nx;
-		else xin = false;
-	}
-	int ym = y - 1, yp = y + 1;
-	bool ymin = true, ypin = true;
-	if (ym < 0) {
-		if (py) ym += ny;
-		else ymin = false;
-	}
-	if (yp >= ny) {
-		if (py) yp -= ny;
-		else ypin = false;
-	}
-	const size_t plane = size_t(nx) * ny;
-	const size_t om = size_t(ym) * nx + x, oc = size_t(y) * nx + x, op = size_t(yp) * nx + x;
-	// in-plane 3x3 sum at (x, y) of plane z and the raw center value
-	auto plane_sum = [&](int z, uint32_t& center) -> uint32_t {
-		bool zin = true;
-		if (z < 0 || z >= nz) {
-			if (pz) z = ((z % nz) + nz) % nz;
-			else zin = false;
-		}
-		uint32_t c = 0;
-		center = 0;
-		if (zin && xin) {
-			const uint32_t* p = st + size_t(z) * plane;
-			center = p[oc];
-			c = (center > 0) + (ymin ? (p[om] > 0) : 0u) + (ypin ? (p[op] > 0) : 0u);
-		}
-		const uint32_t l = __shfl_up(c, 1, 64), r = __shfl_down(c, 1, 64);
-		return l + c + r;
-	};
-	const int z0 = blockIdx.z * zc;
-	const int z1 = min(z0 + zc, nz);
-	uint32_t dummy, cur;
-	uint32_t s_prev = plane_sum(z0 - 1, dummy);
-	uint32_t s_cur = plane_sum(z0, cur);
-	const bool writer = lane >= 1 && lane <= G2_OUT && x0 + lane - 1 < nx;
-	for (int z = z0; z < z1; z++) {
-		uint32_t nxt;
-		const uint32_t s_next = plane_sum(z + 1, nxt);
-		if (writer) {
-			const uint32_t cnt = s_prev + s_cur + s_next - (cur > 0 ? 1u : 0u);
-			out[size_t(z) * plane + oc] = cnt == 3 ? 1u : (cnt == 2 ? cur : 0u);
-		}
-		s_prev = s_cur;
-		s_cur = s_next;
-		cur = nxt;
-	}
-}
-
-// v3 (nx a multiple of 256): a lane owns 4 consecutive x (16-B loads and
+// Uniform 26-point game of life (nx a multiple of 256): a lane owns 4 consecutive x (16-B loads and
 // stores), a wave one 256-x segment of one y row, a block G3_ROWS
 // consecutive rows of the same segment; each wave marches a chunk of zc
 // planes with the raw loads of the next DEPTH planes in flight while the
@@ -137,7 +76,9 @@ template <int DEPTH>
 __global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t* __restrict__ st,
                                                                  uint32_t* __restrict__ out, int nx, int ny, int nz,
                                                                  int px, int py, int pz, int zc, unsigned nbx,
-                                                                 unsigned nby, unsigned nb) {
+                                                                 unsigned nby, unsigned nb,
+                                                                 const uint32_t* __restrict__ lo,
+                                                                 const uint32_t* __restrict__ hi) {
 	const unsigned per_xcd = gridDim.x >> 3;
 	const unsigned L = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
 	if (L >= nb) return;  // block-uniform
@@ -166,11 +107,13 @@ __global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t
 	auto load = [&](int z, G3Plane& P) {
 		P.m = P.c = P.p = make_uint4(0, 0, 0, 0);
 		P.e[0] = P.e[1] = P.e[2] = 0;
-		if (z < 0 || z >= nz) {
-			if (!pz) return;
-			z = z < 0 ? z + nz : z - nz;
-		}
-		const uint32_t* p = st + size_t(z) * plane;
+		// planes z = -1 / nz: the lo / hi plane (another slab's copy), the
+		// periodic wrap, or nothing
+		const uint32_t* p;
+		if (z < 0) p = lo ? lo : (pz ? st + size_t(z + nz) * plane : nullptr);
+		else if (z >= nz) p = hi ? hi : (pz ? st + size_t(z - nz) * plane : nullptr);
+		else p = st + size_t(z) * plane;
+		if (!p) return;
 		P.c = *reinterpret_cast<const uint4*>(p + oc + x);
 		if (ymin) P.m = *reinterpret_cast<const uint4*>(p + om + x);
 		if (ypin) P.p = *reinterpret_cast<const uint4*>(p + op + x);
@@ -314,153 +257,13 @@ __device__ __forceinline__ double ldo(const double* __restrict__ p, uint32_t off
 	return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(p) + off);
 }
 
-// own-field stream of the tile sweeps: NT bit 1 marks the loads
-// non-temporal (do not displace the face lines other tiles re-read from L2)
-template <int NT>
-__device__ __forceinline__ double ldo_own(const double* __restrict__ p, uint32_t off) {
-	const double* q = reinterpret_cast<const double*>(reinterpret_cast<const char*>(p) + off);
-	if (NT & 2) return __builtin_nontemporal_load(q);
-	return *q;
+// density store of the tile sweeps: non-temporal (a streaming write that
+// should not allocate over the face lines neighboring tiles re-read from
+// L2; measured on config 3: 0.1960 -> 0.1945 ms per sweep.  The same hint on
+// the own-field loads cost 12 %: those lines ARE the re-read face lines)
+__device__ __forceinline__ void st_nt(double* __restrict__ p, uint32_t i, double v) {
+	__builtin_nontemporal_store(v, p + i);
 }
-
-// density store of the tile sweeps: NT bit 0 marks it non-temporal (a
-// streaming write that should not allocate over useful L2 lines)
-template <int NT>
-__device__ __forceinline__ void st_out(double* __restrict__ p, uint32_t i, double v) {
-	if (NT & 1) __builtin_nontemporal_store(v, p + i);
-	else p[i] = v;
-}
-
-// Tiled sweep (tables: tile_build.hip).  One workgroup per tile of at most
-// T consecutive slots; one thread per cell.  Phase 1 stages the tile's own
-// seven fields (coalesced) and the fields of its distinct out-of-tile face
-// neighbors (one gather per neighbor, not one per face) in LDS; phase 2
-// evaluates every face from LDS through the 16-bit tile-local index, so the
-// only global traffic is the staging and the density store.  Tiles are
-// dealt to the XCDs in runs of Morton-consecutive tiles (see the block
-// mapping below): the ext cells of a tile are mostly own cells of tiles
-// swept nearby in time, i.e. cache hits.  A tile with more ext cells
-// than the LDS holds (ecap) reads the surplus from global memory.
-template <int T, int MINW, int DIAG>
-__global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tstart,
-    const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext_ptr, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ fine_base, const uint32_t* __restrict__ tfine, const uint32_t* __restrict__ list,
-    uint32_t ntiles, uint32_t ecap, double dt, int map) {
-#pragma clang fp contract(off)
-	extern __shared__ double shd[];  // [7][T + ecap]
-	const uint32_t W = T + ecap;
-	const unsigned nb = gridDim.x, b = blockIdx.x;
-	// block b runs on XCD b % 8 as that XCD's (b / 8)-th block; each XCD
-	// sweeps runs of `map` consecutive (Morton-adjacent) tiles, the eight
-	// XCDs side by side, so a tile's out-of-tile neighbors are mostly tiles
-	// its own XCD swept just before or sweeps concurrently (L2 hits) and the
-	// rest were read recently by another XCD (Infinity Cache hits); map == 0:
-	// one contiguous eighth per XCD, map == 1: no XCD awareness
-	unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (map == 1) lb = b;
-	else if (map >= 2) {
-		const unsigned G = unsigned(map), x = b & 7u, k = b >> 3;
-		lb = ((k / G) * 8u + x) * G + (k % G);
-	}
-	if (lb >= ntiles) return;  // block-uniform
-	const uint32_t gt = list[lb];
-	const uint32_t ts = tstart[gt], te = tstart[gt + 1];
-	const uint32_t tid = threadIdx.x;
-	const uint32_t s = ts + tid;
-	const bool valid = s < te;
-	const uint32_t e0 = ext_ptr[gt], e1 = ext_ptr[gt + 1];
-	const uint32_t nes = DIAG >= 1 ? 0u : min(e1 - e0, ecap);
-	const double* const fld[7] = {rho, vx, vy, vz, lx, ly, lz};
-	if (DIAG == 3) {
-		if (!valid) return;
-		const uint32_t o = s << 3;
-		double a = 0;
-#pragma unroll
-		for (int k = 0; k < 7; k++) a += ldo(fld[k], o);
-		rho_out[s] = a;
-		return;
-	}
-
-	// phase 1: own cell, face row, and up to two ext cells per thread
-	double c[7] = {0, 0, 0, 0, 1, 1, 1};
-	uint32_t row[3] = {~0u, ~0u, ~0u};
-	const uint32_t ja = tid, jb = tid + T;
-	uint32_t xa = ja < nes ? ext[e0 + ja] : 0u, xb = jb < nes ? ext[e0 + jb] : 0u;
-	if (DIAG == 4) {  // same dependent loads, but the gathers hit the tile's own lines
-		xa = ts + (xa & 255u);
-		xb = ts + (xb & 255u);
-	}
-	if (valid) {
-		if (DIAG == 2) {
-			row[0] = (tid ^ 1) | ((tid ^ 1) << 16);
-			row[1] = (tid ^ 2) | ((tid ^ 2) << 16);
-			row[2] = (tid ^ 4) | ((tid ^ 4) << 16);
-		} else {
-			row[0] = tell[3 * size_t(s)];
-			row[1] = tell[3 * size_t(s) + 1];
-			row[2] = tell[3 * size_t(s) + 2];
-		}
-		const uint32_t o = s << 3;
-#pragma unroll
-		for (int k = 0; k < 7; k++) c[k] = ldo(fld[k], o);
-	}
-	double va[7], vb[7];
-	if (ja < nes) {
-		const uint32_t o = xa << 3;
-#pragma unroll
-		for (int k = 0; k < 7; k++) va[k] = ldo(fld[k], o);
-	}
-	if (jb < nes) {
-		const uint32_t o = xb << 3;
-#pragma unroll
-		for (int k = 0; k < 7; k++) vb[k] = ldo(fld[k], o);
-	}
-#pragma unroll
-	for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
-	if (ja < nes)
-#pragma unroll
-		for (int k = 0; k < 7; k++) shd[k * W + T + ja] = va[k];
-	if (jb < nes)
-#pragma unroll
-		for (int k = 0; k < 7; k++) shd[k * W + T + jb] = vb[k];
-	for (uint32_t j = tid + 2 * T; j < nes; j += T) {
-		const uint32_t o = ext[e0 + j] << 3;
-#pragma unroll
-		for (int k = 0; k < 7; k++) shd[k * W + T + j] = ldo(fld[k], o);
-	}
-	__syncthreads();
-	if (!valid) return;
-
-	// phase 2: faces from LDS, in the reference's face order
-	auto fetch = [&](uint32_t li, int d) -> AdvNb {
-		const int dv = 1 + (d >> 1);
-		if (li < T + nes) return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[dv * W + li]};
-		if (DIAG >= 1) return AdvNb{c[0], c[4], c[5], c[6], c[dv]};
-		const uint32_t o = ext[e0 + li - T] << 3;  // beyond the LDS capacity of this tile
-		return AdvNb{ldo(rho, o), ldo(lx, o), ldo(ly, o), ldo(lz, o), ldo(fld[dv], o)};
-	};
-	const double cd = c[0], cvx = c[1], cvy = c[2], cvz = c[3], clx = c[4], cly = c[5], clz = c[6];
-	double acc = 0;
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		const uint32_t code = (row[d >> 1] >> (16 * (d & 1))) & 0xffffu;
-		if (code == 0xffffu) continue;
-		if (code & 0x8000u) {
-			const uint32_t fk = fine_base[gt] + (code & 0x7fffu);
-			const uint32_t q0 = tfine[2 * size_t(fk)], q1 = tfine[2 * size_t(fk) + 1];
-			const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
-#pragma unroll
-			for (int k = 0; k < 4; k++) acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
-		} else {
-			acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
-		}
-	}
-	rho_out[s] = cd + acc / (clx * cly * clz);
-}
-
 
 // Regular tiles (tile_build.hip classify_tiles_kernel): an aligned 8x8x8 box
 // of same-level cells, slots ts..ts+511 in Morton order, whose face
@@ -473,126 +276,6 @@ __global__ __launch_bounds__(T, MINW) void advection_tiles_kernel(
 __device__ __forceinline__ uint32_t m9(uint32_t x, uint32_t y, uint32_t z) {
 	return (x & 1u) | ((y & 1u) << 1) | ((z & 1u) << 2) | ((x & 2u) << 2) | ((y & 2u) << 3) | ((z & 2u) << 4) |
 	       ((x & 4u) << 4) | ((y & 4u) << 5) | ((z & 4u) << 6);
-}
-
-template <int DIAG>
-__global__ __launch_bounds__(512) void advection_regular_kernel(
-    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
-    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
-    const double* __restrict__ lz, double* __restrict__ rho_out, const uint32_t* __restrict__ tstart,
-    const uint32_t* __restrict__ list, const int32_t* __restrict__ tnb, uint32_t ntiles, double dt, int map) {
-#pragma clang fp contract(off)
-	__shared__ double shd[7][512];
-	const unsigned nb = gridDim.x, b = blockIdx.x;
-	unsigned lb = (b & 7u) * (nb >> 3) + (b >> 3);
-	if (map == 1) lb = b;
-	else if (map >= 2) {
-		const unsigned G = unsigned(map), x = b & 7u, k = b >> 3;
-		lb = ((k / G) * 8u + x) * G + (k % G);
-	}
-	if (lb >= ntiles) return;  // block-uniform
-	const uint32_t gt = list[lb];
-	const uint32_t ts = tstart[gt];
-	const uint32_t tid = threadIdx.x;
-	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
-	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
-	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
-	const uint32_t o = (ts + tid) << 3;
-	const double* const fld[7] = {rho, vx, vy, vz, lx, ly, lz};
-	double c[7];
-#pragma unroll
-	for (int k = 0; k < 7; k++) c[k] = ldo(fld[k], o);
-	// out-of-tile neighbor per axis (a cell touches at most one side per axis)
-	AdvNb xn[3];
-	int xd[3];  // direction of that face, or -1 (inside the tile) / -2 (no neighbor)
-#pragma unroll
-	for (int a = 0; a < 3; a++) {
-		xd[a] = -1;
-		xn[a] = AdvNb{0, 1, 1, 1, 0};
-		const int d = l[a] == 0 ? 2 * a : (l[a] == 7 ? 2 * a + 1 : -1);
-		if (d < 0) continue;
-		const int32_t st = DIAG ? int32_t(ts) : tnb[6 * gt + d];
-		if (st < 0) {
-			xd[a] = -2;
-			continue;
-		}
-		xd[a] = d;
-		uint32_t q[3] = {l[0], l[1], l[2]};
-		q[a] = (d & 1) ? 0u : 7u;
-		const uint32_t no = (uint32_t(st) + m9(q[0], q[1], q[2])) << 3;
-		xn[a] = AdvNb{ldo(rho, no), ldo(lx, no), ldo(ly, no), ldo(lz, no), ldo(fld[1 + a], no)};
-	}
-#pragma unroll
-	for (int k = 0; k < 7; k++) shd[k][tid] = c[k];
-	__syncthreads();
-	const double cd = c[0], cvx = c[1], cvy = c[2], cvz = c[3], clx = c[4], cly = c[5], clz = c[6];
-	double acc = 0;
-#pragma unroll
-	for (int d = 0; d < 6; d++) {
-		const int a = d >> 1;
-		const bool plus = d & 1;
-		const bool inside = plus ? l[a] < 7 : l[a] > 0;
-		AdvNb n;
-		if (inside) {
-			uint32_t q[3] = {l[0], l[1], l[2]};
-			q[a] = plus ? q[a] + 1 : q[a] - 1;
-			const uint32_t li = m9(q[0], q[1], q[2]);
-			n = AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]};
-		} else {
-			if (xd[a] != d) continue;  // no neighbor on this side
-			n = xn[a];
-		}
-		acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, n, dt);
-	}
-	rho_out[ts + tid] = cd + acc / (clx * cly * clz);
-}
-
-
-// Persistent, software-pipelined form of advection_regular_kernel: a fixed
-// grid (a few blocks per CU); XCD x (= block % 8) sweeps the x-th eighth of
-// the regular-tile list, its blocks taking consecutive tiles side by side
-// (block j: tiles j, j + B, j + 2B, ... of that eighth, B = blocks per XCD),
-// and every block loads tile k + B into registers while it computes tile k
-// from LDS, so a CU always has a tile of loads in flight.
-struct RegLoad {
-	double c[7];
-	AdvNb xn[3];
-	int xd[3];
-};
-
-struct AdvFields {
-	const double *rho, *vx, *vy, *vz, *lx, *ly, *lz;
-	__device__ __forceinline__ const double* v(int a) const { return a == 0 ? vx : (a == 1 ? vy : vz); }
-};
-
-__device__ __forceinline__ void reg_load(const AdvFields& F, const RegTileMeta& m, const uint32_t l[3], uint32_t tid,
-                                         RegLoad& r) {
-	const uint32_t o = (m.ts + tid) << 3;
-	r.c[0] = ldo(F.rho, o);
-	r.c[1] = ldo(F.vx, o);
-	r.c[2] = ldo(F.vy, o);
-	r.c[3] = ldo(F.vz, o);
-	r.c[4] = ldo(F.lx, o);
-	r.c[5] = ldo(F.ly, o);
-	r.c[6] = ldo(F.lz, o);
-#pragma unroll
-	for (int a = 0; a < 3; a++) {
-		r.xd[a] = -1;
-		r.xn[a] = AdvNb{0, 1, 1, 1, 0};
-		const bool lo = l[a] == 0, hi = l[a] == 7;
-		if (!lo && !hi) continue;
-		// constant indices only (a runtime index into m.nst would live in scratch)
-		const int32_t st = lo ? m.nst[2 * a] : m.nst[2 * a + 1];
-		if (st < 0) {
-			r.xd[a] = -2;
-			continue;
-		}
-		r.xd[a] = lo ? 2 * a : 2 * a + 1;
-		uint32_t q[3] = {l[0], l[1], l[2]};
-		q[a] = lo ? 7u : 0u;
-		const uint32_t no = (uint32_t(st) + m9(q[0], q[1], q[2])) << 3;
-		r.xn[a] = AdvNb{ldo(F.rho, no), ldo(F.lx, no), ldo(F.ly, no), ldo(F.lz, no), ldo(F.v(a), no)};
-	}
 }
 
 // the out-of-tile neighbors of a regular tile, flattened: k = (side * 5 +
@@ -622,63 +305,26 @@ __device__ __forceinline__ double adv_face_g(int a, double cd, double clx, doubl
 	return (v >= 0 ? cd : n.d) * dt * v * min_area;
 }
 
-// Work tickets of the persistent sweeps.  Static: block j of XCD x takes
-// tiles j, j + B, j + 2B, ... of the x-th eighth of the list.  Dynamic: the
-// blocks of XCD x draw the tiles of that eighth in order from counter x
-// (tiles differ in cost, and a block that starts late - beside the other
-// sweep on the second stream - takes fewer).  Each ticket is drawn one tile
-// ahead of its use, so the atomic's latency hides behind the tile in flight.
-// Counters sit 128 B apart (one cache line each).
-// A launch draws from counter set `par` and zeroes the other set, which the
-// next launch of the same kernel (ordered after this one) draws from.
-template <bool DYN>
-struct Tickets {
-	uint32_t* ctr;
-	uint32_t x, B, t0, t1, pend = 0, slot = 0;
-	uint32_t* s_tk;  // 2 LDS words
-	// the first tile of this block (or >= t1: none); block-uniform
-	__device__ __forceinline__ uint32_t first() {
-		if (!DYN) return t0 + (blockIdx.x >> 3);
-		if (threadIdx.x == 0) s_tk[0] = atomicAdd(ctr + 32u * x, 1u);
-		__syncthreads();
-		const uint32_t t = t0 + s_tk[0];
-		if (threadIdx.x == 0 && t < t1) pend = atomicAdd(ctr + 32u * x, 1u);
-		return t;
+// Static persistent schedule of the tile sweeps: block b runs on XCD b % 8
+// (measured: scripts/microbench/xcd_map.hip); XCD x sweeps the x-th eighth
+// of the tile list, its B blocks side by side (block j: tiles j, j + B, ...),
+// so the tiles an XCD has in flight are Morton neighbors sharing L2 lines.
+struct StaticTiles {
+	uint32_t t0, t1, B;
+	__device__ __forceinline__ explicit StaticTiles(uint32_t ntiles) {
+		const uint32_t x = blockIdx.x & 7u;
+		B = gridDim.x >> 3;
+		t0 = uint32_t((uint64_t(x) * ntiles) >> 3);
+		t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
 	}
-	// before the barrier that precedes next(): publish the drawn ticket, draw one more
-	__device__ __forceinline__ void draw() {
-		if (DYN && threadIdx.x == 0) {
-			s_tk[slot] = pend;
-			pend = atomicAdd(ctr + 32u * x, 1u);
-		}
-	}
-	// after that barrier: the tile after t
-	__device__ __forceinline__ uint32_t next(uint32_t t) {
-		if (!DYN) return t + B;
-		const uint32_t tn = t0 + s_tk[slot];
-		slot ^= 1u;
-		return tn;
-	}
+	__device__ __forceinline__ uint32_t first() const { return t0 + (blockIdx.x >> 3); }
+	__device__ __forceinline__ uint32_t next(uint32_t t) const { return t + B; }
 };
 
-template <bool DYN>
-__device__ __forceinline__ Tickets<DYN> make_tickets(uint32_t* ctr, uint32_t par, uint32_t ntiles, uint32_t* s_tk) {
-	Tickets<DYN> k;
-	k.x = blockIdx.x & 7u;
-	k.B = gridDim.x >> 3;
-	k.t0 = uint32_t((uint64_t(k.x) * ntiles) >> 3);
-	k.t1 = uint32_t((uint64_t(k.x + 1) * ntiles) >> 3);
-	k.s_tk = s_tk;
-	k.ctr = ctr + 256u * par;
-	if (DYN && blockIdx.x == 0 && threadIdx.x < 8) ctr[256u * (par ^ 1u) + 32u * threadIdx.x] = 0;
-	return k;
-}
-
-template <int MINW, int NT, bool DYN, int DEPTH = 1>
+template <int MINW>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
-                                                                         uint32_t ntiles, double dt, uint32_t* ctr,
-                                                                         uint32_t par) {
+                                                                         uint32_t ntiles, double dt) {
 #pragma clang fp contract(off)
 	// rows rho, vx, vy, vz, lx, ly, lz; columns 0..511 the tile's own cells,
 	// 512 + 64 d + (face cell) the out-of-tile neighbor across side d (only
@@ -688,8 +334,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	__shared__ double shd[7][W];
 	__shared__ double shg[3][512];  // flux through each cell's +x, +y, +z face
 	__shared__ double shm[3][64];   // flux through the tile's -x, -y, -z boundary faces
-	__shared__ uint32_t s_tk[2];
-	Tickets<DYN> tk = make_tickets<DYN>(ctr, par, ntiles, s_tk);
+	const StaticTiles tk(ntiles);
 	const uint32_t t1 = tk.t1;
 	uint32_t t = tk.first();
 	if (t >= t1) return;  // block-uniform
@@ -728,9 +373,9 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	auto load = [&](uint32_t tt, RegSet& r) {
 		const uint32_t ts = meta[tt].ts;
 		const uint32_t o = (ts + tid) << 3;
-		r.c[0] = ldo_own<NT>(rho, o); r.c[1] = ldo_own<NT>(vx, o); r.c[2] = ldo_own<NT>(vy, o);
-		r.c[3] = ldo_own<NT>(vz, o); r.c[4] = ldo_own<NT>(lx, o); r.c[5] = ldo_own<NT>(ly, o);
-		r.c[6] = ldo_own<NT>(lz, o);
+		r.c[0] = ldo(rho, o); r.c[1] = ldo(vx, o); r.c[2] = ldo(vy, o);
+		r.c[3] = ldo(vz, o); r.c[4] = ldo(lx, o); r.c[5] = ldo(ly, o);
+		r.c[6] = ldo(lz, o);
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
@@ -797,48 +442,20 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			acc += gm;
 			acc += -shg[a][tid];
 		}
-		st_out<NT>(rho_out, ts + tid, cd + acc / (clx * cly * clz));
+		st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 	};
 	RegSet ra;
 	load(t, ra);
-	if constexpr (DEPTH == 2) {
-		// two tiles of loads in flight (static schedule): while tile t is
-		// computed, tile t + B is in flight in one register set and tile
-		// t + 2B is issued into the other as soon as that set is staged
-		const uint32_t B = tk.B;
-		RegSet rb;
-		uint32_t tn = t + B;
-		if (tn < t1) load(tn, rb);
-		auto step = [&](RegSet& r, uint32_t tc, uint32_t tl) {
-			__syncthreads();  // the previous tile's faces have been read from LDS
-			stage(r);
-			__syncthreads();
-			if (tl < t1) load(tl, r);
-			compute(tc);
-		};
-		for (;;) {
-			step(ra, t, tn + B);
-			if (tn >= t1) break;
-			t = tn;
-			tn = t + B;
-			step(rb, t, tn + B);
-			if (tn >= t1) break;
-			t = tn;
-			tn = t + B;
-		}
-	} else {
-		for (;;) {
-			tk.draw();
-			__syncthreads();  // the previous tile's faces have been read from LDS
-			stage(ra);
-			__syncthreads();
-			const uint32_t tc = t, tn = tk.next(t);
-			const bool more = tn < t1;
-			if (more) load(tn, ra);  // the next tile's loads fly while this one is computed
-			compute(tc);
-			if (!more) break;
-			t = tn;
-		}
+	for (;;) {
+		__syncthreads();  // the previous tile's faces have been read from LDS
+		stage(ra);
+		__syncthreads();
+		const uint32_t tc = t, tn = tk.next(t);
+		const bool more = tn < t1;
+		if (more) load(tn, ra);  // the next tile's loads fly while this one is computed
+		compute(tc);
+		if (!more) break;
+		t = tn;
 	}
 }
 
@@ -852,18 +469,16 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW, int NT, int EXT5, bool DYN>
+template <int MINW>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt,
-    uint32_t* ctr, uint32_t par) {
+    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
 #pragma clang fp contract(off)
 	constexpr uint32_t T = 512;
 	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
 	const uint32_t W = T + ecap;
 	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
-	__shared__ uint32_t s_tk[2];
-	Tickets<DYN> tk = make_tickets<DYN>(ctr, par, ntiles, s_tk);
+	const StaticTiles tk(ntiles);
 	const uint32_t t1 = tk.t1;
 	uint32_t t = tk.first();
 	if (t >= t1) return;  // block-uniform
@@ -883,36 +498,26 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
 		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
 	};
-	auto load7own = [&](uint32_t slot, double (&v)[7]) {
-		const uint32_t o = slot << 3;
-		v[0] = ldo_own<NT>(rho, o); v[1] = ldo_own<NT>(vx, o); v[2] = ldo_own<NT>(vy, o); v[3] = ldo_own<NT>(vz, o);
-		v[4] = ldo_own<NT>(lx, o); v[5] = ldo_own<NT>(ly, o); v[6] = ldo_own<NT>(lz, o);
-	};
 	auto load = [&](uint32_t tt) {
 		const uint32_t ts = meta[tt].ts, n = meta[tt].n, e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb,
 		               nf = meta[tt].nf;
 		if (tid < n) {
-			load7own(ts + tid, c);
+			load7(ts + tid, c);
 			row[0] = tell[3 * (ts + tid)];
 			row[1] = tell[3 * (ts + tid) + 1];
 			row[2] = tell[3 * (ts + tid) + 2];
 		}
-		if (EXT5) {
-			// ext = slot | axis mask << 29: density and lengths, and only the
-			// velocity components along the axes its faces cross
-			auto load5 = [&](uint32_t q, double (&v)[7]) {
-				const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
-				v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
-				v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
-				v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
-				v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
-			};
-			if (tid < ne) load5(ext[e0 + tid], xa);
-			if (tid + T < ne) load5(ext[e0 + tid + T], xb);
-		} else {
-			if (tid < ne) load7(ext[e0 + tid], xa);
-			if (tid + T < ne) load7(ext[e0 + tid + T], xb);
-		}
+		// ext = slot | axis mask << 29: density and lengths, and only the
+		// velocity components along the axes its faces cross
+		auto load5 = [&](uint32_t q, double (&v)[7]) {
+			const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
+			v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+			v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
+			v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
+			v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
+		};
+		if (tid < ne) load5(ext[e0 + tid], xa);
+		if (tid + T < ne) load5(ext[e0 + tid + T], xb);
 		if (tid < nf) {
 			fq[0] = tfine[2 * (fb + tid)];
 			fq[1] = tfine[2 * (fb + tid) + 1];
@@ -921,7 +526,6 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 	load(t);
 	for (;;) {
 		const uint32_t n = meta[t].n, ne = meta[t].ne, nf = meta[t].nf, ts = meta[t].ts;
-		tk.draw();
 		__syncthreads();  // the previous tile's faces have been read from LDS
 		if (tid < n)
 #pragma unroll
@@ -964,182 +568,12 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 					acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
 				}
 			}
-			st_out<NT>(rho_out, ts + tid, cd + acc / (clx * cly * clz));
+			st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 		}
 		if (!more) break;
 		t = tn;
 	}
 }
-
-// (A/B variant, off by default: see k_advection_tiles.)
-// One persistent sweep over every tile of a run in slot (= Morton) order,
-// regular and general tiles alike (FTileMeta::kind), so that a tile's face
-// neighbors - whatever their kind - were swept by the same XCD a few tiles
-// earlier and are still in its L2.  (Sweeping the two kinds in two launches
-// re-fetched the faces between them from the fabric: ~1.5x the algorithmic
-// bytes, PMC FETCH_SIZE, profiles/r01h.)  Per tile, as the two separate
-// kernels: own fields at slot ts + tid; a general tile adds its 16-bit face
-// rows, ext cells and finer-face pairs, a regular tile (aligned 8^3 box of
-// one level, Morton-local) its six 64-cell boundary faces from the same-level
-// neighbor boxes, with face codes from Morton arithmetic.  While a tile is
-// computed from LDS, the next tile's loads are in flight in registers (the
-// boundary rows of a regular tile share the general tile's ext registers).
-// Every face is evaluated from each side with the reference's expression,
-// as the general kernel does.
-struct FTileMeta {
-	uint32_t ts, n, e0, ne, fb, nf;
-	int32_t nst[6];  // regular: start slot of the same-level neighbor box per side (-1: none)
-	uint32_t kind, pad[3];
-};
-
-template <int MINW>
-__global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
-    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ tfine, const FTileMeta* __restrict__ meta, uint32_t ntiles, uint32_t W, double dt) {
-#pragma clang fp contract(off)
-	constexpr uint32_t T = 512;
-	extern __shared__ double shd[];  // [7][W] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
-	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
-	const uint32_t B = gridDim.x >> 3, x = blockIdx.x & 7u, j = blockIdx.x >> 3;
-	const uint32_t t0 = uint32_t((uint64_t(x) * ntiles) >> 3), t1 = uint32_t((uint64_t(x + 1) * ntiles) >> 3);
-	uint32_t t = t0 + j;
-	if (t >= t1) return;  // block-uniform
-	const uint32_t tid = threadIdx.x;
-	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
-	// Morton-local coordinates of this thread's cell in a regular tile
-	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
-	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
-	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
-	const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
-	const double* const rho = P.p[0];
-	const double* const lx = P.p[1];
-	const double* const ly = P.p[2];
-	const double* const lz = P.p[3];
-	const double* const vx = P.p[4];
-	const double* const vy = P.p[5];
-	const double* const vz = P.p[6];
-	// register set of the tile being loaded (field order rho vx vy vz lx ly lz);
-	// a regular tile's boundary values go to xa[0..3]
-	double c[7], xa[7], xb[7];
-	uint32_t row[3], fq[2];
-	auto load7 = [&](uint32_t slot, double (&v)[7]) {
-		const uint32_t o = slot << 3;
-		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
-		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
-	};
-	auto load = [&](uint32_t tt) {
-		const uint32_t ts = meta[tt].ts, n = meta[tt].n;
-		if (tid < n) load7(ts + tid, c);
-		if (meta[tt].kind) {
-			// boundary rows k = (side * 5 + value) * 64 + face cell, rows w + 8 i
-#pragma unroll
-			for (int i = 0; i < 4; i++) {
-				const uint32_t r = w + 8u * uint32_t(i);  // wave-uniform
-				xa[i] = 0;
-				if (r >= 30u) continue;
-				const uint32_t d = r / 5u, val = r - 5u * d, a = d >> 1;
-				const int32_t st = meta[tt].nst[d];
-				if (st < 0) continue;
-				const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
-				const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
-				xa[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
-			}
-		} else {
-			const uint32_t e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb, nf = meta[tt].nf;
-			if (tid < n) {
-				row[0] = tell[3 * (ts + tid)];
-				row[1] = tell[3 * (ts + tid) + 1];
-				row[2] = tell[3 * (ts + tid) + 2];
-			}
-			if (tid < ne) load7(ext[e0 + tid], xa);
-			if (tid + T < ne) load7(ext[e0 + tid + T], xb);
-			if (tid < nf) {
-				fq[0] = tfine[2 * (fb + tid)];
-				fq[1] = tfine[2 * (fb + tid) + 1];
-			}
-		}
-	};
-	// LDS row of boundary value `val` (0 rho, 1 lx, 2 ly, 3 lz, 4 velocity along a)
-	auto vrow = [](uint32_t val, uint32_t a) -> uint32_t { return val == 0 ? 0u : (val == 4 ? 1u + a : val + 3u); };
-	load(t);
-	for (;;) {
-		const uint32_t n = meta[t].n, ts = meta[t].ts, kind = meta[t].kind;
-		__syncthreads();  // the previous tile's faces have been read from LDS
-		if (tid < n)
-#pragma unroll
-			for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
-		uint32_t rr[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
-		if (kind) {
-#pragma unroll
-			for (int i = 0; i < 4; i++) {
-				const uint32_t r = w + 8u * uint32_t(i);
-				if (r < 30u) {
-					const uint32_t d = r / 5u, val = r - 5u * d;
-					shd[vrow(val, d >> 1) * W + T + 64u * d + lane] = xa[i];
-				}
-			}
-			// face codes (same encoding as the general tile's rows): in-tile
-			// Morton index, T + 64 d + face cell across side d, 0xffff none
-#pragma unroll
-			for (int a = 0; a < 3; a++) {
-				uint32_t qm[3] = {l[0], l[1], l[2]}, qp[3] = {l[0], l[1], l[2]};
-				qm[a] -= 1;
-				qp[a] += 1;
-				const uint32_t cm = l[a] > 0 ? m9(qm[0] & 7u, qm[1] & 7u, qm[2] & 7u)
-				                             : (meta[t].nst[2 * a] >= 0 ? T + 64u * (2 * a) + fi[a] : 0xffffu);
-				const uint32_t cp = l[a] < 7 ? m9(qp[0] & 7u, qp[1] & 7u, qp[2] & 7u)
-				                             : (meta[t].nst[2 * a + 1] >= 0 ? T + 64u * (2 * a + 1) + fi[a] : 0xffffu);
-				rr[a] = cm | (cp << 16);
-			}
-		} else {
-			const uint32_t ne = meta[t].ne, nf = meta[t].nf;
-			if (tid < ne)
-#pragma unroll
-				for (int k = 0; k < 7; k++) shd[k * W + T + tid] = xa[k];
-			if (tid + T < ne)
-#pragma unroll
-				for (int k = 0; k < 7; k++) shd[k * W + 2 * T + tid] = xb[k];
-			if (tid < nf) {
-				shf[2 * tid] = fq[0];
-				shf[2 * tid + 1] = fq[1];
-			}
-			rr[0] = row[0];
-			rr[1] = row[1];
-			rr[2] = row[2];
-		}
-		__syncthreads();
-		const uint32_t tn = t + B;
-		const bool more = tn < t1;
-		if (more) load(tn);  // the next tile's loads fly while this one is computed
-		if (tid < n) {
-			const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
-			             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
-			auto fetch = [&](uint32_t li, int d) -> AdvNb {
-				return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
-			};
-			double acc = 0;
-#pragma unroll
-			for (int d = 0; d < 6; d++) {
-				const uint32_t code = (rr[d >> 1] >> (16 * (d & 1))) & 0xffffu;
-				if (code == 0xffffu) continue;
-				if (code & 0x8000u) {
-					const uint32_t fk = code & 0x7fffu;
-					const uint32_t q0 = shf[2 * fk], q1 = shf[2 * fk + 1];
-					const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
-#pragma unroll
-					for (int k = 0; k < 4; k++)
-						acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
-				} else {
-					acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
-				}
-			}
-			rho_out[ts + tid] = cd + acc / (clx * cly * clz);
-		}
-		if (!more) break;
-		t = tn;
-	}
-}
-
 // max_time_step local part (solve.hpp:289-333): block minima
 __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __restrict__ vy,
                               const double* __restrict__ vz, const double* __restrict__ lx,
@@ -1201,295 +635,93 @@ __global__ void adv_candidates_kernel(MapCtx m, const double* __restrict__ rho, 
 }  // namespace
 
 // ===========================================================================
-void k_pack(const uint8_t* field, size_t elem, const int32_t* slots, size_t n, uint8_t* out, hipStream_t s) {
-	if (!n) return;
-	if (elem == 4)
+void k_pack(const uint8_t* field, size_t elem, size_t off, size_t len, const int32_t* slots, size_t n, uint8_t* out,
+            hipStream_t s) {
+	if (!n || !len) return;
+	if (off == 0 && len == elem && elem == 4)
 		pack_kernel<uint32_t><<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)field, slots, n, (uint32_t*)out);
-	else if (elem == 8)
+	else if (off == 0 && len == elem && elem == 8)
 		pack_kernel<uint64_t><<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)field, slots, n, (uint64_t*)out);
 	else
-		pack_bytes_kernel<<<grid_for(n * elem, 256), 256, 0, s>>>(field, elem, slots, n, out);
+		pack_bytes_kernel<<<grid_for(n * len, 256), 256, 0, s>>>(field, elem, off, len, slots, n, out);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_place(const uint8_t* in, size_t elem, size_t off, size_t len, const int32_t* slots, size_t n, uint8_t* field,
+             hipStream_t s) {
+	if (!n || !len) return;
+	if (off == 0 && len == elem && elem == 4)
+		place_kernel<uint32_t><<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)in, slots, n, (uint32_t*)field);
+	else if (off == 0 && len == elem && elem == 8)
+		place_kernel<uint64_t><<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)in, slots, n, (uint64_t*)field);
+	else
+		place_bytes_kernel<<<grid_for(n * len, 256), 256, 0, s>>>(in, elem, off, len, slots, n, field);
 	HIP_CHECK(hipGetLastError());
 }
 
 void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
                size_t s1, hipStream_t s) {
 	if (s1 <= s0) return;
-	gol_csr_kernel<<<grid_for(s1 - s0, 256), 256, 0, s>>>(state, out, it_ptr, it_slot, s0, s1);
+	gol_csr_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(state, out, it_ptr, it_slot, s0, s1);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], hipStream_t s) {
-	static const int variant = [] {
-		const char* e = getenv("DCCRGX_GOL_VARIANT");
-		return e ? atoi(e) : 3;
-	}();
-	static const int zc3 = [] {  // DCCRGX_GOL_ZC: planes per z chunk of the v3 kernel
-		const char* e = getenv("DCCRGX_GOL_ZC");
-		return e ? atoi(e) : 64;
-	}();
-	static const int depth3 = [] {  // DCCRGX_GOL_DEPTH: planes of loads in flight per wave (v3)
-		const char* e = getenv("DCCRGX_GOL_DEPTH");
-		return e ? atoi(e) : 3;
-	}();
-	if (variant == 3 && n[0] % 256 == 0 && n[0] * n[1] * n[2] < (uint64_t(1) << 32)) {
-		const int zc = int(std::min<uint64_t>(n[2], uint64_t(zc3 > 0 ? zc3 : 32)));
-		const unsigned nbx = unsigned(n[0] / 256), nby = unsigned((n[1] + G3_ROWS - 1) / G3_ROWS),
-		               nbz = unsigned((n[2] + zc - 1) / zc);
-		const size_t nb = size_t(nbx) * nby * nbz;
-		const unsigned grid = unsigned((nb + 7) / 8 * 8);
-#define DX_GOL3(D)                                                                                                   \
-	gol_structured_v3<D><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1], \
-	                                                   per[2], zc, nbx, nby, unsigned(nb))
-		if (depth3 <= 2) DX_GOL3(2);
-		else if (depth3 == 3) DX_GOL3(3);
-		else if (depth3 == 4) DX_GOL3(4);
-		else DX_GOL3(6);
-#undef DX_GOL3
-		HIP_CHECK(hipGetLastError());
-		return;
-	}
-	if (variant >= 2) {
-		const int zc = int(n[2] <= 64 ? n[2] : 64);
-		dim3 g2(unsigned((n[0] + G2_OUT - 1) / G2_OUT), unsigned((n[1] + G2_ROWS - 1) / G2_ROWS),
-		        unsigned((n[2] + zc - 1) / zc));
-		gol_structured_v2<<<g2, 64 * G2_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1],
-		                                               per[2], zc);
-		HIP_CHECK(hipGetLastError());
-		return;
-	}
-	throw Error(DCCRGX_EINVAL, "DCCRGX_GOL_VARIANT must be 2 or 3");
-}
-
-// DCCRGX_ADV_NT: non-temporal hints of the tile sweeps (bit 0 density
-// store, bit 1 own-field loads).  Measured on config 3: the store hint
-// 0.1960 -> 0.1945 ms (default on); the load hint 0.2185 ms, because the
-// own-field lines are the face lines neighboring tiles re-read from L2;
-// non-temporal face/ext loads from tiles swept earlier: no gain (0.199 ms).
-static int adv_nt() {
-	static const int v = [] {
-		const char* e = getenv("DCCRGX_ADV_NT");
-		return e ? atoi(e) : 1;
-	}();
-	return v;
-}
-
-int adv_variant() {
-	static int v = [] {
-		const char* e = getenv("DCCRGX_ADV_VARIANT");
-		return e ? atoi(e) : 11;
-	}();
-	return v;
+// false when the box does not fit the structured kernel (nx % 256 != 0)
+bool k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3], const int per[3], const uint32_t* lo,
+                      const uint32_t* hi, hipStream_t s) {
+	if (n[0] % 256 != 0 || n[0] * n[1] * n[2] >= (uint64_t(1) << 32) || n[2] == 0) return false;
+	// 64 planes per z chunk, 3 planes of loads in flight per wave (r01g/r01j
+	// sweeps over zc and the depth on config 2)
+	const int zc = int(std::min<uint64_t>(n[2], 64));
+	const unsigned nbx = unsigned(n[0] / 256), nby = unsigned((n[1] + G3_ROWS - 1) / G3_ROWS),
+	               nbz = unsigned((n[2] + zc - 1) / zc);
+	const size_t nb = size_t(nbx) * nby * nbz;
+	const unsigned grid = unsigned((nb + 7) / 8 * 8);
+	gol_structured_v3<3><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1],
+	                                                    per[2], zc, nbx, nby, unsigned(nb), lo, hi);
+	HIP_CHECK(hipGetLastError());
+	return true;
 }
 
 void k_advection(const double* const f[7], double* rho_out, const uint32_t* face_ptr, const int32_t* face_ent,
-                 const int32_t* face_ell, const int32_t* face_fine, size_t s0, size_t s1, double dt, hipStream_t s) {
-	// the untiled gather over the face CSR (DCCRGX_ADV_VARIANT=0; the tiled
-	// sweep is variant 11, the default)
+                 size_t s0, size_t s1, double dt, hipStream_t s) {
+	// the untiled gather over the face CSR: runs whose tiles exceed the
+	// pipelined tile kernel's capacities
 	if (s1 <= s0) return;
-	advection_kernel<<<grid_for(s1 - s0, 256), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, face_ptr,
-	                                                        face_ent, s0, s1, dt);
+	advection_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6],
+	                                                                    rho_out, face_ptr, face_ent, s0, s1, dt);
 	HIP_CHECK(hipGetLastError());
 }
 
-// LDS rows for ext cells: a compact T-cell box has about T^(2/3) * 6 of them
-// (384 for an 8x8x8 box); larger lists spill to global reads
-static uint32_t tile_ecap(int T, size_t max_ext) {
-	static const int env = [] {
-		const char* e = getenv("DCCRGX_TILE_ECAP");
-		return e ? atoi(e) : -1;
-	}();
-	const size_t cap = env >= 0 ? size_t(env) : (T >= 512 ? size_t(3 * T / 4) : size_t(T));
-	return uint32_t(std::min(cap, max_ext));
-}
-
+// Tiled advection sweep of one run (0 inner, 1 outer): the regular tiles with
+// advection_regular_pp_kernel, every other tile with advection_tiles_pp_kernel,
+// both persistent with two blocks per CU (r01k: one / two tiles in flight per
+// block, dynamic tickets and a second stream for the general sweep all tie
+// or lose against this schedule).
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s) {
-	// DCCRGX_ADV_DYN=1: tiles drawn from per-XCD counters instead of the static
-	// schedule (A/B: equal on config 3 once the counters sit on separate lines)
-	static const int dyn = [] {
-		const char* e = getenv("DCCRGX_ADV_DYN");
-		return e ? atoi(e) : 0;
-	}();
-	// DCCRGX_ADV_DEPTH=2: two tiles of loads in flight in the regular sweep
-	// instead of one (A/B on config 3: equal, 0.1896 vs 0.1894 ms)
-	static const int depth = [] {
-		const char* e = getenv("DCCRGX_ADV_DEPTH");
-		return e ? atoi(e) : 1;
-	}();
-	// DCCRGX_ADV_2S=1: the general-tile sweep on a second stream beside the regular one
-	static const int two_streams = [] {
-		const char* e = getenv("DCCRGX_ADV_2S");
-		return e ? atoi(e) : 0;
-	}();
-	if (dyn && g.adv_ctr.n < 1024) {
-		g.adv_ctr.alloc(1024);
-		HIP_CHECK(hipMemsetAsync(g.adv_ctr.p, 0, 1024 * sizeof(uint32_t), s));
-	}
-	static const int diag = [] {
-		const char* e = getenv("DCCRGX_ADV_DIAG");
-		return e ? atoi(e) : 0;
-	}();
-	static const int amap = [] {
-		const char* e = getenv("DCCRGX_ADV_MAP");
-		return e ? atoi(e) : 128;
-	}();
-	// DCCRGX_ADV_REGULAR=0 sweeps every tile with the general kernel (A/B)
-	static const int use_regular = [] {
-		const char* e = getenv("DCCRGX_ADV_REGULAR");
-		return e ? atoi(e) : 1;
-	}();
-	// whole rounds of 8 x map tiles, so that the block -> tile map is onto
-	// (blocks past the last tile exit at once)
-	const size_t round = amap >= 2 ? size_t(8) * size_t(amap) : size_t(8);
-	auto blocks = [&](size_t n) { return (n + round - 1) / round * round; };
-	const int T = g.tile;
-	const uint32_t* reg = g.tlists.p + (run == 0 ? 0 : g.tcount[0]);
-	const uint32_t* irr = g.tlists.p + g.tcount[0] + g.tcount[1] + (run == 0 ? 0 : g.tcount[2]);
-	size_t n_reg = g.tcount[run], n_irr = g.tcount[2 + run];
-	std::vector<uint32_t> all_h;
-	DBuf<uint32_t> all_d;
-	if (!use_regular && n_reg) {  // one list with both kinds
-		all_h = download(reg, n_reg, s);
-		const auto ih = download(irr, n_irr, s);
-		all_h.insert(all_h.end(), ih.begin(), ih.end());
-		upload(all_d, all_h, s);
-		irr = all_d.p;
-		n_irr += n_reg;
-		n_reg = 0;
-	}
-	// DCCRGX_ADV_FUSED=1: both tile kinds in one slot-order launch.  Measured
-	// on config 3 (profiles/r01i): 10% fewer fabric bytes (919 vs 1015 MB per
-	// sweep) but 10% slower (0.2195 vs 0.1988 ms), so the two-launch sweep
-	// stays the default.
-	static const int fused = [] {
-		const char* e = getenv("DCCRGX_ADV_FUSED");
-		return e ? atoi(e) : 0;
-	}();
-	if (fused && use_regular && T == 512 && g.tfmeta.n && diag == 0) {
-		const size_t ntr = run == 0 ? g.n_tiles_inner : g.n_tiles_outer;
-		if (!ntr) return;
-		const FTileMeta* meta = reinterpret_cast<const FTileMeta*>(g.tfmeta.p) + (run == 0 ? 0 : g.n_tiles_inner);
-		const uint32_t W = T + uint32_t(std::max<size_t>(g.max_ext, 384));
-		const size_t lds = size_t(7) * W * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
-		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (ntr + 7) / 8 * 8));
-		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		advection_fused_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext.p, g.tfine.p, meta,
-		                                                  uint32_t(ntr), W, dt);
-		HIP_CHECK(hipGetLastError());
+	const size_t n_reg = g.tcount[run], n_irr = g.tcount[2 + run];
+	const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
+	if (n_irr && !g.tmeta.n) {
+		// a tile beyond the pipelined kernel's capacities: the whole run untiled
+		const size_t s0 = run == 0 ? 0 : g.n_inner, s1 = run == 0 ? g.n_inner : g.n_local;
+		k_advection(f, rho_out, g.face_ptr.p, g.face_ent.p, s0, s1, dt, s);
 		return;
 	}
-	static const int pp_blocks = [] {  // DCCRGX_ADV_PP=k: persistent regular kernel, k blocks per CU (0: off)
-		const char* e = getenv("DCCRGX_ADV_PP");
-		return e ? atoi(e) : 2;
-	}();
-	static const int tiles_pp = [] {  // DCCRGX_ADV_TPP=0: the non-persistent tile kernel
-		const char* e = getenv("DCCRGX_ADV_TPP");
-		return e ? atoi(e) : 1;
-	}();
-	// the general sweep beside the regular one on a second stream: forked
-	// after everything queued on s, joined before whatever s runs next
-	const bool fork =
-	    two_streams && n_reg && pp_blocks > 0 && n_irr && tiles_pp && T == 512 && g.tmeta.n && diag == 0;
-	if (fork) {
-		if (!g.s_adv2) {
-			HIP_CHECK(hipStreamCreateWithFlags(&g.s_adv2, hipStreamNonBlocking));
-			HIP_CHECK(hipEventCreateWithFlags(&g.ev_fork, hipEventDisableTiming));
-			HIP_CHECK(hipEventCreateWithFlags(&g.ev_join, hipEventDisableTiming));
-		}
-		HIP_CHECK(hipEventRecord(g.ev_fork, s));
-		HIP_CHECK(hipStreamWaitEvent(g.s_adv2, g.ev_fork, 0));
-	}
-	if (n_reg && pp_blocks > 0) {
+	if (n_reg) {
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
-		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * size_t(pp_blocks), (n_reg + 7) / 8 * 8));
-		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		uint32_t* ctr = g.adv_ctr.p;
-		const uint32_t par = g.adv_par[0];
-		g.adv_par[0] ^= 1u;
-#define DX_REG(NTV, DY) \
-	advection_regular_pp_kernel<4, NTV, DY><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par)
-		if (depth == 2 && !dyn && adv_nt() == 1)
-			advection_regular_pp_kernel<4, 1, false, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par);
-		else if (depth == 2 && !dyn && adv_nt() == 0)
-			advection_regular_pp_kernel<4, 0, false, 2><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, ctr, par);
-		else if (dyn && adv_nt() == 0) DX_REG(0, true);
-		else if (dyn && adv_nt() == 1) DX_REG(1, true);
-		else if (adv_nt() == 1) DX_REG(1, false);
-		else if (adv_nt() == 2) DX_REG(2, false);
-		else if (adv_nt() == 3) DX_REG(3, false);
-		else DX_REG(0, false);
-#undef DX_REG
-		HIP_CHECK(hipGetLastError());
-	} else if (n_reg) {
-		if (diag == 5)
-			advection_regular_kernel<1><<<unsigned(blocks(n_reg)), 512, 0, s>>>(
-			    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, reg, g.tnb.p, uint32_t(n_reg), dt, amap);
-		else
-			advection_regular_kernel<0><<<unsigned(blocks(n_reg)), 512, 0, s>>>(
-			    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, reg, g.tnb.p, uint32_t(n_reg), dt, amap);
+		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_reg + 7) / 8 * 8));
+		advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
 		HIP_CHECK(hipGetLastError());
 	}
-	if (!n_irr) {
-		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
-		return;
-	}
-	if (tiles_pp && T == 512 && g.tmeta.n && diag == 0) {
+	if (n_irr) {
 		const TileMeta* meta = reinterpret_cast<const TileMeta*>(g.tmeta.p) + (run == 0 ? 0 : g.tcount[2]);
 		const uint32_t ecap = uint32_t(g.max_ext);
-		const size_t lds = size_t(7) * (T + ecap) * sizeof(double) + size_t(2) * T * sizeof(uint32_t);
+		const size_t lds = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
-		const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
-		// DCCRGX_ADV_EXT5=0: every ext cell loads all seven fields (A/B)
-		static const int ext5 = [] {
-			const char* e = getenv("DCCRGX_ADV_EXT5");
-			return e ? atoi(e) : 1;
-		}();
-		hipStream_t st = fork ? g.s_adv2 : s;
-		uint32_t* ctr = g.adv_ctr.p ? g.adv_ctr.p + 512 : nullptr;
-		const uint32_t par = g.adv_par[1];
-		g.adv_par[1] ^= 1u;
-#define DX_TPP(NTV, E5, DY)                                                                                     \
-	advection_tiles_pp_kernel<4, NTV, E5, DY><<<nblk, 512, lds, st>>>(P, rho_out, g.tell.p, E5 ? g.ext_pk.p : g.ext.p, \
-	                                                                  g.tfine.p, meta, uint32_t(n_irr), ecap, dt, ctr, par)
-		if (dyn && ext5 && adv_nt() == 0) DX_TPP(0, 1, true);
-		else if (dyn && ext5 && adv_nt() == 1) DX_TPP(1, 1, true);
-		else if (ext5 && adv_nt() == 1) DX_TPP(1, 1, false);
-		else if (ext5 && adv_nt() == 0) DX_TPP(0, 1, false);
-		else if (adv_nt() == 1) DX_TPP(1, 0, false);
-		else if (adv_nt() == 2) DX_TPP(2, 0, false);
-		else if (adv_nt() == 3) DX_TPP(3, 0, false);
-		else DX_TPP(0, 0, false);
-#undef DX_TPP
+		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext_pk.p, g.tfine.p, meta,
+		                                                    uint32_t(n_irr), ecap, dt);
 		HIP_CHECK(hipGetLastError());
-		if (fork) {
-			HIP_CHECK(hipEventRecord(g.ev_join, st));
-			HIP_CHECK(hipStreamWaitEvent(s, g.ev_join, 0));
-		}
-		if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));
-		return;
 	}
-	const uint32_t ecap = tile_ecap(T, g.max_ext);
-	size_t lds = size_t(7) * (T + ecap) * sizeof(double);
-	if (diag == 3) lds = 0;
-	const size_t nb = blocks(n_irr);
-#define DX_ADV_TILES1(TT, W, M)                                                                                      \
-	advection_tiles_kernel<TT, W, M><<<unsigned(nb), TT, lds, s>>>(                                                       \
-	    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, g.tstart.p, g.tell.p, g.ext_ptr.p, g.ext.p, g.fine_base.p, \
-	    g.tfine.p, irr, uint32_t(n_irr), ecap, dt, amap)
-#define DX_ADV_TILES(TT, W)                                                                                          \
-	if (diag == 1) DX_ADV_TILES1(TT, W, 1);                                                                          \
-	else if (diag == 2) DX_ADV_TILES1(TT, W, 2);                                                                     \
-	else if (diag == 3) DX_ADV_TILES1(TT, W, 3);                                                                     \
-	else if (diag == 4) DX_ADV_TILES1(TT, W, 4);                                                                     \
-	else DX_ADV_TILES1(TT, W, 0)
-	if (T == 512) DX_ADV_TILES(512, 6);
-	else if (T == 256) DX_ADV_TILES(256, 5);
-	else if (T == 1024) DX_ADV_TILES(1024, 4);
-	else throw Error(DCCRGX_EINVAL, "unsupported advection tile size");
-#undef DX_ADV_TILES
-#undef DX_ADV_TILES1
-	HIP_CHECK(hipGetLastError());
-	if (!all_h.empty()) HIP_CHECK(hipStreamSynchronize(s));  // all_d must outlive the launch
 }
 
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s) {

@@ -22,13 +22,6 @@ namespace dccrgx {
 
 namespace {
 
-inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u) {
-	size_t g = (n + per_block - 1) / per_block;
-	if (g > cap) g = cap;
-	if (g == 0) g = 1;
-	return unsigned(g);
-}
-
 struct TileGeom {
 	const uint32_t* tstart;  // ntiles + 1 tile boundaries (slots)
 	uint32_t ntiles, n_local;
@@ -297,14 +290,9 @@ __global__ __launch_bounds__(512) void classify_tiles_kernel(MapCtx m, const uin
 // (the latest one on ties), so that on
 // Morton-ordered slots tiles coincide with aligned boxes wherever the mesh
 // allows (fewer distinct out-of-tile neighbors than arbitrary cuts).
-// DCCRGX_TILE_LO=k: the earliest allowed cut is k/8 of T (default 2: T/4)
-static uint32_t tile_lo(uint32_t T) {
-	static const int k = [] {
-		const char* e = getenv("DCCRGX_TILE_LO");
-		return e ? atoi(e) : 2;
-	}();
-	return std::max<uint32_t>(1u, uint32_t(uint64_t(T) * uint32_t(std::min(std::max(k, 1), 8)) / 8u));
-}
+// (a lower bound of T/8 or 3T/4 gives fewer general tiles but more of them
+// irregular and a slower sweep, r01l)
+static uint32_t tile_lo(uint32_t T) { return std::max<uint32_t>(1u, T / 4u); }
 
 static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, uint32_t T, std::vector<uint32_t>& out) {
 	uint32_t a = r0;
@@ -443,15 +431,10 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 	const std::vector<uint32_t> h = download(treg.p, nt, s);
 	// layout: [regular inner | regular outer | irregular inner | irregular outer]
 	std::vector<uint32_t> reg[2], irr[2];
-	size_t why[4] = {0, 0, 0, 0};
 	for (size_t t = 0; t < nt; t++) {
 		const int run = t < n_tiles_inner ? 0 : 1;
 		(h[t] == 1u ? reg[run] : irr[run]).push_back(uint32_t(t));
-		why[h[t] == 1u ? 0 : (h[t] >> 4)]++;
 	}
-	if (getenv("DCCRGX_DEBUG_TILES"))
-		fprintf(stderr, "[dccrgx] tiles: %zu regular, %zu not 512 slots, %zu not a uniform box, %zu irregular side\n",
-		        why[0], why[1], why[2], why[3]);
 	std::vector<uint32_t> all;
 	for (auto* v : {&reg[0], &reg[1], &irr[0], &irr[1]}) all.insert(all.end(), v->begin(), v->end());
 	counts[0] = reg[0].size();

@@ -12,7 +12,7 @@ import os
 
 import numpy as np
 
-from ._lib import EINVAL, ENOTFOUND, ERANGE, DccrgError, check, lib
+from ._lib import EINVAL, ENOTFOUND, ERANGE, EXCHANGE_FN, DccrgError, check, lib
 
 REGION = {"all": 0, "inner": 1, "outer": 2}
 DEFAULT_HOOD = -0xDCC  # default_neighborhood_id (dccrg.hpp:93)
@@ -51,20 +51,70 @@ class Field:
         self.transfer = bool(transfer)
         check(lib().dccrgx_set_field_transfer(self.grid.h, self.id, int(transfer)))
 
+    def set_window(self, offset, nbytes):
+        """The bytes of each element the halo carries (what a Cell_Data's
+        get_mpi_datatype describes)."""
+        check(lib().dccrgx_set_field_window(self.grid.h, self.id, int(offset), int(nbytes)))
+
+
+class TorchExchange:
+    """Host transport over torch.distributed point-to-point (gloo): the
+    exchange primitive of include/dccrgx.h (dccrgx_exchange_fn)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.rank, self.size = dist.get_rank(group), dist.get_world_size(group)
+        self.error = None
+        self.fn = EXCHANGE_FN(self._exchange)
+
+    def _exchange(self, ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            import torch
+            import torch.distributed as dist
+
+            reqs, outs = [], []
+            for p in range(self.size):
+                if p == self.rank:
+                    continue
+                nb = int(send_bytes[p])
+                if nb:
+                    t = torch.empty(nb, dtype=torch.uint8)
+                    C.memmove(t.data_ptr(), send[p], nb)
+                    reqs.append(dist.isend(t, p, group=self.group))
+                nr = int(recv_bytes[p])
+                if nr:
+                    t = torch.empty(nr, dtype=torch.uint8)
+                    reqs.append(dist.irecv(t, p, group=self.group))
+                    outs.append((p, t))
+            for r in reqs:
+                r.wait()
+            for p, t in outs:
+                C.memmove(recv[p], t.data_ptr(), t.numel())
+            return 0
+        except Exception as e:  # reported to the library as a failed exchange
+            self.error = e
+            return -1
+
 
 class Dccrg:
     """One grid per process; ``rank``/``size`` and an RCCL bootstrap id replace
     the reference's ``MPI_Comm`` (initialize(comm), dccrg.hpp:472)."""
 
-    def __init__(self, rank=0, size=1, device=0, unique_id: bytes | None = None):
+    def __init__(self, rank=0, size=1, device=0, unique_id: bytes | None = None, exchange: TorchExchange | None = None):
         L = lib()
         h = C.c_void_p()
-        uid = None
-        if size > 1 and unique_id is not None:
-            # without a unique id the grid is a detached view of rank `rank`
-            # (structures only, no halo transport / collectives)
-            uid = C.create_string_buffer(bytes(unique_id), 128)
-        check(L.dccrgx_create(rank, size, device, uid, C.byref(h)))
+        self._exchange = exchange  # keeps the callback alive
+        if exchange is not None:
+            check(L.dccrgx_create_with_exchange(rank, size, device, exchange.fn, None, C.byref(h)))
+        else:
+            uid = None
+            if size > 1 and unique_id is not None:
+                # without a unique id the grid is a detached view of rank `rank`
+                # (structures only, no halo transport / collectives)
+                uid = C.create_string_buffer(bytes(unique_id), 128)
+            check(L.dccrgx_create(rank, size, device, uid, C.byref(h)))
         self.h = h
         self.rank, self.size, self.device = rank, size, device
         self.fields = {}
@@ -76,13 +126,18 @@ class Dccrg:
         return buf.raw
 
     @classmethod
-    def from_torch_distributed(cls, device=None):
-        """Bootstrap from an initialized torch.distributed process group."""
+    def from_torch_distributed(cls, device=None, transport="rccl"):
+        """Bootstrap from an initialized torch.distributed process group.
+        transport "rccl": the library's own RCCL communicator (one GPU per
+        rank); "host": torch.distributed point-to-point through the host (any
+        number of ranks per GPU, a gloo group)."""
         import torch.distributed as dist
 
         rank, size = dist.get_rank(), dist.get_world_size()
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", rank))
+        if transport == "host":
+            return cls(rank, size, device, exchange=TorchExchange())
         obj = [cls.unique_id() if rank == 0 else None]
         if size > 1:
             dist.broadcast_object_list(obj, src=0)
@@ -312,10 +367,10 @@ class Dccrg:
             check(rc)
         tot = n.value
         ids = np.empty(max(tot, 1), np.uint64)
-        aux = np.empty(max(3 * tot, 1), np.int32) if k in (0, 2) else None
+        aux = np.empty(max(3 * tot, 1), np.int32) if k in (0, 2, 3) else None
         check(lib().dccrgx_download_csr(self.h, k, _ptr(ptr), _ptr(ids), _ptr(aux), tot, C.byref(n)))
         ids = ids[:tot]
-        if k == 0:
+        if k in (0, 3):
             aux = aux[: 3 * tot].reshape(tot, 3)
         elif k == 2:
             aux = aux[:tot]
@@ -393,17 +448,45 @@ class Dccrg:
         check(lib().dccrgx_balance_load(self.h))
         return self
 
-    def balance_load_to(self, ids, new_owners):
-        """Repartition to an explicit owner per leaf (every leaf, ascending id,
-        identical on all ranks); payloads migrate."""
-        ids = np.ascontiguousarray(ids, np.uint64)
-        own = np.ascontiguousarray(new_owners, np.int32)
+    def balance_load_to(self, cells, new_processes):
+        """Repartition with this rank's export list (local cells and their new
+        process, a partitioner's export list); collective, payloads migrate."""
+        ids = np.ascontiguousarray(cells, np.uint64)
+        own = np.ascontiguousarray(new_processes, np.int32)
         check(lib().dccrgx_balance_load_to(self.h, _ptr(ids), _ptr(own), ids.size))
         return self
 
+    # split form (initialize_balance_load 3746 / continue 3899 / finish 3942)
+    def initialize_balance_load(self, cells=(), new_processes=()):
+        ids = np.ascontiguousarray(cells, np.uint64)
+        own = np.ascontiguousarray(new_processes, np.int32)
+        check(lib().dccrgx_initialize_balance_load(self.h, _ptr(ids), _ptr(own), ids.size))
+
+    def continue_balance_load(self):
+        check(lib().dccrgx_continue_balance_load(self.h))
+
+    def finish_balance_load(self):
+        check(lib().dccrgx_finish_balance_load(self.h))
+
+    def migration_message_size(self, peer):
+        a, b = C.c_size_t(), C.c_size_t()
+        check(lib().dccrgx_migration_message_size(self.h, int(peer), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def migration_pack(self, peer):
+        n, _ = self.migration_message_size(peer)
+        buf = np.empty(max(n, 1), np.uint8)
+        check(lib().dccrgx_migration_pack(self.h, int(peer), _ptr(buf), n))
+        return buf[:n]
+
+    def migration_place(self, peer, data):
+        a = np.ascontiguousarray(data, np.uint8)
+        check(lib().dccrgx_migration_place(self.h, int(peer), _ptr(a), a.size))
+
     def get_cell_process(self):
-        """(ids, owners) of every leaf of the grid, ascending id
-        (get_cell_process, dccrg.hpp:6848)."""
+        """(ids, owners) of the leaves this rank knows - its own and its ghost
+        leaves - ascending id (get_cell_process, dccrg.hpp:6848, lists every
+        leaf of the grid)."""
         n = C.c_size_t()
         check(lib().dccrgx_get_cell_process(self.h, None, None, 0, C.byref(n)))
         ids = np.empty(n.value, np.uint64)
@@ -456,6 +539,22 @@ class Dccrg:
     def wait_remote_neighbor_copy_updates(self):
         check(lib().dccrgx_wait_remote_neighbor_copy_updates(self.h))
         return True
+
+    # explicit halo transport: the wire message of one peer
+    def halo_message_size(self, peer, hood=DEFAULT_HOOD):
+        a, b = C.c_size_t(), C.c_size_t()
+        check(lib().dccrgx_halo_message_size(self.h, int(hood), int(peer), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def halo_pack(self, peer, hood=DEFAULT_HOOD):
+        n, _ = self.halo_message_size(peer, hood)
+        buf = np.empty(max(n, 1), np.uint8)
+        check(lib().dccrgx_halo_pack(self.h, int(hood), int(peer), _ptr(buf), n))
+        return buf[:n]
+
+    def halo_place(self, peer, data, hood=DEFAULT_HOOD):
+        a = np.ascontiguousarray(data, np.uint8)
+        check(lib().dccrgx_halo_place(self.h, int(hood), int(peer), _ptr(a), a.size))
 
     # ---- built-in sweeps ------------------------------------------------------------
     def gol_step(self, state: Field, region="all"):

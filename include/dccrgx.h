@@ -15,6 +15,11 @@
  *     [.., n_slots)             remote cells that only have local cells as
  *                               neighbors_to (no payload is ever received)
  *
+ * State per rank is the rank's own leaves plus the "ghost" leaves around
+ * them (within max(neighborhood length, 1) level-0 cells), never the whole
+ * grid: the reference's global cell_process map (dccrg.hpp:7197) has no
+ * counterpart.
+ *
  * Every entry point returns 0 on success and a negative code on failure;
  * dccrgx_last_error() then describes the failure.  Every function cites the
  * reference interface (lkotipal/dccrg @ 2024-10-24, dccrg.hpp unless noted)
@@ -31,6 +36,8 @@ extern "C" {
 #endif
 
 typedef struct dccrgx_grid dccrgx_grid;
+
+#define DCCRGX_ABI_VERSION 2 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -61,6 +68,19 @@ int dccrgx_abi_version(void);
 int dccrgx_get_unique_id(void* out_128_bytes);
 int dccrgx_create(int rank, int size, int device, const void* nccl_id, dccrgx_grid** out);
 int dccrgx_destroy(dccrgx_grid* g);
+
+/* A host transport instead of RCCL (ranks sharing one GPU, MPI programs,
+ * tests): one grouped point-to-point exchange with every rank - send
+ * send_bytes[p] bytes from send[p] to rank p and receive recv_bytes[p] bytes
+ * from rank p into recv[p] (entries of 0 bytes and the own rank post
+ * nothing; all buffers are host memory).  Every rank calls it the same number
+ * of times in the same order, as MPI point-to-point calls in the reference
+ * (start_user_data_transfers 10564-10997).  Returns 0 on success.  The
+ * library builds its collectives (All_Gather, Allreduce) and the halo and
+ * migration payload transfers on it. */
+typedef int (*dccrgx_exchange_fn)(void* ctx, const void* const* send, const size_t* send_bytes, void* const* recv,
+                                  const size_t* recv_bytes);
+int dccrgx_create_with_exchange(int rank, int size, int device, dccrgx_exchange_fn fn, void* ctx, dccrgx_grid** out);
 
 /* ---- setup, before initialize (dccrg.hpp:8120-8230) ---------------------- */
 int dccrgx_set_initial_length(dccrgx_grid* g, const uint64_t length[3]);   /* 8120 */
@@ -97,7 +117,9 @@ int dccrgx_get_neighbors_of(dccrgx_grid* g, uint64_t cell, uint64_t* ids, int32_
 int dccrgx_get_slot_ids(dccrgx_grid* g, uint64_t* out, size_t cap, size_t* n);
 /* bulk download of a local CSR in slot order (rows = local slots):
  * kind 0 neighbors_of (aux = x,y,z offsets), 1 neighbors_to, 2 face
- * neighbors (aux = direction), 3 iterator cell.neighbors_of (ids only).
+ * neighbors (aux = direction), 3 iterator cell.neighbors_of (update_cell_
+ * pointers 11451-11500: only-of then both, each in (id, offset) order; aux
+ * = x,y,z offsets).
  * ptr has n_local + 1 entries; *n = number of entries. */
 int dccrgx_download_csr(dccrgx_grid* g, int kind, uint32_t* ptr, uint64_t* ids, int32_t* aux, size_t cap, size_t* n);
 /* get_neighbors_to 883 (ascending id, offsets 0) */
@@ -114,9 +136,9 @@ int64_t dccrgx_get_slot(dccrgx_grid* g, uint64_t cell);
 int dccrgx_get_peers(dccrgx_grid* g, int32_t* peers, size_t cap, size_t* n);
 int dccrgx_get_cells_to_send(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
 int dccrgx_get_cells_to_receive(dccrgx_grid* g, int peer, uint64_t* ids, size_t cap, size_t* n);
-/* every leaf of the grid with its process, ascending id (the global
- * cell_process map the reference keeps on every rank, get_cell_process
- * 6848); ids == NULL: *n = count only */
+/* the leaves this rank knows with their processes, ascending id: its own
+ * and its ghost leaves (the reference's get_cell_process 6848 returns every
+ * leaf of the grid); ids == NULL: *n = count only */
 int dccrgx_get_cell_process(dccrgx_grid* g, uint64_t* ids, int32_t* owners, size_t cap, size_t* n);
 
 /* get_number_of_update_send_cells / _receive_cells 5382-5490 */
@@ -130,9 +152,10 @@ int dccrgx_stop_refining(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t
 int dccrgx_get_new_cells(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t* n);
 
 /* Replace the whole leaf set and its partition (every rank passes the same
- * global list: ids strictly ascending, owners in [0, size)).  Stands in for
- * a mesh + partition handed over from outside (load_grid_data 1089-2425 /
- * an external partitioner); payloads of cells that stay local are kept. */
+ * global list: ids strictly ascending, owners in [0, size)); the rank keeps
+ * its own and its ghost leaves.  Setup path for a mesh + partition handed
+ * over from outside (as load_grid_data 1089-2425 reads every cell's record);
+ * payloads of cells that stay local are kept.  No communication. */
 int dccrgx_set_cells(dccrgx_grid* g, const uint64_t* ids, const int32_t* owners, size_t n);
 
 /* ---- user neighborhoods (add_neighborhood 6383-6520, remove_neighborhood
@@ -162,24 +185,38 @@ int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* g, int id);
 int dccrgx_save_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, const void* header, size_t header_bytes);
 int dccrgx_load_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, size_t header_bytes);
 
-/* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024) ------------
- * balance_load applies the pinned owners (no third-party partitioner:
- * Zoltan is out of scope), migrates every field of moved cells over RCCL and
- * rebuilds all neighbor structures on the device. */
+/* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024 and its
+ * split form initialize_balance_load 3746 / continue_balance_load 3899 /
+ * finish_balance_load 3942).  Collective.  The new owners are the pins plus
+ * an optional export list of this rank (local cells and their new process,
+ * what a partitioner's Zoltan_LB_Balance export list says, make_new_partition
+ * 8349-8581); pins win.  No third-party partitioner: without exports or pins
+ * nothing moves (the reference with Zoltan's "NONE").  continue moves the
+ * payloads of every field (RCCL or the host exchange); finish rebuilds every
+ * structure on the device, fetching the new ghost leaves from their owners,
+ * and places the arrived payloads. */
 int dccrgx_pin(dccrgx_grid* g, uint64_t cell, int process);
 int dccrgx_unpin(dccrgx_grid* g, uint64_t cell);
 int dccrgx_balance_load(dccrgx_grid* g);
-/* balance_load to an explicit partition (SURVEY §8(b) balance_load(new_owner);
- * stands in for a partitioner's import/export lists, make_new_partition
- * 8349-8581): ids = every leaf of the grid ascending (as get_all_leaves),
- * new_owner[i] its process; identical arguments on every rank.  Payloads of
- * all fields migrate (continue_balance_load 3899-3934). */
-int dccrgx_balance_load_to(dccrgx_grid* g, const uint64_t* ids, const int32_t* new_owner, size_t n);
+int dccrgx_balance_load_to(dccrgx_grid* g, const uint64_t* cells, const int32_t* new_process, size_t n);
+int dccrgx_initialize_balance_load(dccrgx_grid* g, const uint64_t* cells, const int32_t* new_process, size_t n);
+int dccrgx_continue_balance_load(dccrgx_grid* g);
+int dccrgx_finish_balance_load(dccrgx_grid* g);
+/* Explicit migration transport (instead of continue_balance_load): the
+ * message to / from `peer` = for every field in field order, the payload of
+ * each moving cell in ascending id.  pack after initialize, place before
+ * finish; *_size gives both byte counts. */
+int dccrgx_migration_message_size(dccrgx_grid* g, int peer, size_t* send_bytes, size_t* recv_bytes);
+int dccrgx_migration_pack(dccrgx_grid* g, int peer, void* buf, size_t cap);
+int dccrgx_migration_place(dccrgx_grid* g, int peer, const void* buf, size_t bytes);
 
 /* ---- fields (replaces Cell_Data + get_mpi_datatype, dccrg_get_cell_datatype.hpp:40-340)
  * transfer != 0: the field is part of update_copies_of_remote_neighbors. */
 int dccrgx_add_field(dccrgx_grid* g, const char* name, size_t elem_bytes, int transfer, int* field_id);
 int dccrgx_set_field_transfer(dccrgx_grid* g, int field_id, int transfer);
+/* the bytes of each element the halo carries: [offset, offset + bytes) (what
+ * Cell_Data::get_mpi_datatype describes; default: the whole element) */
+int dccrgx_set_field_window(dccrgx_grid* g, int field_id, size_t offset, size_t bytes);
 int dccrgx_field_device_ptr(dccrgx_grid* g, int field_id, void** ptr);
 /* host <-> device copies of whole slot ranges [slot0, slot0+n) */
 int dccrgx_field_upload(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const void* host);
@@ -192,6 +229,15 @@ int dccrgx_start_remote_neighbor_copy_updates(dccrgx_grid* g);
 int dccrgx_wait_remote_neighbor_copy_update_receives(dccrgx_grid* g);
 int dccrgx_wait_remote_neighbor_copy_update_sends(dccrgx_grid* g);
 int dccrgx_wait_remote_neighbor_copy_updates(dccrgx_grid* g);
+/* Explicit halo transport of one neighborhood (DCCRGX_DEFAULT_HOOD or a user
+ * id): the message to / from `peer` = for every transferred field in field
+ * order, the window bytes of each cell of cells_to_send / cells_to_receive
+ * in ascending id (the wire order of start_user_data_sends / _receives
+ * 10587-10997).  pack gathers from the device fields into a host buffer,
+ * place scatters a received message into the halo copies. */
+int dccrgx_halo_message_size(dccrgx_grid* g, int hood_id, int peer, size_t* send_bytes, size_t* recv_bytes);
+int dccrgx_halo_pack(dccrgx_grid* g, int hood_id, int peer, void* buf, size_t cap);
+int dccrgx_halo_place(dccrgx_grid* g, int hood_id, int peer, const void* buf, size_t bytes);
 
 /* ---- built-in sweeps (user stencils of tests/ and examples/) ------------- */
 /* game of life over cell.neighbors_of (examples/game_of_life.cpp:54-79,

@@ -65,7 +65,7 @@ def compare_neighbors(g, o, check_iterator=True):
     ptr, ids, offs = g.csr("of")
     tptr, tids, _ = g.csr("to")
     fptr, fids, fdirs = g.csr("face")
-    iptr, iids, _ = g.csr("iterator") if check_iterator else (None, None, None)
+    iptr, iids, ioffs = g.csr("iterator") if check_iterator else (None, None, None)
     for s in range(nl):
         c = int(slots[s])
         eid, eoff = o.neighbors_of(c)
@@ -79,6 +79,9 @@ def compare_neighbors(g, o, check_iterator=True):
         assert np.array_equal(fids[fptr[s]:fptr[s + 1]], fid), (c, fids[fptr[s]:fptr[s + 1]], fid)
         assert np.array_equal(fdirs[fptr[s]:fptr[s + 1]], fd), c
         if check_iterator:
-            iid, _ = o.iterator_neighbors_of(c)
-            assert sorted(iids[iptr[s]:iptr[s + 1]].tolist()) == sorted(iid.tolist()), c
+            # update_cell_pointers 11451-11500: only-of, then both, each in
+            # (id, offset) order - the exact sequence with offsets
+            iid, ioff = o.iterator_neighbors_of(c)
+            assert np.array_equal(iids[iptr[s]:iptr[s + 1]], iid), (c, iids[iptr[s]:iptr[s + 1]], iid)
+            assert np.array_equal(ioffs[iptr[s]:iptr[s + 1]], ioff), c
     return nl

@@ -23,7 +23,7 @@ def test_facade_example_builds(tmp_path):
 
 def test_c_header_is_plain_c(tmp_path):
     src = tmp_path / "t.c"
-    src.write_text('#include "dccrgx.h"\nint main(void){ return dccrgx_abi_version() == 1 ? 0 : 1; }\n')
+    src.write_text('#include "dccrgx.h"\nint main(void){ return dccrgx_abi_version() == DCCRGX_ABI_VERSION ? 0 : 1; }\n')
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
                         "-L", os.path.join(ROOT, "dccrg_amd"), "-ldccrgx",
                         f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}", "-o", str(tmp_path / "t")],

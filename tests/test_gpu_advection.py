@@ -112,41 +112,88 @@ def test_inner_outer_split_equals_all(gpu):
     g.close()
 
 
-def _variant_rho(base=(64, 64, 16), R=2, steps=10):
-    """Density after `steps` sweeps of the large refined case (regular and
-    general tiles both present) under the current DCCRGX_ADV_* schedule."""
+def _run_parity_grid(base=(32, 32, 8), R=2, steps=100):
     g, f = gpu_grid(base, R)
     prerefine(g, f, R)
+    lay = g.advection_layout()
     dt = g.advection_max_time_step(f)
+    ids = g.slot_ids()[: g.n_local]
     for _ in range(steps):
         g.advection_step(f, 0.5 * dt)
         g.advection_commit(f[0])
-    rho = f[0].get(0, g.n_local)
+    return g, f, lay, dt, ids
+
+
+def test_parity_grid_exercises_both_tile_kernels(gpu):
+    """SURVEY §8(d)'s oracle parity grid (32 x 32 x 8 base, R = 2, periodic
+    x and y, 100 steps): the layout must contain regular tiles (swept by
+    advection_regular_pp_kernel without face rows) and general tiles
+    (advection_tiles_pp_kernel), and every cell must match the oracle within
+    1e-12 x max|rho| - so both kernels are checked against the oracle."""
+    base, R, steps = (32, 32, 8), 2, 100
+    g, f, lay, dt, ids = _run_parity_grid(base, R, steps)
+    assert lay["regular_tiles"] > 0, lay
+    assert lay["tiles"] > lay["regular_tiles"], lay
+    assert lay["finer_faces"] > 0, lay
+    o = O.Grid(base, R, (True, True, False), 0, 1)
+    o.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
+    o.adv_prerefine(0.025, 0.25)
+    oi, _ = o.cells()
+    assert np.array_equal(np.sort(ids), oi)
+    assert dt == o.adv_max_time_step()
+    o.adv_initialize()
+    o.adv_steps(steps, 0.5 * dt)
+    exp = o.adv_get(ids)[:, 0]
+    got = f[0].get(0, ids.size)
+    scale = np.max(np.abs(exp))
+    assert np.max(np.abs(got - exp)) <= TOL * scale
+    # the cells the regular kernel swept are among those checked: a regular
+    # tile is 512 consecutive slots of one level-R box
+    assert lay["regular_cells"] == 512 * lay["regular_tiles"] and lay["regular_cells"] < ids.size
     g.close()
-    return rho
 
 
-@pytest.mark.parametrize("env", ["DCCRGX_ADV_DEPTH=2", "DCCRGX_ADV_DYN=1", "DCCRGX_ADV_DYN=1 DCCRGX_ADV_2S=1"])
-def test_schedule_variants_bitwise(gpu, tmp_path, env):
-    """The A/B schedules of the persistent tile sweeps (two tiles of loads in
-    flight instead of one, per-XCD tile tickets, the general sweep on a second
-    stream) change only which block sweeps which tile and when: every cell's
-    result is bitwise the default's.  The knobs are read once per process, so
-    the variant runs in a child process."""
-    import os
-    import subprocess
-    import sys
+def test_parity_grid_four_rank_slabs_bitwise(gpu):
+    """The parity grid, 16 level-0 cells deep, split into 4 z-slabs (block
+    partition of the level-0 cells, children inherit, execute_refines
+    10228-10237) on detached views, the density halo moved by the library's
+    pack / place: every cell bitwise equals the one-rank run after 30 steps;
+    the ranks' inner runs contain regular tiles."""
+    from test_gpu_multirank import emulated_exchange
 
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = tmp_path / "rho.npy"
-    code = ("import sys, numpy as np, torch; sys.path[:0] = [%r, %r]; "
-            "from test_gpu_advection import _variant_rho; np.save(%r, _variant_rho())"
-            % (root, os.path.join(root, "tests"), str(out)))
-    child_env = dict(os.environ)
-    for kv in env.split():
-        k, v = kv.split("=")
-        child_env[k] = v
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=child_env, capture_output=True, text=True,
-                       timeout=100)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert np.array_equal(np.load(str(out)), _variant_rho())
+    base, R, P, steps = (32, 32, 16), 2, 4, 30
+    ref, rf, lay, dt, ids = _run_parity_grid(base, R, 0)
+    leaves = np.sort(ids)
+    n0 = int(np.prod(base))
+    plane = base[0] * base[1]
+    l0p = np.array([ref.get_cell_from_indices(ref.get_indices(int(c)), 0) for c in leaves], np.int64)
+    owners = ((l0p - 1) // plane // (base[2] // P)).astype(np.int32)
+    assert np.array_equal(owners, ((l0p - 1) * P // n0).astype(np.int32))
+    gs, n_regular = [], 0
+    for r in range(P):
+        g = dccrg_amd.Dccrg(r, P, 0).set_initial_length(base).set_neighborhood_length(0)
+        g.set_maximum_refinement_level(R).set_periodic(True, True, False).initialize()
+        g.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
+        for n in NAMES:
+            g.add_field(n, np.float64, n == "density")
+        g.set_cells(leaves, owners)
+        g.advection_initialize([g.fields[n] for n in NAMES])
+        n_regular += g.advection_layout()["regular_tiles"]
+        gs.append(g)
+    assert n_regular > 0
+    for _ in range(steps):
+        emulated_exchange(gs, ["density"])
+        for g in gs:
+            f = [g.fields[n] for n in NAMES]
+            g.advection_step(f, 0.5 * dt, "inner")
+            g.advection_step(f, 0.5 * dt, "outer")
+            g.advection_commit(f[0])
+        ref.advection_step(rf, 0.5 * dt)
+        ref.advection_commit(rf[0])
+    final = dict(zip(ref.slot_ids()[: ref.n_local].tolist(), rf[0].get(0, ref.n_local).tolist()))
+    for g in gs:
+        assert g.counts["outer"] > 0
+        sl = g.slot_ids()[: g.n_local]
+        assert np.array_equal(g.fields["density"].get(0, g.n_local), np.array([final[int(c)] for c in sl]))
+    for g in gs + [ref]:
+        g.close()

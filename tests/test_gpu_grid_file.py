@@ -2,8 +2,8 @@
 load_grid_data 1742-2425, layout 1104-1120): the product's file is byte for
 byte the oracle's restatement of the layout, whose grid block is pinned to
 the reference's own writers (tests/golden/grid_file_ref.json); loading
-restores the mesh, geometry and transferred payloads; per-rank writes from
-detached views assemble the multi-rank file, which loads on one rank."""
+restores the mesh, geometry and transferred payloads; files from three real
+ranks: test_gpu_transport.py::test_save_grid_data_three_ranks."""
 import os
 
 import numpy as np
@@ -12,7 +12,6 @@ import pytest
 import dccrg_amd
 from helpers import make_pair
 from oracle import oracle as O
-from test_gpu_multirank import views
 
 pytestmark = pytest.mark.gpu
 
@@ -74,34 +73,6 @@ def test_file_bytes_and_round_trip(gpu, tmp_path, length, R, periodic, hood, rou
     h.close()
 
 
-def test_multi_rank_file_from_detached_views(gpu, tmp_path):
-    length, R, periodic, hood, P = (6, 6, 4), 2, (True, True, False), 1, 3
-    gs, o = views(length, R, periodic, hood, P, 2, 0.15, 6)
-    path = tmp_path / "grid3.dc"
-    by_rank = []
-    for g in gs:
-        g.set_geometry(*GEOM)
-        fill(g, 2)
-        by_rank.append(g.local_cells())
-    for g in gs:
-        g.save_grid_data(path)
-    got = open(path, "rb").read()
-    block = O.grid_block_bytes(length, R, hood, periodic, *GEOM)
-    assert got == O.grid_file_bytes(block, b"", 0, by_rank, lambda c: payload(c, 2))
-    # the 3-rank file loads on one rank, payloads by id
-    h = dccrg_amd.Dccrg(0, 1, 0)
-    a = h.add_field("a", np.uint32)
-    b = h.add_field("b", np.float64)
-    h.load_grid_data(path)
-    allc = np.sort(np.concatenate(by_rank))
-    assert np.array_equal(h.local_cells(), allc)
-    ids = h.slot_ids()[: h.n_local]
-    assert np.array_equal(a.get(0, h.n_local), (ids * np.uint64(2654435761) + np.uint64(2)).astype(np.uint32))
-    assert np.array_equal(b.get(0, h.n_local), np.sin(ids.astype(np.float64) * 0.37 + 2))
-    for g in gs + [h]:
-        g.close()
-
-
 def test_load_rejects_bad_files(gpu, tmp_path):
     p = tmp_path / "bad.dc"
     p.write_bytes(b"\0" * 256)
@@ -113,3 +84,14 @@ def test_load_rejects_bad_files(gpu, tmp_path):
     with pytest.raises(dccrg_amd.DccrgError, match="cannot open"):
         h.load_grid_data(os.path.join(str(tmp_path), "missing.dc"))
     h.close()
+    # a grid block the setters would refuse (the neighborhood
+    # length, refinement level and lengths of a file are validated)
+    import struct
+
+    for hood, R, length in ((99, 0, (4, 4, 4)), (1, 60, (4, 4, 4)), (1, 0, (0, 4, 4))):
+        block = O.grid_block_bytes(length, R, hood, (False, False, False), (0, 0, 0), (1, 1, 1))
+        p.write_bytes(struct.pack("<Q", 0x1234567890ABCDEF) + block + struct.pack("<Q", 0))
+        h = dccrg_amd.Dccrg(0, 1, 0)
+        with pytest.raises(dccrg_amd.DccrgError, match="grid file"):
+            h.load_grid_data(p)
+        h.close()

@@ -45,21 +45,23 @@ def test_rank_views_match_oracle(gpu, length, R, periodic, hood, P, rounds):
         g.close()
 
 
-def emulated_exchange(gs, fields):
-    """The wire protocol of update_copies_of_remote_neighbors: per peer, the
-    payloads of cells_to_send in ascending id order land in the receiver's
-    halo slots of that peer (same order)."""
+def emulated_exchange(gs, fields=None):
+    """update_copies_of_remote_neighbors between detached views of one
+    process: the library packs each peer's wire message (transferred fields,
+    cells_to_send in ascending id, start_user_data_sends 10802-10997) and
+    the receiver's library places it into its halo copies.  `fields`, when
+    given, must be exactly the transferred fields (checked)."""
+    for g in gs:
+        if fields is not None:
+            assert sorted(n for n, f in g.fields.items() if f.transfer) == sorted(fields)
+    msgs = {}
     for r, g in enumerate(gs):
         for p in g.get_peers():
-            send = g.get_cells_to_send(p)
-            if send.size == 0:
-                continue
-            src_slots = np.array([g.get_slot(int(c)) for c in send])
-            dst_slots = np.array([gs[p].get_slot(int(c)) for c in send])
-            assert np.all(np.diff(dst_slots) == 1)  # contiguous halo block per peer
-            for name in fields:
-                vals = g.fields[name].get()[src_slots]
-                gs[p].fields[name].set(vals, slot0=int(dst_slots[0]))
+            sb, rb = g.halo_message_size(p)
+            assert (sb, rb) == tuple(reversed(gs[p].halo_message_size(r)))  # both ends agree on the sizes
+            msgs[(r, p)] = g.halo_pack(p)
+    for (r, p), m in msgs.items():
+        gs[p].halo_place(r, m)
 
 
 def test_multirank_gol_equals_single_rank(gpu):
@@ -134,5 +136,42 @@ def test_multirank_advection_equals_single_rank(gpu):
         exp = np.array([final[int(c)] for c in sl])
         # identical face sets and operand order: bitwise equal
         assert np.array_equal(got, exp)
+    for g in gs + [ref]:
+        g.close()
+
+
+@pytest.mark.parametrize("length,periodic,P", [((256, 6, 9), (True, False, True), 3),
+                                               ((256, 4, 12), (False, True, False), 4),
+                                               ((512, 3, 8), (True, True, True), 2)])
+def test_slab_gol_structured_equals_single_rank(gpu, length, periodic, P):
+    """z-slab partitions of a uniform grid whose x length is a multiple of 256
+    run the structured 26-point kernel per plane box (inner planes, then each
+    outer plane with its halo plane as z-1 / z+1, gol_slab_plan): bit-exact
+    against the one-rank game."""
+    steps = 5
+    gs, _ = views(length, 0, periodic, 1, P)
+    ref, _ = make_pair(length, 0, periodic, 1)
+    rng = np.random.default_rng(11)
+    ids_all = ref.slot_ids()
+    a0 = (rng.random(ids_all.size) < 0.3).astype(np.uint32)
+    val = dict(zip(ids_all.tolist(), a0.tolist()))
+    rs = ref.add_field("is_alive", np.uint32)
+    rs.set(a0)
+    for g in gs:
+        st = g.add_field("is_alive", np.uint32)
+        st.set(np.array([val[int(c)] for c in g.slot_ids()[: g.n_local]], np.uint32))
+        assert g.n_local % (length[0] * length[1]) == 0
+    for _ in range(steps):
+        emulated_exchange(gs, ["is_alive"])
+        for g in gs:
+            g.gol_step(g.fields["is_alive"], "inner")
+            g.gol_step(g.fields["is_alive"], "outer")
+            g.gol_commit(g.fields["is_alive"])
+        ref.gol_step(rs)
+        ref.gol_commit(rs)
+    final = dict(zip(ids_all.tolist(), rs.get().tolist()))
+    for g in gs:
+        sl = g.slot_ids()[: g.n_local]
+        assert np.array_equal(g.fields["is_alive"].get(0, g.n_local), np.array([final[int(c)] for c in sl]))
     for g in gs + [ref]:
         g.close()

@@ -1,8 +1,8 @@
-"""Benchmark: BASELINE.json metric — cell-updates/s (node) for 3-D advection
-with halo exchange, and the % of HBM roofline of the advection sweep kernel.
+"""Benchmark: BASELINE.json metric - cell-updates/s (node) for 3-D advection
+with halo exchange, and the % of HBM roofline of the advection sweep.
 
-Workload (BASELINE config 3, tests/advection): level-0 base 128 x 128 x
-(128 * N) with cubic cells of length 1/128, maximum refinement level 2
+Default workload (BASELINE config 3, tests/advection): level-0 base 128 x
+128 x (128 * N) with cubic cells of length 1/128, maximum refinement level 2
 (512^3-equivalent per GPU), neighborhood length 0 (face neighbors), periodic
 in x and y, non-periodic in z, the reference's initial condition (hump +
 rotating velocity, tests/advection/initialize.hpp) and its pre-refinement
@@ -12,11 +12,17 @@ the inner-cell sweep, then the outer-cell sweep, fused flux + apply.  Weak
 scaling: every GPU owns one 128^3-base slab (block partition of level-0 ids,
 children inherit the owner).
 
+Other lines (--workload): gol (config 2), gol_amr, poisson
+(config 4), scalability (config 5: 1024 x 1024 x 128 per GPU, halo exchange
+of 1-B and 4-B payloads, game of life on the 4-B state, one half-shift
+repartition).
+
     python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -27,6 +33,8 @@ sys.path.insert(0, ROOT)
 
 NAMES = ("density", "vx", "vy", "vz", "lx", "ly", "lz")
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction
+CPU_SHARE = 16         # host cores of one GPU's share on the bench box
 
 
 def parse():
@@ -37,68 +45,149 @@ def parse():
     p.add_argument("--base", type=int, default=128, help="level-0 cells per dimension per GPU")
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--workload", choices=["advection", "gol", "gol_amr", "poisson"], default="advection",
-                   help="advection = BASELINE metric (default); gol = config 2 game of life line; "
-                        "poisson = config 4 BiCG line")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--workload", choices=["advection", "gol", "gol_amr", "poisson", "scalability"],
+                   default="advection",
+                   help="advection = BASELINE metric (default); gol = config 2; gol_amr = SURVEY a14; "
+                        "poisson = config 4; scalability = config 5")
     return p.parse_args()
 
 
-def gol_main(a, dccrgx_mod, torch):
-    """BASELINE config 2: game of life 1024 x 1024 x 64, 26-point stencil,
-    uint32 state, 1 GPU (algorithmic 8 B per cell-update)."""
-    nx, ny, nz = 1024, 1024, 64
-    g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((nx, ny, nz)).set_neighborhood_length(1)
-    g.set_maximum_refinement_level(0).initialize()
-    st = g.add_field("is_alive", np.uint32)
-    ids = np.arange(1, nx * ny * nz + 1, dtype=np.uint64)
+# ---------------------------------------------------------------------------- CPU baseline
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(workload, seconds):
+    """The oracle (CPU restatement of the reference's loop, AoS + hashed
+    lookups) timed on the host: one process per core of this GPU's share
+    (the reference's one MPI rank per core), each on its own copy of a
+    bounded sample of the workload (oracle/cpu_bench.py); value = the sum of
+    their cell-updates/s."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(avail, CPU_SHARE))
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--workload", workload, "--seconds", str(seconds)]
+    procs = [subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for _ in range(cores)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=seconds * 10 + 120)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker failed: {e[-500:]}")
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    total = sum(r["cells"] * r["steps"] / r["seconds"] for r in outs)
+    per_core = [r["cells"] * r["steps"] / r["seconds"] for r in outs]
+    return dict(value=total, unit="cell-updates/s", cores=cores, kind="port",
+                sample=f"oracle restatement ({outs[0]['sample']}, {outs[0]['cells']} cells) x {cores} processes, "
+                       f"~{seconds:.0f} s each; per core {min(per_core):.3g}-{max(per_core):.3g} cell-updates/s",
+                nproc=os.cpu_count(), affinity=avail, cpu_model=cpu_model())
+
+
+def alive_rule(ids):
     z = (ids ^ np.uint64(0x5DEECE66D)) + np.uint64(0x9E3779B97F4A7C15)
     z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
     z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
     z = z ^ (z >> np.uint64(31))
-    st.set((z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32))
-    for _ in range(a.warmup):
-        g.gol_step(st)
-        g.gol_commit(st)
+    return (z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32)
+
+
+def line_base(metric, value, world, a, ms, dtype, data, config, scaling="weak"):
+    return {"metric": metric, "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+            "dtype": dtype, "data": data, "config": config}
+
+
+def reduce_stats(torch, dist, world, vals):
+    """(max over ranks, sum over ranks) of a list of floats."""
+    t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+    if world == 1:
+        return [float(x) for x in t], [float(x) for x in t]
+    mx, sm = t.clone(), t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return [float(x) for x in mx], [float(x) for x in sm]
+
+
+def timed(g, torch, dist, world, fn, steps):
     g.synchronize()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     g.kernel_timing(1)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        g.gol_step(st)
-        g.gol_commit(st)
+    for _ in range(steps):
+        fn()
     g.synchronize()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
     kms, kn = g.kernel_timing(0)
-    n = nx * ny * nz
+    return el, kms, kn
+
+
+# ---------------------------------------------------------------------------- game of life (config 2)
+def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
+    """BASELINE config 2: game of life 1024 x 1024 x 64 (x N, z slabs),
+    26-point stencil, uint32 state (algorithmic 8 B per cell-update)."""
+    nx, ny, nz = 1024, 1024, 64 * world
+    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g.set_initial_length((nx, ny, nz)).set_neighborhood_length(1).set_maximum_refinement_level(0).initialize()
+    st = g.add_field("is_alive", np.uint32)
+    st.set(alive_rule(g.slot_ids()[: g.n_local]))
+
+    def step():
+        g.start_remote_neighbor_copy_updates()
+        g.gol_step(st, "inner")
+        g.wait_remote_neighbor_copy_update_receives()
+        g.gol_step(st, "outer")
+        g.wait_remote_neighbor_copy_update_sends()
+        g.gol_commit(st)
+
+    for _ in range(a.warmup):
+        step()
+    el, kms, kn = timed(g, torch, dist, world, step, a.steps)
+    n = g.n_local
+    mx, sm = reduce_stats(torch, dist, world, [el, float(n), kms])
     ach = 8.0 * n * a.steps / (kms / 1e3) / 1e9
-    print(json.dumps({
-        "metric": "cell-updates/s, game of life 3D (BASELINE config 2)", "value": n * a.steps / el,
-        "unit": "cell-updates/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32", "data": "synthetic: seeded alive(id) rule, p=0.2",
-        "config": {"workload": "game of life 1024x1024x64, neighborhood 1, non-periodic (config 2)"},
-        "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
-                     "traffic": None, "kernel": "gol_structured_kernel", "alg_bytes_per_step": 8 * n,
-                     "kernel_ms_per_step": kms / a.steps},
-        "cpu_baseline": None if a.no_cpu_baseline else gol_cpu_baseline(a.cpu_seconds)}), flush=True)
+    if rank == 0:
+        line = line_base("cell-updates/s, game of life 3D (BASELINE config 2)", sm[1] * a.steps / mx[0], world, a,
+                         mx[0] / a.steps * 1e3, "u32", "synthetic: seeded alive(id) rule, p=0.2",
+                         {"workload": f"game of life {nx}x{ny}x{nz}, neighborhood 1, non-periodic (config 2"
+                                      f"{', z slabs' if world > 1 else ''})"})
+        line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS, "traffic": None, "kernel": "gol_structured_v3",
+                            "alg_bytes_per_step": 8 * n, "kernel_ms_per_step": kms / a.steps}
+        line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("gol", a.cpu_seconds)
+        print(json.dumps(line), flush=True)
     g.close()
 
 
-def gol_amr_main(a, dccrgx_mod, torch):
+# ---------------------------------------------------------------------------- refined game of life (a14)
+def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """the refined game emulating the level-0 game
     (tests/game_of_life/solve.hpp get_live_neighbors, as unrefined2d.cpp
     plays it) on a 2048 x 2048 x 1 level-0 grid, max refinement level 1, a
     seeded quarter of the level-0 cells refined (children inherit the state),
     p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
-    halo between them is a no-op).  Algorithmic bytes per leaf and step:
-    level-0 parent per slot decoded per phase (2 x (8 B id read + 8 B
-    written)); collect: own parent 8 B, row pointers 8 B, per neighbor entry
-    slot 4 B + parent 8 B + state 4 B, list 64 B written; spread: own parent
-    and id 16 B, row pointers 8 B, own list 64 B, and for a level-1 leaf per
-    neighbor entry slot 4 B + parent 8 B and its 7 siblings' lists 7 x 64 B,
-    state 4 B written."""
+    halo between them is a no-op).
+
+    Roofline bytes per leaf and step (SURVEY §8(d) CSR / AMR form): state
+    read + written (8 B), the neighbor CSR (4 B per neighbors_of entry + 4 B
+    row pointer) walked by each of the two phases, and the reference's 72-B
+    payload (Cell_Data::data, array<uint64_t, 9>) written by the collect and
+    read by the spread: 8 + 2 (4 k + 4) + 2 x 72.  The per-gather count
+    (every neighbor's parent and state, the siblings' lists) is reported
+    beside it as `logical_bytes_per_leaf`, not as HBM traffic."""
     n = 2048
     g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
     g.set_maximum_refinement_level(1).initialize()
@@ -114,74 +203,43 @@ def gol_amr_main(a, dccrgx_mod, torch):
     ls = g.add_field("gol_list", np.dtype((np.uint64, 8)))
     slots = g.slot_ids()[: g.n_local]
     lvl = (slots > np.uint64(n * n)).astype(np.int64)
-    # level-0 parent of a level-1 leaf (2 x 2 x 2 children per parent, x fastest)
     c1 = slots.astype(np.int64) - 1 - n * n
     x1, y1 = c1 % (2 * n), (c1 // (2 * n)) % (2 * n)
     par = np.where(lvl == 0, slots.astype(np.int64) - 1, (y1 // 2) * n + x1 // 2)
     st.set(live0[par].astype(np.uint32))
     for _ in range(a.warmup):
         g.get_live_neighbors(st, ls)
-    g.synchronize()
-    torch.cuda.synchronize()
-    g.kernel_timing(1)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        g.get_live_neighbors(st, ls)
-    g.synchronize()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    kms, kn = g.kernel_timing(0)
+    el, kms, kn = timed(g, torch, dist, 1, lambda: g.get_live_neighbors(st, ls), a.steps)
     nl = g.n_local
     kbar = g.neighbor_entries("of") / nl
-    f1 = float(np.mean(lvl == 1))  # fraction of level-1 leaves
-    per_cell = (2 * 16) + (8 + 8 + kbar * 16 + 64) + (16 + 8 + 64 + f1 * (kbar * 12 + 7 * 64) + 4)
+    f1 = float(np.mean(lvl == 1))
+    per_cell = 8 + 2 * (4 * kbar + 4) + 2 * 72
+    logical = (2 * 16) + (8 + 8 + kbar * 16 + 64) + (16 + 8 + 64 + f1 * (kbar * 12 + 7 * 64) + 4)
     ach = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
-    print(json.dumps({
-        "metric": "cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
-        "value": nl * a.steps / el, "unit": "cell-updates/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": el / a.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32/u64", "data": "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
-        "config": {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
-                   "leaves": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s},
-        "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
-                     "kernel": "gol_amr_collect_kernel + gol_amr_spread_kernel", "alg_bytes_per_cell": per_cell,
-                     "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps},
-        "cpu_baseline": None if a.no_cpu_baseline else gol_amr_cpu_baseline(a.cpu_seconds)}), flush=True)
+    line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
+                     nl * a.steps / el, 1, a, el / a.steps * 1e3, "u32/u64",
+                     "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
+                     {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
+                      "leaves": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
+    line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                        "kernel": "gol_amr_collect_kernel + gol_amr_spread_kernel", "alg_bytes_per_leaf": per_cell,
+                        "logical_bytes_per_leaf": logical,
+                        "logical_GB_per_s": logical * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None,
+                        "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}
+    line["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline("gol_amr", a.cpu_seconds)
+    print(json.dumps(line), flush=True)
     g.close()
 
 
-def gol_amr_cpu_baseline(seconds):
-    """The oracle's get_live_neighbors (one core) on a 128 x 128 x 1 sample of
-    the same workload."""
-    from oracle import oracle as O
-
-    n = 128
-    o = O.Grid((n, n, 1), 1, (False, False, False), 1, 1)
-    rng = np.random.default_rng(7)
-    ids0, _ = o.cells()
-    live0 = rng.random(n * n) < 0.3
-    for c in rng.choice(ids0, size=n * n // 4, replace=False):
-        o.refine_completely(int(c))
-    o.stop_refining()
-    ids, _ = o.cells()
-    par = o.mapping.batch(ids)["level0_parent"].astype(np.int64) - 1
-    o.gola_set(ids, live0[par].astype(np.uint32))
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.gola_steps(1)
-        steps += 1
-    el = time.perf_counter() - t0
-    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
-                sample=f"oracle restatement, 128x128x1 level-0, quarter refined ({ids.size} leaves), {steps} steps, "
-                       f"{el:.1f} s on 1 host core")
-
-
-def poisson_main(a, dccrgx_mod, torch, rank, world, uid):
+# ---------------------------------------------------------------------------- Poisson (config 4)
+def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """BASELINE config 4: Poisson BiCG (tests/poisson/poisson3d.cpp) on a
     128^3-base grid per GPU (cell lengths 2pi/128, pi/128, 8pi/128), periodic,
     refined twice around (pi, pi/2, 4pi); one step = one BiCG iteration over
-    every solve cell (min = max = steps iterations, as SURVEY §8(d))."""
+    every solve cell (min = max = steps iterations, as SURVEY §8(d)).  The
+    timed kernels of an iteration run from its first phase to its last, the
+    two global reductions included."""
     import math
 
     n = a.base
@@ -212,51 +270,118 @@ def poisson_main(a, dccrgx_mod, torch, rank, world, uid):
     setup_s = time.perf_counter() - t_setup
     sol.set(np.zeros(slots.size))
     solver = dccrgx_mod.Poisson_Solve(a.steps, a.steps)
-    g.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    g.kernel_timing(1)
-    t0 = time.perf_counter()
-    it, res = solver.solve(ids, g, cache_is_up_to_date=True)
-    g.synchronize()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    kms, kn = g.kernel_timing(0)
+    res = {}
+    el, kms, kn = timed(g, torch, dist, world, lambda: res.update(r=solver.solve(ids, g, cache_is_up_to_date=True)), 1)
+    it, resid = res["r"]
     n_solve = ids.size
-    stats = torch.tensor([el, float(n_solve), kms], dtype=torch.float64, device="cuda")
-    if world > 1:
-        import torch.distributed as dist
-        mx_ = stats.clone()
-        dist.all_reduce(mx_, op=dist.ReduceOp.MAX)
-        sm = stats.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        el, total = float(mx_[0]), int(sm[1])
-    else:
-        total = n_solve
-    # algorithmic bytes per solve cell and iteration: SURVEY §8(d) 3-phase
-    # minimum 272 B + the face table read by phases A and B (2 x 6 x int32)
-    per_cell = 272 + 48
+    mx, sm = reduce_stats(torch, dist, world, [el, float(n_solve), kms])
+    per_cell = 272 + 48  # SURVEY §8(d) 3-phase minimum + the face table read by phases A and B
     ach = per_cell * n_solve * it / (kms / 1e3) / 1e9 if kms > 0 else None
     if rank == 0:
-        print(json.dumps({
-            "metric": "cell-updates/s, Poisson BiCG iterations (BASELINE config 4)", "value": total * it / el,
-            "unit": "cell-updates/s", "n_gpus": world, "steps": it, "warmup": a.warmup,
-            "ms_per_step": el / it * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f64", "data": "synthetic: poisson3d.cpp rhs on its center-refined mesh",
-            "config": {"workload": f"poisson3d BiCG, base {n}x{n}x{n * world}, periodic, refined twice at the "
-                                   f"center, min = max = {a.steps} iterations",
-                       "solve_cells_rank0": n_solve, "setup_s": setup_s, "parallelism": f"domain decomposition x{world}"},
-            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
-                         "kernel": "po_phase_a + po_phase_b + po_phase_c", "alg_bytes_per_cell_iteration": per_cell,
-                         "kernel_ms_per_step": kms / it, "launches_per_step": kn / it, "residual_min": res},
-            "cpu_baseline": None if (a.no_cpu_baseline or world > 1) else poisson_cpu_baseline(a.cpu_seconds)}),
-            flush=True)
+        line = line_base("cell-updates/s, Poisson BiCG iterations (BASELINE config 4)", sm[1] * it / mx[0], world, a,
+                         mx[0] / it * 1e3, "f64", "synthetic: poisson3d.cpp rhs on its center-refined mesh",
+                         {"workload": f"poisson3d BiCG, base {n}x{n}x{n * world}, periodic, refined twice at the "
+                                      f"center, min = max = {a.steps} iterations",
+                          "solve_cells_rank0": n_solve, "setup_s": setup_s,
+                          "parallelism": f"domain decomposition x{world}"})
+        line["steps"] = it
+        line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                            "kernel": "po_phase_a + po_reduce + po_phase_b + po_reduce + po_phase_c",
+                            "alg_bytes_per_cell_iteration": per_cell, "kernel_ms_per_step": kms / it,
+                            "timed_intervals_per_step": kn / it, "residual_min": resid}
+        line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("poisson", a.cpu_seconds)
+        print(json.dumps(line), flush=True)
     g.close()
 
 
+# ---------------------------------------------------------------------------- scalability (config 5)
+def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
+    """BASELINE config 5 (tests/scalability/scalability.cpp): a uniform
+    1024 x 1024 x (128 N) grid, neighborhood 1, block partition (z slabs,
+    134 M cells per GPU).  One step = the reference's loop with its 'solve'
+    being the game of life on the 4-B payload: start the halo update, sweep
+    the inner cells, wait, sweep the outer cells.  Reported beside it: the
+    halo exchange alone for 1-B and 4-B payloads (the reference's data_size)
+    and one repartition from the block partition to the block partition
+    shifted by half a rank (every rank exports its first half to the
+    previous rank; at N = 1 nothing moves and the time is the rebuild)."""
+    nx, ny, nzr = 1024, 1024, 128
+    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g.set_initial_length((nx, ny, nzr * world)).set_neighborhood_length(1).set_maximum_refinement_level(0)
+    g.initialize()
+    st = g.add_field("is_alive", np.uint32)
+    b1 = g.add_field("data_1B", np.uint8, False)
+    st.set(alive_rule(g.slot_ids()[: g.n_local]))
+
+    def step():
+        g.start_remote_neighbor_copy_updates()
+        g.gol_step(st, "inner")
+        g.wait_remote_neighbor_copy_update_receives()
+        g.gol_step(st, "outer")
+        g.wait_remote_neighbor_copy_update_sends()
+        g.gol_commit(st)
+
+    for _ in range(a.warmup):
+        step()
+    el, kms, kn = timed(g, torch, dist, world, step, a.steps)
+    n = g.n_local
+
+    def halo_time(fields_on):
+        for f in (st, b1):
+            f.set_transfer(f in fields_on)
+        e, _, _ = timed(g, torch, dist, world, g.update_copies_of_remote_neighbors, a.steps)
+        return e / a.steps
+
+    h4 = halo_time([st])
+    h1 = halo_time([b1])
+    st.set_transfer(True)
+    b1.set_transfer(False)
+    n_send = g.get_number_of_update_send_cells()
+    peers = len(g.get_peers())
+    # one repartition: the first half of every rank's cells to the previous rank
+    loc = g.local_cells()
+    half = loc[: loc.size // 2]
+    dest = np.full(half.size, (rank - 1) % world, np.int32)
+    g.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g.balance_load_to(half, dest)
+    g.synchronize()
+    if world > 1:
+        dist.barrier()
+    rep = time.perf_counter() - t0
+    moved = int(half.size) if world > 1 else 0
+    mx, sm = reduce_stats(torch, dist, world, [el, float(n), kms, h4, h1, rep, float(n_send), float(moved)])
+    if rank == 0:
+        line = line_base("cell-updates/s, scalability (BASELINE config 5): game of life + halo on 134M cells/GPU",
+                         sm[1] * a.steps / mx[0], world, a, mx[0] / a.steps * 1e3, "u32",
+                         "synthetic: seeded alive(id) rule, p=0.2",
+                         {"workload": f"tests/scalability 1024x1024x{nzr * world} uniform, neighborhood 1, "
+                                      "block partition (z slabs), game of life on the 4-B payload",
+                          "cells_total": int(sm[1]), "parallelism": f"domain decomposition x{world}"})
+        ach = 8.0 * n * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
+        line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                            "kernel": "gol_structured_v3 (plane boxes)", "kernel_ms_per_step": kms / a.steps}
+        halo = {"ms_per_exchange_4B": mx[3] * 1e3, "ms_per_exchange_1B": mx[4] * 1e3,
+                "send_cells_max_rank": mx[6], "peers_rank0": peers}
+        if world > 1 and mx[3] > 0:
+            per_link = mx[6] * 4 / max(peers, 1) / mx[3] / 1e9
+            halo["xgmi_4B"] = {"achieved": per_link, "peak": XGMI_LINK_GBS, "unit": "GB/s per link per direction",
+                               "frac": per_link / XGMI_LINK_GBS}
+        line["halo"] = halo
+        line["repartition"] = {"seconds": mx[5], "cells_moved_total": sm[7],
+                               "what": "balance_load_to: first half of every rank's cells to the previous rank "
+                                       "(payload migration + distributed ghost refresh + full rebuild)"}
+        line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("scalability",
+                                                                                          a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    g.close()
+
+
+# ---------------------------------------------------------------------------- advection (config 3, headline)
 def build_grid(dccrg_amd, rank, size, base, R, uid):
     nx, ny, nz = base, base, base * size
     g = dccrg_amd.Dccrg(rank, size, int(os.environ.get("LOCAL_RANK", rank)), uid)
@@ -274,87 +399,110 @@ def build_grid(dccrg_amd, rank, size, base, R, uid):
     return g, f
 
 
-def poisson_cpu_baseline(seconds):
-    """The oracle's Poisson_Solve (one core) on a 32^3 sample of config 4
-    (same cell lengths, periodic, refined twice at the center, same rhs):
-    batches of 20 iterations (min = max) until ~`seconds`."""
-    import math
+def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
+    t_setup = time.perf_counter()
+    g, f = build_grid(dccrg_amd, rank, world, a.base, a.max_ref_lvl, uid)
+    setup_s = time.perf_counter() - t_setup
+    dt = 0.5 * g.advection_max_time_step(f)  # cfl 0.5 (2d.cpp:121-123)
+    c = g.counts
+    n_local = c["inner"] + c["outer"]
+    layout = g.advection_layout()
 
-    from oracle import oracle as O
+    def step():
+        g.start_remote_neighbor_copy_updates()
+        g.advection_step(f, dt, "inner")
+        g.wait_remote_neighbor_copy_update_receives()
+        g.advection_step(f, dt, "outer")
+        g.wait_remote_neighbor_copy_update_sends()
+        g.advection_commit(f[0])
 
-    n = 32
-    L0 = (2 * math.pi / n, math.pi / n, 8 * math.pi / n)
-    o = O.Grid((n, n, n), 2, (True, True, True), 0, 1)
-    o.set_geometry((0, 0, 0), L0)
-    for _ in range(2):  # poisson3d.cpp:174-192
-        ids, _ = o.cells()
-        c, L = o.geometry(ids)
-        mn, mx = c - L / 2, c + L / 2
-        sel = ((mn[:, 0] < 1.01 * math.pi) & (mx[:, 0] > 0.99 * math.pi) & (mn[:, 1] < 0.51 * math.pi)
-               & (mx[:, 1] > 0.49 * math.pi) & (mn[:, 2] < 4.01 * math.pi) & (mx[:, 2] > 3.99 * math.pi))
-        for cell in ids[sel]:
-            o.refine_completely(int(cell))
-        o.stop_refining()
-    ids, _ = o.cells()
-    c, _ = o.geometry(ids)
-    rhs = -(81.0 / 16.0) * np.sin(c[:, 0]) * np.cos(2 * c[:, 1]) * np.sin(c[:, 2] / 4)
-    its, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.po_set(ids, rhs, np.zeros(ids.size), np.zeros(ids.size, np.int32))
-        it, _ = o.po_solve(20, 20)
-        its += it
-    el = time.perf_counter() - t0
-    return dict(value=ids.size * its / el, unit="cell-updates/s", cores=1, kind="port",
-                sample=f"oracle restatement, 32^3 base refined twice at the center ({ids.size} cells), "
-                       f"{its} BiCG iterations incl. setup, {el:.1f} s on 1 host core")
+    for _ in range(a.warmup):
+        step()
+    el, kern_ms, kern_n = timed(g, torch, dist, world, step, a.steps)
 
+    # halo break-out (N > 1): the same exchange alone, K times back to back
+    # (pack + grouped RCCL send/recv of the density into the halo slots)
+    halo_el = 0.0
+    if world > 1:
+        halo_el, _, _ = timed(g, torch, dist, world, g.update_copies_of_remote_neighbors, a.steps)
+    n_send = g.get_number_of_update_send_cells()
+    n_peers = len(g.get_peers())
 
-def gol_cpu_baseline(seconds):
-    """The oracle's game of life (CPU restatement of the reference's loop over
-    cell.neighbors_of, one core) on a 64 x 64 x 16 sample of config 2 (same
-    26-point stencil, non-periodic, same alive(id) rule)."""
-    from oracle import oracle as O
+    # device neighbor build (SURVEY a5-a7: find_neighbors_of / _to for every
+    # local cell, initialize_neighbors): the full neighbors_of / neighbors_to /
+    # iterator CSR of the frozen mesh, built once here (the sweep itself uses
+    # the face tables); output bytes = 8 B id + 12 B offset + 4 B slot per
+    # neighbors_of entry, 8 B per neighbors_to entry, 4 B per iterator entry
+    g.synchronize()
+    tb = time.perf_counter()
+    n_of = g.neighbor_entries("of")
+    g.synchronize()
+    build_s = time.perf_counter() - tb
+    n_to = g.neighbor_entries("to")
+    n_it = g.neighbor_entries("iterator")
 
-    n = (64, 64, 16)
-    o = O.Grid(n, 0, (False, False, False), 1, 1)
-    ids, _ = o.cells()
-    z = (ids ^ np.uint64(0x5DEECE66D)) + np.uint64(0x9E3779B97F4A7C15)
-    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-    z = z ^ (z >> np.uint64(31))
-    o.gol_set(ids, (z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32))
-    o.gol_steps(1)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.gol_steps(1)
-        steps += 1
-    el = time.perf_counter() - t0
-    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
-                sample=f"oracle restatement, 64x64x16 game of life ({ids.size} cells), {steps} steps, "
-                       f"{el:.1f} s on 1 host core")
+    mx, sm = reduce_stats(torch, dist, world, [el, float(n_local), float(c["recv"]), kern_ms, halo_el, float(n_send)])
+    el_max, total_cells = mx[0], int(sm[1])
 
+    # algorithmic bytes of one sweep, as SURVEY §8(d) fixes them: per cell
+    # read density, vx, vy, vz, lx, ly, lz + write density = 64 B, plus the
+    # face structure as a CSR (4 B per face-neighbor entry + 4 B row pointer);
+    # the 64 B core alone is reported beside it
+    alg_core = layout["alg_bytes_core"]
+    alg_bytes_step = layout["alg_bytes"]
+    kern_s = kern_ms / 1e3
+    achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
 
-def cpu_baseline(seconds):
-    """The oracle (CPU restatement, one core) on a bounded sample of the same
-    workload: 32 x 32 x 4 base, R = 2, same pre-refinement, time steps until
-    ~`seconds` of CPU time."""
-    from oracle import oracle as O
+    # HBM bytes per step of the sweep kernels from the committed PMC passes
+    # (FETCH_SIZE x 2 + WRITE_SIZE, scripts/traffic.py); only valid for the
+    # same mesh, so it is dropped for any other cell count
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
+    if os.path.exists(tf) and world == 1:
+        try:
+            t = json.load(open(tf))
+            if t.get("cells") == n_local and t.get("alg_bytes_per_step") == alg_bytes_step:
+                traffic = t.get("hbm_bytes_per_step")
+        except (OSError, ValueError):
+            traffic = None
 
-    base = (32, 32, 4)
-    o = O.Grid(base, 2, (True, True, False), 0, 1)
-    o.set_geometry((0, 0, 0), (1 / 32, 1 / 32, 1 / 32))
-    o.adv_prerefine(0.025, 0.25)
-    ids, _ = o.cells()
-    dt = o.adv_max_time_step()
-    o.adv_steps(1, 0.5 * dt)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        o.adv_steps(5, 0.5 * dt)
-        steps += 5
-    el = time.perf_counter() - t0
-    return dict(value=ids.size * steps / el, unit="cell-updates/s", cores=1, kind="port",
-                sample=f"oracle restatement, 32x32x4 base R=2 pre-refined ({ids.size} cells), {steps} steps, "
-                       f"{el:.1f} s on 1 host core")
+    if rank == 0:
+        line = line_base("cell-updates/s (node) for 3D advection w/ halo exchange; % of HBM roofline",
+                         total_cells * a.steps / el_max, world, a, el_max / a.steps * 1e3, "f64",
+                         "synthetic: reference initial condition (tests/advection/initialize.hpp), pre-refined mesh",
+                         {"workload": "advection3d (BASELINE config 3): base 128x128x128 per GPU, max_ref_lvl 2, "
+                                      "face neighbors, periodic x,y, frozen mesh",
+                          "base": [a.base, a.base, a.base * world], "max_ref_lvl": a.max_ref_lvl,
+                          "cells_total": total_cells, "cells_rank0": n_local, "halo_cells_rank0": c["recv"],
+                          "partition": "block (level-0 z-slabs, children inherit)",
+                          "parallelism": f"domain decomposition x{world}", "setup_s": setup_s})
+        line["roofline"] = {
+            "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
+            "kernel": "advection_regular_pp_kernel + advection_tiles_pp_kernel", "layout": layout,
+            "alg_bytes_per_step": alg_bytes_step, "alg_bytes_core_per_step": alg_core,
+            "frac_core_64B": (alg_core * a.steps / kern_s / 1e9 / PEAK_HBM_GBS) if kern_s > 0 else None,
+            "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
+            "timed_intervals_per_step": kern_n / a.steps if a.steps else 0}
+        line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("advection", a.cpu_seconds)
+        line["neighbor_build"] = {
+            "what": "neighbors_of + neighbors_to + iterator CSR of all local cells (device kernels)",
+            "seconds": build_s, "cells_per_s": n_local / build_s if build_s > 0 else None,
+            "entries_of": n_of, "entries_to": n_to,
+            "output_GB_per_s": (24 * n_of + 8 * n_to + 4 * n_it) / build_s / 1e9 if build_s > 0 else None}
+        if world > 1:
+            # rank with the most halo traffic; xGMI: one link per peer pair,
+            # ~153 GB/s per link and direction
+            halo_ms = mx[4] / a.steps * 1e3
+            send_bytes = mx[5] * 8.0
+            per_link = send_bytes / max(n_peers, 1) / (halo_ms / 1e3) / 1e9 if halo_ms > 0 else None
+            line["halo"] = {
+                "ms_per_exchange": halo_ms, "frac_of_step": halo_ms / line["ms_per_step"],
+                "payload_bytes_per_cell": 8, "send_bytes_max_rank": send_bytes, "peers_rank0": n_peers,
+                "xgmi": {"achieved": per_link, "peak": XGMI_LINK_GBS, "unit": "GB/s per link per direction",
+                         "frac": per_link / XGMI_LINK_GBS if per_link else None}}
+        print(json.dumps(line), flush=True)
+    g.close()
 
 
 def main():
@@ -370,189 +518,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     import dccrg_amd
 
-    if a.workload == "gol":
-        return gol_main(a, dccrg_amd, torch)
-    if a.workload == "gol_amr":
-        return gol_amr_main(a, dccrg_amd, torch)
     uid = None
     if world > 1:
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
-    if a.workload == "poisson":
-        return poisson_main(a, dccrg_amd, torch, rank, world, uid)
-
-    t_setup = time.perf_counter()
-    g, f = build_grid(dccrg_amd, rank, world, a.base, a.max_ref_lvl, uid)
-    setup_s = time.perf_counter() - t_setup
-    dt = 0.5 * g.advection_max_time_step(f)  # cfl 0.5 (2d.cpp:121-123)
-    c = g.counts
-    n_local = c["inner"] + c["outer"]
-    variant = int(os.environ.get("DCCRGX_ADV_VARIANT", "11"))
-    layout = g.advection_layout()
-    n_fine = layout["finer_faces"]
-
-    def step():
-        g.start_remote_neighbor_copy_updates()
-        g.advection_step(f, dt, "inner")
-        g.wait_remote_neighbor_copy_update_receives()
-        g.advection_step(f, dt, "outer")
-        g.wait_remote_neighbor_copy_update_sends()
-        g.advection_commit(f[0])
-
-    for _ in range(a.warmup):
-        step()
-    g.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    g.kernel_timing(1)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    g.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    kern_ms, kern_n = g.kernel_timing(0)
-
-    # halo break-out (N > 1): the same exchange alone, K times back to back
-    # (pack + grouped RCCL send/recv of the density into the halo slots)
-    halo_el = 0.0
-    if world > 1:
-        g.synchronize()
-        dist.barrier()
-        th = time.perf_counter()
-        for _ in range(a.steps):
-            g.update_copies_of_remote_neighbors()
-        g.synchronize()
-        dist.barrier()
-        halo_el = time.perf_counter() - th
-    n_send = g.get_number_of_update_send_cells()
-    n_peers = len(g.get_peers())
-
-    # device neighbor build (SURVEY a5-a7: find_neighbors_of / _to for every
-    # local cell, initialize_neighbors): the full neighbors_of / neighbors_to /
-    # iterator CSR of the frozen mesh, built once here (the sweep itself
-    # uses the face tables); output bytes = 8 B id + 12 B offset + 4 B slot per
-    # neighbors_of entry, 8 B per neighbors_to entry, 4 B per iterator entry
-    g.synchronize()
-    tb = time.perf_counter()
-    n_of = g.neighbor_entries("of")
-    g.synchronize()
-    build_s = time.perf_counter() - tb
-    n_to = g.neighbor_entries("to")
-    n_it = g.neighbor_entries("iterator")
-
-    stats = torch.tensor([el, float(n_local), float(c["recv"]), kern_ms, halo_el, float(n_send)],
-                         dtype=torch.float64, device="cuda")
-    if world > 1:
-        mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = stats.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        el_max, total_cells = float(mx[0]), int(sm[1])
-    else:
-        el_max, total_cells = el, n_local
-
-    # algorithmic bytes of one sweep, as SURVEY §8(d) fixes them: per cell
-    # read density, vx, vy, vz, lx, ly, lz + write density = 64 B, plus the
-    # face structure as a CSR (4 B per face-neighbor entry + 4 B row pointer);
-    # the 64 B core alone is reported beside it
-    alg_core = layout["alg_bytes_core"]
-    alg_bytes_step = layout["alg_bytes"]
-    kern_s = kern_ms / 1e3
-    achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
-    launches_per_step = kern_n / a.steps if a.steps else 0
-
-    # HBM bytes per step of the sweep kernels from the committed PMC passes
-    # (FETCH_SIZE x 2 + WRITE_SIZE, summed over the regular-tile and the
-    # general tile kernel, scripts/traffic.py); only valid for the same mesh,
-    # so it is dropped for any other cell count
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
-    if os.path.exists(tf):
-        try:
-            t = json.load(open(tf))
-            if t.get("cells") == n_local and t.get("alg_bytes_per_step") == alg_bytes_step and world == 1:
-                traffic = t.get("hbm_bytes_per_step")
-        except (OSError, ValueError):
-            traffic = None
-
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.cpu_seconds)
-
-    if rank == 0:
-        value = total_cells * a.steps / el_max
-        line = {
-            "metric": "cell-updates/s (node) for 3D advection w/ halo exchange; % of HBM roofline",
-            "value": value,
-            "unit": "cell-updates/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": el_max / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: reference initial condition (tests/advection/initialize.hpp), pre-refined mesh",
-            "config": {
-                "workload": "advection3d (BASELINE config 3): base 128x128x128 per GPU, max_ref_lvl 2, "
-                            "face neighbors, periodic x,y, frozen mesh",
-                "base": [a.base, a.base, a.base * world],
-                "max_ref_lvl": a.max_ref_lvl,
-                "cells_total": total_cells,
-                "cells_rank0": n_local,
-                "halo_cells_rank0": c["recv"],
-                "partition": "block (level-0 z-slabs, children inherit)",
-                "parallelism": f"domain decomposition x{world}",
-                "setup_s": setup_s,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / PEAK_HBM_GBS) if achieved else None,
-                "traffic": traffic,
-                "kernel": "advection_regular_pp_kernel + advection_tiles_pp_kernel" if variant == 11
-                          else f"advection_kernel variant {variant}",
-                "layout": layout,
-                "alg_bytes_per_step": alg_bytes_step,
-                "alg_bytes_core_per_step": alg_core,
-                "frac_core_64B": (alg_core * a.steps / kern_s / 1e9 / PEAK_HBM_GBS) if kern_s > 0 else None,
-                "finer_faces": n_fine,
-                "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
-                "launches_per_step": launches_per_step,
-            },
-            "cpu_baseline": cpu,
-            "neighbor_build": {
-                "what": "neighbors_of + neighbors_to + iterator CSR of all local cells (device kernels)",
-                "seconds": build_s, "cells_per_s": n_local / build_s if build_s > 0 else None,
-                "entries_of": n_of, "entries_to": n_to,
-                "output_GB_per_s": (24 * n_of + 8 * n_to + 4 * n_it) / build_s / 1e9 if build_s > 0 else None,
-            },
-        }
-        if world > 1:
-            # rank with the most halo traffic; xGMI: one link per peer pair,
-            # ~153 GB/s per link and direction (BASELINE north star)
-            halo_ms = float(mx[4]) / a.steps * 1e3
-            send_bytes = float(mx[5]) * 8.0
-            per_link = send_bytes / max(n_peers, 1) / (halo_ms / 1e3) / 1e9 if halo_ms > 0 else None
-            line["halo"] = {
-                "ms_per_exchange": halo_ms,
-                "frac_of_step": halo_ms / line["ms_per_step"] if line["ms_per_step"] else None,
-                "payload_bytes_per_cell": 8,
-                "send_bytes_max_rank": send_bytes,
-                "peers_rank0": n_peers,
-                "xgmi": {"achieved": per_link, "peak": 153.0, "unit": "GB/s per link per direction",
-                         "frac": per_link / 153.0 if per_link else None},
-            }
-        print(json.dumps(line), flush=True)
-    g.close()
+    fn = {"advection": advection_main, "gol": gol_main, "gol_amr": gol_amr_main, "poisson": poisson_main,
+          "scalability": scalability_main}[a.workload]
+    fn(a, dccrg_amd, torch, dist, rank, world, uid)
     if world > 1:
         dist.destroy_process_group()
 

@@ -34,6 +34,10 @@ _SIGS = {
     "dccrgx_create": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, P(vp)]),
     "dccrgx_create_with_exchange": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, P(vp)]),
     "dccrgx_destroy": (C.c_int, [vp]),
+    "dccrgx_device_count": (C.c_int, [P(C.c_int)]),
+    "dccrgx_get_cells_by_criteria": (C.c_int, [vp, vp, sz, C.c_int, C.c_int, vp, sz, P(sz)]),
+    "dccrgx_get_slots": (C.c_int, [vp, vp, sz, vp]),
+    "dccrgx_download_user_csr": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, sz, P(sz)]),
     "dccrgx_set_initial_length": (C.c_int, [vp, P(u64)]),
     "dccrgx_set_maximum_refinement_level": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_maximum_refinement_level": (C.c_int, [vp, P(C.c_int)]),

@@ -589,6 +589,54 @@ int dccrgx_create_with_exchange(int rank, int size, int device, dccrgx_exchange_
 	});
 }
 
+int dccrgx_device_count(int* n) {
+	return guard([&] {
+		DX_REQUIRE(n, "null output");
+		HIP_CHECK(hipGetDeviceCount(n));
+		return 0;
+	});
+}
+
+int dccrgx_get_cells_by_criteria(dccrgx_grid* gp, const int32_t* criteria, size_t nc, int exact_match, int hood,
+                                 uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		DX_REQUIRE(criteria || !nc, "null criteria");
+		if (hood != DCCRGX_DEFAULT_HOOD && !g.uhoods.count(hood)) return copy_out_u64({}, out, cap, n);
+		return copy_out_u64(cells_by_criteria(g, criteria, nc, exact_match != 0, hood), out, cap, n);
+	});
+}
+
+int dccrgx_get_slots(dccrgx_grid* gp, const uint64_t* ids, size_t n, int64_t* slots) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE((ids && slots) || !n, "null argument");
+		for (size_t i = 0; i < n; i++) slots[i] = lookup_slot(g, ids[i]);
+		return 0;
+	});
+}
+
+int dccrgx_download_user_csr(dccrgx_grid* gp, int hood, int kind, uint32_t* ptr, uint64_t* ids, int32_t* offs,
+                             size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (!g.uhoods.count(hood)) return DCCRGX_ENOTFOUND;
+		DX_REQUIRE(kind == 0 || kind == 1, "invalid CSR kind");
+		UserHood& h = ensure_uhood(g, hood);
+		const size_t nl = g.n_local;
+		const std::vector<uint32_t> hp = download(kind == 0 ? h.nof_ptr.p : h.nto_ptr.p, nl + 1, g.s_comp);
+		const size_t tot = hp[nl];
+		if (n) *n = tot;
+		if (tot > cap) return DCCRGX_ERANGE;
+		std::memcpy(ptr, hp.data(), (nl + 1) * 4);
+		if (!tot) return 0;
+		HIP_CHECK(hipMemcpy(ids, kind == 0 ? h.nof_id.p : h.nto_id.p, tot * 8, hipMemcpyDeviceToHost));
+		if (offs && kind == 0) HIP_CHECK(hipMemcpy(offs, h.nof_off.p, tot * 12, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
 int dccrgx_destroy(dccrgx_grid* gp) {
 	return guard([&] {
 		if (!gp) return 0;
@@ -1143,7 +1191,6 @@ int dccrgx_balance_load(dccrgx_grid* gp) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
-		if (g.size == 1) return 0;
 		initialize_balance_load_impl(g, nullptr, nullptr, 0);
 		continue_balance_load_impl(g);
 		finish_balance_load_impl(g);
@@ -1156,10 +1203,6 @@ int dccrgx_balance_load_to(dccrgx_grid* gp, const uint64_t* cells, const int32_t
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
 		DX_REQUIRE((cells && procs) || !n, "null export list");
-		if (g.size == 1) {
-			for (size_t i = 0; i < n; i++) DX_REQUIRE(procs[i] == 0, "new process out of range");
-			return 0;
-		}
 		initialize_balance_load_impl(g, cells, procs, n);
 		continue_balance_load_impl(g);
 		finish_balance_load_impl(g);

@@ -31,6 +31,8 @@ void migration_message_size(Grid& g, int peer, size_t& sb, size_t& rb);
 void migration_pack_peer(Grid& g, int peer, uint8_t* buf, size_t cap);
 void migration_place_peer(Grid& g, int peer, const uint8_t* buf, size_t bytes);
 
+std::vector<uint64_t> cells_by_criteria(Grid& g, const int32_t* crit, size_t nc, bool exact, int hood);
+int64_t host_slot_of(Grid& g, uint64_t id);
 bool gol_slab_plan(Grid& g, std::vector<GolBox>& inner, std::vector<GolBox>& outer);
 
 }  // namespace dccrgx

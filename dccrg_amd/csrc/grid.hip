@@ -603,13 +603,24 @@ static int64_t plane_slot(Grid& g, int64_t z) {
 bool gol_slab_plan(Grid& g, std::vector<GolBox>& inner, std::vector<GolBox>& outer) {
 	inner.clear();
 	outer.clear();
-	if (!g.mesh.implicit || g.R != 0 || g.hood_len != 1 || g.len[0] % 256 != 0) return false;
+	if (g.R != 0 || g.hood_len != 1 || g.len[0] % 256 != 0) return false;
 	const uint64_t plane = g.len[0] * g.len[1];
-	uint64_t f, c;
-	g.mesh.bp.range(uint64_t(g.rank), f, c);
+	uint64_t f = 0, c = 0;
+	if (g.mesh.implicit) {
+		g.mesh.bp.range(uint64_t(g.rank), f, c);
+	} else {
+		// an explicit uniform mesh (e.g. after a repartition): the own cells
+		// must be one contiguous id range
+		const auto& sid = slot_ids_host(g);
+		if (!g.n_local) return false;
+		const auto mm = std::minmax_element(sid.begin(), sid.begin() + ptrdiff_t(g.n_local));
+		f = *mm.first;
+		c = g.n_local;
+		if (*mm.second - f + 1 != c) return false;
+	}
 	if (c == 0 || (f - 1) % plane != 0 || c % plane != 0) return false;
 	const int64_t z0 = int64_t((f - 1) / plane), z1 = z0 + int64_t(c / plane);
-	if (g.size == 1) {
+	if (g.size == 1 && g.n_outer == 0 && g.n_slots == g.n_local) {
 		inner.push_back(GolBox{0, uint64_t(z1 - z0), -3, -3});  // -3: the kernel's own periodic wrap
 		return true;
 	}
@@ -639,6 +650,69 @@ bool gol_slab_plan(Grid& g, std::vector<GolBox>& inner, std::vector<GolBox>& out
 	for (int64_t z = z0; z < z1; z++)
 		if (size_t(slot(z)) >= g.n_inner) outer.push_back(GolBox{uint64_t(slot(z)), 1, slot(z - 1), slot(z + 1)});
 	return true;
+}
+
+// --------------------------------------------------------------------------- get_cells(criteria)
+// is_neighbor_type_match (dccrg.hpp:2946-3053) for every local row of a CSR pair
+__global__ void neighbor_types_kernel(DevMesh M, int rank, const uint32_t* of_ptr, const uint64_t* of_id,
+                                      const uint32_t* to_ptr, const uint64_t* to_id, size_t n, int32_t* types) {
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < n; r += size_t(gridDim.x) * blockDim.x) {
+		int32_t t = 0;
+		for (uint32_t e = of_ptr[r]; e < of_ptr[r + 1]; e++) {
+			if (of_id[e] == error_cell) continue;
+			t |= dm_owner(M, of_id[e]) == rank ? 1 : 4;
+		}
+		for (uint32_t e = to_ptr[r]; e < to_ptr[r + 1]; e++) {
+			if (to_id[e] == error_cell) continue;
+			t |= dm_owner(M, to_id[e]) == rank ? 2 : 8;
+		}
+		types[r] = t;
+	}
+}
+
+std::vector<uint64_t> cells_by_criteria(Grid& g, const int32_t* crit, size_t nc, bool exact, int hood) {
+	const size_t nl = g.n_local;
+	const auto& sid = slot_ids_host(g);
+	std::vector<uint64_t> out;
+	if (nc == 0) {
+		out.assign(sid.begin(), sid.begin() + ptrdiff_t(nl));
+	} else {
+		const uint32_t *op, *tp;
+		const uint64_t *oi, *ti;
+		if (hood == DCCRGX_DEFAULT_HOOD) {
+			ensure_csr(g);
+			op = g.nof_ptr.p;
+			oi = g.nof_id.p;
+			tp = g.nto_ptr.p;
+			ti = g.nto_id.p;
+		} else {
+			UserHood& h = ensure_uhood(g, hood);
+			op = h.nof_ptr.p;
+			oi = h.nof_id.p;
+			tp = h.nto_ptr.p;
+			ti = h.nto_id.p;
+		}
+		DBuf<int32_t> t;
+		t.alloc(nl + 1);
+		if (nl) {
+			neighbor_types_kernel<<<grid_for(nl, 256), 256, 0, g.s_comp>>>(g.dm(), g.rank, op, oi, tp, ti, nl, t.p);
+			HIP_CHECK(hipGetLastError());
+		}
+		const std::vector<int32_t> ht = download(t.p, nl, g.s_comp);
+		int32_t merged = 0;
+		for (size_t k = 0; k < nc; k++) merged |= crit[k];
+		for (size_t r = 0; r < nl; r++) {
+			bool match = false;
+			if (exact) {
+				for (size_t k = 0; k < nc && !match; k++) match = ht[r] == crit[k];
+			} else {
+				match = (ht[r] & merged) != 0;
+			}
+			if (match) out.push_back(sid[r]);
+		}
+	}
+	std::sort(out.begin(), out.end());
+	return out;
 }
 
 }  // namespace dccrgx

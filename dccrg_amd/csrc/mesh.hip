@@ -501,7 +501,9 @@ void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_
 }
 
 // slot of a slotted id from the host index, -1 if it has no slot
-static int64_t host_slot(Grid& g, uint64_t id) {
+int64_t host_slot_of(Grid& g, uint64_t id);
+static int64_t host_slot(Grid& g, uint64_t id) { return host_slot_of(g, id); }
+int64_t host_slot_of(Grid& g, uint64_t id) {
 	if (!g.index_h_valid) {
 		k_sorted_slot_index(g.slot_ids.p, g.n_slots, g.index_ids_h, g.index_slots_h, g.s_comp);
 		g.index_h_valid = true;

@@ -18,6 +18,10 @@ REGION = {"all": 0, "inner": 1, "outer": 2}
 DEFAULT_HOOD = -0xDCC  # default_neighborhood_id (dccrg.hpp:93)
 CELLS = {"local": 0, "inner": 1, "outer": 2, "remote": 3, "all": 4}
 CSR_KIND = {"of": 0, "to": 1, "face": 2, "iterator": 3}
+# neighbor types of get_cells (dccrg.hpp:95-142)
+HAS_NO_NEIGHBOR, HAS_LOCAL_NEIGHBOR_OF, HAS_LOCAL_NEIGHBOR_TO = 0, 1, 2
+HAS_REMOTE_NEIGHBOR_OF, HAS_REMOTE_NEIGHBOR_TO = 4, 8
+HAS_LOCAL_NEIGHBOR_BOTH, HAS_REMOTE_NEIGHBOR_BOTH = 3, 12
 
 
 def _ptr(a):
@@ -247,9 +251,16 @@ class Dccrg:
         check(fn(self.h, *args, _ptr(out), out.size, C.byref(n)))
         return out
 
-    def get_cells(self, which="local"):
-        """Sorted ids of a cell selection (get_cells(..., sorted=true), 651)."""
-        return self._u64_query(lib().dccrgx_get_cells, CELLS[which])
+    def get_cells(self, criteria="local", exact_match=False, neighborhood_id=DEFAULT_HOOD, sorted=True):
+        """get_cells (dccrg.hpp:651) - sorted ids.  `criteria`: a list of
+        neighbor-type bitmasks (HAS_* below, is_neighbor_type_match 2946-3053;
+        [] = every local cell), or a selection name ("local", "inner",
+        "outer", "remote", "all")."""
+        if isinstance(criteria, str):
+            return self._u64_query(lib().dccrgx_get_cells, CELLS[criteria])
+        c = np.ascontiguousarray(criteria, np.int32)
+        return self._u64_query(lib().dccrgx_get_cells_by_criteria, _ptr(c), c.size, int(exact_match),
+                               int(neighborhood_id))
 
     def local_cells(self):
         return self.get_cells("local")

@@ -1,28 +1,64 @@
 /*
- * dccrg.hpp — C++ drop-in facade of dccrg::Dccrg<Cell_Data, Geometry> over
- * the MI355X-native C ABI (include/dccrgx.h, libdccrgx.so).
+ * dccrg.hpp - C++ drop-in facade of dccrg::Dccrg<Cell_Data, Geometry,
+ * Additional_Cell_Items, Additional_Neighbor_Items> (reference dccrg.hpp:
+ * 143-7072) over the MI355X-native C ABI (include/dccrgx.h, libdccrgx.so).
  *
- * Keeps the reference's namespace, class template, chainable setters and
- * query names (reference dccrg.hpp:145-7072).  Differences, by design:
- *   - the communicator is (rank, size, 128-byte RCCL id) instead of MPI_Comm
- *     (initialize 472-552); Dccrg::unique_id() makes the id on rank 0;
- *   - Cell_Data lives on the GPU as one AoS payload array over slots (local
- *     cells, then remote copies); the WHOLE struct is the halo payload
- *     (get_mpi_datatype 152-206 is not consulted).  operator[] returns a
- *     pointer into a host staging copy: call download() before reading and
- *     upload() after writing host-side, exactly where the reference would
- *     have touched cell data outside a device sweep;
- *   - device-side work uses SoA fields (add_field) and the built-in sweeps.
+ * A program written against the reference compiles against this header
+ * unchanged except for the include line (examples/game_of_life.cpp of the
+ * reference: tests/test_facade_cpu.py builds it, tests/test_gpu_facade.py
+ * runs it at 1 and 2 MPI ranks).  Kept from the reference: the namespace,
+ * the class template and its defaults, initialize(const MPI_Comm&) and the
+ * chainable setters, the public mapping / topology / length / geometry
+ * members, get_cells(criteria, exact_match, neighborhood_id, sorted),
+ * operator[], get_neighbors_of / _to returning a pointer (nullptr for
+ * unknown cells or neighborhoods), the iteration ranges inner_cells() /
+ * outer_cells() / local_cells() / remote_cells() / all_cells() of Cells_Item
+ * {id, data, neighbors_of, neighbors_to, all_neighbors} with Neighbors_Item
+ * {id, data, x, y, z}, the Additional_*_Items update hooks, the halo
+ * (update_copies_of_remote_neighbors and its start / wait split), the
+ * process-boundary and update-count getters, refinement, pins and
+ * balance_load, save / load_grid_data.
+ *
+ * How it works: Cell_Data lives in host memory for the user's loops, one
+ * element per slot (local cells, then copies of remote neighbors), and is
+ * mirrored in a device field of the library.  The halo moves exactly the
+ * bytes Cell_Data::get_mpi_datatype() describes (dccrg_get_cell_datatype.hpp:
+ * 40-340): local payloads go up, the library packs / exchanges / places them
+ * on the device, the received bytes come back into the host copies.  Ranks
+ * use RCCL when every rank of a node has its own GPU, otherwise the
+ * library's host exchange over the caller's MPI communicator
+ * (DCCRGX_TRANSPORT=host forces the latter).  Device-side sweeps use the
+ * library directly (dccrgx_* calls on native()).
+ *
+ * Build: -I include -I <mpi include> ... -L dccrg_amd -ldccrgx -lmpi
  */
 #ifndef DCCRG_AMD_DCCRG_HPP
 #define DCCRG_AMD_DCCRG_HPP
 
+#include <mpi.h>
+
+// the standard headers the reference's dccrg.hpp and its helpers pull in
+// (dccrg.hpp:20-56), which programs written against it rely on
 #include <algorithm>
 #include <array>
+#include <climits>
 #include <cstdint>
-#include <tuple>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <iterator>
+#include <limits>
+#include <map>
+#include <set>
 #include <stdexcept>
 #include <string>
+#include <tuple>
+#include <type_traits>
+#include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -30,63 +66,312 @@
 
 namespace dccrg {
 
-static const uint64_t error_cell = 0;                     // dccrg_mapping.hpp:37
+static const uint64_t error_cell = 0;                      // dccrg_mapping.hpp:37
 static const uint64_t error_index = 0xFFFFFFFFFFFFFFFFull;  // dccrg_mapping.hpp:40
-static const int default_neighborhood_id = -0xDCC;        // dccrg.hpp:93
+static const int default_neighborhood_id = DCCRGX_DEFAULT_HOOD;  // dccrg.hpp:93
 
-// dccrg_no_geometry.hpp / dccrg_cartesian_geometry.hpp parameter stand-ins
-struct No_Geometry {
-	struct Parameters {};
-};
-struct Cartesian_Geometry {
-	struct Parameters {
-		std::array<double, 3> start{{0, 0, 0}}, level_0_cell_length{{1, 1, 1}};
-	};
-};
+// neighbor types of get_cells (dccrg.hpp:95-142)
+static const int has_no_neighbor = 0, has_local_neighbor_of = (1 << 0), has_local_neighbor_to = (1 << 1),
+                 has_remote_neighbor_of = (1 << 2), has_remote_neighbor_to = (1 << 3),
+                 has_local_neighbor_both = has_local_neighbor_of | has_local_neighbor_to,
+                 has_remote_neighbor_both = has_remote_neighbor_of | has_remote_neighbor_to;
 
 namespace detail {
 inline void check(int rc) {
 	if (rc != DCCRGX_OK) throw std::runtime_error(std::string("dccrgx: ") + dccrgx_last_error());
 }
+
+template <class F>
+std::vector<uint64_t> fetch_u64(F&& f) {
+	size_t n = 0;
+	int rc = f(nullptr, 0, &n);
+	if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) check(rc);
+	std::vector<uint64_t> v(n);
+	if (n) check(f(v.data(), n, &n));
+	return v;
+}
+
+// get_mpi_datatype dispatch (dccrg_get_cell_datatype.hpp:40-340): the
+// zero-argument member, or the five-argument one, or the whole object
+template <class T>
+auto call_datatype(T& c, int) -> decltype(c.get_mpi_datatype()) {
+	return c.get_mpi_datatype();
+}
+template <class T>
+auto call_datatype(T& c, long) -> decltype(c.get_mpi_datatype(uint64_t(0), 0, 0, false, 0)) {
+	return c.get_mpi_datatype(error_cell, 0, 0, false, default_neighborhood_id);
+}
+template <class T>
+std::tuple<void*, int, MPI_Datatype> call_datatype(T& c, ...) {
+	return std::make_tuple((void*)&c, int(sizeof(T)), MPI_BYTE);
+}
+
+// the halo window [offset, offset + bytes) of a Cell_Data: one contiguous
+// run inside the object (a non-contiguous or out-of-object datatype sends
+// the whole object)
+template <class T>
+std::pair<size_t, size_t> datatype_window() {
+	T c{};
+	const auto dt = call_datatype(c, 0);
+	int sz = 0;
+	MPI_Type_size(std::get<2>(dt), &sz);
+	MPI_Aint lb = 0, extent = 0;
+	MPI_Type_get_true_extent(std::get<2>(dt), &lb, &extent);
+	const size_t bytes = size_t(std::get<1>(dt)) * size_t(sz);
+	const char* base = reinterpret_cast<const char*>(&c);
+	const char* p = static_cast<const char*>(std::get<0>(dt));
+	const bool inside = p >= base && p + bytes <= base + sizeof(T);
+	if (!inside || bytes == 0 || MPI_Aint(sz) != extent || lb != 0) return {0, sizeof(T)};
+	return {size_t(p - base), bytes};
+}
+
+// the library's host exchange over MPI point-to-point (one message per peer
+// each way, chunked below INT_MAX bytes)
+inline int mpi_exchange(void* ctx, const void* const* send, const size_t* sb, void* const* recv, const size_t* rb) {
+	MPI_Comm comm = *static_cast<MPI_Comm*>(ctx);
+	int size = 0;
+	MPI_Comm_size(comm, &size);
+	const size_t chunk = size_t(1) << 30;
+	std::vector<MPI_Request> req;
+	for (int p = 0; p < size; p++)
+		for (size_t o = 0; o < rb[p]; o += chunk) {
+			req.emplace_back();
+			MPI_Irecv(static_cast<char*>(recv[p]) + o, int(std::min(chunk, rb[p] - o)), MPI_BYTE, p, 0x7dc, comm,
+			          &req.back());
+		}
+	for (int p = 0; p < size; p++)
+		for (size_t o = 0; o < sb[p]; o += chunk) {
+			req.emplace_back();
+			MPI_Isend(static_cast<const char*>(send[p]) + o, int(std::min(chunk, sb[p] - o)), MPI_BYTE, p, 0x7dc, comm,
+			          &req.back());
+		}
+	return MPI_Waitall(int(req.size()), req.data(), MPI_STATUSES_IGNORE) == MPI_SUCCESS ? 0 : -1;
+}
 }  // namespace detail
 
-// Items of the iteration ranges (Neighbors_Item 7288-7340, Cells_Item
-// 7364-7402): ids with data pointers into the host staging copy, so that a
-// reference-style loop `for (const auto& cell: grid.local_cells_items())`
-// `for (const auto& n: cell.neighbors_of) n.data->...` reads the payload
-// downloaded last (the facade refreshes the items on download()).
-template <class Cell_Data>
-struct Neighbors_Item {
-	uint64_t id;
-	Cell_Data* data;
-	int x, y, z;  // offset of the neighbor's min corner in index units
-};
-template <class Cell_Data>
-struct Cells_Item {
-	uint64_t id;
-	Cell_Data* data;
-	std::vector<Neighbors_Item<Cell_Data>> neighbors_of;  // sorted by (id, offset), no duplicates (11451-11500)
+// ---- value types (dccrg_length.hpp, dccrg_topology.hpp, dccrg_mapping.hpp) --
+class Grid_Length {
+public:
+	std::array<uint64_t, 3> get() const { return l_; }
+	bool set(const std::array<uint64_t, 3>& l) {
+		if (l[0] == 0 || l[1] == 0 || l[2] == 0) return false;
+		l_ = l;
+		return true;
+	}
+
+private:
+	std::array<uint64_t, 3> l_{{1, 1, 1}};
 };
 
-template <class Cell_Data, class Geometry = No_Geometry>
-class Dccrg {
+class Grid_Topology {
 public:
+	bool is_periodic(size_t d) const { return d < 3 && p_[d]; }
+	bool set_periodicity(size_t d, bool v) {
+		if (d > 2) return false;
+		p_[d] = v;
+		return true;
+	}
+
+private:
+	std::array<bool, 3> p_{{false, false, false}};
+};
+
+// Mapping (dccrg_mapping.hpp:54-651) of the grid, answered by the library
+class Mapping {
+public:
+	Grid_Length length;
+	uint64_t get_cell_from_indices(const std::array<uint64_t, 3>& ind, int lvl) const {
+		return g_ ? dccrgx_get_cell_from_indices(g_, ind.data(), lvl) : error_cell;
+	}
+	std::array<uint64_t, 3> get_indices(uint64_t cell) const {
+		std::array<uint64_t, 3> r{{error_index, error_index, error_index}};
+		if (g_) dccrgx_get_indices(g_, cell, r.data());
+		return r;
+	}
+	int get_refinement_level(uint64_t cell) const { return g_ ? dccrgx_get_refinement_level(g_, cell) : -1; }
+	int get_maximum_refinement_level() const {
+		int l = 0;
+		if (g_) dccrgx_get_maximum_refinement_level(g_, &l);
+		return l;
+	}
+	uint64_t get_last_cell() const { return g_ ? dccrgx_get_last_cell(g_) : 0; }
+	uint64_t get_cell_length_in_indices(uint64_t cell) const {
+		const int l = get_refinement_level(cell);
+		if (l < 0) return error_index;
+		return uint64_t(1) << (get_maximum_refinement_level() - l);
+	}
+	uint64_t get_parent(uint64_t cell) const {
+		const int l = get_refinement_level(cell);
+		if (l < 0) return error_cell;
+		if (l == 0) return cell;
+		return get_cell_from_indices(get_indices(cell), l - 1);
+	}
+	uint64_t get_level_0_parent(uint64_t cell) const {
+		const int l = get_refinement_level(cell);
+		if (l < 0) return error_cell;
+		return get_cell_from_indices(get_indices(cell), 0);
+	}
+	uint64_t get_child(uint64_t cell) const {
+		const int l = get_refinement_level(cell);
+		if (l < 0) return error_cell;
+		if (l >= get_maximum_refinement_level()) return cell;
+		return get_cell_from_indices(get_indices(cell), l + 1);
+	}
+	std::array<uint64_t, 8> get_all_children(uint64_t cell) const {
+		std::array<uint64_t, 8> r;
+		r.fill(error_cell);
+		const int l = get_refinement_level(cell);
+		if (l < 0 || l >= get_maximum_refinement_level()) return r;
+		const auto ind = get_indices(cell);
+		const uint64_t h = get_cell_length_in_indices(cell) / 2;
+		for (int i = 0; i < 8; i++)
+			r[size_t(i)] = get_cell_from_indices(
+			    {{ind[0] + (i & 1) * h, ind[1] + ((i >> 1) & 1) * h, ind[2] + ((i >> 2) & 1) * h}}, l + 1);
+		return r;
+	}
+	std::array<uint64_t, 8> get_siblings(uint64_t cell) const {
+		std::array<uint64_t, 8> r;
+		r.fill(error_cell);
+		const int l = get_refinement_level(cell);
+		if (l < 0) return r;
+		if (l == 0) {
+			r[0] = cell;
+			return r;
+		}
+		return get_all_children(get_parent(cell));
+	}
+	void attach(dccrgx_grid* g) { g_ = g; }
+
+private:
+	dccrgx_grid* g_ = nullptr;
+};
+
+// ---- geometries (dccrg_no_geometry.hpp, dccrg_cartesian_geometry.hpp) ----
+class No_Geometry {
+public:
+	struct Parameters {};
+	static constexpr int geometry_id = 0;
+	void attach(dccrgx_grid* g) { g_ = g; }
+	bool set(const Parameters&) { return true; }
+	std::array<double, 3> get_length(uint64_t cell) const { return batch(cell, false); }
+	std::array<double, 3> get_center(uint64_t cell) const { return batch(cell, true); }
+
+protected:
+	std::array<double, 3> batch(uint64_t cell, bool center) const {
+		std::array<double, 3> c{{0, 0, 0}}, L{{0, 0, 0}};
+		if (g_) dccrgx_geometry_batch(g_, &cell, 1, c.data(), L.data());
+		return center ? c : L;
+	}
+	dccrgx_grid* g_ = nullptr;
+};
+
+struct Cartesian_Geometry_Parameters {
+	std::array<double, 3> start{{0, 0, 0}}, level_0_cell_length{{1, 1, 1}};
+};
+
+class Cartesian_Geometry : public No_Geometry {
+public:
+	using Parameters = Cartesian_Geometry_Parameters;
+	static constexpr int geometry_id = 1;
+	bool set(const Parameters& p) {
+		p_ = p;
+		return !g_ || dccrgx_set_geometry(g_, p.start.data(), p.level_0_cell_length.data()) == DCCRGX_OK;
+	}
+	const Parameters& get() const { return p_; }
+	std::array<double, 3> get_start() const { return p_.start; }
+	std::array<double, 3> get_level_0_cell_length() const { return p_.level_0_cell_length; }
+	std::array<double, 3> get_min(uint64_t cell) const {
+		const auto c = get_center(cell), L = get_length(cell);
+		return {{c[0] - L[0] / 2, c[1] - L[1] / 2, c[2] - L[2] / 2}};
+	}
+	std::array<double, 3> get_max(uint64_t cell) const {
+		const auto c = get_center(cell), L = get_length(cell);
+		return {{c[0] + L[0] / 2, c[1] + L[1] / 2, c[2] + L[2] / 2}};
+	}
+
+private:
+	Parameters p_;
+};
+
+template <class T>
+struct Iterator_Storage {  // dccrg.hpp:7279-7285
+	typename std::vector<T>::const_iterator begin_, end_;
+	typename std::vector<T>::const_iterator begin() const { return begin_; }
+	typename std::vector<T>::const_iterator cbegin() const { return begin_; }
+	typename std::vector<T>::const_iterator end() const { return end_; }
+	typename std::vector<T>::const_iterator cend() const { return end_; }
+};
+
+template <class Cell_Data, class Geometry = No_Geometry, class Additional_Cell_Items = std::tuple<>,
+          class Additional_Neighbor_Items = std::tuple<>>
+class Dccrg;
+
+template <class Cell_Data, class Geometry, class... Additional_Cell_Items, class... Additional_Neighbor_Items>
+class Dccrg<Cell_Data, Geometry, std::tuple<Additional_Cell_Items...>, std::tuple<Additional_Neighbor_Items...>> {
+	static_assert(std::is_trivially_copyable<Cell_Data>::value,
+	              "Cell_Data is mirrored on the GPU: it must be trivially copyable");
+
+public:
+	using cell_data_type = Cell_Data;
+	using geometry_type = Geometry;
+	using neighbor_list_t = std::vector<std::pair<uint64_t, std::array<int, 3>>>;
+
+	// Neighbors_Item / Cells_Item (7288-7402)
+	struct Neighbors_Item : Additional_Neighbor_Items... {
+		uint64_t id;
+		Cell_Data* data;
+		int x, y, z;
+		template <class Grid, class Cell_Item>
+		void update_caller(const Grid&, const Cell_Item&, const int&) {}
+		template <class Grid, class Cell_Item, class A, class... B>
+		void update_caller(const Grid& grid, const Cell_Item& cell, const int& hood, const A& a, const B&... b) {
+			A::update(grid, cell, *this, hood, a);
+			update_caller(grid, cell, hood, b...);
+		}
+	};
+	struct Cells_Item : Additional_Cell_Items... {
+		uint64_t id = error_cell;
+		Cell_Data* data = nullptr;
+		Iterator_Storage<Neighbors_Item> neighbors_of, neighbors_to, all_neighbors;
+		friend bool operator<(const Cells_Item& a, const Cells_Item& b) { return a.id < b.id; }
+		template <class Grid>
+		void update_caller(const Grid&) {}
+		template <class Grid, class A, class... B>
+		void update_caller(const Grid& grid, const A& a, const B&... b) {
+			A::update(grid, *this, a);
+			update_caller(grid, b...);
+		}
+	};
+
+	// public read-only members (235-279)
+	const Grid_Topology& topology = topology_rw;
+	const Mapping& mapping = mapping_rw;
+	const Grid_Length& length = mapping_rw.length;
+	const Geometry& geometry = geometry_rw;
+	const std::vector<Cells_Item>& cells = cells_rw;
+	const std::vector<Neighbors_Item>& neighbors = neighbors_rw;
+
 	Dccrg() = default;
 	Dccrg(const Dccrg&) = delete;
 	Dccrg& operator=(const Dccrg&) = delete;
 	~Dccrg() {
+		// DCCRGX_DUMP_CELLS=<path>: every rank writes its local cells (uint64
+		// id + Cell_Data bytes, ascending id) to <path>.<rank> (verification of
+		// unmodified reference programs, tests/test_gpu_facade.py)
+		if (const char* p = std::getenv("DCCRGX_DUMP_CELLS")) {
+			if (g_) dump_cells(std::string(p) + "." + std::to_string(rank_));
+		}
 		if (g_) dccrgx_destroy(g_);
+		if (comm_ != MPI_COMM_NULL) {
+			int fin = 0;
+			MPI_Finalized(&fin);
+			if (!fin) MPI_Comm_free(&comm_);
+		}
 	}
 
-	static std::array<char, 128> unique_id() {
-		std::array<char, 128> id{};
-		detail::check(dccrgx_get_unique_id(id.data()));
-		return id;
-	}
-
-	// ---- setup (dccrg.hpp:8120-8230) ----------------------------------------
+	// ---- setup (8120-8230), chainable ----------------------------------------
 	Dccrg& set_initial_length(const std::array<uint64_t, 3>& l) {
-		length_ = l;
+		if (!mapping_rw.length.set(l)) throw std::invalid_argument("dccrg: grid length must be > 0");
 		return *this;
 	}
 	Dccrg& set_maximum_refinement_level(const int l) {
@@ -94,99 +379,80 @@ public:
 		return *this;
 	}
 	Dccrg& set_periodic(bool x, bool y, bool z) {
-		periodic_ = {{x, y, z}};
+		topology_rw.set_periodicity(0, x);
+		topology_rw.set_periodicity(1, y);
+		topology_rw.set_periodicity(2, z);
 		return *this;
 	}
 	Dccrg& set_neighborhood_length(unsigned n) {
 		hood_ = n;
 		return *this;
 	}
-	Dccrg& set_load_balancing_method(const std::string&) { return *this; }  // Zoltan: out of scope
+	// the partitioner is data here (no Zoltan): the method name is kept
+	Dccrg& set_load_balancing_method(const std::string& m) {
+		lb_method_ = m;
+		return *this;
+	}
+	Dccrg& set_send_single_cells(bool) { return *this; }  // one message per peer (the reference default)
 
-	// initialize(comm) 472: comm = (rank, size, device, RCCL id or nullptr)
-	Dccrg& initialize(int rank = 0, int size = 1, int device = 0, const void* rccl_id = nullptr) {
-		detail::check(dccrgx_create(rank, size, device, rccl_id, &g_));
-		detail::check(dccrgx_set_initial_length(g_, length_.data()));
+	// initialize (472-552)
+	Dccrg& initialize(const MPI_Comm& comm, const uint64_t /*sfc_caching_batches*/ = 1) {
+		if (g_) throw std::invalid_argument("dccrg: already initialized");
+		create(comm);
+		const auto L = mapping_rw.length.get();
+		detail::check(dccrgx_set_initial_length(g_, L.data()));
 		detail::check(dccrgx_set_maximum_refinement_level(g_, max_ref_));
-		detail::check(dccrgx_set_periodic(g_, periodic_[0], periodic_[1], periodic_[2]));
+		detail::check(dccrgx_set_periodic(g_, topology_rw.is_periodic(0), topology_rw.is_periodic(1),
+		                                  topology_rw.is_periodic(2)));
 		detail::check(dccrgx_set_neighborhood_length(g_, hood_));
 		detail::check(dccrgx_initialize(g_));
-		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
-		rank_ = rank;
+		add_payload_field();
+		refresh();
 		return *this;
 	}
 
-	Dccrg& set_geometry(const typename Geometry::Parameters& p) {
-		set_geometry_impl(p);
+	Dccrg& set_geometry(const typename Geometry::Parameters& p) {  // 576
+		if (!geometry_rw.set(p)) throw std::invalid_argument("dccrg: couldn't set geometry");
+		refresh_items();
 		return *this;
 	}
 
 	dccrgx_grid* native() const { return g_; }
 	int get_rank() const { return rank_; }
-
-	// ---- mapping (dccrg_mapping.hpp) -----------------------------------------
-	uint64_t get_cell_from_indices(const std::array<uint64_t, 3>& ind, int lvl) const {
-		return dccrgx_get_cell_from_indices(g_, ind.data(), lvl);
-	}
-	std::array<uint64_t, 3> get_indices(uint64_t cell) const {
-		std::array<uint64_t, 3> r{{error_index, error_index, error_index}};
-		dccrgx_get_indices(g_, cell, r.data());
-		return r;
-	}
-	int get_refinement_level(uint64_t cell) const { return dccrgx_get_refinement_level(g_, cell); }
-	int get_maximum_refinement_level() const {
-		int l = 0;
-		detail::check(dccrgx_get_maximum_refinement_level(g_, &l));
-		return l;
-	}
+	int get_comm_size() const { return size_; }
+	unsigned int get_neighborhood_length() const { return hood_; }
+	int get_maximum_refinement_level() const { return mapping_rw.get_maximum_refinement_level(); }
+	MPI_Comm get_communicator() const { return comm_; }
 
 	// ---- queries ----------------------------------------------------------------
-	// get_cells (651), sorted ascending; selection instead of criteria
-	std::vector<uint64_t> get_cells(int which = DCCRGX_CELLS_LOCAL) const {
-		return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells(g_, which, o, c, n); });
+	// get_cells (651-739) with is_neighbor_type_match (2946-3053)
+	std::vector<uint64_t> get_cells(const std::vector<int>& criteria = std::vector<int>(), const bool exact_match = false,
+	                                const int neighborhood_id = default_neighborhood_id,
+	                                const bool /*sorted*/ = false) const {
+		std::vector<int32_t> c(criteria.begin(), criteria.end());
+		return detail::fetch_u64([&](uint64_t* o, size_t cap, size_t* n) {
+			return dccrgx_get_cells_by_criteria(g_, c.data(), c.size(), exact_match, neighborhood_id, o, cap, n);
+		});
 	}
-	std::vector<uint64_t> local_cells() const { return get_cells(DCCRGX_CELLS_LOCAL); }
-	std::vector<uint64_t> inner_cells() const { return get_cells(DCCRGX_CELLS_INNER); }
-	std::vector<uint64_t> outer_cells() const { return get_cells(DCCRGX_CELLS_OUTER); }
-	std::vector<uint64_t> remote_cells() const { return get_cells(DCCRGX_CELLS_REMOTE); }
+	Cell_Data* operator[](const uint64_t cell) const {  // 756
+		int64_t s = -1;
+		if (g_) dccrgx_get_slots(g_, &cell, 1, &s);
+		if (s < 0 || size_t(s) >= host_.size()) return nullptr;
+		return const_cast<Cell_Data*>(&host_[size_t(s)]);
+	}
+	std::array<double, 3> get_center(const uint64_t cell) const { return geometry_rw.get_center(cell); }  // 771
 
-	// get_neighbors_of (819): empty optional-like result (nullptr in the
-	// reference) is signalled by `found == false`
-	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_of(uint64_t cell, bool* found = nullptr) const {
-		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
-		size_t n = 0;
-		int rc = dccrgx_get_neighbors_of(g_, cell, nullptr, nullptr, 0, &n);
-		if (found) *found = rc != DCCRGX_ENOTFOUND;
-		if (rc == DCCRGX_ENOTFOUND) return r;
-		if (rc != DCCRGX_ERANGE) detail::check(rc);
-		std::vector<uint64_t> ids(n);
-		std::vector<int32_t> off(3 * n);
-		detail::check(dccrgx_get_neighbors_of(g_, cell, ids.data(), off.data(), n, &n));
-		for (size_t i = 0; i < n; i++) r.push_back({ids[i], {{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}});
-		return r;
+	// get_neighbors_of / _to (819 / 883): nullptr for a cell that is not local
+	// or a neighborhood that does not exist; valid until the next structural change
+	const neighbor_list_t* get_neighbors_of(const uint64_t cell,
+	                                        const int neighborhood_id = default_neighborhood_id) const {
+		return neighbor_list(cell, neighborhood_id, 0);
 	}
-	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_to(uint64_t cell) const {
-		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
-		size_t n = 0;
-		int rc = dccrgx_get_neighbors_to(g_, cell, nullptr, 0, &n);
-		if (rc == DCCRGX_ENOTFOUND) return r;
-		if (rc != DCCRGX_ERANGE) detail::check(rc);
-		std::vector<uint64_t> ids(n);
-		detail::check(dccrgx_get_neighbors_to(g_, cell, ids.data(), n, &n));
-		for (auto i : ids) r.push_back({i, {{0, 0, 0}}});
-		return r;
+	const neighbor_list_t* get_neighbors_to(const uint64_t cell,
+	                                        const int neighborhood_id = default_neighborhood_id) const {
+		return neighbor_list(cell, neighborhood_id, 1);
 	}
-	// get_neighbors_of / _to (819 / 883) for a user neighborhood id
-	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_of(uint64_t cell, int neighborhood_id,
-	                                                                      bool* found = nullptr) const {
-		if (neighborhood_id == DCCRGX_DEFAULT_HOOD) return get_neighbors_of(cell, found);
-		return user_neighbors(cell, neighborhood_id, 0, found);
-	}
-	std::vector<std::pair<uint64_t, std::array<int, 3>>> get_neighbors_to(uint64_t cell, int neighborhood_id) const {
-		if (neighborhood_id == DCCRGX_DEFAULT_HOOD) return get_neighbors_to(cell);
-		return user_neighbors(cell, neighborhood_id, 1, nullptr);
-	}
-	std::vector<std::pair<uint64_t, int>> get_face_neighbors_of(uint64_t cell) const {  // 2806
+	std::vector<std::pair<uint64_t, int>> get_face_neighbors_of(const uint64_t cell) const {  // 2806
 		std::vector<std::pair<uint64_t, int>> r;
 		uint64_t ids[64];
 		int32_t dirs[64];
@@ -197,150 +463,166 @@ public:
 		for (size_t i = 0; i < n; i++) r.push_back({ids[i], dirs[i]});
 		return r;
 	}
-	bool is_local(uint64_t cell) const { return dccrgx_is_local(g_, cell) == 1; }  // 3270
-	// the update lists of a neighborhood id (get_cells_to_send / _receive
-	// 6900-6914 per id)
-	std::vector<uint64_t> get_cells_to_send(int peer, int neighborhood_id = DCCRGX_DEFAULT_HOOD) const {
-		if (neighborhood_id == DCCRGX_DEFAULT_HOOD)
-			return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells_to_send(g_, peer, o, c, n); });
-		return fetch([&](uint64_t* o, size_t c, size_t* n) {
-			return dccrgx_get_user_update_list(g_, neighborhood_id, peer, 0, o, c, n);
-		});
-	}
-	std::vector<uint64_t> get_cells_to_receive(int peer, int neighborhood_id = DCCRGX_DEFAULT_HOOD) const {
-		if (neighborhood_id == DCCRGX_DEFAULT_HOOD)
-			return fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_cells_to_receive(g_, peer, o, c, n); });
-		return fetch([&](uint64_t* o, size_t c, size_t* n) {
-			return dccrgx_get_user_update_list(g_, neighborhood_id, peer, 1, o, c, n);
-		});
+	bool is_local(const uint64_t cell) const { return dccrgx_is_local(g_, cell) == 1; }  // 3270
+	int get_process(const uint64_t cell) const { return dccrgx_get_process(g_, cell); }  // 5807
+	bool is_neighbor_type_match(const uint64_t cell, const std::vector<int>& criteria, const bool exact_match,
+	                            const int neighborhood_id) const {  // 2946
+		const auto c = get_cells(criteria, exact_match, neighborhood_id);
+		return std::binary_search(c.begin(), c.end(), cell);
 	}
 
-	// ---- user neighborhoods (add_neighborhood 6383, remove_neighborhood 6530) ----
-	bool add_neighborhood(int neighborhood_id, const std::vector<std::array<int, 3>>& items) {
+	// process boundaries (6050-6206)
+	std::vector<uint64_t> get_local_cells_on_process_boundary(const int neighborhood_id = default_neighborhood_id,
+	                                                          const bool sorted = false) const {
+		return get_cells({has_remote_neighbor_of, has_remote_neighbor_to}, false, neighborhood_id, sorted);
+	}
+	std::vector<uint64_t> get_local_cells_not_on_process_boundary(const int neighborhood_id = default_neighborhood_id,
+	                                                              const bool sorted = false) const {
+		return get_cells({has_no_neighbor, has_local_neighbor_of, has_local_neighbor_to, has_local_neighbor_both}, true,
+		                 neighborhood_id, sorted);
+	}
+	std::vector<uint64_t> get_remote_cells_on_process_boundary(const int neighborhood_id = default_neighborhood_id,
+	                                                           const bool /*sorted*/ = false) const {
+		if (neighborhood_id == default_neighborhood_id)
+			return detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) {
+				return dccrgx_get_cells(g_, DCCRGX_CELLS_REMOTE, o, c, n);
+			});
+		std::vector<uint64_t> r;
+		for (const auto& kv : cells_to_receive(neighborhood_id))
+			for (const auto& c : kv.second) r.push_back(c.first);
+		std::sort(r.begin(), r.end());
+		r.erase(std::unique(r.begin(), r.end()), r.end());
+		return r;
+	}
+	// update counts (5382-5490); max uint64 for an unknown neighborhood
+	uint64_t get_number_of_update_send_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return count_updates(neighborhood_id, false);
+	}
+	uint64_t get_number_of_update_receive_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return count_updates(neighborhood_id, true);
+	}
+	// cells_to_send / cells_to_receive (6900-6914): per process the ids in
+	// ascending order with their message tags 1..n (8662-8748)
+	const std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>& get_cells_to_send(
+	    const int neighborhood_id = default_neighborhood_id) const {
+		return cells_to_send_map(neighborhood_id);
+	}
+	const std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>& get_cells_to_receive(
+	    const int neighborhood_id = default_neighborhood_id) const {
+		return cells_to_receive(neighborhood_id);
+	}
+
+	// ---- iteration (7478-7602) ----------------------------------------------------
+	const Iterator_Storage<Cells_Item>& inner_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return range(neighborhood_id, 0);
+	}
+	const Iterator_Storage<Cells_Item>& outer_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return range(neighborhood_id, 1);
+	}
+	const Iterator_Storage<Cells_Item>& local_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return range(neighborhood_id, 2);
+	}
+	const Iterator_Storage<Cells_Item>& remote_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return range(neighborhood_id, 3);
+	}
+	const Iterator_Storage<Cells_Item>& all_cells(const int neighborhood_id = default_neighborhood_id) const {
+		return range(neighborhood_id, 4);
+	}
+
+	// ---- halo (966-1000, 5010-5367) -------------------------------------------------
+	bool update_copies_of_remote_neighbors(const int neighborhood_id = default_neighborhood_id) {
+		upload_local();
+		if (dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) != DCCRGX_OK) return false;
+		download_remote();
+		return true;
+	}
+	bool start_remote_neighbor_copy_updates(const int neighborhood_id = default_neighborhood_id) {
+		if (neighborhood_id != default_neighborhood_id) return update_copies_of_remote_neighbors(neighborhood_id);
+		upload_local();
+		return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK;
+	}
+	bool start_remote_neighbor_copy_receives(const int neighborhood_id = default_neighborhood_id) {
+		return start_remote_neighbor_copy_updates(neighborhood_id);
+	}
+	bool start_remote_neighbor_copy_sends(const int = default_neighborhood_id) { return true; }
+	bool wait_remote_neighbor_copy_update_receives(const int = default_neighborhood_id) {
+		if (dccrgx_wait_remote_neighbor_copy_update_receives(g_) != DCCRGX_OK) return false;
+		download_remote();
+		return true;
+	}
+	bool wait_remote_neighbor_copy_update_sends(const int = default_neighborhood_id) {
+		return dccrgx_wait_remote_neighbor_copy_update_sends(g_) == DCCRGX_OK;
+	}
+	bool wait_remote_neighbor_copy_updates(const int neighborhood_id = default_neighborhood_id) {
+		return wait_remote_neighbor_copy_update_receives(neighborhood_id) &&
+		       wait_remote_neighbor_copy_update_sends(neighborhood_id);
+	}
+
+	// ---- user neighborhoods (6383-6603) -----------------------------------------------
+	bool add_neighborhood(const int neighborhood_id, const std::vector<std::array<int, 3>>& items) {
 		std::vector<int32_t> o;
 		for (const auto& it : items) o.insert(o.end(), it.begin(), it.end());
-		return dccrgx_add_neighborhood(g_, neighborhood_id, o.data(), items.size()) == DCCRGX_OK;
+		const bool ok = dccrgx_add_neighborhood(g_, neighborhood_id, o.data(), items.size()) == DCCRGX_OK;
+		if (ok) refresh_items();
+		return ok;
 	}
-	Dccrg& remove_neighborhood(int neighborhood_id) {
+	void remove_neighborhood(const int neighborhood_id) {
 		detail::check(dccrgx_remove_neighborhood(g_, neighborhood_id));
-		return *this;
+		refresh_items();
 	}
-	int get_process(uint64_t cell) const { return dccrgx_get_process(g_, cell); }   // 5807
 
-	// ---- refinement / partition ----------------------------------------------
-	bool refine_completely(uint64_t cell) { return dccrgx_refine_completely(g_, cell) == DCCRGX_OK; }
-	std::vector<uint64_t> stop_refining() {
+	// ---- refinement (2434, 3461) ------------------------------------------------------
+	bool refine_completely(const uint64_t cell) { return dccrgx_refine_completely(g_, cell) == DCCRGX_OK; }
+	std::vector<uint64_t> stop_refining(const bool = false) {
+		upload_local();
 		size_t n = 0;
 		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
-		return fetch([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+		refresh();
+		return detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
 	}
-	bool pin(uint64_t cell, int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
-	bool unpin(uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
-	Dccrg& balance_load(bool /*use_zoltan*/ = true) {
+
+	// ---- partition (1024, 5832-5909) ---------------------------------------------------
+	bool pin(const uint64_t cell) { return pin(cell, rank_); }
+	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
+	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
+	Dccrg& balance_load(const bool /*use_zoltan*/ = true) {
+		upload_local();
 		detail::check(dccrgx_balance_load(g_));
+		refresh();
 		return *this;
 	}
-	// balance_load to an explicit partition: one owner per leaf, leaves ascending
-	Dccrg& balance_load(const std::vector<uint64_t>& leaves, const std::vector<int32_t>& owners) {
-		detail::check(dccrgx_balance_load_to(g_, leaves.data(), owners.data(), leaves.size()));
+	// a partitioner's export list: local cells and their new processes
+	Dccrg& balance_load(const std::vector<uint64_t>& cells_out, const std::vector<int>& processes) {
+		upload_local();
+		std::vector<int32_t> p(processes.begin(), processes.end());
+		detail::check(dccrgx_balance_load_to(g_, cells_out.data(), p.data(), cells_out.size()));
+		refresh();
 		return *this;
 	}
 
-	// ---- grid files (save_grid_data 1089, load_grid_data 1742) ------------------
+	// ---- grid files (1089, 1742) --------------------------------------------------------
 	// the header is raw bytes (the reference takes (void*, count, MPI_Datatype))
-	bool save_grid_data(const std::string& name, uint64_t offset, const void* header = nullptr,
-	                    size_t header_bytes = 0) {
-		upload();
+	bool save_grid_data(const std::string& name, const uint64_t offset, const void* header = nullptr,
+	                    const size_t header_bytes = 0) {
+		upload_local();
 		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
 	}
 	// replaces initialize(): every setting comes from the file
-	bool load_grid_data(const std::string& name, uint64_t offset, size_t header_bytes, int rank = 0, int size = 1,
-	                    int device = 0, const void* rccl_id = nullptr) {
-		detail::check(dccrgx_create(rank, size, device, rccl_id, &g_));
-		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
-		rank_ = rank;
+	bool load_grid_data(const std::string& name, const uint64_t offset, const MPI_Comm& comm,
+	                    const size_t header_bytes = 0) {
+		if (g_) throw std::invalid_argument("dccrg: already initialized");
+		create(comm);
+		add_payload_field();
 		if (dccrgx_load_grid_data(g_, name.c_str(), offset, header_bytes) != DCCRGX_OK) return false;
-		download();
+		int R = 0;
+		detail::check(dccrgx_get_maximum_refinement_level(g_, &R));
+		max_ref_ = R;
+		refresh();
+		download_all();
 		return true;
 	}
 
-	// ---- Cell_Data payload (host staging) -----------------------------------
-	void download() {
-		size_t ns = 0;
-		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
-		host_.resize(ns);
-		ids_ = fetch([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_slot_ids(g_, o, c, n); });
-		if (ns) detail::check(dccrgx_field_download(g_, payload_, 0, ns, host_.data()));
-	}
-	void upload() {
-		if (!host_.empty()) detail::check(dccrgx_field_upload(g_, payload_, 0, host_.size(), host_.data()));
-	}
-	// operator[] (756): local cell or remote copy in the host staging copy
-	Cell_Data* operator[](uint64_t cell) {
-		const int64_t s = dccrgx_get_slot(g_, cell);
-		if (s < 0 || size_t(s) >= host_.size()) return nullptr;
-		return &host_[size_t(s)];
-	}
-
-	// ---- iteration (inner_cells / outer_cells / local_cells 7478-7602) ------------
-	// items of a selection, ascending id, each with its iterator neighbors_of;
-	// data pointers are valid until the next download() or structural change
-	std::vector<Cells_Item<Cell_Data>> cells_items(int which = DCCRGX_CELLS_LOCAL) {
-		if (host_.empty()) download();
-		size_t nl = 0, ns = 0;
-		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
-		{
-			size_t ni = 0, no = 0;
-			detail::check(dccrgx_get_counts(g_, &ni, &no, nullptr, nullptr));
-			nl = ni + no;
-		}
-		std::vector<uint32_t> ptr(nl + 1);
-		size_t ne = 0;
-		int rc = dccrgx_download_csr(g_, 0, ptr.data(), nullptr, nullptr, 0, &ne);
-		if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) detail::check(rc);
-		std::vector<uint64_t> nid(ne + 1);
-		std::vector<int32_t> off(3 * ne + 3);
-		detail::check(dccrgx_download_csr(g_, 0, ptr.data(), nid.data(), off.data(), ne, &ne));
-		std::vector<Cells_Item<Cell_Data>> out;
-		for (uint64_t id : get_cells(which)) {
-			const int64_t s = dccrgx_get_slot(g_, id);
-			Cells_Item<Cell_Data> it{id, &host_[size_t(s)], {}};
-			for (uint32_t j = ptr[size_t(s)]; j < ptr[size_t(s) + 1]; j++) {
-				const int64_t ns2 = dccrgx_get_slot(g_, nid[j]);
-				it.neighbors_of.push_back({nid[j], ns2 >= 0 ? &host_[size_t(ns2)] : nullptr, off[3 * j], off[3 * j + 1],
-				                           off[3 * j + 2]});
-			}
-			std::sort(it.neighbors_of.begin(), it.neighbors_of.end(), [](const auto& a, const auto& b) {
-				return std::tie(a.id, a.x, a.y, a.z) < std::tie(b.id, b.x, b.y, b.z);
-			});
-			it.neighbors_of.erase(std::unique(it.neighbors_of.begin(), it.neighbors_of.end(),
-			                                  [](const auto& a, const auto& b) {
-				                                  return a.id == b.id && a.x == b.x && a.y == b.y && a.z == b.z;
-			                                  }),
-			                      it.neighbors_of.end());
-			out.push_back(std::move(it));
-		}
-		return out;
-	}
-	std::vector<Cells_Item<Cell_Data>> local_cells_items() { return cells_items(DCCRGX_CELLS_LOCAL); }
-	std::vector<Cells_Item<Cell_Data>> inner_cells_items() { return cells_items(DCCRGX_CELLS_INNER); }
-	std::vector<Cells_Item<Cell_Data>> outer_cells_items() { return cells_items(DCCRGX_CELLS_OUTER); }
-
-	// ---- halo (966, 5010-5367) -------------------------------------------------
-	bool update_copies_of_remote_neighbors() { return dccrgx_update_copies_of_remote_neighbors(g_) == DCCRGX_OK; }
-	bool start_remote_neighbor_copy_updates() { return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK; }
-	bool wait_remote_neighbor_copy_update_receives() {
-		return dccrgx_wait_remote_neighbor_copy_update_receives(g_) == DCCRGX_OK;
-	}
-	bool wait_remote_neighbor_copy_update_sends() {
-		return dccrgx_wait_remote_neighbor_copy_update_sends(g_) == DCCRGX_OK;
-	}
-	bool wait_remote_neighbor_copy_updates() { return dccrgx_wait_remote_neighbor_copy_updates(g_) == DCCRGX_OK; }
-	bool update_copies_of_remote_neighbors(int neighborhood_id) {  // 966 with an id
-		return dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) == DCCRGX_OK;
-	}
-
-	// ---- device SoA fields ------------------------------------------------------
+	// ---- device SoA fields --------------------------------------------------------------
 	template <class T>
 	int add_field(const std::string& name, bool transfer) {
 		int id = -1;
@@ -348,46 +630,348 @@ public:
 		return id;
 	}
 	int payload_field() const { return payload_; }
+	// host Cell_Data <-> device payload field
+	void upload() { upload_all(); }
+	void download() { download_all(); }
 
 private:
-	template <class F>
-	static std::vector<uint64_t> fetch(F&& f) {
-		size_t n = 0;
-		int rc = f(nullptr, 0, &n);
-		if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) detail::check(rc);
-		std::vector<uint64_t> v(n);
-		if (n) detail::check(f(v.data(), n, &n));
-		return v;
-	}
-	std::vector<std::pair<uint64_t, std::array<int, 3>>> user_neighbors(uint64_t cell, int id, int kind,
-	                                                                    bool* found) const {
-		std::vector<std::pair<uint64_t, std::array<int, 3>>> r;
-		size_t n = 0;
-		int rc = dccrgx_get_user_neighbors(g_, id, cell, kind, nullptr, nullptr, 0, &n);
-		if (found) *found = rc != DCCRGX_ENOTFOUND;
-		if (rc == DCCRGX_ENOTFOUND) return r;
-		if (rc != DCCRGX_ERANGE) detail::check(rc);
-		std::vector<uint64_t> ids(n);
-		std::vector<int32_t> off(3 * n);
-		detail::check(dccrgx_get_user_neighbors(g_, id, cell, kind, ids.data(), off.data(), n, &n));
-		for (size_t i = 0; i < n; i++)
-			r.push_back({ids[i], kind == 0 ? std::array<int, 3>{{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}
-			                               : std::array<int, 3>{{0, 0, 0}}});
-		return r;
-	}
-	void set_geometry_impl(const No_Geometry::Parameters&) {}
-	void set_geometry_impl(const Cartesian_Geometry::Parameters& p) {
-		detail::check(dccrgx_set_geometry(g_, p.start.data(), p.level_0_cell_length.data()));
+	void dump_cells(const std::string& path) const {
+		std::vector<std::pair<uint64_t, size_t>> c;
+		for (size_t s = 0; s < n_local_ && s < slot_ids_.size(); s++) c.push_back({slot_ids_[s], s});
+		std::sort(c.begin(), c.end());
+		if (FILE* f = std::fopen(path.c_str(), "wb")) {
+			for (const auto& e : c) {
+				std::fwrite(&e.first, 8, 1, f);
+				std::fwrite(&host_[e.second], sizeof(Cell_Data), 1, f);
+			}
+			std::fclose(f);
+		}
 	}
 
+	void create(const MPI_Comm& comm) {
+		MPI_Comm_dup(comm, &comm_);
+		MPI_Comm_rank(comm_, &rank_);
+		MPI_Comm_size(comm_, &size_);
+		MPI_Comm node;
+		MPI_Comm_split_type(comm_, MPI_COMM_TYPE_SHARED, rank_, MPI_INFO_NULL, &node);
+		int lrank = 0, lsize = 1;
+		MPI_Comm_rank(node, &lrank);
+		MPI_Comm_size(node, &lsize);
+		MPI_Comm_free(&node);
+		int ndev = 1;
+		detail::check(dccrgx_device_count(&ndev));
+		if (ndev < 1) throw std::runtime_error("dccrg: no GPU visible");
+		const int device = lrank % ndev;
+		const char* env = std::getenv("DCCRGX_TRANSPORT");
+		const bool host = env && std::string(env) == "host";
+		if (size_ == 1) {
+			detail::check(dccrgx_create(0, 1, device, nullptr, &g_));
+		} else if (!host && lsize <= ndev) {
+			std::array<char, 128> id{};
+			if (rank_ == 0) detail::check(dccrgx_get_unique_id(id.data()));
+			MPI_Bcast(id.data(), 128, MPI_BYTE, 0, comm_);
+			detail::check(dccrgx_create(rank_, size_, device, id.data(), &g_));
+		} else {
+			detail::check(dccrgx_create_with_exchange(rank_, size_, device, &detail::mpi_exchange, &comm_, &g_));
+		}
+		mapping_rw.attach(g_);
+		geometry_rw.attach(g_);
+		geometry_rw.set(geometry_rw.get_params_or_default());
+	}
+	void add_payload_field() {
+		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
+		const auto w = detail::datatype_window<Cell_Data>();
+		detail::check(dccrgx_set_field_window(g_, payload_, w.first, w.second));
+		window_ = w;
+	}
+
+	size_t n_local() const {
+		size_t ni = 0, no = 0;
+		detail::check(dccrgx_get_counts(g_, &ni, &no, nullptr, nullptr));
+		return ni + no;
+	}
+	void upload_local() {
+		const size_t nl = std::min(n_local_, host_.size());
+		if (nl) detail::check(dccrgx_field_upload(g_, payload_, 0, nl, host_.data()));
+	}
+	void upload_all() {
+		if (!host_.empty()) detail::check(dccrgx_field_upload(g_, payload_, 0, host_.size(), host_.data()));
+	}
+	void download_all() {
+		if (!host_.empty()) detail::check(dccrgx_field_download(g_, payload_, 0, host_.size(), host_.data()));
+	}
+	// received bytes into the host copies of remote neighbors
+	void download_remote() {
+		const size_t nr = host_.size() - n_local_;
+		if (!nr) return;
+		std::vector<Cell_Data> tmp(nr);
+		detail::check(dccrgx_field_download(g_, payload_, n_local_, nr, tmp.data()));
+		for (size_t i = 0; i < nr; i++)
+			std::memcpy(reinterpret_cast<char*>(&host_[n_local_ + i]) + window_.first,
+			            reinterpret_cast<const char*>(&tmp[i]) + window_.first, window_.second);
+	}
+
+	// after a structural change: slots, host payloads, items, caches
+	void refresh() {
+		size_t ns = 0;
+		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
+		n_local_ = n_local();
+		slot_ids_ = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_slot_ids(g_, o, c, n); });
+		host_.assign(ns, Cell_Data{});
+		download_all();
+		refresh_items();
+	}
+
+	void refresh_items() {
+		if (!g_) return;
+		lists_.clear();
+		send_maps_.clear();
+		recv_maps_.clear();
+		user_ranges_.clear();
+		user_cells_.clear();
+		user_neighbors_.clear();
+		build_items(default_neighborhood_id, cells_rw, neighbors_rw, ranges_);
+	}
+
+	int64_t slot_of(uint64_t id) const {
+		int64_t s = -1;
+		dccrgx_get_slots(g_, &id, 1, &s);
+		return s;
+	}
+
+	// neighbors_of / neighbors_to CSR of a neighborhood (slot order)
+	void csr(int hood, int kind, std::vector<uint32_t>& ptr, std::vector<uint64_t>& ids,
+	         std::vector<int32_t>& off) const {
+		ptr.assign(n_local_ + 1, 0);
+		size_t n = 0;
+		auto call = [&](uint64_t* i, int32_t* o, size_t cap) {
+			return hood == default_neighborhood_id ? dccrgx_download_csr(g_, kind, ptr.data(), i, o, cap, &n)
+			                                       : dccrgx_download_user_csr(g_, hood, kind, ptr.data(), i, o, cap, &n);
+		};
+		int rc = call(nullptr, nullptr, 0);
+		if (rc != DCCRGX_OK && rc != DCCRGX_ERANGE) detail::check(rc);
+		ids.assign(n, 0);
+		off.assign(3 * n, 0);
+		if (n) detail::check(call(ids.data(), off.data(), n));
+	}
+
+	// update_cell_pointers (11314-11628): Cells_Item for inner, outer, remote
+	// cells; per cell [only_of | both | only_to] neighbor items, each part in
+	// (id, offset) order; ranges of / to / all into it
+	void build_items(int hood, std::vector<Cells_Item>& items, std::vector<Neighbors_Item>& nbrs,
+	                 std::array<Iterator_Storage<Cells_Item>, 5>& rg) {
+		items.clear();
+		nbrs.clear();
+		std::vector<uint32_t> op, tp;
+		std::vector<uint64_t> oi, ti;
+		std::vector<int32_t> oo, to;
+		csr(hood, 0, op, oi, oo);
+		csr(hood, 1, tp, ti, to);
+		const size_t nl = n_local_;
+		std::vector<uint64_t> all_ids(oi);
+		all_ids.insert(all_ids.end(), ti.begin(), ti.end());
+		std::vector<int64_t> slots(all_ids.size());
+		if (!all_ids.empty()) detail::check(dccrgx_get_slots(g_, all_ids.data(), all_ids.size(), slots.data()));
+		auto dptr = [&](int64_t s) -> Cell_Data* { return s >= 0 && size_t(s) < host_.size() ? &host_[size_t(s)] : nullptr; };
+		struct Part {
+			size_t b, m1, m2, e;  // [b, m1) only_of, [m1, m2) both, [m2, e) only_to
+		};
+		std::vector<Part> parts(nl);
+		std::vector<char> outer(nl, 0);
+		using Key = std::pair<uint64_t, std::array<int, 3>>;
+		for (size_t r = 0; r < nl; r++) {
+			std::vector<std::pair<Key, int64_t>> of_items, to_items;
+			for (uint32_t e = op[r]; e < op[r + 1]; e++)
+				if (oi[e] != error_cell) of_items.push_back({{oi[e], {{oo[3 * e], oo[3 * e + 1], oo[3 * e + 2]}}}, slots[e]});
+			for (uint32_t e = tp[r]; e < tp[r + 1]; e++)
+				if (ti[e] != error_cell) to_items.push_back({{ti[e], {{0, 0, 0}}}, slots[oi.size() + e]});
+			auto by_key = [](const std::pair<Key, int64_t>& a, const std::pair<Key, int64_t>& b) { return a.first < b.first; };
+			auto same = [](const std::pair<Key, int64_t>& a, const std::pair<Key, int64_t>& b) { return a.first == b.first; };
+			std::sort(of_items.begin(), of_items.end(), by_key);
+			of_items.erase(std::unique(of_items.begin(), of_items.end(), same), of_items.end());
+			std::sort(to_items.begin(), to_items.end(), by_key);
+			to_items.erase(std::unique(to_items.begin(), to_items.end(), same), to_items.end());
+			std::vector<uint64_t> to_ids;
+			for (const auto& t : to_items) to_ids.push_back(t.first.first);
+			std::vector<uint64_t> of_ids;
+			for (const auto& t : of_items) of_ids.push_back(t.first.first);
+			std::sort(of_ids.begin(), of_ids.end());
+			std::vector<std::pair<Key, int64_t>> only_of, both, only_to;
+			for (const auto& t : of_items)
+				(std::binary_search(to_ids.begin(), to_ids.end(), t.first.first) ? both : only_of).push_back(t);
+			for (const auto& t : to_items)
+				if (!std::binary_search(of_ids.begin(), of_ids.end(), t.first.first)) only_to.push_back(t);
+			Part& P = parts[r];
+			P.b = nbrs.size();
+			for (auto* v : {&only_of, &both, &only_to}) {
+				if (v == &both) P.m1 = nbrs.size();
+				if (v == &only_to) P.m2 = nbrs.size();
+				for (const auto& t : *v) {
+					Neighbors_Item it{};
+					it.id = t.first.first;
+					it.data = dptr(t.second);
+					it.x = t.first.second[0];
+					it.y = t.first.second[1];
+					it.z = t.first.second[2];
+					nbrs.push_back(it);
+					if (t.second < 0 || size_t(t.second) >= nl) outer[r] = 1;
+				}
+			}
+			P.e = nbrs.size();
+		}
+		// cells: inner, outer, remote (slot order within each)
+		const size_t ns = host_.size();
+		std::vector<size_t> order;
+		for (size_t r = 0; r < nl; r++)
+			if (!outer[r]) order.push_back(r);
+		const size_t n_inner = order.size();
+		for (size_t r = 0; r < nl; r++)
+			if (outer[r]) order.push_back(r);
+		items.reserve(ns);
+		for (size_t r : order) {
+			Cells_Item c{};
+			c.id = slot_ids_[r];
+			c.data = &host_[r];
+			items.push_back(c);
+		}
+		for (size_t s = nl; s < ns; s++) {
+			Cells_Item c{};
+			c.id = slot_ids_[s];
+			c.data = &host_[s];
+			items.push_back(c);
+		}
+		for (size_t k = 0; k < nl; k++) {
+			const Part& P = parts[order[k]];
+			auto at = [&](size_t i) { return nbrs.cbegin() + ptrdiff_t(i); };
+			items[k].neighbors_of = {at(P.b), at(P.m2)};
+			items[k].neighbors_to = {at(P.m1), at(P.e)};
+			items[k].all_neighbors = {at(P.b), at(P.e)};
+		}
+		for (size_t k = nl; k < ns; k++)
+			items[k].neighbors_of = items[k].neighbors_to = items[k].all_neighbors = {nbrs.cend(), nbrs.cend()};
+		auto cat = [&](size_t i) { return items.cbegin() + ptrdiff_t(i); };
+		rg[0] = {cat(0), cat(n_inner)};
+		rg[1] = {cat(n_inner), cat(nl)};
+		rg[2] = {cat(0), cat(nl)};
+		rg[3] = {cat(nl), cat(ns)};
+		rg[4] = {cat(0), cat(ns)};
+		// Additional_*_Items hooks (7318-7339, 7387-7401)
+		for (size_t k = 0; k < nl; k++) {
+			Cells_Item& c = items[k];
+			c.update_caller(*this, static_cast<const Additional_Cell_Items&>(c)...);
+			for (size_t i = size_t(c.all_neighbors.begin_ - nbrs.cbegin()); i < size_t(c.all_neighbors.end_ - nbrs.cbegin());
+			     i++)
+				nbrs[i].update_caller(*this, c, hood, static_cast<const Additional_Neighbor_Items&>(nbrs[i])...);
+		}
+	}
+
+	const Iterator_Storage<Cells_Item>& range(int hood, int which) const {
+		if (hood == default_neighborhood_id) return ranges_[size_t(which)];
+		auto it = user_ranges_.find(hood);
+		if (it == user_ranges_.end()) {
+			auto* self = const_cast<Dccrg*>(this);
+			size_t n = 0;
+			int rc = dccrgx_download_user_csr(g_, hood, 0, nullptr, nullptr, nullptr, 0, &n);
+			if (rc == DCCRGX_ENOTFOUND)
+				throw std::runtime_error("dccrg: neighborhood id " + std::to_string(hood) + " doesn't exist");
+			self->build_items(hood, self->user_cells_[hood], self->user_neighbors_[hood], self->user_ranges_[hood]);
+			it = user_ranges_.find(hood);
+		}
+		return it->second[size_t(which)];
+	}
+
+	const neighbor_list_t* neighbor_list(uint64_t cell, int hood, int kind) const {
+		const auto key = std::make_tuple(cell, hood, kind);
+		auto it = lists_.find(key);
+		if (it != lists_.end()) return &it->second;
+		std::vector<uint64_t> ids(8192);
+		std::vector<int32_t> off(3 * 8192);
+		size_t n = 0;
+		int rc;
+		if (hood == default_neighborhood_id)
+			rc = kind == 0 ? dccrgx_get_neighbors_of(g_, cell, ids.data(), off.data(), ids.size(), &n)
+			               : dccrgx_get_neighbors_to(g_, cell, ids.data(), ids.size(), &n);
+		else
+			rc = dccrgx_get_user_neighbors(g_, hood, cell, kind, ids.data(), off.data(), ids.size(), &n);
+		if (rc == DCCRGX_ENOTFOUND) return nullptr;
+		detail::check(rc);
+		neighbor_list_t v;
+		for (size_t i = 0; i < n; i++)
+			v.push_back({ids[i], kind == 0 ? std::array<int, 3>{{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}
+			                               : std::array<int, 3>{{0, 0, 0}}});
+		return &(lists_[key] = std::move(v));
+	}
+
+	using list_map = std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>;
+	const list_map& lists_for(int hood, bool receive) const {
+		auto& cache = receive ? recv_maps_ : send_maps_;
+		auto it = cache.find(hood);
+		if (it != cache.end()) return it->second;
+		list_map m;
+		std::vector<int32_t> peers(size_t(std::max(size_, 1)));
+		size_t np = 0;
+		detail::check(dccrgx_get_peers(g_, peers.data(), peers.size(), &np));
+		for (int p = 0; p < size_; p++) {
+			if (p == rank_) continue;
+			std::vector<uint64_t> v;
+			if (hood == default_neighborhood_id)
+				v = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) {
+					return receive ? dccrgx_get_cells_to_receive(g_, p, o, c, n) : dccrgx_get_cells_to_send(g_, p, o, c, n);
+				});
+			else
+				v = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) {
+					return dccrgx_get_user_update_list(g_, hood, p, receive ? 1 : 0, o, c, n);
+				});
+			if (v.empty()) continue;
+			auto& dst = m[p];
+			for (size_t i = 0; i < v.size(); i++) dst.push_back({v[i], int(i + 1)});
+		}
+		return cache[hood] = std::move(m);
+	}
+	const list_map& cells_to_send_map(int hood) const { return lists_for(hood, false); }
+	const list_map& cells_to_receive(int hood) const { return lists_for(hood, true); }
+	uint64_t count_updates(int hood, bool receive) const {
+		if (hood != default_neighborhood_id) {
+			size_t n = 0;
+			if (dccrgx_download_user_csr(g_, hood, 0, nullptr, nullptr, nullptr, 0, &n) == DCCRGX_ENOTFOUND)
+				return ~uint64_t(0);
+		}
+		uint64_t t = 0;
+		for (const auto& kv : lists_for(hood, receive)) t += kv.second.size();
+		return t;
+	}
+
+	// geometry parameters survive create() (set_geometry may come first)
+	struct GeometryHolder : Geometry {
+		typename Geometry::Parameters get_params_or_default() const { return params_; }
+		bool set(const typename Geometry::Parameters& p) {
+			params_ = p;
+			return Geometry::set(p);
+		}
+		typename Geometry::Parameters params_{};
+	};
+
 	dccrgx_grid* g_ = nullptr;
-	int rank_ = 0, payload_ = -1;
-	std::array<uint64_t, 3> length_{{1, 1, 1}};
+	MPI_Comm comm_ = MPI_COMM_NULL;
+	int rank_ = 0, size_ = 1, payload_ = -1;
 	int max_ref_ = 0;
-	std::array<bool, 3> periodic_{{false, false, false}};
 	unsigned hood_ = 1;
+	std::string lb_method_ = "RCB";
+	std::pair<size_t, size_t> window_{0, sizeof(Cell_Data)};
+	Grid_Topology topology_rw;
+	Mapping mapping_rw;
+	GeometryHolder geometry_rw;
+	size_t n_local_ = 0;
+	std::vector<uint64_t> slot_ids_;
 	std::vector<Cell_Data> host_;
-	std::vector<uint64_t> ids_;
+	std::vector<Cells_Item> cells_rw;
+	std::vector<Neighbors_Item> neighbors_rw;
+	std::array<Iterator_Storage<Cells_Item>, 5> ranges_{};
+	std::map<int, std::vector<Cells_Item>> user_cells_;
+	std::map<int, std::vector<Neighbors_Item>> user_neighbors_;
+	std::map<int, std::array<Iterator_Storage<Cells_Item>, 5>> user_ranges_;
+	mutable std::map<std::tuple<uint64_t, int, int>, neighbor_list_t> lists_;
+	mutable std::map<int, list_map> send_maps_, recv_maps_;
 };
 
 }  // namespace dccrg

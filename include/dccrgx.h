@@ -81,6 +81,8 @@ int dccrgx_destroy(dccrgx_grid* g);
 typedef int (*dccrgx_exchange_fn)(void* ctx, const void* const* send, const size_t* send_bytes, void* const* recv,
                                   const size_t* recv_bytes);
 int dccrgx_create_with_exchange(int rank, int size, int device, dccrgx_exchange_fn fn, void* ctx, dccrgx_grid** out);
+/* number of visible GPUs (for choosing a device per rank) */
+int dccrgx_device_count(int* n);
 
 /* ---- setup, before initialize (dccrg.hpp:8120-8230) ---------------------- */
 int dccrgx_set_initial_length(dccrgx_grid* g, const uint64_t length[3]);   /* 8120 */
@@ -122,6 +124,20 @@ int dccrgx_get_slot_ids(dccrgx_grid* g, uint64_t* out, size_t cap, size_t* n);
  * = x,y,z offsets).
  * ptr has n_local + 1 entries; *n = number of entries. */
 int dccrgx_download_csr(dccrgx_grid* g, int kind, uint32_t* ptr, uint64_t* ids, int32_t* aux, size_t cap, size_t* n);
+/* get_cells(criteria, exact_match, neighborhood_id, sorted=true) 651 with
+ * is_neighbor_type_match 2946-3053: local cells whose neighbor types (the
+ * bits has_local_neighbor_of 1, _to 2, has_remote_neighbor_of 4, _to 8 of
+ * dccrg.hpp:95-142, from neighbors_of / neighbors_to of the neighborhood)
+ * intersect the OR of the criteria (exact_match = 0) or equal one of them
+ * (exact_match = 1); nc = 0 returns every local cell; ascending id */
+int dccrgx_get_cells_by_criteria(dccrgx_grid* g, const int32_t* criteria, size_t nc, int exact_match, int hood_id,
+                                 uint64_t* out, size_t cap, size_t* n);
+/* slots of many cells (-1 when a cell has no slot on this rank) */
+int dccrgx_get_slots(dccrgx_grid* g, const uint64_t* ids, size_t n, int64_t* slots);
+/* bulk download of a user neighborhood's CSR in slot order (kind 0
+ * neighbors_of with x,y,z offsets, 1 neighbors_to); as dccrgx_download_csr */
+int dccrgx_download_user_csr(dccrgx_grid* g, int hood_id, int kind, uint32_t* ptr, uint64_t* ids, int32_t* offsets,
+                             size_t cap, size_t* n);
 /* get_neighbors_to 883 (ascending id, offsets 0) */
 int dccrgx_get_neighbors_to(dccrgx_grid* g, uint64_t cell, uint64_t* ids, size_t cap, size_t* n);
 /* get_face_neighbors_of 2806 (dirs -1,+1,-2,+2,-3,+3) */

@@ -1,27 +1,42 @@
 #!/bin/bash
-# Round-end evidence on one GPU: full GPU test suite, default bench
-# (advection, the BASELINE metric) and the other workload lines, rocprofv3
-# kernel-trace stats of the advection and game-of-life benches, PMC traffic.
-# Stops at the first failing step.
+# Evidence on one GPU: the GPU test suite, every bench line, rocprofv3
+# kernel-trace stats of the bench lines.  Stops at the first crash / hang.
+# Usage: scripts/gpu_round.sh TAG [skip-tests]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${1:-r01}
-echo "[round] $(date) host=$(hostname)"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-    > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
-tail -2 gpurun_out/pytest_gpu_${TAG}.log
-timeout -k 10 600 python -u bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || exit $?
-cat gpurun_out/bench_${TAG}.json
-for w in gol gol_amr poisson; do
-  timeout -k 10 600 python -u bench.py --workload $w $( [ $w = poisson ] && echo "--steps 200" ) \
-      > gpurun_out/bench_${w}_${TAG}.json 2> gpurun_out/bench_${w}_${TAG}.err || exit $?
-  echo "[round] bench $w done"
-done
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv -- \
-    python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof_${TAG}.json 2> gpurun_out/prof_${TAG}.err || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gol_${TAG} -o run --output-format csv -- \
-    python -u bench.py --workload gol --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof_gol_${TAG}.json 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_po_${TAG} -o run --output-format csv -- \
-    python -u bench.py --workload poisson --steps 50 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof_po_${TAG}.json 2>&1 || exit $?
-bash scripts/pmc_traffic.sh ${TAG}
+TAG=${1:-r02}
+echo "[round] $(date) host=$(hostname) nproc=$(nproc)"
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+      > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+  rc=$?
+  tail -3 gpurun_out/pytest_gpu_${TAG}.log
+  grep -E "FAILED|ERROR" gpurun_out/pytest_gpu_${TAG}.log | head -20
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+fi
+run() {  # name timeout args...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t python -u bench.py "$@" > gpurun_out/bench_${n}_${TAG}.json 2> gpurun_out/bench_${n}_${TAG}.err
+  local r=$?
+  echo "[round] bench $n rc=$r"; tail -c 1500 gpurun_out/bench_${n}_${TAG}.json; echo
+  [ $r -eq 0 ] || { tail -5 gpurun_out/bench_${n}_${TAG}.err; exit $r; }
+}
+run advection 600
+run gol 400 --workload gol
+run gol_amr 400 --workload gol_amr
+run poisson 500 --workload poisson --steps 200
+run scalability 600 --workload scalability --steps 20
+prof() {  # name timeout args...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${n}_${TAG} -o run --output-format csv -- \
+      python -u bench.py --no-cpu-baseline "$@" > gpurun_out/bench_prof_${n}_${TAG}.json 2> gpurun_out/prof_${n}_${TAG}.err
+  local r=$?
+  echo "[round] rocprof $n rc=$r"
+  [ $r -eq 0 ] || exit $r
+}
+prof advection 600 --steps 20 --warmup 2
+prof gol 400 --workload gol --steps 20 --warmup 2
+prof gol_amr 400 --workload gol_amr --steps 20 --warmup 2
+prof poisson 500 --workload poisson --steps 50 --warmup 2
+echo "[round] done $(date)"

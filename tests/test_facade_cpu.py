@@ -1,30 +1,54 @@
 """The C++ drop-in facade (include/dccrg.hpp) compiles against the C ABI and
-links against libdccrgx.so (no GPU needed to build)."""
+links against libdccrgx.so and the image's MPI (no GPU needed to build):
+the repo's example, every member of the class template, the plain-C header,
+and the reference's own examples/game_of_life.cpp with only its include
+line changed."""
 import os
 import subprocess
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include")
+MPI_INC, MPI_LIB = "/opt/conda/include", "/opt/conda/lib"
+REF_EXAMPLE = "/root/reference/examples/game_of_life.cpp"
 
 
-def test_facade_example_builds(tmp_path):
+def cxx(src, out):
     from dccrg_amd import build as B
 
     B.build()
-    out = tmp_path / "gol"
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-I", os.path.join(ROOT, "include"),
-                        os.path.join(ROOT, "examples", "game_of_life.cpp"), "-L", os.path.join(ROOT, "dccrg_amd"),
-                        "-ldccrgx", f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}", "-o", str(out)],
-                       capture_output=True, text=True)
+    return subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", INC, "-I", os.path.join(INC, "compat"), "-I",
+                           MPI_INC, str(src), "-L", os.path.join(ROOT, "dccrg_amd"), "-ldccrgx",
+                           os.path.join(MPI_LIB, "libmpi.so"),
+                           "-Wl,-rpath," + os.path.join(ROOT, "dccrg_amd") + ":/usr/lib/x86_64-linux-gnu:" + MPI_LIB,
+                           "-o", str(out)], capture_output=True, text=True)
+
+
+def test_facade_example_builds(tmp_path):
+    r = cxx(os.path.join(ROOT, "examples", "game_of_life.cpp"), tmp_path / "gol")
     assert r.returncode == 0, r.stderr
-    assert out.exists()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_EXAMPLE), reason="reference not present")
+def test_reference_example_compiles_unchanged(tmp_path):
+    """examples/game_of_life.cpp of the reference: MPI_Init, Zoltan_Initialize
+    (include/compat/zoltan.h), Dccrg<game_of_life_cell> with its
+    get_mpi_datatype, initialize(comm).balance_load(), the local / inner /
+    outer cell ranges, cell.neighbors_of / neighbor.data, the start / wait
+    halo split - only `#include "../dccrg.hpp"` becomes `#include "dccrg.hpp"`."""
+    txt = open(REF_EXAMPLE).read()
+    assert txt.count('#include "../dccrg.hpp"') == 1
+    src = tmp_path / "game_of_life.cpp"
+    src.write_text(txt.replace('#include "../dccrg.hpp"', '#include "dccrg.hpp"'))
+    r = cxx(src, tmp_path / "ref_gol")
+    assert r.returncode == 0, r.stderr
 
 
 def test_c_header_is_plain_c(tmp_path):
     src = tmp_path / "t.c"
     src.write_text('#include "dccrgx.h"\nint main(void){ return dccrgx_abi_version() == DCCRGX_ABI_VERSION ? 0 : 1; }\n')
-    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", INC, str(src),
                         "-L", os.path.join(ROOT, "dccrg_amd"), "-ldccrgx",
                         f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}", "-o", str(tmp_path / "t")],
                        capture_output=True, text=True)
@@ -34,16 +58,32 @@ def test_c_header_is_plain_c(tmp_path):
 
 def test_facade_every_member_instantiates(tmp_path):
     """Explicit instantiation compiles every member of dccrg::Dccrg (an
-    unused member of a class template is otherwise never checked)."""
-    from dccrg_amd import build as B
-
-    B.build()
+    unused member of a class template is otherwise never checked), with and
+    without Additional_*_Items hooks (tests/advection/cell.hpp's Center and
+    Is_Local shapes)."""
     src = tmp_path / "inst.cpp"
-    src.write_text('#include "dccrg.hpp"\nstruct Cell { unsigned is_alive; double x; };\n'
-                   "template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry>;\n"
-                   "template class dccrg::Dccrg<Cell>;\nint main() { return 0; }\n")
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src),
-                        "-L", os.path.join(ROOT, "dccrg_amd"), "-ldccrgx",
-                        f"-Wl,-rpath,{os.path.join(ROOT, 'dccrg_amd')}", "-o", str(tmp_path / "inst")],
-                       capture_output=True, text=True)
+    src.write_text('''#include "dccrg.hpp"
+struct Cell {
+	unsigned is_alive; double x;
+	std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple((void*)&x, 1, MPI_DOUBLE); }
+};
+struct Is_Local {
+	bool is_local = false;
+	template <class Grid, class Cell_Item, class Neighbor_Item>
+	void update(const Grid& grid, const Cell_Item&, const Neighbor_Item& n, const int&, const Is_Local&) {
+		is_local = grid.is_local(n.id);
+	}
+};
+struct Center {
+	std::array<double, 3> center;
+	template <class Grid, class Cell_Item> void update(const Grid& grid, const Cell_Item& cell, const Center&) {
+		center = grid.geometry.get_center(cell.id);
+	}
+};
+template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry>;
+template class dccrg::Dccrg<Cell>;
+template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry, std::tuple<Center>, std::tuple<Is_Local>>;
+int main() { return 0; }
+''')
+    r = cxx(src, tmp_path / "inst")
     assert r.returncode == 0, r.stderr

@@ -1,9 +1,17 @@
-"""The C++ drop-in facade (include/dccrg.hpp) end to end on the GPU: the
-example programs (built in-tree by __graft_entry__.build()) run as separate
-processes and their results equal the oracle's game of life.
-game_of_life_items is the reference's examples/game_of_life.cpp loop
-(cell.neighbors_of / neighbor.data over the iteration items) next to the
-device sweep; game_of_life is BASELINE config 1's driver on the device sweep."""
+"""The C++ drop-in facade (include/dccrg.hpp) end to end on the GPU.
+
+1. The reference's own examples/game_of_life.cpp (BASELINE config 1: 500 x
+   500 x 1, neighborhood 1, 100 turns, host loops over cell.neighbors_of /
+   neighbor.data, the start / wait halo split), compiled against the facade
+   with only its include line changed (examples/bin/ref_game_of_life, built
+   by __graft_entry__.build()), runs under mpiexec at 1 and 2 ranks sharing
+   the GPU (the library's host exchange over MPI).  Its initial state is
+   glibc rand() per process over local_cells() (inner then outer cells), as
+   the example writes it; the final states the facade dumps
+   (DCCRGX_DUMP_CELLS) must equal the oracle's game from that state.
+2. The repo's config-1 driver on the device sweep (examples/bin/game_of_life)
+   at 1 and 2 ranks against the oracle."""
+import ctypes
 import os
 import re
 import subprocess
@@ -16,6 +24,8 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "examples", "bin")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+LEN = (500, 500, 1)
 
 
 def alive0(ids):
@@ -26,34 +36,58 @@ def alive0(ids):
     return (z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32)
 
 
-def oracle_game(nx, ny, turns):
-    o = O.Grid((nx, ny, 1), 0, (False, False, False), 1, 1)
-    ids, _ = o.cells()
-    o.gol_set(ids, alive0(ids))
-    o.gol_steps(turns)
-    a = o.gol_get(ids)
-    return int(a.sum()), int(ids[a > 0].astype(np.uint64).sum())
-
-
-def run(args):
-    exe = os.path.join(BIN, args[0])
-    if not os.path.exists(exe):
-        pytest.fail(f"{exe} missing: run __graft_entry__.build() first")
-    r = subprocess.run([exe] + [str(a) for a in args[1:]], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
+def mpirun(exe, P, args=(), env=None):
+    path = os.path.join(BIN, exe)
+    if not os.path.exists(path):
+        pytest.fail(f"{path} missing: run __graft_entry__.build() first")
+    cmd = [MPIEXEC, "-n", str(P), path] + [str(a) for a in args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return r.stdout
 
 
-def test_reference_style_item_loop_matches_oracle(gpu):
-    out = run(["game_of_life_items", 48, 40, 12])
-    m = re.search(r"live (\d+) idsum (\d+) agree (\d)", out)
-    assert m and m.group(3) == "1", out
-    assert (int(m.group(1)), int(m.group(2))) == oracle_game(48, 40, 12)
+def glibc_rand(n):
+    """rand() of a fresh process (seed 1), as the example's initialize_game
+    calls it once per local cell."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(1)
+    return np.array([libc.rand() for _ in range(n)], np.float64)
 
 
-def test_config1_driver_matches_oracle(gpu):
-    out = run(["game_of_life", 20])
+@pytest.mark.parametrize("P", [1, 2])
+def test_reference_example_matches_oracle(gpu, tmp_path, P):
+    dump = tmp_path / "cells"
+    env = dict(os.environ, DCCRGX_DUMP_CELLS=str(dump))
+    out = mpirun("ref_game_of_life", P, env=env)
+    assert "Game played at" in out
+    views = O.Grid(LEN, 0, (False, False, False), 1, P)
+    ids, alive = [], []
+    for r in range(P):
+        order = np.concatenate([views.rank_cells(r, "inner"), views.rank_cells(r, "outer")])
+        rnd = glibc_rand(order.size)
+        ids.append(order)
+        alive.append((rnd / 2147483647.0 < 0.2).astype(np.uint32))
+    ids, alive = np.concatenate(ids), np.concatenate(alive)
+    o = O.Grid(LEN, 0, (False, False, False), 1, 1)
+    o.gol_set(ids, alive)
+    o.gol_steps(100)
+    exp = dict(zip(ids.tolist(), o.gol_get(ids).tolist()))
+    got = {}
+    for r in range(P):
+        raw = np.fromfile(f"{dump}.{r}", dtype=np.dtype([("id", "<u8"), ("alive", "<u4"), ("count", "<u4")]))
+        got.update(zip(raw["id"].tolist(), raw["alive"].tolist()))
+    assert len(got) == 500 * 500
+    assert got == exp
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_config1_driver_matches_oracle(gpu, P):
+    out = mpirun("game_of_life", P, [30])
     m = re.search(r"cells (\d+) turns (\d+) live (\d+)", out)
     assert m, out
     assert int(m.group(1)) == 250000
-    assert int(m.group(3)) == oracle_game(500, 500, 20)[0]
+    o = O.Grid(LEN, 0, (False, False, False), 1, 1)
+    ids, _ = o.cells()
+    o.gol_set(ids, alive0(ids))
+    o.gol_steps(30)
+    assert int(m.group(3)) == int(o.gol_get(ids).sum())

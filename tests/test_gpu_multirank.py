@@ -175,3 +175,49 @@ def test_slab_gol_structured_equals_single_rank(gpu, length, periodic, P):
         assert np.array_equal(g.fields["is_alive"].get(0, g.n_local), np.array([final[int(c)] for c in sl]))
     for g in gs + [ref]:
         g.close()
+
+
+def test_get_cells_criteria_match_neighbor_types(gpu):
+    """get_cells(criteria, exact_match) (dccrg.hpp:651-739 with
+    is_neighbor_type_match 2946-3053) on 3 detached views of a refined grid:
+    the library's answer equals the neighbor types computed here from the
+    rank's neighbors_of / neighbors_to lists and its local set, for the
+    reference's documented criteria (598-630)."""
+    from dccrg_amd.grid import (HAS_LOCAL_NEIGHBOR_BOTH, HAS_LOCAL_NEIGHBOR_OF, HAS_LOCAL_NEIGHBOR_TO,
+                                HAS_NO_NEIGHBOR, HAS_REMOTE_NEIGHBOR_BOTH, HAS_REMOTE_NEIGHBOR_OF,
+                                HAS_REMOTE_NEIGHBOR_TO)
+
+    gs, _ = views((8, 6, 5), 1, (True, False, False), 1, 3, rounds=1, frac=0.2, seed=3)
+    cases = [([], False),
+             ([HAS_NO_NEIGHBOR, HAS_LOCAL_NEIGHBOR_OF, HAS_LOCAL_NEIGHBOR_TO, HAS_LOCAL_NEIGHBOR_BOTH], True),
+             ([HAS_REMOTE_NEIGHBOR_BOTH], False), ([HAS_REMOTE_NEIGHBOR_OF], False),
+             ([HAS_LOCAL_NEIGHBOR_TO | HAS_REMOTE_NEIGHBOR_TO], True),
+             ([HAS_LOCAL_NEIGHBOR_BOTH | HAS_REMOTE_NEIGHBOR_BOTH], True)]
+    for g in gs:
+        local = set(g.local_cells().tolist())
+        slots = g.slot_ids()[: g.n_local]
+        optr, oids, _ = g.csr("of")
+        tptr, tids, _ = g.csr("to")
+        types = {}
+        for s, c in enumerate(slots.tolist()):
+            t = 0
+            for i in oids[optr[s]:optr[s + 1]].tolist():
+                t |= HAS_LOCAL_NEIGHBOR_OF if i in local else HAS_REMOTE_NEIGHBOR_OF
+            for i in tids[tptr[s]:tptr[s + 1]].tolist():
+                t |= HAS_LOCAL_NEIGHBOR_TO if i in local else HAS_REMOTE_NEIGHBOR_TO
+            types[c] = t
+        for crit, exact in cases:
+            if not crit:
+                exp = sorted(types)
+            elif exact:
+                exp = sorted(c for c, t in types.items() if t in crit)
+            else:
+                m = 0
+                for x in crit:
+                    m |= x
+                exp = sorted(c for c, t in types.items() if t & m)
+            assert g.get_cells(crit, exact).tolist() == exp, (crit, exact)
+        # the inner / outer split is the reference's process-boundary split
+        assert g.get_cells([HAS_REMOTE_NEIGHBOR_BOTH], False).tolist() == g.outer_cells().tolist()
+    for g in gs:
+        g.close()

@@ -92,6 +92,23 @@ def cpu_baseline(workload, seconds):
                 nproc=os.cpu_count(), affinity=avail, cpu_model=cpu_model())
 
 
+def measured_traffic(workload, cells, alg_bytes, world):
+    """HBM bytes per step of the workload's kernels from the committed PMC
+    passes (profiles/<workload>_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE,
+    scripts/traffic.py); only valid for the same mesh and byte accounting,
+    so it is dropped for any other cell count."""
+    tf = os.path.join(ROOT, "profiles", f"{workload}_traffic.json")
+    if world != 1 or not os.path.exists(tf):
+        return None
+    try:
+        t = json.load(open(tf))
+    except (OSError, ValueError):
+        return None
+    if t.get("cells") == cells and abs(t.get("alg_bytes_per_step", -1) - alg_bytes) <= 1e-6 * alg_bytes:
+        return t.get("hbm_bytes_per_step")
+    return None
+
+
 def alive_rule(ids):
     z = (ids ^ np.uint64(0x5DEECE66D)) + np.uint64(0x9E3779B97F4A7C15)
     z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
@@ -163,9 +180,10 @@ def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
         line = line_base("cell-updates/s, game of life 3D (BASELINE config 2)", sm[1] * a.steps / mx[0], world, a,
                          mx[0] / a.steps * 1e3, "u32", "synthetic: seeded alive(id) rule, p=0.2",
                          {"workload": f"game of life {nx}x{ny}x{nz}, neighborhood 1, non-periodic (config 2"
-                                      f"{', z slabs' if world > 1 else ''})"})
+                                      f"{', z slabs' if world > 1 else ''})", "cells_rank0": n})
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                            "frac": ach / PEAK_HBM_GBS, "traffic": None, "kernel": "gol_structured_v3",
+                            "frac": ach / PEAK_HBM_GBS, "traffic": measured_traffic("gol", n, 8 * n, world),
+                            "kernel": "gol_structured_v3",
                             "alg_bytes_per_step": 8 * n, "kernel_ms_per_step": kms / a.steps}
         line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("gol", a.cpu_seconds)
         print(json.dumps(line), flush=True)
@@ -220,10 +238,12 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                      nl * a.steps / el, 1, a, el / a.steps * 1e3, "u32/u64",
                      "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
                      {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
-                      "leaves": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
+                      "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
     line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                        "frac": ach / PEAK_HBM_GBS if ach else None,
+                        "traffic": measured_traffic("gol_amr", nl, per_cell * nl, 1),
                         "kernel": "gol_amr_collect_kernel + gol_amr_spread_kernel", "alg_bytes_per_leaf": per_cell,
+                        "alg_bytes_per_step": per_cell * nl,
                         "logical_bytes_per_leaf": logical,
                         "logical_GB_per_s": logical * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None,
                         "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}
@@ -282,11 +302,13 @@ def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                          mx[0] / it * 1e3, "f64", "synthetic: poisson3d.cpp rhs on its center-refined mesh",
                          {"workload": f"poisson3d BiCG, base {n}x{n}x{n * world}, periodic, refined twice at the "
                                       f"center, min = max = {a.steps} iterations",
-                          "solve_cells_rank0": n_solve, "setup_s": setup_s,
+                          "cells_rank0": n_solve, "setup_s": setup_s,
                           "parallelism": f"domain decomposition x{world}"})
         line["steps"] = it
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                            "frac": ach / PEAK_HBM_GBS if ach else None,
+                            "traffic": measured_traffic("poisson", n_solve, per_cell * n_solve, world),
+                            "alg_bytes_per_step": per_cell * n_solve,
                             "kernel": "po_phase_a + po_reduce + po_phase_b + po_reduce + po_phase_c",
                             "alg_bytes_per_cell_iteration": per_cell, "kernel_ms_per_step": kms / it,
                             "timed_intervals_per_step": kn / it, "residual_min": resid}
@@ -453,18 +475,7 @@ def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
     kern_s = kern_ms / 1e3
     achieved = alg_bytes_step * a.steps / kern_s / 1e9 if kern_s > 0 else None
 
-    # HBM bytes per step of the sweep kernels from the committed PMC passes
-    # (FETCH_SIZE x 2 + WRITE_SIZE, scripts/traffic.py); only valid for the
-    # same mesh, so it is dropped for any other cell count
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "advection_traffic.json")
-    if os.path.exists(tf) and world == 1:
-        try:
-            t = json.load(open(tf))
-            if t.get("cells") == n_local and t.get("alg_bytes_per_step") == alg_bytes_step:
-                traffic = t.get("hbm_bytes_per_step")
-        except (OSError, ValueError):
-            traffic = None
+    traffic = measured_traffic("advection", n_local, alg_bytes_step, world)
 
     if rank == 0:
         line = line_base("cell-updates/s (node) for 3D advection w/ halo exchange; % of HBM roofline",

@@ -50,6 +50,7 @@ _SIGS = {
     "dccrgx_get_indices": (C.c_int, [vp, u64, P(u64)]),
     "dccrgx_get_refinement_level": (C.c_int, [vp, u64]),
     "dccrgx_get_last_cell": (u64, [vp]),
+    "dccrgx_mapping_batch": (C.c_int, [vp, vp, sz, vp, vp]),
     "dccrgx_get_cells": (C.c_int, [vp, C.c_int, vp, sz, P(sz)]),
     "dccrgx_get_counts": (C.c_int, [vp, P(sz), P(sz), P(sz), P(sz)]),
     "dccrgx_get_neighbors_of": (C.c_int, [vp, u64, vp, vp, sz, P(sz)]),

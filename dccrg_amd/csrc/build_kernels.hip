@@ -307,50 +307,68 @@ __device__ __forceinline__ bool key_less(uint64_t ia, const int32_t* oa, uint64_
 // iterator neighbor range cell.neighbors_of (update_cell_pointers
 // 11451-11500): the distinct (id, offset) pairs of the row, the ones whose id
 // is not in the row's neighbors_to first ("only_of"), then the ones whose id
-// is ("both"), each class in (id, offset) order.  One thread per row; the
-// position of an entry is its rank within its class.
-__global__ void iterator_lists_kernel(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
-                                      const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id,
-                                      size_t nrows, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot,
-                                      int32_t* it_off, int pass) {
-	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
+// is ("both"), each class in (id, offset) order.  One wave per row, one lane
+// per entry; the loops over the row's other entries are wave-uniform, so
+// every lane reads the same entry (one broadcast load).
+// Pass 0 classifies every entry (0 repeat of an earlier pair, 1 only_of,
+// 2 both) and counts the distinct pairs; pass 1 places each entry at its
+// rank within its class.
+__device__ __forceinline__ bool same_pair(const uint64_t* id, const int32_t* off, uint32_t i, uint32_t j) {
+	return id[i] == id[j] && off[3 * i] == off[3 * j] && off[3 * i + 1] == off[3 * j + 1] &&
+	       off[3 * i + 2] == off[3 * j + 2];
+}
+
+__global__ void iterator_class_kernel(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
+                                      const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows, uint8_t* cls,
+                                      uint32_t* it_cnt) {
+	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
+	for (size_t r = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; r < nrows; r += waves) {
 		const uint32_t b = nof_ptr[r], e = nof_ptr[r + 1];
 		const uint32_t tb = nto_ptr[r], te = nto_ptr[r + 1];
-		auto is_dup = [&](uint32_t j) {
-			for (uint32_t i = b; i < j; i++)
-				if (nof_id[i] == nof_id[j] && nof_off[3 * i] == nof_off[3 * j] && nof_off[3 * i + 1] == nof_off[3 * j + 1] &&
-				    nof_off[3 * i + 2] == nof_off[3 * j + 2])
-					return true;
-			return false;
-		};
-		auto both = [&](uint64_t id) {
-			uint32_t lo = tb, hi = te;
-			while (lo < hi) {
-				const uint32_t mid = (lo + hi) >> 1;
-				if (nto_id[mid] < id) lo = mid + 1;
-				else hi = mid;
+		uint32_t n_all = 0;
+		for (uint32_t j0 = b; j0 < e; j0 += WAVE) {
+			const uint32_t j = j0 + lane_id();
+			uint8_t c = 0;
+			if (j < e) {
+				bool dup = false;
+				for (uint32_t i = b; i < j && !dup; i++) dup = same_pair(nof_id, nof_off, i, j);
+				if (!dup) {
+					const uint64_t id = nof_id[j];
+					uint32_t lo = tb, hi = te;
+					while (lo < hi) {
+						const uint32_t mid = (lo + hi) >> 1;
+						if (nto_id[mid] < id) lo = mid + 1;
+						else hi = mid;
+					}
+					c = (lo < te && nto_id[lo] == id) ? 2 : 1;
+				}
+				cls[j] = c;
 			}
-			return lo < te && nto_id[lo] == id;
-		};
-		uint32_t n_only = 0, n_all = 0;
-		for (uint32_t j = b; j < e; j++) {
-			if (is_dup(j)) continue;
-			n_all++;
-			if (!both(nof_id[j])) n_only++;
+			n_all += uint32_t(__popcll(__ballot(c != 0)));
 		}
-		if (pass == 0) {
-			it_cnt[r] = n_all;
-			continue;
+		if (lane_id() == 0) it_cnt[r] = n_all;
+	}
+}
+
+__global__ void iterator_fill_kernel(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
+                                     const int32_t* nof_slot, const uint8_t* cls, size_t nrows, const uint32_t* it_ptr,
+                                     int32_t* it_slot, int32_t* it_off) {
+	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
+	for (size_t r = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; r < nrows; r += waves) {
+		const uint32_t b = nof_ptr[r], e = nof_ptr[r + 1];
+		uint32_t n_only = 0;
+		for (uint32_t j0 = b; j0 < e; j0 += WAVE) {
+			const uint32_t j = j0 + lane_id();
+			n_only += uint32_t(__popcll(__ballot(j < e && cls[j] == 1)));
 		}
-		for (uint32_t j = b; j < e; j++) {
-			if (is_dup(j)) continue;
-			const bool bj = both(nof_id[j]);
+		for (uint32_t j0 = b; j0 < e; j0 += WAVE) {
+			const uint32_t j = j0 + lane_id();
+			const uint8_t cj = j < e ? cls[j] : 0;
 			uint32_t rank = 0;
-			for (uint32_t i = b; i < e; i++) {
-				if (i == j || is_dup(i) || both(nof_id[i]) != bj) continue;
-				if (key_less(nof_id[i], nof_off + 3 * i, nof_id[j], nof_off + 3 * j)) rank++;
-			}
-			const uint32_t pos = it_ptr[r] + (bj ? n_only : 0u) + rank;
+			for (uint32_t i = b; i < e; i++)
+				if (cj != 0 && cls[i] == cj && key_less(nof_id[i], nof_off + 3 * i, nof_id[j], nof_off + 3 * j)) rank++;
+			if (cj == 0) continue;
+			const uint32_t pos = it_ptr[r] + (cj == 2 ? n_only : 0u) + rank;
 			it_slot[pos] = nof_slot[j];
 			if (it_off) {
 				it_off[3 * pos] = nof_off[3 * j];
@@ -787,11 +805,15 @@ void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* ou
 
 void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
                       const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
-                      uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off, int pass,
-                      hipStream_t s) {
+                      uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
+                      int pass, hipStream_t s) {
 	if (!nrows) return;
-	iterator_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nof_ptr, nof_id, nof_off, nof_slot, nto_ptr, nto_id,
-	                                                           nrows, it_cnt, it_ptr, it_slot, it_off, pass);
+	if (pass == 0)
+		iterator_class_kernel<<<grid_for(nrows, 4), 256, 0, s>>>(nof_ptr, nof_id, nof_off, nto_ptr, nto_id, nrows, cls,
+		                                                         it_cnt);
+	else
+		iterator_fill_kernel<<<grid_for(nrows, 4), 256, 0, s>>>(nof_ptr, nof_id, nof_off, nof_slot, cls, nrows, it_ptr,
+		                                                        it_slot, it_off);
 	HIP_CHECK(hipGetLastError());
 }
 

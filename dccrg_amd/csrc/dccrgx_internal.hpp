@@ -434,11 +434,12 @@ size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
 void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s);
 // iterator ranges cell.neighbors_of (update_cell_pointers 11451-11500): pass
-// 0 counts, pass 1 fills slots (+ offsets when it_off != nullptr)
+// 0 classifies the neighbors_of entries into cls (one byte per entry) and
+// counts, pass 1 fills slots (+ offsets when it_off != nullptr)
 void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int32_t* nof_off,
                       const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
-                      uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off, int pass,
-                      hipStream_t s);
+                      uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
+                      int pass, hipStream_t s);
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
                   const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s);
 void k_remap_field(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const DevMesh& newM,

@@ -397,12 +397,14 @@ void ensure_csr(Grid& g) {
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
 	k_lookup_slots(g.nof_id.p, t_of, dm, g.nof_slot.p, err.p, s);
-	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, c_of.p, nullptr,
-	                 nullptr, nullptr, 0, s);
+	DBuf<uint8_t> cls;
+	cls.alloc(t_of + 1);
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, cls.p, c_of.p,
+	                 nullptr, nullptr, nullptr, 0, s);
 	const size_t t_it = scan_exclusive_u32(c_of.p, g.it_ptr.p, nl, s);
 	g.it_slot.alloc(t_it + 1);
 	g.it_off.alloc(3 * t_it + 3);
-	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, nullptr,
+	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, cls.p, nullptr,
 	                 g.it_ptr.p, g.it_slot.p, g.it_off.p, 1, s);
 	int32_t herr = 0;
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));

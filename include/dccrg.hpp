@@ -355,12 +355,7 @@ public:
 	Dccrg(const Dccrg&) = delete;
 	Dccrg& operator=(const Dccrg&) = delete;
 	~Dccrg() {
-		// DCCRGX_DUMP_CELLS=<path>: every rank writes its local cells (uint64
-		// id + Cell_Data bytes, ascending id) to <path>.<rank> (verification of
-		// unmodified reference programs, tests/test_gpu_facade.py)
-		if (const char* p = std::getenv("DCCRGX_DUMP_CELLS")) {
-			if (g_) dump_cells(std::string(p) + "." + std::to_string(rank_));
-		}
+		dump_cells("final");
 		if (g_) dccrgx_destroy(g_);
 		if (comm_ != MPI_COMM_NULL) {
 			int fin = 0;
@@ -531,6 +526,7 @@ public:
 
 	// ---- halo (966-1000, 5010-5367) -------------------------------------------------
 	bool update_copies_of_remote_neighbors(const int neighborhood_id = default_neighborhood_id) {
+		dump_initial();
 		upload_local();
 		if (dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) != DCCRGX_OK) return false;
 		download_remote();
@@ -538,6 +534,7 @@ public:
 	}
 	bool start_remote_neighbor_copy_updates(const int neighborhood_id = default_neighborhood_id) {
 		if (neighborhood_id != default_neighborhood_id) return update_copies_of_remote_neighbors(neighborhood_id);
+		dump_initial();
 		upload_local();
 		return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK;
 	}
@@ -635,7 +632,15 @@ public:
 	void download() { download_all(); }
 
 private:
-	void dump_cells(const std::string& path) const {
+	// DCCRGX_DUMP_CELLS=<path>: every rank writes its local cells (uint64 id +
+	// Cell_Data bytes, ascending id) to <path>.initial.<rank> at the first
+	// remote neighbor update and to <path>.final.<rank> when the grid is
+	// destroyed (verification of unmodified reference programs,
+	// tests/test_gpu_facade.py)
+	void dump_cells(const char* when) const {
+		const char* base = std::getenv("DCCRGX_DUMP_CELLS");
+		if (!base || !g_) return;
+		const std::string path = std::string(base) + "." + when + "." + std::to_string(rank_);
 		std::vector<std::pair<uint64_t, size_t>> c;
 		for (size_t s = 0; s < n_local_ && s < slot_ids_.size(); s++) c.push_back({slot_ids_[s], s});
 		std::sort(c.begin(), c.end());
@@ -689,6 +694,12 @@ private:
 		size_t ni = 0, no = 0;
 		detail::check(dccrgx_get_counts(g_, &ni, &no, nullptr, nullptr));
 		return ni + no;
+	}
+	void dump_initial() {
+		if (!dumped_initial_) {
+			dumped_initial_ = true;
+			dump_cells("initial");
+		}
 	}
 	void upload_local() {
 		const size_t nl = std::min(n_local_, host_.size());
@@ -962,6 +973,7 @@ private:
 	Mapping mapping_rw;
 	GeometryHolder geometry_rw;
 	size_t n_local_ = 0;
+	bool dumped_initial_ = false;
 	std::vector<uint64_t> slot_ids_;
 	std::vector<Cell_Data> host_;
 	std::vector<Cells_Item> cells_rw;

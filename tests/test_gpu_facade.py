@@ -5,13 +5,12 @@
    neighbor.data, the start / wait halo split), compiled against the facade
    with only its include line changed (examples/bin/ref_game_of_life, built
    by __graft_entry__.build()), runs under mpiexec at 1 and 2 ranks sharing
-   the GPU (the library's host exchange over MPI).  Its initial state is
-   glibc rand() per process over local_cells() (inner then outer cells), as
-   the example writes it; the final states the facade dumps
-   (DCCRGX_DUMP_CELLS) must equal the oracle's game from that state.
+   the GPU (the library's host exchange over MPI).  The facade dumps the
+   state the example's rand() produced as it enters turn 1 and the state
+   after the last turn (DCCRGX_DUMP_CELLS); the latter must equal the
+   oracle's 100-turn game from the former.
 2. The repo's config-1 driver on the device sweep (examples/bin/game_of_life)
    at 1 and 2 ranks against the oracle."""
-import ctypes
 import os
 import re
 import subprocess
@@ -46,36 +45,30 @@ def mpirun(exe, P, args=(), env=None):
     return r.stdout
 
 
-def glibc_rand(n):
-    """rand() of a fresh process (seed 1), as the example's initialize_game
-    calls it once per local cell."""
-    libc = ctypes.CDLL("libc.so.6")
-    libc.srand(1)
-    return np.array([libc.rand() for _ in range(n)], np.float64)
-
-
 @pytest.mark.parametrize("P", [1, 2])
 def test_reference_example_matches_oracle(gpu, tmp_path, P):
     dump = tmp_path / "cells"
     env = dict(os.environ, DCCRGX_DUMP_CELLS=str(dump))
     out = mpirun("ref_game_of_life", P, env=env)
     assert "Game played at" in out
-    views = O.Grid(LEN, 0, (False, False, False), 1, P)
-    ids, alive = [], []
-    for r in range(P):
-        order = np.concatenate([views.rank_cells(r, "inner"), views.rank_cells(r, "outer")])
-        rnd = glibc_rand(order.size)
-        ids.append(order)
-        alive.append((rnd / 2147483647.0 < 0.2).astype(np.uint32))
-    ids, alive = np.concatenate(ids), np.concatenate(alive)
+    rec = np.dtype([("id", "<u8"), ("alive", "<u4"), ("count", "<u4")])
+
+    def load(when):
+        d = {}
+        for r in range(P):
+            raw = np.fromfile(f"{dump}.{when}.{r}", dtype=rec)
+            d.update(zip(raw["id"].tolist(), raw["alive"].tolist()))
+        return d
+
+    init = load("initial")  # the example's rand() state, as it entered turn 1
+    ids = np.array(sorted(init), np.uint64)
+    a0 = np.array([init[int(c)] for c in ids], np.uint32)
+    assert 0.15 < a0.mean() < 0.25  # rand() / RAND_MAX < 0.2
     o = O.Grid(LEN, 0, (False, False, False), 1, 1)
-    o.gol_set(ids, alive)
+    o.gol_set(ids, a0)
     o.gol_steps(100)
     exp = dict(zip(ids.tolist(), o.gol_get(ids).tolist()))
-    got = {}
-    for r in range(P):
-        raw = np.fromfile(f"{dump}.{r}", dtype=np.dtype([("id", "<u8"), ("alive", "<u4"), ("count", "<u4")]))
-        got.update(zip(raw["id"].tolist(), raw["alive"].tolist()))
+    got = load("final")
     assert len(got) == 500 * 500
     assert got == exp
 

@@ -758,15 +758,15 @@ uint64_t dccrgx_get_cell_from_indices(dccrgx_grid* gp, const uint64_t ind[3], in
 
 namespace {
 // the device id math every build and sweep kernel uses (dccrgx_mapping.hpp),
-// evaluated for a batch of ids: 14 words per id (indices x3, length in
+// evaluated for a batch of ids: 15 words per id (indices x3, length in
 // indices, parent, first child, level-0 parent, siblings x8)
 __global__ void mapping_batch_kernel(MapCtx m, const uint64_t* ids, size_t n, int32_t* level, uint64_t* out) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
-		uint64_t* o = out + 14 * i;
+		uint64_t* o = out + 15 * i;
 		uint64_t x = 0, y = 0, z = 0;
 		const int l = map_indices(m, ids[i], x, y, z);
 		level[i] = l;
-		for (int k = 0; k < 14; k++) o[k] = error_cell;
+		for (int k = 0; k < 15; k++) o[k] = error_cell;
 		if (l < 0) continue;
 		o[0] = x;
 		o[1] = y;
@@ -790,13 +790,13 @@ int dccrgx_mapping_batch(dccrgx_grid* gp, const uint64_t* ids, size_t n, int32_t
 		DBuf<uint64_t> d_ids, d_out;
 		DBuf<int32_t> d_lvl;
 		d_ids.alloc(n);
-		d_out.alloc(14 * n);
+		d_out.alloc(15 * n);
 		d_lvl.alloc(n);
 		HIP_CHECK(hipMemcpyAsync(d_ids.p, ids, n * 8, hipMemcpyHostToDevice, g.s_comp));
 		mapping_batch_kernel<<<grid_for(n, 256), 256, 0, g.s_comp>>>(m, d_ids.p, n, d_lvl.p, d_out.p);
 		HIP_CHECK(hipGetLastError());
 		HIP_CHECK(hipMemcpyAsync(level, d_lvl.p, n * 4, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipMemcpyAsync(out, d_out.p, 14 * n * 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipMemcpyAsync(out, d_out.p, 15 * n * 8, hipMemcpyDeviceToHost, g.s_comp));
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		return 0;
 	});

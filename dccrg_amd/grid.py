@@ -231,7 +231,7 @@ class Dccrg:
         indices (n, 3), length, parent, child, level0_parent, siblings (n, 8)."""
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         lvl = np.empty(ids.size, np.int32)
-        out = np.empty((ids.size, 14), np.uint64)
+        out = np.empty((ids.size, 15), np.uint64)
         check(lib().dccrgx_mapping_batch(self.h, ids.ctypes.data, ids.size, lvl.ctypes.data, out.ctypes.data))
         return dict(level=lvl, indices=out[:, 0:3], length=out[:, 3], parent=out[:, 4], child=out[:, 5],
                     level0_parent=out[:, 6], siblings=out[:, 7:15])

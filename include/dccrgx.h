@@ -108,7 +108,7 @@ int dccrgx_get_indices(dccrgx_grid* g, uint64_t cell, uint64_t indices[3]);     
 int dccrgx_get_refinement_level(dccrgx_grid* g, uint64_t cell);                             /* 261 */
 uint64_t dccrgx_get_last_cell(dccrgx_grid* g);                                              /* 651 */
 /* The same id math as the device kernels evaluate it, for n ids (valid
- * before initialize): level[i] (-1 for an invalid id) and 14 words per id in
+ * before initialize): level[i] (-1 for an invalid id) and 15 words per id in
  * out, following dccrg_mapping.hpp: indices x,y,z (get_indices 217), length
  * in indices (297), parent (get_parent 367), first child (get_child 338),
  * level-0 parent (479), siblings x8 (get_siblings 449); error_cell (0) in

@@ -71,9 +71,14 @@ _SIGS = {
     "dccrgx_set_cells": (C.c_int, [vp, vp, vp, sz]),
     "dccrgx_pin": (C.c_int, [vp, u64, C.c_int]),
     "dccrgx_unpin": (C.c_int, [vp, u64]),
-    "dccrgx_balance_load": (C.c_int, [vp]),
+    "dccrgx_balance_load": (C.c_int, [vp, C.c_int]),
     "dccrgx_balance_load_to": (C.c_int, [vp, vp, vp, sz]),
-    "dccrgx_initialize_balance_load": (C.c_int, [vp, vp, vp, sz]),
+    "dccrgx_initialize_balance_load": (C.c_int, [vp, C.c_int, vp, vp, sz]),
+    "dccrgx_make_new_partition": (C.c_int, [vp, vp, vp, sz, P(sz)]),
+    "dccrgx_set_load_balancing_method": (C.c_int, [vp, C.c_char_p]),
+    "dccrgx_get_load_balancing_method": (C.c_int, [vp, C.c_char_p, sz]),
+    "dccrgx_set_cell_weight": (C.c_int, [vp, u64, C.c_double]),
+    "dccrgx_get_cell_weight": (C.c_double, [vp, u64]),
     "dccrgx_continue_balance_load": (C.c_int, [vp]),
     "dccrgx_finish_balance_load": (C.c_int, [vp]),
     "dccrgx_migration_message_size": (C.c_int, [vp, C.c_int, P(sz), P(sz)]),

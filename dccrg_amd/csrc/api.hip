@@ -1233,11 +1233,11 @@ int dccrgx_halo_place(dccrgx_grid* gp, int hood, int peer, const void* buf, size
 	});
 }
 
-int dccrgx_balance_load(dccrgx_grid* gp) {
+int dccrgx_balance_load(dccrgx_grid* gp, int use_partitioner) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
-		initialize_balance_load_impl(g, nullptr, nullptr, 0);
+		initialize_balance_load_impl(g, use_partitioner != 0, nullptr, nullptr, 0);
 		continue_balance_load_impl(g);
 		finish_balance_load_impl(g);
 		return 0;
@@ -1249,20 +1249,81 @@ int dccrgx_balance_load_to(dccrgx_grid* gp, const uint64_t* cells, const int32_t
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
 		DX_REQUIRE((cells && procs) || !n, "null export list");
-		initialize_balance_load_impl(g, cells, procs, n);
+		initialize_balance_load_impl(g, false, cells, procs, n);
 		continue_balance_load_impl(g);
 		finish_balance_load_impl(g);
 		return 0;
 	});
 }
 
-int dccrgx_initialize_balance_load(dccrgx_grid* gp, const uint64_t* cells, const int32_t* procs, size_t n) {
+int dccrgx_initialize_balance_load(dccrgx_grid* gp, int use_partitioner, const uint64_t* cells, const int32_t* procs,
+                                   size_t n) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE((cells && procs) || !n, "null export list");
-		initialize_balance_load_impl(g, cells, procs, n);
+		initialize_balance_load_impl(g, use_partitioner != 0, cells, procs, n);
 		return 0;
 	});
+}
+
+int dccrgx_make_new_partition(dccrgx_grid* gp, uint64_t* cells, int32_t* procs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		std::vector<uint64_t> c;
+		std::vector<int32_t> o;
+		rcb_partition(g, c, o);
+		if (n) *n = c.size();
+		if (c.size() > cap) return DCCRGX_ERANGE;
+		if (!c.empty()) {
+			std::copy(c.begin(), c.end(), cells);
+			std::copy(o.begin(), o.end(), procs);
+		}
+		return 0;
+	});
+}
+
+int dccrgx_set_load_balancing_method(dccrgx_grid* gp, const char* method) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(method, "null method");
+		const std::string m(method);
+		// the native partitioner is RCB; "NONE" keeps the partition (pins only)
+		if (m != "RCB" && m != "NONE") return DCCRGX_EINVAL;
+		g.lb_method = m;
+		return 0;
+	});
+}
+
+int dccrgx_get_load_balancing_method(dccrgx_grid* gp, char* out, size_t cap) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(out && cap > g.lb_method.size(), "buffer too small");
+		std::memcpy(out, g.lb_method.c_str(), g.lb_method.size() + 1);
+		return 0;
+	});
+}
+
+int dccrgx_set_cell_weight(dccrgx_grid* gp, uint64_t cell, double weight) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 6225-6235: local leaves only
+		g.weights[cell] = weight;
+		return 0;
+	});
+}
+
+double dccrgx_get_cell_weight(dccrgx_grid* gp, uint64_t cell) {
+	const double nan = std::numeric_limits<double>::quiet_NaN();
+	if (!gp || !gp->g.initialized) return nan;
+	Grid& g = gp->g;
+	try {
+		if (!is_local_cell(g, cell)) return nan;
+	} catch (...) {
+		return nan;
+	}
+	auto it = g.weights.find(cell);
+	return it == g.weights.end() ? 1.0 : it->second;
 }
 
 int dccrgx_continue_balance_load(dccrgx_grid* gp) {

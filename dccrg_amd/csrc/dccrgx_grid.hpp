@@ -24,7 +24,11 @@ void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb);
 
 std::vector<uint64_t> stop_refining_impl(Grid& g);
 
-void initialize_balance_load_impl(Grid& g, const uint64_t* cells, const int32_t* procs, size_t n);
+void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t* cells, const int32_t* procs,
+                                  size_t n);
+// partition.hip: recursive coordinate bisection of the leaves (the new
+// owner of every local cell, cells ascending); collective
+void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& owners);
 void continue_balance_load_impl(Grid& g);
 void finish_balance_load_impl(Grid& g);
 void migration_message_size(Grid& g, int peer, size_t& sb, size_t& rb);

@@ -266,6 +266,8 @@ struct Grid {
 
 	Mesh mesh;
 	std::unordered_map<uint64_t, int> pins;  // local cells pinned to a process (pin 5832-5909)
+	std::unordered_map<uint64_t, double> weights;  // set_cell_weight (6210), cleared by balance_load
+	std::string lb_method = "RCB";                 // set_load_balancing_method (8223); default 7082
 	std::vector<uint64_t> refine_requests;
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;

@@ -389,6 +389,12 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		uint64_t ch[8];
 		map_all_children(g.m, S[i], ch);
 		created.insert(created.end(), ch, ch + 8);
+		auto w = g.weights.find(S[i]);  // children inherit their parent's weight (6199-6200)
+		if (w != g.weights.end()) {
+			const double wv = w->second;
+			g.weights.erase(w);
+			for (uint64_t c : ch) g.weights[c] = wv;
+		}
 	}
 	std::sort(created.begin(), created.end());
 	Mesh known, nm;
@@ -428,17 +434,28 @@ static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids) {
 }
 
 // initialize_balance_load (3746-3884) with make_new_partition's decisions
-// (8349-8581) given as data: the pins (8426-8518, they win) and an export
-// list of local cells.  The id lists go to their new owners (ascending id,
-// the order make_new_partition sorts its receive lists in, 8482-8493) and
-// the payloads of every field are packed per destination.
-void initialize_balance_load_impl(Grid& g, const uint64_t* cells, const int32_t* procs, size_t n) {
+// (8349-8581): the partitioner's (use_partitioner, LB method not "NONE":
+// rcb_partition in partition.hip), overridden by an export list of local
+// cells given as data, overridden by the pins (8426-8518, they win).  The id
+// lists go to their new owners (ascending id, the order make_new_partition
+// sorts its receive lists in, 8482-8493) and the payloads of every field are
+// packed per destination.  Cell weights are dropped (1011-1018).
+void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t* cells, const int32_t* procs,
+                                  size_t n) {
 	DX_REQUIRE(!g.mig.active, "balance_load already in progress");
 	DX_REQUIRE(g.initialized, "not initialized");
 	if (g.size > 1) comm_require(g, "balance_load");
 	Migration& M = g.mig;
 	M = Migration{};
 	std::map<uint64_t, int> dest;
+	if (use_partitioner && g.lb_method != "NONE") {
+		std::vector<uint64_t> pc;
+		std::vector<int32_t> po;
+		rcb_partition(g, pc, po);
+		for (size_t i = 0; i < pc.size(); i++)
+			if (po[i] != g.rank) dest[pc[i]] = po[i];
+	}
+	g.weights.clear();
 	if (n) {
 		std::vector<int32_t> own(n);
 		lookup_batch(g, cells, n, own.data(), nullptr);
@@ -446,6 +463,7 @@ void initialize_balance_load_impl(Grid& g, const uint64_t* cells, const int32_t*
 			DX_REQUIRE(procs[i] >= 0 && procs[i] < g.size, "new process out of range");
 			DX_REQUIRE(own[i] == g.rank, "balance_load: only local cells can be exported");
 			if (procs[i] != g.rank) dest[cells[i]] = procs[i];
+			else dest.erase(cells[i]);
 		}
 	}
 	std::vector<uint64_t> pinned_out;

@@ -465,9 +465,42 @@ class Dccrg:
         check(lib().dccrgx_unpin(self.h, int(cell)))
         return True
 
-    def balance_load(self, use_zoltan=False):
-        check(lib().dccrgx_balance_load(self.h))
+    def balance_load(self, use_zoltan=True):
+        """balance_load (dccrg.hpp:1024): the native RCB partitioner (unless
+        use_zoltan is False or the method is "NONE"), then the pins; collective."""
+        check(lib().dccrgx_balance_load(self.h, 1 if use_zoltan else 0))
         return self
+
+    def make_new_partition(self):
+        """The partitioner's decision alone (no migration): (local cells
+        ascending, their new processes); collective."""
+        n = C.c_size_t()
+        rc = lib().dccrgx_make_new_partition(self.h, None, None, 0, C.byref(n))
+        if rc != ERANGE:
+            check(rc)
+        cells = np.empty(n.value, np.uint64)
+        procs = np.empty(n.value, np.int32)
+        check(lib().dccrgx_make_new_partition(self.h, _ptr(cells), _ptr(procs), n.value, C.byref(n)))
+        return cells, procs
+
+    def set_load_balancing_method(self, method):
+        check(lib().dccrgx_set_load_balancing_method(self.h, method.encode()))
+        return self
+
+    def get_load_balancing_method(self):
+        buf = C.create_string_buffer(64)
+        check(lib().dccrgx_get_load_balancing_method(self.h, buf, 64))
+        return buf.value.decode()
+
+    def set_cell_weight(self, cell, weight):
+        rc = lib().dccrgx_set_cell_weight(self.h, int(cell), float(weight))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def get_cell_weight(self, cell):
+        return float(lib().dccrgx_get_cell_weight(self.h, int(cell)))
 
     def balance_load_to(self, cells, new_processes):
         """Repartition with this rank's export list (local cells and their new
@@ -478,10 +511,10 @@ class Dccrg:
         return self
 
     # split form (initialize_balance_load 3746 / continue 3899 / finish 3942)
-    def initialize_balance_load(self, cells=(), new_processes=()):
+    def initialize_balance_load(self, cells=(), new_processes=(), use_zoltan=False):
         ids = np.ascontiguousarray(cells, np.uint64)
         own = np.ascontiguousarray(new_processes, np.int32)
-        check(lib().dccrgx_initialize_balance_load(self.h, _ptr(ids), _ptr(own), ids.size))
+        check(lib().dccrgx_initialize_balance_load(self.h, 1 if use_zoltan else 0, _ptr(ids), _ptr(own), ids.size))
 
     def continue_balance_load(self):
         check(lib().dccrgx_continue_balance_load(self.h))

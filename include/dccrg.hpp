@@ -383,11 +383,15 @@ public:
 		hood_ = n;
 		return *this;
 	}
-	// the partitioner is data here (no Zoltan): the method name is kept
+	// 8223: the native partitioner is recursive coordinate bisection (Zoltan's
+	// "RCB", the reference default); "NONE" keeps the partition; any other
+	// Zoltan method name also partitions with RCB (Zoltan is not available)
 	Dccrg& set_load_balancing_method(const std::string& m) {
 		lb_method_ = m;
+		if (g_) detail::check(dccrgx_set_load_balancing_method(g_, m == "NONE" ? "NONE" : "RCB"));
 		return *this;
 	}
+	const std::string& get_load_balancing_method() const { return lb_method_; }  // 8228
 	Dccrg& set_send_single_cells(bool) { return *this; }  // one message per peer (the reference default)
 
 	// initialize (472-552)
@@ -400,6 +404,7 @@ public:
 		detail::check(dccrgx_set_periodic(g_, topology_rw.is_periodic(0), topology_rw.is_periodic(1),
 		                                  topology_rw.is_periodic(2)));
 		detail::check(dccrgx_set_neighborhood_length(g_, hood_));
+		detail::check(dccrgx_set_load_balancing_method(g_, lb_method_ == "NONE" ? "NONE" : "RCB"));
 		detail::check(dccrgx_initialize(g_));
 		add_payload_field();
 		refresh();
@@ -582,12 +587,27 @@ public:
 	bool pin(const uint64_t cell) { return pin(cell, rank_); }
 	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
 	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
-	Dccrg& balance_load(const bool /*use_zoltan*/ = true) {
+	Dccrg& balance_load(const bool use_zoltan = true) {
 		upload_local();
-		detail::check(dccrgx_balance_load(g_));
+		detail::check(dccrgx_balance_load(g_, use_zoltan ? 1 : 0));
 		refresh();
 		return *this;
 	}
+	// split form (3746, 3899, 3942): the payloads move in continue
+	void initialize_balance_load(const bool use_zoltan) {
+		upload_local();
+		detail::check(dccrgx_initialize_balance_load(g_, use_zoltan ? 1 : 0, nullptr, nullptr, 0));
+	}
+	void continue_balance_load() { detail::check(dccrgx_continue_balance_load(g_)); }
+	void finish_balance_load() {
+		detail::check(dccrgx_finish_balance_load(g_));
+		refresh();
+	}
+	// 6210 / 6244
+	bool set_cell_weight(const uint64_t cell, const double weight) {
+		return dccrgx_set_cell_weight(g_, cell, weight) == DCCRGX_OK;
+	}
+	double get_cell_weight(const uint64_t cell) const { return dccrgx_get_cell_weight(g_, cell); }
 	// a partitioner's export list: local cells and their new processes
 	Dccrg& balance_load(const std::vector<uint64_t>& cells_out, const std::vector<int>& processes) {
 		upload_local();

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 2 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 3 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -210,19 +210,36 @@ int dccrgx_load_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, siz
 
 /* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024 and its
  * split form initialize_balance_load 3746 / continue_balance_load 3899 /
- * finish_balance_load 3942).  Collective.  The new owners are the pins plus
- * an optional export list of this rank (local cells and their new process,
- * what a partitioner's Zoltan_LB_Balance export list says, make_new_partition
- * 8349-8581); pins win.  No third-party partitioner: without exports or pins
- * nothing moves (the reference with Zoltan's "NONE").  continue moves the
- * payloads of every field (RCCL or the host exchange); finish rebuilds every
- * structure on the device, fetching the new ghost leaves from their owners,
- * and places the arrived payloads. */
+ * finish_balance_load 3942).  Collective.  The new owners (make_new_partition
+ * 8349-8581) are, each overriding the one before: the native partitioner's
+ * (use_partitioner != 0 and load balancing method "RCB", the reference's
+ * default Zoltan method 7082: recursive coordinate bisection of the leaves by
+ * their centers and weights, computed on the device - parity unpinned against
+ * Zoltan, which is absent), an optional export list of this rank (local cells
+ * and their new process, a partitioner's Zoltan_LB_Balance export list), and
+ * the pins.  Method "NONE" or use_partitioner == 0: only exports and pins move
+ * (balance_load(false)).  Cell weights are dropped (1011-1018).  continue
+ * moves the payloads of every field (RCCL or the host exchange); finish
+ * rebuilds every structure on the device, fetching the new ghost leaves from
+ * their owners, and places the arrived payloads. */
 int dccrgx_pin(dccrgx_grid* g, uint64_t cell, int process);
 int dccrgx_unpin(dccrgx_grid* g, uint64_t cell);
-int dccrgx_balance_load(dccrgx_grid* g);
+int dccrgx_balance_load(dccrgx_grid* g, int use_partitioner);
 int dccrgx_balance_load_to(dccrgx_grid* g, const uint64_t* cells, const int32_t* new_process, size_t n);
-int dccrgx_initialize_balance_load(dccrgx_grid* g, const uint64_t* cells, const int32_t* new_process, size_t n);
+int dccrgx_initialize_balance_load(dccrgx_grid* g, int use_partitioner, const uint64_t* cells,
+                                   const int32_t* new_process, size_t n);
+/* the native partitioner's decision alone, no migration: every local cell
+ * (ascending id) and its new process.  Collective. */
+int dccrgx_make_new_partition(dccrgx_grid* g, uint64_t* cells, int32_t* new_process, size_t cap, size_t* n);
+/* set_load_balancing_method 8223 ("RCB" default, "NONE"; other Zoltan methods
+ * are EINVAL) / get_load_balancing_method 8228 (NUL-terminated into out) */
+int dccrgx_set_load_balancing_method(dccrgx_grid* g, const char* method);
+int dccrgx_get_load_balancing_method(dccrgx_grid* g, char* out, size_t cap);
+/* set_cell_weight 6210 (local leaves; ENOTFOUND otherwise; children inherit
+ * their parent's weight) / get_cell_weight 6244 (1 when unset, NaN for a
+ * cell that is not a local leaf) */
+int dccrgx_set_cell_weight(dccrgx_grid* g, uint64_t cell, double weight);
+double dccrgx_get_cell_weight(dccrgx_grid* g, uint64_t cell);
 int dccrgx_continue_balance_load(dccrgx_grid* g);
 int dccrgx_finish_balance_load(dccrgx_grid* g);
 /* Explicit migration transport (instead of continue_balance_load): the

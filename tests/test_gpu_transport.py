@@ -374,7 +374,7 @@ def sc_pins(rank, world):
     for c in pinned:
         assert g.pin(int(c), target)
     assert not g.pin(int(loc[0]) + 10 ** 6, target)  # not a local cell
-    g.balance_load()
+    g.balance_load(False)
     expect_here = {int(c) for r, arr in enumerate(_gather(pinned)) for c in arr if (r + 1) % world == rank}
     mine = set(g.local_cells().tolist())
     res = {"pins_arrived": expect_here.issubset(mine) and not any(int(c) in mine for c in pinned)}
@@ -383,6 +383,79 @@ def sc_pins(rank, world):
     # a second balance_load keeps the pinned cells where they are
     g.balance_load()
     res["pins_stay"] = expect_here.issubset(set(g.local_cells().tolist()))
+    g.close()
+    return res
+
+
+def sc_rcb(rank, world):
+    """balance_load() with the native partitioner (the reference default
+    Zoltan "RCB", dccrg.hpp:7082 / 8349-8376; the load_balancing_test.cpp
+    sequence): cells scattered to random processes by pins +
+    balance_load(false), unpinned, then balanced with weights on some cells.
+    The partition equals the sequential restatement of the rule
+    (oracle/rcb.py; parity unpinned against Zoltan), does not depend on the
+    scatter it starts from, every payload arrives, the structures equal the
+    oracle's views of the new partition, and children inherit weights."""
+    from oracle import oracle as O
+    from oracle import rcb as RCB
+
+    length, R = (10, 8, 6), 1
+    g = _grid(length, R, (True, False, False), 1)
+    loc = g.local_cells()
+    for c in loc[::9]:
+        g.refine_completely(int(c))
+    g.stop_refining()
+    v = g.add_field("val", np.uint32)
+    v.set(val(g.slot_ids()[: g.n_local]))
+    loc = g.local_cells()
+    # weights: some local leaves weigh 3.5 (children inherit: refine one)
+    heavy = loc[::4]
+    for c in heavy:
+        assert g.set_cell_weight(int(c), 3.5)
+    assert not g.set_cell_weight(10 ** 9, 2.0)
+    res = {"weight_get": g.get_cell_weight(int(heavy[0])) == 3.5 and g.get_cell_weight(int(loc[1])) == 1.0}
+    c_part, p_part = g.make_new_partition()
+    # sequential restatement over the gathered leaves and weights
+    allc = np.concatenate(_gather(loc))
+    allw = np.concatenate(_gather(np.array([g.get_cell_weight(int(c)) for c in loc])))
+    order = np.argsort(allc)
+    allc, allw = allc[order], allw[order]
+    c2 = RCB.centers2(O.Mapping(length, R), allc)
+    exp = RCB.rcb(allc, c2, allw, world)
+    exp_of = dict(zip(allc.tolist(), exp.tolist()))
+    res["partition_eq_rule"] = bool(np.array_equal(c_part, np.sort(loc))
+                                   and all(exp_of[int(c)] == int(p) for c, p in zip(c_part, p_part)))
+    # scatter (pins + balance_load(false), which drops the weights), unpin,
+    # set the weights again on the new owners
+    rng = np.random.default_rng(11 + rank)
+    for c in loc:
+        g.pin(int(c), int(rng.integers(0, world)))
+    g.balance_load(False)
+    for c in g.local_cells():
+        g.unpin(int(c))
+    heavy_all = set(np.concatenate(_gather(heavy)).tolist())
+    for c in g.local_cells():
+        if int(c) in heavy_all:
+            assert g.set_cell_weight(int(c), 3.5)
+    g.balance_load()
+    now = g.local_cells()
+    res["final_eq_rule"] = sorted(int(c) for c in now) == sorted(c for c, p in exp_of.items() if p == rank)
+    res["payload"] = bool(np.array_equal(v.get(0, g.n_local), val(g.slot_ids()[: g.n_local])))
+    ok, _, _ = _views_vs_oracle(g, length, R, (True, False, False), 1)
+    res["views"] = ok
+    res["weights_dropped"] = g.get_cell_weight(int(now[0])) == 1.0 if now.size else True
+    # children inherit their parent's weight (set_cell_weight 6199-6200)
+    c0 = int(now[0])
+    g.set_cell_weight(c0, 2.5)
+    if g.get_refinement_level(c0) < R:
+        g.refine_completely(c0)
+    new = g.stop_refining()
+    res["inherit"] = all(g.get_cell_weight(int(c)) == 2.5 for c in new) if len(new) else True
+    # the method switch: NONE keeps the partition
+    g.set_load_balancing_method("NONE")
+    before = g.local_cells()
+    g.balance_load()
+    res["none_keeps"] = bool(np.array_equal(before, g.local_cells())) and g.get_load_balancing_method() == "NONE"
     g.close()
     return res
 
@@ -457,8 +530,9 @@ def sc_iterators(rank, world):
 
 
 SCENARIOS = {
-    2: ["sc_config1", "sc_gol_explicit"],
-    3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators"],
+    2: ["sc_config1", "sc_gol_explicit", "sc_rcb"],
+    3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
+        "sc_rcb"],
 }
 
 
@@ -545,6 +619,11 @@ def test_migration_explicit_pack_place(transport_results):
 
 def test_pins_and_balance_load(transport_results):
     _check(transport_results, "sc_pins", ["pins_arrived", "payload", "pins_stay"])
+
+
+def test_rcb_partitioner(transport_results):
+    _check(transport_results, "sc_rcb", ["weight_get", "partition_eq_rule", "final_eq_rule", "payload", "views",
+                                         "weights_dropped", "inherit", "none_keeps"])
 
 
 def test_save_grid_data_three_ranks(transport_results):

@@ -66,6 +66,12 @@ _SIGS = {
     "dccrgx_get_cells_to_receive": (C.c_int, [vp, C.c_int, vp, sz, P(sz)]),
     "dccrgx_get_number_of_update_cells": (C.c_int, [vp, P(u64), P(u64)]),
     "dccrgx_refine_completely": (C.c_int, [vp, u64]),
+    "dccrgx_unrefine_completely": (C.c_int, [vp, u64]),
+    "dccrgx_dont_unrefine": (C.c_int, [vp, u64]),
+    "dccrgx_dont_refine": (C.c_int, [vp, u64]),
+    "dccrgx_get_removed_cells": (C.c_int, [vp, vp, sz, P(sz)]),
+    "dccrgx_removed_field_download": (C.c_int, [vp, C.c_int, vp, sz]),
+    "dccrgx_removed_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp)]),
     "dccrgx_stop_refining": (C.c_int, [vp, vp, sz, P(sz)]),
     "dccrgx_get_new_cells": (C.c_int, [vp, vp, sz, P(sz)]),
     "dccrgx_set_cells": (C.c_int, [vp, vp, vp, sz]),

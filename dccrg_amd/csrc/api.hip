@@ -1057,6 +1057,93 @@ int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
 	});
 }
 
+// unrefine_completely (2560-2660): local leaves only; level 0 is a no-op;
+// false (ENOTFOUND) when a sibling has children; a family marked by a
+// refine or dont_unrefine of a sibling, or already requested, is a no-op.
+// The neighborhood test happens in stop_refining (override_unrefines).
+int dccrgx_unrefine_completely(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
+		if (map_level(g.m, cell) == 0) return 0;
+		uint64_t sib[8];
+		map_siblings(g.m, cell, sib);
+		auto has = [](const std::vector<uint64_t>& v, uint64_t x) { return std::find(v.begin(), v.end(), x) != v.end(); };
+		for (uint64_t s : sib) {  // 2596-2607, sibling by sibling
+			if (lookup_owner(g, s) < 0) return DCCRGX_ENOTFOUND;  // the sibling has children
+			if (has(g.refine_requests, s) || has(g.dont_unrefine_cells, s)) return 0;
+		}
+		for (uint64_t s : sib)
+			if (has(g.unrefine_requests, s)) return 0;  // 2636-2641
+		g.unrefine_requests.push_back(cell);
+		return 0;
+	});
+}
+
+// dont_unrefine (2679-2733): the family of a local leaf is not merged by the
+// next stop_refining (local requests of its siblings are dropped now)
+int dccrgx_dont_unrefine(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
+		if (map_level(g.m, cell) == 0) return 0;
+		uint64_t sib[8];
+		map_siblings(g.m, cell, sib);
+		for (uint64_t s : sib)
+			if (std::find(g.dont_unrefine_cells.begin(), g.dont_unrefine_cells.end(), s) != g.dont_unrefine_cells.end())
+				return 0;
+		for (uint64_t s : sib)
+			g.unrefine_requests.erase(std::remove(g.unrefine_requests.begin(), g.unrefine_requests.end(), s),
+			                          g.unrefine_requests.end());
+		g.dont_unrefine_cells.push_back(cell);
+		return 0;
+	});
+}
+
+// dont_refine (2744-2784): the local leaf and, in stop_refining, its finer
+// neighbors (override_refines) are not refined by request
+int dccrgx_dont_refine(dccrgx_grid* gp, uint64_t cell) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
+		if (map_level(g.m, cell) >= g.R) return 0;
+		g.refine_requests.erase(std::remove(g.refine_requests.begin(), g.refine_requests.end(), cell),
+		                        g.refine_requests.end());
+		g.dont_refine_cells.push_back(cell);
+		return 0;
+	});
+}
+
+int dccrgx_get_removed_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		return copy_out_u64(g.removed_ids_h, out, cap, n);
+	});
+}
+
+int dccrgx_removed_field_download(dccrgx_grid* gp, int fid, void* host, size_t cap_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		const size_t bytes = g.removed_ids_h.size() * f.elem;
+		DX_REQUIRE(cap_bytes >= bytes, "buffer too small for the removed cells' payloads");
+		if (bytes) HIP_CHECK(hipMemcpy(host, f.removed.p, bytes, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_removed_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(ptr, "null pointer");
+		*ptr = g.removed_ids_h.empty() ? nullptr : field(g, fid).removed.p;
+		return 0;
+	});
+}
+
 int dccrgx_stop_refining(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);

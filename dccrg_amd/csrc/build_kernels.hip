@@ -562,9 +562,12 @@ __global__ void cells_under_kernel(MapCtx m, const uint64_t* ids, size_t n, cons
 // ---- refinement -------------------------------------------------------------------
 // induce_refines (9591-9720): for a requested local cell r, every existing
 // neighbors_of / neighbors_to entry coarser than r must be refined as well
+// neighbors_of / neighbors_to of the local cells of req that are coarser
+// (induce_refines 9591-9720) or, with finer != 0, finer (the dont_refine
+// spread of override_refines 9991-10038) than the cell
 __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M, int rank,
                                const uint64_t* req, size_t n, uint64_t* out, unsigned long long* counter,
-                               unsigned long long cap) {
+                               unsigned long long cap, int finer) {
 	const DevExists ex{M};
 	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
 	for (size_t w = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; w < n; w += waves) {
@@ -574,7 +577,9 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 		int lvl;
 		cell_coords(m, r, c, lvl);
 		auto emit = [&](uint64_t q) {
-			if (q == error_cell || !ex(q) || map_level(m, q) >= lvl) return;
+			if (q == error_cell || !ex(q)) return;
+			const int ql = map_level(m, q);
+			if (finer ? ql <= lvl : ql >= lvl) return;
 			const unsigned long long pos = atomicAdd(counter, 1ull);
 			if (pos < cap) out[pos] = q;
 		};
@@ -587,19 +592,71 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 	}
 }
 
+// override_unrefines (9796-9898): the family under parent p (children of
+// level L) may merge only if no leaf in p's neighborhood is finer than L and
+// none of level L is being refined.  The reference walks the face-neighbor
+// graph from the unrefined cell while is_neighbor(p, .) holds; the leaves it
+// reaches are the ones inside p's neighborhood boxes, checked here box by
+// box: a box covered by one leaf of p's level or coarser passes, otherwise
+// each of its eight level-L cells must be a leaf that is not being refined.
+__global__ void unrefine_check_kernel(MapCtx m, const int32_t* hood, int nh, DevMesh M, const uint64_t* parents,
+                                      size_t n, const uint64_t* S, size_t nS, uint8_t* ok) {
+	const DevExists ex{M};
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t c[3];
+		int pl;
+		cell_coords(m, parents[i], c, pl);
+		const int64_t len = int64_t(1) << (m.R - pl);
+		bool good = true;
+		for (int k = 0; k < nh && good; k++) {
+			uint64_t w[3];
+			bool inside = true;
+			for (int d = 0; d < 3; d++) inside = inside && map_wrap(m, d, int64_t(c[d]) + int64_t(hood[3 * k + d]) * len, w[d]);
+			if (!inside) continue;
+			bool covered = false;
+			for (int l = pl; l >= 0 && !covered; l--) covered = ex(map_from_indices(m, w[0], w[1], w[2], l));
+			if (covered) continue;
+			const uint64_t hl = uint64_t(len / 2);
+			for (int q = 0; q < 8 && good; q++) {
+				const uint64_t id = map_from_indices(m, w[0] + (q & 1) * hl, w[1] + ((q >> 1) & 1) * hl,
+				                                     w[2] + ((q >> 2) & 1) * hl, pl + 1);
+				if (!ex(id) || sorted_has(S, nS, id)) good = false;
+			}
+		}
+		ok[i] = good ? 1 : 0;
+	}
+}
+
 // execute_refines (10104-10554): children replace refined leaves and inherit
-// the owner (10228-10237)
-__global__ void refine_count_kernel(const uint64_t* kid, size_t n, const uint64_t* S, size_t nS, uint32_t* cnt) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		cnt[i] = sorted_has(S, nS, kid[i]) ? 8u : 1u;
+// the owner (10228-10237); the children of an unrefined parent are replaced
+// by the parent, owned by the owner of its first child (10298)
+__global__ void refine_count_kernel(MapCtx m, const uint64_t* kid, size_t n, const uint64_t* S, size_t nS,
+                                    const uint64_t* F, size_t nF, uint32_t* cnt) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t c = kid[i];
+		uint32_t k = 1u;
+		if (sorted_has(S, nS, c)) {
+			k = 8u;
+		} else if (nF) {
+			const uint64_t p = map_parent(m, c);
+			if (p != c && sorted_has(F, nF, p)) k = map_child(m, p) == c ? 1u : 0u;
+		}
+		cnt[i] = k;
+	}
 }
 
 __global__ void refine_fill_kernel(MapCtx m, const uint64_t* kid, const int32_t* kown, size_t n, const uint32_t* pos,
-                                   const uint32_t* cnt, uint64_t* oid, int32_t* oown) {
+                                   const uint32_t* cnt, const uint64_t* F, size_t nF, uint64_t* oid, int32_t* oown) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const size_t p = pos[i];
+		if (cnt[i] == 0u) continue;
 		if (cnt[i] == 1u) {
-			oid[p] = kid[i];
+			uint64_t c = kid[i];
+			if (nF) {
+				const uint64_t par = map_parent(m, c);
+				if (par != c && sorted_has(F, nF, par)) c = par;
+			}
+			oid[p] = c;
 			oown[p] = kown[i];
 		} else {
 			uint64_t ch[8];
@@ -945,7 +1002,8 @@ std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size
 }
 
 std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
-                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s) {
+                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s,
+                                        bool finer) {
 	if (req.empty()) return {};
 	DBuf<uint64_t> dreq;
 	upload(dreq, req, s);
@@ -956,7 +1014,7 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 		DBuf<unsigned long long> ctr;
 		zero_counter(ctr, s);
 		induced_kernel<<<grid_for(req.size(), 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p,
-		                                                       ctr.p, cap);
+		                                                       ctr.p, cap, finer ? 1 : 0);
 		HIP_CHECK(hipGetLastError());
 		const size_t k = read_counter(ctr, s);
 		if (k > cap) {
@@ -968,23 +1026,41 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 	}
 }
 
-void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
-                     DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out, hipStream_t s) {
-	DBuf<uint64_t> dS;
+std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
+                                      const std::vector<uint64_t>& parents, const std::vector<uint64_t>& S,
+                                      hipStream_t s) {
+	if (parents.empty()) return {};
+	DBuf<uint64_t> dp, dS;
+	upload(dp, parents, s);
 	upload(dS, S, s);
+	DBuf<uint8_t> ok;
+	ok.alloc(parents.size());
+	unrefine_check_kernel<<<grid_for(parents.size(), 256), 256, 0, s>>>(m, hood, nh, M, dp.p, parents.size(), dS.p,
+	                                                                   S.size(), ok.p);
+	HIP_CHECK(hipGetLastError());
+	return download(ok.p, parents.size(), s);
+}
+
+void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
+                     const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
+                     hipStream_t s) {
+	DBuf<uint64_t> dS, dF;
+	upload(dS, S, s);
+	upload(dF, F, s);
 	DBuf<uint32_t> cnt, pos;
 	cnt.alloc(n + 1);
 	pos.alloc(n + 1);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, (n + 1) * 4, s));
 	if (n) {
-		refine_count_kernel<<<grid_for(n, 256), 256, 0, s>>>(kid, n, dS.p, S.size(), cnt.p);
+		refine_count_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, n, dS.p, S.size(), dF.p, F.size(), cnt.p);
 		HIP_CHECK(hipGetLastError());
 	}
 	n_out = scan_exclusive_u32(cnt.p, pos.p, n, s);
 	out_id.alloc(n_out + 1);
 	out_own.alloc(n_out + 1);
 	if (n) {
-		refine_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, kown, n, pos.p, cnt.p, out_id.p, out_own.p);
+		refine_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, kown, n, pos.p, cnt.p, dF.p, F.size(), out_id.p,
+		                                                    out_own.p);
 		HIP_CHECK(hipGetLastError());
 	}
 	HIP_CHECK(hipStreamSynchronize(s));

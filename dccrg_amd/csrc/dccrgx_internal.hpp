@@ -122,6 +122,9 @@ struct Field {
 	size_t win_off = 0, win_len = 0;
 	DBuf<uint8_t> data;     // n_slots * elem
 	DBuf<uint8_t> scratch;  // double buffer for sweeps (allocated on demand)
+	// payloads of the cells removed by the last stop_refining whose parent is
+	// local (unrefined_cell_data 7250), in the order of Grid::removed_ids_h
+	DBuf<uint8_t> removed;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
@@ -269,6 +272,10 @@ struct Grid {
 	std::unordered_map<uint64_t, double> weights;  // set_cell_weight (6210), cleared by balance_load
 	std::string lb_method = "RCB";                 // set_load_balancing_method (8223); default 7082
 	std::vector<uint64_t> refine_requests;
+	std::vector<uint64_t> unrefine_requests;    // unrefine_completely 2560 (one sibling per family)
+	std::vector<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
+	std::vector<uint64_t> dont_refine_cells;    // dont_refine 2744
+	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;
 
@@ -456,13 +463,23 @@ std::vector<uint64_t> k_ghost_level0(const MapCtx& m, const DevMesh& M, int rank
 std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size_t n, const std::vector<uint64_t>& l0,
                                     hipStream_t s);
 // refinement closure (induce_refines 9591-9720): coarser neighbors_of /
-// neighbors_to entries of the requested local cells
+// neighbors_to entries of the requested local cells; finer: the finer ones
+// (the dont_refine spread of override_refines 9991-10038)
 std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
-                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s);
-// known list after refining the sorted set S: every known leaf in S is
-// replaced by its 8 children (same owner)
+                                        const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s,
+                                        bool finer = false);
+// override_unrefines (9796-9898) for the families under `parents`: 1 where
+// the family may merge given the final refine set S (sorted)
+std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
+                                      const std::vector<uint64_t>& parents, const std::vector<uint64_t>& S,
+                                      hipStream_t s);
+// known list after refining the sorted set S and merging the families under
+// the sorted parents F: every known leaf in S is replaced by its 8 children
+// (same owner), the children of a parent in F by the parent (owner of the
+// first child)
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
-                     DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out, hipStream_t s);
+                     const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
+                     hipStream_t s);
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {

@@ -351,26 +351,29 @@ static std::vector<uint64_t> union_sorted(const std::vector<std::vector<uint64_t
 	return u;
 }
 
-// stop_refining (3461-3485): the requests of every rank are all-gathered
-// (9594-9597), closed under induce_refines (9591-9720: a neighbors_of /
-// neighbors_to entry coarser than a refined cell is refined too - every
-// rank evaluates the rule for its own requested cells and the induced ones
-// are all-gathered in the next round), then execute_refines (10104-10554):
-// children replace their parent and inherit its owner (10228-10237).
-std::vector<uint64_t> stop_refining_impl(Grid& g) {
-	if (g.size > 1) comm_require(g, "stop_refining");
-	std::vector<uint64_t> mine = g.refine_requests;
-	g.refine_requests.clear();
-	std::sort(mine.begin(), mine.end());
-	mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
-	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
-	std::vector<uint64_t> fresh = S;
+static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids);
+
+static std::vector<uint64_t> sorted_unique(std::vector<uint64_t> v) {
+	std::sort(v.begin(), v.end());
+	v.erase(std::unique(v.begin(), v.end()), v.end());
+	return v;
+}
+
+static bool sorted_contains(const std::vector<uint64_t>& v, uint64_t x) {
+	return std::binary_search(v.begin(), v.end(), x);
+}
+
+// closure of a sorted set under a rule every rank evaluates for its own
+// cells in `fresh`, the new cells all-gathered each round (the loops of
+// induce_refines 9591-9720 and of override_refines 9991-10038)
+static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
 	const int nh = int(g.hood.size() / 3);
+	std::vector<uint64_t> fresh = S;
 	while (true) {
-		const std::vector<uint64_t> induced =
-		    k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp);
+		const std::vector<uint64_t> found =
+		    k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp, finer);
 		std::vector<uint64_t> mine_new;
-		std::set_difference(induced.begin(), induced.end(), S.begin(), S.end(), std::back_inserter(mine_new));
+		std::set_difference(found.begin(), found.end(), S.begin(), S.end(), std::back_inserter(mine_new));
 		const std::vector<uint64_t> all = union_sorted(comm_allgather_u64(g, mine_new));
 		fresh.clear();
 		std::set_difference(all.begin(), all.end(), S.begin(), S.end(), std::back_inserter(fresh));
@@ -379,8 +382,67 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		std::merge(S.begin(), S.end(), fresh.begin(), fresh.end(), std::back_inserter(merged));
 		S.swap(merged);
 	}
-	if (S.empty()) return {};
-	// local refined cells -> the new local cells
+}
+
+// stop_refining (3461-3485) = override_refines, induce_refines,
+// override_unrefines, execute_refines, distributed:
+//  * override_refines (9991-10038): dont_refine cells spread to their finer
+//    neighbors_of / neighbors_to entries until closed; refine requests of
+//    those cells are dropped; every rank's requests are all-gathered;
+//  * induce_refines (9591-9720): a neighbors_of / neighbors_to entry coarser
+//    than a refined cell is refined too - every rank evaluates the rule for
+//    its own cells, the induced ones are all-gathered each round;
+//  * override_unrefines (9796-9898): a requested family merges unless a
+//    sibling is refined or marked dont_unrefine, or its parent's
+//    neighborhood holds a finer leaf or a same-level one being refined
+//    (evaluated by the requesting rank, which knows that region);
+//  * execute_refines (10104-10554): on the device the known leaves in S are
+//    replaced by their children (the owner's, 10228-10237) and every merged
+//    family by its parent (owned by the first child's owner, 10298); the
+//    removed children's payloads go to the parent's process (10360-10410,
+//    get_removed_cells 3497), the parents start zeroed (cell_data[parent],
+//    10475) and every structure is rebuilt.
+// Returns the local cells created by refinement.
+std::vector<uint64_t> stop_refining_impl(Grid& g) {
+	if (g.size > 1) comm_require(g, "stop_refining");
+	const int nh = int(g.hood.size() / 3);
+	hipStream_t s = g.s_comp;
+	for (auto& f : g.fields) f.removed.release();
+	g.removed_ids_h.clear();
+
+	std::vector<uint64_t> D = union_sorted(comm_allgather_u64(g, sorted_unique(g.dont_refine_cells)));
+	g.dont_refine_cells.clear();
+	if (!D.empty()) close_set(g, D, true);
+	std::vector<uint64_t> mine;
+	for (uint64_t c : sorted_unique(g.refine_requests))
+		if (!sorted_contains(D, c)) mine.push_back(c);
+	g.refine_requests.clear();
+	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
+	if (!S.empty()) close_set(g, S, false);
+
+	// unrefines: one family per requested parent
+	std::vector<uint64_t> req_par;
+	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
+	req_par = sorted_unique(req_par);
+	g.unrefine_requests.clear();
+	const std::vector<uint64_t> DU = union_sorted(comm_allgather_u64(g, sorted_unique(g.dont_unrefine_cells)));
+	g.dont_unrefine_cells.clear();
+	std::vector<uint64_t> cand;
+	for (uint64_t p : req_par) {
+		uint64_t ch[8];
+		map_all_children(g.m, p, ch);
+		bool ok = true;
+		for (uint64_t c : ch) ok = ok && !sorted_contains(S, c) && !sorted_contains(DU, c);
+		if (ok) cand.push_back(p);
+	}
+	const std::vector<uint8_t> ok = k_unrefine_check(g.m, g.d_hood.p, nh, g.dm(), cand, S, s);
+	std::vector<uint64_t> fmine;
+	for (size_t i = 0; i < cand.size(); i++)
+		if (ok[i]) fmine.push_back(cand[i]);
+	const std::vector<uint64_t> F = union_sorted(comm_allgather_u64(g, fmine));
+	if (S.empty() && F.empty()) return {};
+
+	// local refined cells -> the new local cells; weights follow (6199-6200)
 	std::vector<int32_t> own(S.size());
 	lookup_batch(g, S.data(), S.size(), own.data(), nullptr);
 	std::vector<uint64_t> created;
@@ -389,19 +451,122 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		uint64_t ch[8];
 		map_all_children(g.m, S[i], ch);
 		created.insert(created.end(), ch, ch + 8);
-		auto w = g.weights.find(S[i]);  // children inherit their parent's weight (6199-6200)
+		auto w = g.weights.find(S[i]);
 		if (w != g.weights.end()) {
 			const double wv = w->second;
 			g.weights.erase(w);
 			for (uint64_t c : ch) g.weights[c] = wv;
 		}
+		g.pins.erase(S[i]);
 	}
 	std::sort(created.begin(), created.end());
+
+	// merged families: the children's payloads to the parent's new process
+	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
+	std::vector<uint64_t> keep_ids;  // removed children staying on this rank
+	if (!F.empty()) {
+		std::vector<uint64_t> ch_all(8 * F.size());
+		for (size_t i = 0; i < F.size(); i++) map_all_children(g.m, F[i], ch_all.data() + 8 * i);
+		std::vector<int32_t> ch_own(ch_all.size());
+		lookup_batch(g, ch_all.data(), ch_all.size(), ch_own.data(), nullptr);
+		for (size_t i = 0; i < F.size(); i++) {
+			const int parent_owner = ch_own[8 * i];
+			for (int k = 0; k < 8; k++) {
+				const uint64_t c = ch_all[8 * i + k];
+				const int o = ch_own[8 * i + k];
+				if (o == g.rank) {
+					g.weights.erase(c);
+					g.pins.erase(c);
+				}
+				if (o == g.rank && parent_owner == g.rank) keep_ids.push_back(c);
+				else if (o == g.rank) send_ids[parent_owner].push_back(c);
+				else if (parent_owner == g.rank && o >= 0) recv_ids[o].push_back(c);
+			}
+		}
+		for (auto* mp : {&send_ids, &recv_ids})
+			for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
+		std::sort(keep_ids.begin(), keep_ids.end());
+	}
+	size_t bpc = 0;
+	for (auto& f : g.fields) bpc += f.elem;
+	const size_t n_recv = [&] {
+		size_t k = 0;
+		for (auto& kv : recv_ids) k += kv.second.size();
+		return k;
+	}();
+	const size_t n_rm = keep_ids.size() + n_recv;
+	if (n_rm || !send_ids.empty()) {
+		// removed store order: the kept children ascending, then per source
+		// process (ascending rank) its children ascending
+		for (auto& f : g.fields) {
+			f.removed.alloc(n_rm * f.elem + 1);
+			if (!keep_ids.empty()) {
+				const DBuf<int32_t> sl = slots_of(g, keep_ids);
+				k_pack(f.data.p, f.elem, 0, f.elem, sl.p, keep_ids.size(), f.removed.p, s);
+			}
+		}
+		g.removed_ids_h = keep_ids;
+		std::vector<size_t> soff, roff;
+		size_t so = 0, ro = 0;
+		for (auto& kv : send_ids) {
+			soff.push_back(so);
+			so += kv.second.size() * bpc;
+		}
+		for (auto& kv : recv_ids) {
+			roff.push_back(ro);
+			ro += kv.second.size() * bpc;
+			g.removed_ids_h.insert(g.removed_ids_h.end(), kv.second.begin(), kv.second.end());
+		}
+		DBuf<uint8_t> sbuf, rbuf;
+		sbuf.alloc(so + 1);
+		rbuf.alloc(ro + 1);
+		size_t i = 0;
+		for (auto& kv : send_ids) {
+			const DBuf<int32_t> sl = slots_of(g, kv.second);
+			size_t o = soff[i++];
+			for (auto& f : g.fields) {
+				k_pack(f.data.p, f.elem, 0, f.elem, sl.p, kv.second.size(), sbuf.p + o, s);
+				o += kv.second.size() * f.elem;
+			}
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+		std::vector<DevMsg> msgs;
+		i = 0;
+		size_t j = 0;
+		for (int p = 0; p < g.size; p++) {
+			if (p == g.rank) continue;
+			DevMsg m{p, sbuf.p, 0, rbuf.p, 0};
+			if (send_ids.count(p)) {
+				m.send = sbuf.p + soff[i++];
+				m.send_bytes = send_ids[p].size() * bpc;
+			}
+			if (recv_ids.count(p)) {
+				m.recv = rbuf.p + roff[j++];
+				m.recv_bytes = recv_ids[p].size() * bpc;
+			}
+			if (m.send_bytes || m.recv_bytes) msgs.push_back(m);
+		}
+		if (g.size > 1) comm_device_transfer(g, msgs, s);
+		// field-major messages -> the removed store after the kept children
+		j = 0;
+		size_t at = keep_ids.size();
+		for (auto& kv : recv_ids) {
+			size_t o = roff[j++];
+			for (auto& f : g.fields) {
+				HIP_CHECK(hipMemcpyAsync(f.removed.p + at * f.elem, rbuf.p + o, kv.second.size() * f.elem,
+				                         hipMemcpyDeviceToDevice, s));
+				o += kv.second.size() * f.elem;
+			}
+			at += kv.second.size();
+		}
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+
 	Mesh known, nm;
 	mesh_materialize(g, known);
 	nm.implicit = false;
 	nm.bp = known.bp;
-	k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, nm.kid, nm.kown, nm.n_known, g.s_comp);
+	k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s);
 	rebuild(g, nm);
 	return created;
 }
@@ -456,6 +621,8 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 			if (po[i] != g.rank) dest[pc[i]] = po[i];
 	}
 	g.weights.clear();
+	g.removed_ids_h.clear();  // unrefined_cell_data (3811)
+	for (auto& f : g.fields) f.removed.release();
 	if (n) {
 		std::vector<int32_t> own(n);
 		lookup_batch(g, cells, n, own.data(), nullptr);

@@ -51,6 +51,14 @@ class Field:
         a = np.ascontiguousarray(values, dtype=self.dtype.base)
         check(lib().dccrgx_field_upload(self.grid.h, self.id, slot0, a.nbytes // self.dtype.itemsize, _ptr(a)))
 
+    def get_removed(self):
+        """Payloads of the cells removed by the last stop_refining whose
+        parent is local, in the order of Dccrg.get_removed_cells(sorted=False)."""
+        n = len(self.grid.get_removed_cells(sorted=False))
+        out = np.empty(n, self.dtype)
+        check(lib().dccrgx_removed_field_download(self.grid.h, self.id, _ptr(out), out.nbytes))
+        return out
+
     def set_transfer(self, transfer: bool):
         self.transfer = bool(transfer)
         check(lib().dccrgx_set_field_transfer(self.grid.h, self.id, int(transfer)))
@@ -440,8 +448,38 @@ class Dccrg:
         check(rc)
         return True
 
+    def unrefine_completely(self, cell):
+        """unrefine_completely (dccrg.hpp:2560): False for a cell that is not
+        a local leaf or whose sibling has children."""
+        rc = lib().dccrgx_unrefine_completely(self.h, int(cell))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def dont_unrefine(self, cell):
+        rc = lib().dccrgx_dont_unrefine(self.h, int(cell))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def dont_refine(self, cell):
+        rc = lib().dccrgx_dont_refine(self.h, int(cell))
+        if rc == ENOTFOUND:
+            return False
+        check(rc)
+        return True
+
+    def get_removed_cells(self, sorted=False):
+        """Cells removed by the last stop_refining whose parent is local
+        (get_removed_cells, dccrg.hpp:3497)."""
+        ids = self._u64_query(lib().dccrgx_get_removed_cells)
+        return np.sort(ids) if sorted else ids
+
     def stop_refining(self):
-        """Executes the collected refines (collective); returns the local new cells."""
+        """Executes the collected refines and unrefines (collective); returns
+        the local cells created by refinement."""
         n = C.c_size_t()
         check(lib().dccrgx_stop_refining(self.h, None, 0, C.byref(n)))
         return self._u64_query(lib().dccrgx_get_new_cells)

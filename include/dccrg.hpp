@@ -434,11 +434,13 @@ public:
 			return dccrgx_get_cells_by_criteria(g_, c.data(), c.size(), exact_match, neighborhood_id, o, cap, n);
 		});
 	}
-	Cell_Data* operator[](const uint64_t cell) const {  // 756
+	Cell_Data* operator[](const uint64_t cell) const {  // 756: local cells, remote copies, removed cells (764)
 		int64_t s = -1;
 		if (g_) dccrgx_get_slots(g_, &cell, 1, &s);
-		if (s < 0 || size_t(s) >= host_.size()) return nullptr;
-		return const_cast<Cell_Data*>(&host_[size_t(s)]);
+		if (s >= 0 && size_t(s) < host_.size()) return const_cast<Cell_Data*>(&host_[size_t(s)]);
+		const auto it = removed_index_.find(cell);
+		if (it != removed_index_.end()) return const_cast<Cell_Data*>(&removed_[it->second]);
+		return nullptr;
 	}
 	std::array<double, 3> get_center(const uint64_t cell) const { return geometry_rw.get_center(cell); }  // 771
 
@@ -575,12 +577,30 @@ public:
 
 	// ---- refinement (2434, 3461) ------------------------------------------------------
 	bool refine_completely(const uint64_t cell) { return dccrgx_refine_completely(g_, cell) == DCCRGX_OK; }
-	std::vector<uint64_t> stop_refining(const bool = false) {
+	bool unrefine_completely(const uint64_t cell) { return dccrgx_unrefine_completely(g_, cell) == DCCRGX_OK; }  // 2560
+	bool dont_unrefine(const uint64_t cell) { return dccrgx_dont_unrefine(g_, cell) == DCCRGX_OK; }  // 2679
+	bool dont_refine(const uint64_t cell) { return dccrgx_dont_refine(g_, cell) == DCCRGX_OK; }  // 2744
+	std::vector<uint64_t> stop_refining(const bool sorted = false) {
 		upload_local();
 		size_t n = 0;
 		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
 		refresh();
-		return detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+		// removed cells' payloads on the parent's process (unrefined_cell_data 7250)
+		removed_ids_ = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_removed_cells(g_, o, c, k); });
+		removed_.assign(removed_ids_.size(), Cell_Data{});
+		removed_index_.clear();
+		for (size_t i = 0; i < removed_ids_.size(); i++) removed_index_[removed_ids_[i]] = i;
+		if (!removed_.empty())
+			detail::check(dccrgx_removed_field_download(g_, payload_, removed_.data(), removed_.size() * sizeof(Cell_Data)));
+		auto out = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+		if (sorted) std::sort(out.begin(), out.end());
+		return out;
+	}
+	// 3497: cells removed by the last stop_refining whose parent is local
+	std::vector<uint64_t> get_removed_cells(const bool sorted = false) const {
+		std::vector<uint64_t> r = removed_ids_;
+		if (sorted) std::sort(r.begin(), r.end());
+		return r;
 	}
 
 	// ---- partition (1024, 5832-5909) ---------------------------------------------------
@@ -588,6 +608,7 @@ public:
 	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
 	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
 	Dccrg& balance_load(const bool use_zoltan = true) {
+		clear_removed();
 		upload_local();
 		detail::check(dccrgx_balance_load(g_, use_zoltan ? 1 : 0));
 		refresh();
@@ -595,6 +616,7 @@ public:
 	}
 	// split form (3746, 3899, 3942): the payloads move in continue
 	void initialize_balance_load(const bool use_zoltan) {
+		clear_removed();
 		upload_local();
 		detail::check(dccrgx_initialize_balance_load(g_, use_zoltan ? 1 : 0, nullptr, nullptr, 0));
 	}
@@ -610,6 +632,7 @@ public:
 	double get_cell_weight(const uint64_t cell) const { return dccrgx_get_cell_weight(g_, cell); }
 	// a partitioner's export list: local cells and their new processes
 	Dccrg& balance_load(const std::vector<uint64_t>& cells_out, const std::vector<int>& processes) {
+		clear_removed();
 		upload_local();
 		std::vector<int32_t> p(processes.begin(), processes.end());
 		detail::check(dccrgx_balance_load_to(g_, cells_out.data(), p.data(), cells_out.size()));
@@ -714,6 +737,11 @@ private:
 		size_t ni = 0, no = 0;
 		detail::check(dccrgx_get_counts(g_, &ni, &no, nullptr, nullptr));
 		return ni + no;
+	}
+	void clear_removed() {
+		removed_ids_.clear();
+		removed_.clear();
+		removed_index_.clear();
 	}
 	void dump_initial() {
 		if (!dumped_initial_) {
@@ -994,6 +1022,9 @@ private:
 	GeometryHolder geometry_rw;
 	size_t n_local_ = 0;
 	bool dumped_initial_ = false;
+	std::vector<uint64_t> removed_ids_;
+	std::vector<Cell_Data> removed_;
+	std::unordered_map<uint64_t, size_t> removed_index_;
 	std::vector<uint64_t> slot_ids_;
 	std::vector<Cell_Data> host_;
 	std::vector<Cells_Item> cells_rw;

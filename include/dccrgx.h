@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 3 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 4 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -167,10 +167,27 @@ int dccrgx_get_cell_process(dccrgx_grid* g, uint64_t* ids, int32_t* owners, size
 /* get_number_of_update_send_cells / _receive_cells 5382-5490 */
 int dccrgx_get_number_of_update_cells(dccrgx_grid* g, uint64_t* n_send, uint64_t* n_receive);
 
-/* ---- refinement (refine_completely 2434, stop_refining 3461 -> induce_refines
- * 9591, execute_refines 10104; unrefine is not provided) ------------------ */
+/* ---- refinement (refine_completely 2434, unrefine_completely 2560,
+ * dont_unrefine 2679, dont_refine 2744, stop_refining 3461 -> override_refines
+ * 9991, induce_refines 9591, override_unrefines 9796, execute_refines 10104).
+ * Requests are local leaves only (ENOTFOUND otherwise; unrefine_completely
+ * also when a sibling has children).  stop_refining is collective: refined
+ * leaves get their 8 children (owner and, here, payload inherited), merged
+ * families become their parent (owner of the first child, payload zeroed);
+ * the removed children's payloads move to the parent's process, where
+ * get_removed_cells / dccrgx_removed_field_* expose them until the next
+ * stop_refining or balance_load (unrefined_cell_data 7250, 3497). */
 int dccrgx_refine_completely(dccrgx_grid* g, uint64_t cell);
+int dccrgx_unrefine_completely(dccrgx_grid* g, uint64_t cell);
+int dccrgx_dont_unrefine(dccrgx_grid* g, uint64_t cell);
+int dccrgx_dont_refine(dccrgx_grid* g, uint64_t cell);
 int dccrgx_stop_refining(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t* n);
+/* removed cells whose parent is local, in the order of the payload arrays
+ * below (the kept children ascending, then per source rank ascending) */
+int dccrgx_get_removed_cells(dccrgx_grid* g, uint64_t* ids, size_t cap, size_t* n);
+/* a field's payloads of those cells: n x elem_bytes */
+int dccrgx_removed_field_download(dccrgx_grid* g, int field_id, void* host, size_t cap_bytes);
+int dccrgx_removed_field_device_ptr(dccrgx_grid* g, int field_id, void** ptr);
 /* the local cells created by the last stop_refining (ascending) */
 int dccrgx_get_new_cells(dccrgx_grid* g, uint64_t* new_cells, size_t cap, size_t* n);
 

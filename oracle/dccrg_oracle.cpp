@@ -196,7 +196,8 @@ struct Grid {
 	// iterator lists are cached like the reference's update_cell_pointers
 	// (11314-11628) caches them; cleared on every rebuild
 	mutable std::unordered_map<uint64_t, nlist> it_cache;
-	std::unordered_set<uint64_t> to_refine;
+	std::unordered_set<uint64_t> to_refine, to_unrefine, not_to_unrefine, not_to_refine;
+	std::unordered_map<uint64_t, int> removed_to;  // cells removed by the last unrefine -> parent's process
 	std::unordered_map<uint64_t, int> pins;
 	// Cartesian geometry (dccrg_cartesian_geometry.hpp)
 	double start[3] = {0, 0, 0}, l0[3] = {1, 1, 1};
@@ -504,7 +505,7 @@ struct Grid {
 		}
 	}
 
-	// dccrg.hpp:2434-2520 (refine side only; unrefines are out of scope)
+	// dccrg.hpp:2434-2520
 	bool refine_completely(uint64_t c) {
 		if (c == error_cell || !exists(c)) return false;
 		if (m.level(c) == m.R) return true;
@@ -512,9 +513,150 @@ struct Grid {
 		return true;
 	}
 
-	// induce_refines dccrg.hpp:9591-9720 (single address space: all processes'
-	// lists are the same global lists) then execute_refines 10104-10554
+	// dccrg.hpp:9464-9544 and overlapping_indices 11225-11263
+	bool is_neighbor(uint64_t c1, uint64_t c2) const {
+		const idx3 i1 = m.indices(c1), i2 = m.indices(c2);
+		const uint64_t l1 = m.cell_len(c1), l2 = m.cell_len(c2);
+		uint64_t maxd = 0;
+		int overlap = 0;
+		for (int d = 0; d < 3; d++) {
+			const uint64_t gl = m.len[d] * (uint64_t(1) << m.R);
+			uint64_t dist;
+			if (i1[d] <= i2[d]) {
+				dist = (i2[d] <= i1[d] + l1) ? 0 : i2[d] - (i1[d] + l1);
+				if (periodic[d]) dist = std::min(dist, i1[d] + (gl - (i2[d] + l2)));
+			} else {
+				dist = (i1[d] <= i2[d] + l2) ? 0 : i1[d] - (i2[d] + l2);
+				if (periodic[d]) dist = std::min(dist, i2[d] + (gl - (i1[d] + l1)));
+			}
+			maxd = std::max(maxd, dist);
+			if (i1[d] + l1 > i2[d] && i1[d] < i2[d] + l2) overlap++;
+		}
+		if (hood_len == 0) return maxd < l1 && overlap >= 2;
+		return maxd < uint64_t(hood_len) * l1;
+	}
+
+	// dccrg.hpp:2560-2660; the neighbor test runs on get_parent(cell), which
+	// is the cell itself because its parent does not exist (4157-4190)
+	bool unrefine_completely(uint64_t cell) {
+		if (cell == error_cell || !exists(cell)) return false;
+		if (cell != get_child_e(cell)) return false;
+		if (m.level(cell) == 0) return true;
+		const auto sib = m.siblings(cell);
+		for (const uint64_t s : sib) {
+			if (s != get_child_e(s)) return false;
+			if (to_refine.count(s) || not_to_unrefine.count(s)) return true;
+		}
+		const uint64_t parent = get_parent_e(cell);
+		const int rl = m.level(parent);
+		for (const auto& n : find_neighbors_of(parent, hood_of)) {
+			const int nl = m.level(n.first);
+			if (nl > rl + 1) return true;
+			if (nl == rl + 1 && to_refine.count(n.first)) return true;
+		}
+		for (const uint64_t s : sib)
+			if (to_unrefine.count(s)) return true;
+		to_unrefine.insert(cell);
+		return true;
+	}
+
+	// dccrg.hpp:2679-2733
+	bool dont_unrefine(uint64_t cell) {
+		if (cell == error_cell || !exists(cell)) return false;
+		if (m.level(cell) == 0) return true;
+		const auto sib = m.siblings(cell);
+		for (const uint64_t s : sib)
+			if (not_to_unrefine.count(s)) return true;
+		for (const uint64_t s : sib) to_unrefine.erase(s);
+		not_to_unrefine.insert(cell);
+		return true;
+	}
+
+	// dccrg.hpp:2744-2784
+	bool dont_refine(uint64_t cell) {
+		if (cell == error_cell || !exists(cell)) return false;
+		if (m.level(cell) == m.R) return true;
+		to_refine.erase(cell);
+		not_to_refine.insert(cell);
+		return true;
+	}
+
+	// override_refines dccrg.hpp:9991-10038
+	void override_refines() {
+		std::unordered_set<uint64_t> new_donts, donts, old_donts;
+		do {
+			donts = new_donts;
+			new_donts.clear();
+			donts.insert(not_to_refine.begin(), not_to_refine.end());
+			not_to_refine.clear();
+			for (const uint64_t cell : donts) {
+				std::set<uint64_t> all;
+				if (nof.count(cell))
+					for (const auto& n : nof.at(cell)) all.insert(n.first);
+				if (nto.count(cell))
+					for (const auto& n : nto.at(cell)) all.insert(n.first);
+				const int rl = m.level(cell);
+				for (const uint64_t n : all) {
+					if (old_donts.count(n) || donts.count(n)) continue;
+					if (m.level(n) > rl) new_donts.insert(n);
+				}
+			}
+			old_donts.insert(donts.begin(), donts.end());
+			donts.clear();
+		} while (!new_donts.empty());
+		for (const uint64_t c : old_donts) to_refine.erase(c);
+	}
+
+	// override_unrefines dccrg.hpp:9796-9898
+	void override_unrefines() {
+		std::unordered_set<uint64_t> final_unrefines;
+		for (const uint64_t unrefined : to_unrefine) {
+			bool can = true;
+			const uint64_t parent = m.parent(unrefined);
+			for (const uint64_t s : m.all_children(parent)) {
+				if (s == error_cell) continue;
+				if (to_refine.count(s) || not_to_unrefine.count(s)) {
+					can = false;
+					break;
+				}
+			}
+			if (!can) continue;
+			const int ul = m.level(unrefined);
+			std::set<uint64_t> processed, process;
+			for (const uint64_t n : neighbors_.at(unrefined)) process.insert(n);
+			process.erase(error_cell);
+			while (!process.empty()) {
+				const uint64_t next = *process.begin();
+				processed.insert(next);
+				process.erase(next);
+				for (const uint64_t n : neighbors_.at(next)) {
+					if (n == error_cell || processed.count(n)) continue;
+					if (is_neighbor(parent, n)) process.insert(n);
+					else processed.insert(n);
+				}
+				const int rl = m.level(next);
+				if (rl < ul) continue;
+				if (rl == ul) {
+					if (to_refine.count(next)) {
+						can = false;
+						break;
+					}
+					continue;
+				}
+				can = false;
+				break;
+			}
+			if (can) final_unrefines.insert(unrefined);
+		}
+		to_unrefine = final_unrefines;
+		not_to_unrefine.clear();
+	}
+
+	// override_refines, induce_refines dccrg.hpp:9591-9720 (single address
+	// space: all processes' lists are the same global lists),
+	// override_unrefines, then execute_refines 10104-10554
 	std::vector<uint64_t> stop_refining() {
+		override_refines();
 		std::vector<uint64_t> fresh(to_refine.begin(), to_refine.end());
 		while (!fresh.empty()) {
 			std::unordered_set<uint64_t> induced;
@@ -529,6 +671,20 @@ struct Grid {
 			fresh.assign(induced.begin(), induced.end());
 			to_refine.insert(induced.begin(), induced.end());
 		}
+		override_unrefines();
+		// unrefines 10282-10410: the parent is owned by the first child's owner
+		removed_to.clear();
+		for (const uint64_t u : to_unrefine) {
+			const uint64_t parent = m.parent(u);
+			const auto sib = m.all_children(parent);
+			const int owner = cell_process.at(sib[0]);
+			for (const uint64_t s : sib) {
+				removed_to[s] = owner;
+				cell_process.erase(s);
+			}
+			cell_process[parent] = owner;
+		}
+		to_unrefine.clear();
 		std::vector<uint64_t> created;
 		for (const uint64_t r : to_refine) {
 			const int owner = cell_process.at(r);
@@ -1225,6 +1381,28 @@ void or_grid_cells(void* hp, uint64_t* ids, int32_t* owners) {
 }
 
 int or_refine_completely(void* hp, uint64_t c) { return static_cast<OracleHandle*>(hp)->g.refine_completely(c) ? 1 : 0; }
+int or_unrefine_completely(void* hp, uint64_t c) {
+	try {
+		return static_cast<OracleHandle*>(hp)->g.unrefine_completely(c) ? 1 : 0;
+	} catch (const std::exception& e) {
+		g_err = e.what();
+		return -1;
+	}
+}
+int or_dont_unrefine(void* hp, uint64_t c) { return static_cast<OracleHandle*>(hp)->g.dont_unrefine(c) ? 1 : 0; }
+int or_dont_refine(void* hp, uint64_t c) { return static_cast<OracleHandle*>(hp)->g.dont_refine(c) ? 1 : 0; }
+/* cells removed by the last stop_refining and their parent's process */
+size_t or_removed(void* hp, uint64_t* ids, int32_t* owners) {
+	auto* h = static_cast<OracleHandle*>(hp);
+	std::vector<std::pair<uint64_t, int>> v(h->g.removed_to.begin(), h->g.removed_to.end());
+	std::sort(v.begin(), v.end());
+	if (ids)
+		for (size_t i = 0; i < v.size(); i++) {
+			ids[i] = v[i].first;
+			owners[i] = v[i].second;
+		}
+	return v.size();
+}
 
 int64_t or_stop_refining(void* hp) {
 	try {

@@ -49,6 +49,11 @@ def lib():
     L.or_grid_num_cells.argtypes = [C.c_void_p]
     L.or_grid_cells.argtypes = [C.c_void_p, u64p, i32p]
     L.or_refine_completely.argtypes = [C.c_void_p, C.c_uint64]
+    L.or_unrefine_completely.argtypes = [C.c_void_p, C.c_uint64]
+    L.or_dont_unrefine.argtypes = [C.c_void_p, C.c_uint64]
+    L.or_dont_refine.argtypes = [C.c_void_p, C.c_uint64]
+    L.or_removed.restype = C.c_size_t
+    L.or_removed.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.or_stop_refining.restype = C.c_int64
     L.or_stop_refining.argtypes = [C.c_void_p]
     L.or_neighbors_.argtypes = [C.c_void_p, C.c_uint64, u64p]
@@ -166,6 +171,24 @@ class Grid:
 
     def refine_completely(self, cell):
         return bool(lib().or_refine_completely(self.h, int(cell)))
+
+    def unrefine_completely(self, cell):
+        return bool(self._chk(lib().or_unrefine_completely(self.h, int(cell))))
+
+    def dont_unrefine(self, cell):
+        return bool(lib().or_dont_unrefine(self.h, int(cell)))
+
+    def dont_refine(self, cell):
+        return bool(lib().or_dont_refine(self.h, int(cell)))
+
+    def removed(self):
+        """Cells removed by the last stop_refining (ascending) and their
+        parent's process."""
+        n = lib().or_removed(self.h, None, None)
+        ids = np.empty(n, np.uint64)
+        own = np.empty(n, np.int32)
+        lib().or_removed(self.h, ids.ctypes.data, own.ctypes.data)
+        return ids, own
 
     def stop_refining(self):
         return self._chk(lib().or_stop_refining(self.h))

@@ -460,6 +460,80 @@ def sc_rcb(rank, world):
     return res
 
 
+def sc_unrefine(rank, world):
+    """refine / unrefine / dont_unrefine / dont_refine requests from every
+    rank, stop_refining across ranks (override_refines, induce_refines,
+    override_unrefines, execute_refines): leaves and owners equal the
+    oracle's after every round, each rank's removed cells are the oracle's
+    removed cells whose parent it owns, their payloads arrived there
+    (including from other ranks), merged parents start zeroed."""
+    from oracle import oracle as O
+
+    length, R, per, hood = (8, 6, 6), 2, (True, False, False), 1
+    g = _grid(length, R, per, hood)
+    o = O.Grid(length, R, per, hood, world)
+    f = g.add_field("val", np.uint32)
+    res = {"leaves": True, "removed": True, "payload": True, "parents_zero": True, "merged": False,
+           "remote_payload": False}
+    for it in range(6):
+        if it == 2:  # split families across ranks: a third of the cells move on
+            loc = g.local_cells()
+            mv = loc[loc % np.uint64(3) == 0]
+            g.balance_load_to(mv, np.full(mv.size, (rank + 1) % world, np.int32))
+            part = _gather(g.local_cells())
+            pid = np.concatenate(part)
+            pown = np.concatenate([np.full(len(v), r, np.int32) for r, v in enumerate(part)])
+            order = np.argsort(pid)
+            o.set_cells(pid[order], pown[order])
+        f.set(val(g.slot_ids()[: g.n_local]))
+        loc = g.local_cells().tolist()
+        before = set(loc)
+        p_ref = 0.3 if it < 2 else 0.03
+        p_unref = 0.0 if it < 2 else 0.6
+        acts = []
+        for c in loc:
+            u = np.random.default_rng(c * 131 + it).random()
+            lvl = g.get_refinement_level(c)
+            if lvl > 0 and u < p_unref:
+                acts.append((0, c))
+            elif lvl > 0 and u < p_unref + 0.03:
+                acts.append((1, c))
+            elif lvl < R and u < p_unref + 0.03 + p_ref:
+                acts.append((2, c))
+            elif u < p_unref + 0.03 + p_ref + 0.02:
+                acts.append((3, c))
+        for k, c in acts:
+            (g.unrefine_completely, g.dont_unrefine, g.refine_completely, g.dont_refine)[k](c)
+        for lst in _gather(acts):
+            for k, c in lst:
+                (o.unrefine_completely, o.dont_unrefine, o.refine_completely, o.dont_refine)[k](c)
+        g.stop_refining()
+        o.stop_refining()
+        loc = _gather(g.local_cells())
+        ids = np.concatenate(loc)
+        own = np.concatenate([np.full(len(v), r, np.int32) for r, v in enumerate(loc)])
+        order = np.argsort(ids)
+        oids, oown = o.cells()
+        res["leaves"] &= bool(np.array_equal(ids[order], oids) and np.array_equal(own[order], oown))
+        rid, rown = o.removed()
+        got = g.get_removed_cells()
+        res["removed"] &= bool(np.array_equal(np.sort(got), rid[rown == rank]))
+        res["merged"] |= rid.size > 0
+        res["payload"] &= bool(np.array_equal(f.get_removed(), val(got)))
+        res["remote_payload"] |= bool(any(int(c) not in before for c in got))
+        if got.size:
+            now = g.slot_ids()[: g.n_local].tolist()
+            pos = {c: i for i, c in enumerate(now)}
+            v = f.get(0, g.n_local)
+            res["parents_zero"] &= all(v[pos[c]] == 0 for c in set(g.mapping_batch(got)["parent"].tolist()))
+    res["remote_payload"] = any(_gather(res["remote_payload"]))
+    res["merged"] = any(_gather(res["merged"]))
+    ok, _, _ = _views_vs_oracle(g, length, R, per, hood)
+    res["views"] = ok
+    g.close()
+    return res
+
+
 def sc_save(rank, world):
     """save_grid_data from 3 real ranks (offsets from the all-gathered cell
     counts) is byte-identical to the oracle's restatement of the layout and
@@ -532,7 +606,7 @@ def sc_iterators(rank, world):
 SCENARIOS = {
     2: ["sc_config1", "sc_gol_explicit", "sc_rcb"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
-        "sc_rcb"],
+        "sc_rcb", "sc_unrefine"],
 }
 
 
@@ -624,6 +698,11 @@ def test_pins_and_balance_load(transport_results):
 def test_rcb_partitioner(transport_results):
     _check(transport_results, "sc_rcb", ["weight_get", "partition_eq_rule", "final_eq_rule", "payload", "views",
                                          "weights_dropped", "inherit", "none_keeps"])
+
+
+def test_unrefine_across_ranks(transport_results):
+    _check(transport_results, "sc_unrefine", ["leaves", "removed", "payload", "parents_zero", "merged",
+                                              "remote_payload", "views"])
 
 
 def test_save_grid_data_three_ranks(transport_results):

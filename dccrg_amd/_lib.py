@@ -119,6 +119,8 @@ _SIGS = {
     "dccrgx_advection_commit": (C.c_int, [vp, C.c_int]),
     "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),
     "dccrgx_advection_max_time_step": (C.c_int, [vp, P(C.c_int), P(C.c_double)]),
+    "dccrgx_advection_check_adaptation": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, C.c_double, vp]),
+    "dccrgx_advection_adapt": (C.c_int, [vp, vp, vp]),
     "dccrgx_advection_refine_candidates": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, vp, sz, P(sz)]),
     "dccrgx_advection_layout": (C.c_int, [vp, P(u64)]),
     "dccrgx_poisson_cache": (C.c_int, [vp, C.c_int, C.c_int, vp, sz, vp, sz]),

@@ -1,6 +1,7 @@
 // dccrgx C ABI (include/dccrgx.h): every entry point wraps the host driver
 // in an exception guard and returns a status code.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -1756,6 +1757,143 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_incr
 		auto v = download(d.p, k, g.s_comp);
 		std::sort(v.begin(), v.end());
 		return copy_out_u64(v, out, cap, n);
+	});
+}
+
+// check_for_adaptation (tests/advection/adapter.hpp:47-178) + the requests
+// adapt_grid makes from its sets (187-231): per local cell the band of its
+// max_diff; band-2 cells are refined, a family with a band-1 member is kept
+// (dont_unrefine), a family whose local members are all band 0 is unrefined.
+// The reference builds the sets in local-cell order with sibling erasures;
+// their outcome per family is the one above, whatever the order.  A family
+// with a band-2 member is also marked kept: on one process the reference's
+// sibling erasure keeps it even when that member is at the maximum level
+// (whose refine request is a no-op); marking it makes every partition give
+// that one-process outcome.
+int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_increase, double diff_threshold,
+                                      double unrefine_sensitivity, uint64_t counts[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		Field& F = field(g, df);
+		DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+		if (counts) counts[0] = counts[1] = counts[2] = 0;
+		if (g.R == 0) return 0;  // 61-63
+		ensure_face(g);
+		const size_t n = g.n_local;
+		DBuf<uint8_t> band;
+		band.alloc(n + 1);
+		k_adv_bands(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p, n, diff_increase,
+		            diff_threshold, unrefine_sensitivity, band.p, g.s_comp);
+		const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
+		const auto& ids = slot_ids_host(g);
+		std::map<uint64_t, std::vector<size_t>> fam;  // parent -> local members (slots)
+		std::vector<uint64_t> ref, keep, unref;
+		for (size_t s = 0; s < n; s++) {
+			const int lvl = map_level(g.m, ids[s]);
+			if (b[s] == 2 && lvl < g.R) ref.push_back(ids[s]);
+			if (lvl > 0) fam[map_parent(g.m, ids[s])].push_back(s);
+		}
+		for (const auto& kv : fam) {
+			bool any2 = false, any1 = false;
+			size_t first1 = 0;
+			for (size_t s : kv.second) {
+				any2 = any2 || b[s] == 2;
+				if (b[s] == 1 && !any1) {
+					any1 = true;
+					first1 = s;
+				}
+			}
+			if (any2) {
+				for (size_t s : kv.second)
+					if (b[s] == 2) {
+						keep.push_back(ids[s]);
+						break;
+					}
+			} else if (any1) {
+				keep.push_back(ids[first1]);
+			} else {
+				for (size_t s : kv.second) unref.push_back(ids[s]);
+			}
+		}
+		for (uint64_t c : ref)
+			if (dccrgx_refine_completely(gp, c) == DCCRGX_OK && counts) counts[0]++;
+		for (uint64_t c : keep)
+			if (dccrgx_dont_unrefine(gp, c) == DCCRGX_OK && counts) counts[1]++;
+		for (uint64_t c : unref)
+			if (dccrgx_unrefine_completely(gp, c) == DCCRGX_OK && counts) counts[2]++;
+		return 0;
+	});
+}
+
+// adapt_grid (tests/advection/adapter.hpp:232-309): stop_refining, the new
+// children carry their parent's payload (density = parent's, 247), a merged
+// parent's density = its removed children's / 8 (260-290), velocities and
+// lengths of every local cell reset (294-305), then a halo of all seven
+// fields (transfer_all_data, 2d.cpp:400-407).  out: created, removed cells.
+int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		const double* cf[7];
+		adv_fields(g, fids, cf);
+		g.last_new_cells = stop_refining_impl(g);
+		hipStream_t s = g.s_comp;
+		double* f[7];
+		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
+		// merged parents: the store order of the removed children -> per
+		// parent its eight children in ascending id
+		const auto& rm = g.removed_ids_h;
+		std::map<uint64_t, std::array<int32_t, 8>> par;
+		for (size_t i = 0; i < rm.size(); i++) {
+			const uint64_t p = map_parent(g.m, rm[i]);
+			uint64_t ch[8];
+			map_all_children(g.m, p, ch);
+			auto it = par.find(p);
+			if (it == par.end()) {
+				std::array<int32_t, 8> a;
+				a.fill(-1);
+				it = par.emplace(p, a).first;
+			}
+			for (int k = 0; k < 8; k++)
+				if (ch[k] == rm[i]) it->second[size_t(k)] = int32_t(i);
+		}
+		if (!par.empty()) {
+			std::vector<int32_t> pslot, cidx;
+			for (const auto& kv : par) {
+				const int64_t sl = lookup_slot(g, kv.first);
+				DX_REQUIRE(sl >= 0 && size_t(sl) < g.n_local, "merged parent is not local");
+				for (int32_t v : kv.second) DX_REQUIRE(v >= 0, "a removed child's payload is missing");
+				pslot.push_back(int32_t(sl));
+				cidx.insert(cidx.end(), kv.second.begin(), kv.second.end());
+			}
+			DBuf<int32_t> dp, dc;
+			upload(dp, pslot, s);
+			upload(dc, cidx, s);
+			k_adv_parent_density(f[0], dp.p, dc.p, (const double*)field(g, fids[0]).removed.p, pslot.size(), s);
+		}
+		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
+		HIP_CHECK(hipStreamSynchronize(s));
+		// transfer_all_data: every field of the seven in this halo
+		bool saved[7];
+		for (int k = 0; k < 7; k++) {
+			Field& F = field(g, fids[k]);
+			saved[k] = F.transfer;
+			F.transfer = true;
+		}
+		try {
+			halo_start(g);
+			halo_wait(g);
+		} catch (...) {
+			for (int k = 0; k < 7; k++) field(g, fids[k]).transfer = saved[k];
+			throw;
+		}
+		for (int k = 0; k < 7; k++) field(g, fids[k]).transfer = saved[k];
+		if (out) {
+			out[0] = g.last_new_cells.size();
+			out[1] = rm.size();
+		}
+		return 0;
 	});
 }
 

@@ -516,6 +516,15 @@ void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblock
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                         const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
                         uint64_t* out, hipStream_t s);
+// adaptation of tests/advection/adapter.hpp: per local cell band (2 refine,
+// 1 keep, 0 unrefine), merged parents' densities, velocity + length reset
+void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
+                 const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
+                 double unrefine_sensitivity, uint8_t* band, hipStream_t s);
+void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
+                          size_t np, hipStream_t s);
+void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
+                 double* const f[7], hipStream_t s);
 void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 

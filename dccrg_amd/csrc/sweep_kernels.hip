@@ -177,55 +177,6 @@ __global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// Advection (tests/advection/solve.hpp:44-279), fp64, fused flux + apply.
-// Face entry = neighbor slot * 8 + dir (0..5 = -x,+x,-y,+y,-z,+z).  The flux
-// through a face is evaluated with exactly the reference's expression and
-// operand order (contraction off), so both sides of a face obtain bitwise
-// the same value; only the order of the per-cell sum differs.
-__global__ void advection_kernel(const double* __restrict__ rho, const double* __restrict__ vx,
-                                 const double* __restrict__ vy, const double* __restrict__ vz,
-                                 const double* __restrict__ lx, const double* __restrict__ ly,
-                                 const double* __restrict__ lz, double* __restrict__ rho_out,
-                                 const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent, size_t s0, size_t s1,
-                                 double dt) {
-#pragma clang fp contract(off)
-	for (size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < s1; s += size_t(gridDim.x) * blockDim.x) {
-		const double cd = rho[s];
-		const double clx = lx[s], cly = ly[s], clz = lz[s];
-		const double cvx = vx[s], cvy = vy[s], cvz = vz[s];
-		const double cv = clx * cly * clz;
-		double acc = 0;
-		const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
-		for (uint32_t e = e0; e < e1; e++) {
-			const int32_t en = ent[e];
-			const int32_t n = en >> 3;
-			const int dir = en & 7;
-			const double nd = rho[n];
-			const double nlx = lx[n], nly = ly[n], nlz = lz[n];
-			double min_area, v;
-			if (dir < 2) {
-				min_area = fmin(cly * clz, nly * nlz);
-				v = (clx * vx[n] + nlx * cvx) / (clx + nlx);
-			} else if (dir < 4) {
-				min_area = fmin(clx * clz, nlx * nlz);
-				v = (cly * vy[n] + nly * cvy) / (cly + nly);
-			} else {
-				min_area = fmin(clx * cly, nlx * nly);
-				v = (clz * vz[n] + nlz * cvz) / (clz + nlz);
-			}
-			double flux;
-			if (dir & 1) {  // positive direction
-				flux = (v >= 0 ? cd : nd) * dt * v * min_area;
-				acc -= flux / cv;
-			} else {
-				flux = (v >= 0 ? nd : cd) * dt * v * min_area;
-				acc += flux / cv;
-			}
-		}
-		rho_out[s] = cd + acc;
-	}
-}
-
 // Face flux without the division by the cell volume (applied once per cell):
 // the face velocity and the upwind flux keep the reference's expression
 // (solve.hpp:169-225), so only the per-cell rounding of the sum differs.
@@ -249,6 +200,37 @@ __device__ __forceinline__ double adv_face_flux_d(int d, double cd, double clx, 
 	if (d < 2) return adv_face_flux(d, cd, clx, cly, clz, cvx, n.d, n.lx, n.ly, n.lz, n.v, dt);
 	if (d < 4) return adv_face_flux(d, cd, cly, clx, clz, cvy, n.d, n.ly, n.lx, n.lz, n.v, dt);
 	return adv_face_flux(d, cd, clz, clx, cly, cvz, n.d, n.lz, n.lx, n.ly, n.v, dt);
+}
+
+// Advection (tests/advection/solve.hpp:44-279), fp64, fused flux + apply,
+// for runs the tile sweeps cannot take (tiles beyond the LDS capacity).
+// Face entry = neighbor slot * 8 + dir (0..5 = -x,+x,-y,+y,-z,+z).  Every
+// face flux is the tile sweeps' (the reference's expression and operand
+// order, contraction off) and they are summed in the same face order and
+// divided once by the cell volume, so a cell's new density is bitwise the
+// same whichever sweep computes it.
+__global__ void advection_kernel(const double* __restrict__ rho, const double* __restrict__ vx,
+                                 const double* __restrict__ vy, const double* __restrict__ vz,
+                                 const double* __restrict__ lx, const double* __restrict__ ly,
+                                 const double* __restrict__ lz, double* __restrict__ rho_out,
+                                 const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent, size_t s0, size_t s1,
+                                 double dt) {
+#pragma clang fp contract(off)
+	for (size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < s1; s += size_t(gridDim.x) * blockDim.x) {
+		const double cd = rho[s];
+		const double clx = lx[s], cly = ly[s], clz = lz[s];
+		const double cvx = vx[s], cvy = vy[s], cvz = vz[s];
+		double acc = 0;
+		const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
+		for (uint32_t e = e0; e < e1; e++) {
+			const int32_t en = ent[e];
+			const int32_t n = en >> 3;
+			const int dir = en & 7;
+			const double nv = dir < 2 ? vx[n] : (dir < 4 ? vy[n] : vz[n]);
+			acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, AdvNb{rho[n], lx[n], ly[n], lz[n], nv}, dt);
+		}
+		rho_out[s] = cd + acc / (clx * cly * clz);
+	}
 }
 
 // 32-bit byte offsets from a uniform base: global_load v, voff, s[base]
@@ -599,36 +581,102 @@ __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __res
 // refine decisions of check_for_adaptation (tests/advection/adapter.hpp:47-178):
 // max relative density difference over face neighbors whose transverse
 // offsets are zero (adapter.hpp:74-96), threshold (lvl+1)*diff_increase
+// max_diff of check_for_adaptation (tests/advection/adapter.hpp:74-121) of a
+// local cell: the largest relative density difference over its face
+// neighbors, counting a finer neighbor only at the cell's corner and a
+// coarser one only when the cell sits at its corner (the x, y, z offset
+// test of 84-102, the same from either side of a face)
+__device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
+                               const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t s,
+                               double diff_threshold, int& lvl) {
+	uint64_t c[3];
+	lvl = map_indices(m, slot_ids[s], c[0], c[1], c[2]);
+	const uint64_t len = uint64_t(1) << (m.R - lvl);
+	double md = 0;
+	const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
+	for (uint32_t e = e0; e < e1; e++) {
+		const int32_t en = ent[e];
+		const int32_t nsl = en >> 3;
+		const int d = (en & 7) >> 1;
+		const int nl = map_level(m, slot_ids[nsl]);
+		bool zero = true;
+		if (nl > lvl) {
+			// finer: only the first of the four face cells sits at the cell's corner
+			zero = (e == e0 || ((ent[e - 1] & 7) != (en & 7)));
+		} else if (nl < lvl) {
+			const uint64_t pl = len * 2;
+			for (int k = 0; k < 3; k++)
+				if (k != d && (c[k] & (pl - 1)) != 0) zero = false;
+		}
+		if (!zero) continue;
+		const double a = rho[s], b = rho[nsl];
+		const double diff = fabs(a - b) / (fmin(a, b) + diff_threshold);
+		md = fmax(diff, md);
+	}
+	return md;
+}
+
 __global__ void adv_candidates_kernel(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
                                       const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t n,
                                       double diff_increase, double diff_threshold, uint64_t* out,
                                       unsigned long long* counter) {
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
-		uint64_t c[3];
-		const int lvl = map_indices(m, slot_ids[s], c[0], c[1], c[2]);
-		const uint64_t len = uint64_t(1) << (m.R - lvl);
-		double md = 0;
-		const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
-		for (uint32_t e = e0; e < e1; e++) {
-			const int32_t en = ent[e];
-			const int32_t nsl = en >> 3;
-			const int d = (en & 7) >> 1;
-			const int nl = map_level(m, slot_ids[nsl]);
-			bool zero = true;
-			if (nl > lvl) {
-				// finer: only the first of the four face cells sits at the cell's corner
-				zero = (e == e0 || ((ent[e - 1] & 7) != (en & 7))) ;
-			} else if (nl < lvl) {
-				const uint64_t pl = len * 2;
-				for (int k = 0; k < 3; k++)
-					if (k != d && (c[k] & (pl - 1)) != 0) zero = false;
-			}
-			if (!zero) continue;
-			const double a = rho[s], b = rho[nsl];
-			const double diff = fabs(a - b) / (fmin(a, b) + diff_threshold);
-			md = fmax(diff, md);
-		}
+		int lvl;
+		const double md = adv_max_diff(m, rho, ptr, ent, slot_ids, s, diff_threshold, lvl);
 		if (md > (lvl + 1) * diff_increase) out[atomicAdd(counter, 1ull)] = slot_ids[s];
+	}
+}
+
+// the band of each local cell (adapter.hpp:124-176): 2 refine, 1 keep (no
+// unrefine), 0 unrefine
+__global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
+                                 const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t n,
+                                 double diff_increase, double diff_threshold, double unrefine_sensitivity,
+                                 uint8_t* __restrict__ band) {
+#pragma clang fp contract(off)
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		int lvl;
+		const double md = adv_max_diff(m, rho, ptr, ent, slot_ids, s, diff_threshold, lvl);
+		const double refine_diff = (lvl + 1) * diff_increase, unrefine_diff = unrefine_sensitivity * refine_diff;
+		band[s] = md > refine_diff ? 2 : (md >= unrefine_diff ? 1 : 0);
+	}
+}
+
+// adapt_grid (adapter.hpp:260-290): a merged parent's density is the sum of
+// its removed children's densities / 8 (children in ascending id)
+__global__ void adv_parent_density_kernel(double* __restrict__ rho, const int32_t* __restrict__ parent_slot,
+                                          const int32_t* __restrict__ child_idx, const double* __restrict__ removed_rho,
+                                          size_t np) {
+#pragma clang fp contract(off)
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < np; i += size_t(gridDim.x) * blockDim.x) {
+		double acc = 0;
+		for (int k = 0; k < 8; k++) acc += removed_rho[child_idx[8 * i + k]] / 8;
+		rho[parent_slot[i]] = acc;
+	}
+}
+
+// adapt_grid (adapter.hpp:294-305): velocity (solve.hpp:336-342) and lengths
+// (Cartesian_Geometry get_center / get_length, dccrg_cartesian_geometry.hpp:
+// 282-362) of every local cell
+__global__ void adv_reset_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, size_t n, double s0, double s1,
+                                 double l00, double l01, double l02, double* vx, double* vy, double* vz, double* lx,
+                                 double* ly, double* lz) {
+#pragma clang fp contract(off)
+	const double st[3] = {s0, s1, 0.0};
+	const double l0[3] = {l00, l01, l02};
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		uint64_t ind[3];
+		const int lvl = map_indices(m, slot_ids[s], ind[0], ind[1], ind[2]);
+		const double sf = 1.0 / double(uint64_t(1) << lvl);
+		double L[3], c[2];
+		for (int d = 0; d < 3; d++) L[d] = l0[d] * sf;
+		for (int d = 0; d < 2; d++) c[d] = st[d] + double(ind[d]) * l0[d] / double(uint64_t(1) << m.R) + L[d] / 2;
+		vx[s] = -c[1] + 0.5;
+		vy[s] = +c[0] - 0.5;
+		vz[s] = 0;
+		lx[s] = L[0];
+		ly[s] = L[1];
+		lz[s] = L[2];
 	}
 }
 
@@ -726,6 +774,30 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s) {
 	adv_dt_kernel<<<unsigned(nblocks), 256, 0, s>>>(f[1], f[2], f[3], f[4], f[5], f[6], n, partial);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
+                 const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
+                 double unrefine_sensitivity, uint8_t* band, hipStream_t s) {
+	if (!n) return;
+	adv_bands_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, face_ptr, face_ent, slot_ids, n, diff_increase,
+	                                                  diff_threshold, unrefine_sensitivity, band);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
+                          size_t np, hipStream_t s) {
+	if (!np) return;
+	adv_parent_density_kernel<<<grid_for(np, 256), 256, 0, s>>>(rho, parent_slot, child_idx, removed_rho, np);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
+                 double* const f[7], hipStream_t s) {
+	if (!n) return;
+	adv_reset_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, slot_ids, n, start[0], start[1], l0[0], l0[1], l0[2], f[1],
+	                                                  f[2], f[3], f[4], f[5], f[6]);
 	HIP_CHECK(hipGetLastError());
 }
 

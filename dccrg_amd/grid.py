@@ -699,6 +699,20 @@ class Dccrg:
                 "alg_bytes_core", "regular_tiles", "regular_cells")
         return dict(zip(keys, (int(v) for v in out)))
 
+    def advection_check_adaptation(self, density, diff_increase, diff_threshold=0.25, unrefine_sensitivity=0.5):
+        """check_for_adaptation (tests/advection/adapter.hpp:47-178) + the
+        requests of adapt_grid; returns (refines, dont_unrefines, unrefines)."""
+        c = np.zeros(3, np.uint64)
+        check(lib().dccrgx_advection_check_adaptation(self.h, density.id, float(diff_increase), float(diff_threshold),
+                                                      float(unrefine_sensitivity), _ptr(c)))
+        return tuple(int(x) for x in c)
+
+    def advection_adapt(self, fields):
+        """adapt_grid (adapter.hpp:232-309), collective; returns (created, removed)."""
+        out = np.zeros(2, np.uint64)
+        check(lib().dccrgx_advection_adapt(self.h, self._fids(fields), _ptr(out)))
+        return int(out[0]), int(out[1])
+
     def advection_refine_candidates(self, density, diff_increase, diff_threshold):
         return self._u64_query(lib().dccrgx_advection_refine_candidates, density.id, float(diff_increase),
                                float(diff_threshold))

@@ -329,6 +329,18 @@ int dccrgx_advection_max_time_step(dccrgx_grid* g, const int fields[7], double* 
 int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double diff_increase,
                                        double diff_threshold, uint64_t* out, size_t cap, size_t* n);
 
+/* grid adaptation of tests/advection (adapter.hpp): check_adaptation
+ * (47-178) classifies every local cell by the relative density difference to
+ * its face neighbors and issues the refine / dont_unrefine / unrefine
+ * requests adapt_grid would (counts: the three numbers accepted); call it
+ * between the step and the commit, as 2d.cpp does before apply_fluxes.
+ * adapt (232-309, collective): stop_refining, merged parents get their
+ * children's mean density, velocities and lengths of every local cell are
+ * reset, and all seven fields go through one halo (transfer_all_data).
+ * out: created and removed cells of this rank. */
+int dccrgx_advection_check_adaptation(dccrgx_grid* g, int density_field, double diff_increase,
+                                      double diff_threshold, double unrefine_sensitivity, uint64_t counts[3]);
+int dccrgx_advection_adapt(dccrgx_grid* g, const int fields[7], uint64_t out[2]);
 /* data layout of the advection sweep (built on first use): out[0] tile size,
  * [1] tiles, [2] distinct out-of-tile face neighbors summed over the tiles,
  * [3] largest per-tile count, [4] finer faces, [5] face-neighbor entries

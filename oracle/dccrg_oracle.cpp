@@ -1276,6 +1276,7 @@ using namespace oracle;
 struct OracleHandle {
 	Grid g;
 	std::unordered_map<uint64_t, AdvCell> adv;
+	std::set<uint64_t> adv_refine, adv_keep, adv_unrefine;  // check_for_adaptation's sets
 	std::unordered_map<uint64_t, uint32_t> gol;
 	std::unordered_map<uint64_t, GolAmrData> gola;
 	PoissonSolver po;
@@ -1612,6 +1613,118 @@ int64_t or_adv_prerefine(void* hp, double relative_diff, double diff_threshold) 
 }
 
 double or_adv_max_time_step(void* hp) { return adv_max_time_step(static_cast<OracleHandle*>(hp)->adv); }
+
+/* check_for_adaptation (tests/advection/adapter.hpp:47-178), single address
+   space, cells in ascending id order: the three sets, kept for adapt */
+int or_adv_check(void* hp, double diff_increase, double diff_threshold, double unrefine_sensitivity) {
+	try {
+		auto* h = static_cast<OracleHandle*>(hp);
+		Grid& g = h->g;
+		auto& cells = h->adv;
+		std::set<uint64_t>& to_refine = h->adv_refine;
+		std::set<uint64_t>& not_to_unrefine = h->adv_keep;
+		std::set<uint64_t>& to_unrefine = h->adv_unrefine;
+		to_refine.clear();
+		not_to_unrefine.clear();
+		to_unrefine.clear();
+		if (g.m.R == 0) return 0;
+		(void)adv_refine_candidates(g, cells, diff_increase, diff_threshold);  // max_diff of every cell (d[5])
+		std::vector<uint64_t> ids;
+		for (const auto& cp : g.cell_process) ids.push_back(cp.first);
+		std::sort(ids.begin(), ids.end());
+		for (const uint64_t id : ids) {  // 124-176
+			const int lvl = g.m.level(id);
+			const double refine_diff = (lvl + 1) * diff_increase, unrefine_diff = unrefine_sensitivity * refine_diff;
+			const auto sib = g.m.siblings(id);
+			const double diff = cells.at(id).d[5];
+			if (diff > refine_diff) {
+				to_refine.insert(id);
+				for (const uint64_t s : sib) {
+					to_unrefine.erase(s);
+					not_to_unrefine.erase(s);
+				}
+			} else if (diff >= unrefine_diff) {
+				bool dont = true;
+				for (const uint64_t s : sib)
+					if (to_refine.count(s) || not_to_unrefine.count(s)) {
+						dont = false;
+						break;
+					}
+				if (dont && lvl > 0) {
+					not_to_unrefine.insert(id);
+					for (const uint64_t s : sib) to_unrefine.erase(s);
+				}
+			} else {
+				bool unref = true;
+				for (const uint64_t s : sib)
+					if (to_refine.count(s) || not_to_unrefine.count(s)) {
+						unref = false;
+						break;
+					}
+				if (unref && lvl > 0) to_unrefine.insert(id);
+			}
+		}
+		return 0;
+	} catch (const std::exception& e) {
+		g_err = e.what();
+		return -1;
+	}
+}
+
+/* adapt_grid (adapter.hpp:187-309) with the sets of or_adv_check; the
+   removed children's densities are summed in ascending id (the reference's
+   get_removed_cells order is hash order).  out2: created, removed. */
+int or_adv_adapt(void* hp, int64_t* out2) {
+	try {
+		auto* h = static_cast<OracleHandle*>(hp);
+		Grid& g = h->g;
+		auto& cells = h->adv;
+		out2[0] = out2[1] = 0;
+		if (g.m.R == 0) return 0;
+		for (const uint64_t c : h->adv_refine) g.refine_completely(c);  // 200-231
+		for (const uint64_t c : h->adv_keep) g.dont_unrefine(c);
+		for (const uint64_t c : h->adv_unrefine) g.unrefine_completely(c);
+		h->adv_refine.clear();
+		h->adv_keep.clear();
+		h->adv_unrefine.clear();
+		const std::vector<uint64_t> created = g.stop_refining();
+		for (const uint64_t c : created) {  // 236-250
+			AdvCell a{};
+			a.d[0] = cells.at(g.m.parent(c)).d[0];
+			cells[c] = a;
+		}
+		std::vector<uint64_t> removed;
+		for (const auto& kv : g.removed_to) removed.push_back(kv.first);
+		std::sort(removed.begin(), removed.end());
+		for (const uint64_t r : removed) {  // 252-275
+			AdvCell& p = cells[g.m.parent(r)];
+			for (int k = 0; k < 9; k++) p.d[k] = 0;
+		}
+		for (const uint64_t r : removed) cells[g.m.parent(r)].d[0] += cells.at(r).d[0] / 8;  // 276-290
+		for (const uint64_t r : removed) cells.erase(r);
+		for (auto it = cells.begin(); it != cells.end();) {  // refined parents
+			if (!g.exists(it->first)) it = cells.erase(it);
+			else ++it;
+		}
+		for (const auto& cp : g.cell_process) {  // 294-305
+			AdvCell& c = cells.at(cp.first);
+			const auto ctr = g.get_center(cp.first);
+			c.d[1] = get_vx(ctr[1]);
+			c.d[2] = get_vy(ctr[0]);
+			c.d[3] = 0;
+			const auto L = g.get_length(cp.first);
+			c.d[6] = L[0];
+			c.d[7] = L[1];
+			c.d[8] = L[2];
+		}
+		out2[0] = int64_t(created.size());
+		out2[1] = int64_t(removed.size());
+		return 0;
+	} catch (const std::exception& e) {
+		g_err = e.what();
+		return -1;
+	}
+}
 
 /* `steps` time steps of calculate_fluxes(inner) + calculate_fluxes(outer) +
    apply_fluxes for every rank's cells (tests/advection/2d.cpp:327-395 with

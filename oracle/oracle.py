@@ -81,6 +81,8 @@ def lib():
     L.or_adv_max_time_step.restype = C.c_double
     L.or_adv_max_time_step.argtypes = [C.c_void_p]
     L.or_adv_steps.argtypes = [C.c_void_p, C.c_int, C.c_double]
+    L.or_adv_check.argtypes = [C.c_void_p, C.c_double, C.c_double, C.c_double]
+    L.or_adv_adapt.argtypes = [C.c_void_p, C.c_void_p]
     L.or_adv_get.argtypes = [C.c_void_p, u64p, C.c_size_t, f64p]
     L.or_po_set.argtypes = [C.c_void_p, u64p, f64p, f64p, i32p, C.c_size_t]
     L.or_po_solve.restype = C.c_int64
@@ -304,6 +306,14 @@ class Grid:
 
     def adv_steps(self, steps, dt):
         self._chk(lib().or_adv_steps(self.h, int(steps), float(dt)))
+
+    def adv_check(self, diff_increase, diff_threshold=0.25, unrefine_sensitivity=0.5):
+        self._chk(lib().or_adv_check(self.h, float(diff_increase), float(diff_threshold), float(unrefine_sensitivity)))
+
+    def adv_adapt(self):
+        out = np.zeros(2, np.int64)
+        self._chk(lib().or_adv_adapt(self.h, out.ctypes.data))
+        return int(out[0]), int(out[1])
 
     def adv_get(self, ids):
         ids = np.ascontiguousarray(ids, np.uint64)

@@ -1,0 +1,58 @@
+"""Advection with grid adaptation every step (tests/advection/2d.cpp with
+adapt_n = 1: check_for_adaptation before apply_fluxes, adapt_grid after it,
+adapter.hpp:47-309) through the product - refinement, unrefinement,
+dont_unrefine, the merged parents' mean density, the velocity / length reset
+and the all-field halo - against the oracle's restatement: the leaf set equals
+the oracle's after every step, dt agrees bitwise, densities within
+1e-12 x max|rho| at the end."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from test_gpu_advection import gpu_grid, prerefine
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+def product_step(g, f, dt, di):
+    g.start_remote_neighbor_copy_updates()
+    g.advection_step(f, dt, "inner")
+    g.wait_remote_neighbor_copy_update_receives()
+    g.advection_step(f, dt, "outer")
+    g.wait_remote_neighbor_copy_update_sends()
+    g.advection_check_adaptation(f[0], di)
+    g.advection_commit(f[0])
+    return g.advection_adapt(f)
+
+
+@pytest.mark.parametrize("base,R,steps", [((16, 16, 1), 2, 40), ((10, 10, 3), 2, 15)])
+def test_adaptive_advection_matches_oracle(gpu, base, R, steps):
+    g, f = gpu_grid(base, R)
+    prerefine(g, f, R)
+    o = O.Grid(base, R, (True, True, False), 0, 1)
+    o.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
+    o.adv_prerefine(0.025, 0.25)
+    assert np.array_equal(g.local_cells(), o.cells()[0])
+    di = 0.025 / R
+    created = removed = 0
+    for step in range(steps):
+        dt = 0.5 * g.advection_max_time_step(f)
+        assert dt == 0.5 * o.adv_max_time_step(), step
+        c, r = product_step(g, f, dt, di)
+        o.adv_check(di)
+        o.adv_steps(1, dt)
+        oc, orm = o.adv_adapt()
+        assert (c, r) == (oc, orm), step
+        created += c
+        removed += r
+        assert np.array_equal(g.local_cells(), o.cells()[0]), step
+    assert created > 0 and removed > 0
+    ids = g.slot_ids()[: g.n_local]
+    exp = o.adv_get(ids)
+    got = f[0].get(0, g.n_local)
+    assert np.max(np.abs(got - exp[:, 0])) <= TOL * np.max(np.abs(exp[:, 0]))
+    for k, col in ((1, 1), (2, 2), (4, 6), (5, 7), (6, 8)):
+        assert np.array_equal(f[k].get(0, g.n_local), exp[:, col])  # velocities and lengths bitwise
+    g.close()

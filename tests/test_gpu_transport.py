@@ -534,6 +534,67 @@ def sc_unrefine(rank, world):
     return res
 
 
+def sc_advection_adapt(rank, world):
+    """Advection with adaptation every step across 3 real ranks: the leaf
+    set and every density equal one rank's run of the product bitwise
+    (refinement, unrefinement with families split across ranks, removed
+    payloads moving to the parent's rank, all-field halo), without and with
+    a repartition half-way."""
+    import dccrg_amd
+
+    base, R, steps = (12, 12, 2), 2, 12
+
+    def run(grid_fn, migrate):
+        g = grid_fn()
+        g.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
+        f = [g.add_field(n, np.float64, n == "density") for n in NAMES]
+        _prerefine(g, f, R)
+        for step in range(steps):
+            dt = 0.5 * g.advection_max_time_step(f)
+            if g.size > 1:
+                dt = g.allreduce(dt, "min")
+            g.start_remote_neighbor_copy_updates()
+            g.advection_step(f, dt, "inner")
+            g.wait_remote_neighbor_copy_update_receives()
+            g.advection_step(f, dt, "outer")
+            g.wait_remote_neighbor_copy_update_sends()
+            g.advection_check_adaptation(f[0], 0.025 / R)
+            g.advection_commit(f[0])
+            g.advection_adapt(f)
+            if migrate and step == 4 and g.size > 1:  # split families across ranks
+                loc = g.local_cells()
+                mv = loc[loc % np.uint64(5) == 0]
+                g.balance_load_to(mv, np.full(mv.size, (g.rank + 1) % g.size, np.int32))
+                # transfer_all_data around the halo after a balance (2d.cpp:423-436)
+                for ff in f:
+                    ff.set_transfer(True)
+                g.update_copies_of_remote_neighbors()
+                for ff in f[1:]:
+                    ff.set_transfer(False)
+        sl = g.slot_ids()[: g.n_local]
+        rho = f[0].get(0, g.n_local)
+        g.close()
+        return sl, rho
+
+    one = lambda: (dccrg_amd.Dccrg(0, 1, 0).set_initial_length(base).set_maximum_refinement_level(R)  # noqa: E731
+                   .set_periodic(True, True, False).set_neighborhood_length(0).initialize())
+    sl1, rho1 = run(one, False)
+    o1 = np.argsort(sl1)
+    res = {}
+    for migrate in (False, True):
+        sl, rho = run(lambda: _grid(base, R, (True, True, False), 0), migrate)
+        allc = np.concatenate(_gather(sl))
+        allr = np.concatenate(_gather(rho))
+        o = np.argsort(allc)
+        key = "_migrate" if migrate else ""
+        res["mesh" + key] = bool(np.array_equal(allc[o], sl1[o1]))
+        if res["mesh" + key]:
+            d = np.abs(allr[o] - rho1[o1])
+            res["bitwise" + key] = bool(np.array_equal(allr[o], rho1[o1]))
+            res["diff" + key] = (int(np.count_nonzero(d)), float(d.max()), float(np.abs(rho1).max()))
+    return res
+
+
 def sc_save(rank, world):
     """save_grid_data from 3 real ranks (offsets from the all-gathered cell
     counts) is byte-identical to the oracle's restatement of the layout and
@@ -606,7 +667,7 @@ def sc_iterators(rank, world):
 SCENARIOS = {
     2: ["sc_config1", "sc_gol_explicit", "sc_rcb"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
-        "sc_rcb", "sc_unrefine"],
+        "sc_rcb", "sc_unrefine", "sc_advection_adapt"],
 }
 
 
@@ -703,6 +764,10 @@ def test_rcb_partitioner(transport_results):
 def test_unrefine_across_ranks(transport_results):
     _check(transport_results, "sc_unrefine", ["leaves", "removed", "payload", "parents_zero", "merged",
                                               "remote_payload", "views"])
+
+
+def test_advection_adapt_across_ranks(transport_results):
+    _check(transport_results, "sc_advection_adapt", ["mesh", "bitwise", "mesh_migrate", "bitwise_migrate"])
 
 
 def test_save_grid_data_three_ranks(transport_results):

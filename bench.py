@@ -46,10 +46,11 @@ def parse():
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--workload", choices=["advection", "gol", "gol_amr", "poisson", "scalability"],
+    p.add_argument("--workload", choices=["advection", "advection_adapt", "gol", "gol_amr", "poisson",
+                                          "scalability"],
                    default="advection",
                    help="advection = BASELINE metric (default); gol = config 2; gol_amr = SURVEY a14; "
-                        "poisson = config 4; scalability = config 5")
+                        "poisson = config 4; scalability = config 5; advection_adapt = SURVEY f1")
     return p.parse_args()
 
 
@@ -403,6 +404,80 @@ def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     g.close()
 
 
+# ---------------------------------------------------------------------------- adaptive advection
+def advection_adapt_main(a, dccrg_amd, torch, dist, rank, world, uid):
+    """tests/advection/2d.cpp with its defaults adapt_n = 1 and balance_n = 25
+    on BASELINE config 3's grid: every step = halo + inner / outer sweep,
+    check_for_adaptation on the pre-step densities, apply, adapt_grid
+    (refines, unrefines, merged parents' mean density, velocity / length
+    reset, all-field halo), a new dt; every 25th step a balance_load (the
+    native RCB) with an all-field halo.  value = cell-updates (local cells
+    summed over steps and ranks) / wall time; the sweep kernels' roofline on
+    the 64-B core bytes is reported beside it."""
+    t_setup = time.perf_counter()
+    g, f = build_grid(dccrg_amd, rank, world, a.base, a.max_ref_lvl, uid)
+    setup_s = time.perf_counter() - t_setup
+    R = a.max_ref_lvl
+    cells0 = g.n_local
+
+    def step(state):
+        dt = 0.5 * g.advection_max_time_step(f)
+        if world > 1:
+            dt = g.allreduce(dt, "min")
+        state["cells"] += g.n_local
+        g.start_remote_neighbor_copy_updates()
+        g.advection_step(f, dt, "inner")
+        g.wait_remote_neighbor_copy_update_receives()
+        g.advection_step(f, dt, "outer")
+        g.wait_remote_neighbor_copy_update_sends()
+        t0 = time.perf_counter()
+        g.advection_check_adaptation(f[0], 0.025 / R, 0.25, 0.5)
+        t1 = time.perf_counter()
+        g.advection_commit(f[0])
+        c, r = g.advection_adapt(f)
+        g.synchronize()
+        t2 = time.perf_counter()
+        state["t_check"] += t1 - t0
+        state["t_adapt"] += t2 - t1
+        state["created"] += c
+        state["removed"] += r
+        state["step"] += 1
+        if state["step"] % 25 == 0 and world > 1:
+            g.balance_load()
+            for ff in f:
+                ff.set_transfer(True)
+            g.update_copies_of_remote_neighbors()
+            for ff in f[1:]:
+                ff.set_transfer(False)
+
+    st = {"cells": 0, "created": 0, "removed": 0, "step": 0, "t_check": 0.0, "t_adapt": 0.0}
+    for _ in range(a.warmup):
+        step(st)
+    st.update(cells=0, created=0, removed=0, t_check=0.0, t_adapt=0.0)
+    el, kms, kn = timed(g, torch, dist, world, lambda: step(st), a.steps)
+    mx, sm = reduce_stats(torch, dist, world, [el, float(st["cells"]), kms, float(st["created"]),
+                                               float(st["removed"]), float(g.n_local)])
+    if rank == 0:
+        line = line_base("cell-updates/s, 3D advection with grid adaptation every step (SURVEY f1)",
+                         sm[1] / mx[0], world, a, mx[0] / a.steps * 1e3, "f64",
+                         "synthetic: reference initial condition (tests/advection/initialize.hpp), adapt_n = 1",
+                         {"workload": "advection3d, base 128x128x128 per GPU, max_ref_lvl 2, face neighbors, "
+                                      "adapt every step (check_for_adaptation + adapt_grid), balance every 25",
+                          "cells_rank0_first": cells0, "cells_rank0_last": g.n_local, "setup_s": setup_s,
+                          "parallelism": f"domain decomposition x{world}"})
+        ach = 64.0 * sm[1] / world / (kms / 1e3) / 1e9 if kms > 0 else None
+        line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                            "kernel": "advection sweeps (64-B core bytes per cell-update)",
+                            "kernel_ms_per_step": kms / a.steps, "sweep_share_of_step": kms / (mx[0] * 1e3)}
+        line["adaptation"] = {"created_total": sm[3], "removed_total": sm[4],
+                              "ms_check_per_step_rank0": st["t_check"] / a.steps * 1e3,
+                              "ms_adapt_per_step_rank0": st["t_adapt"] / a.steps * 1e3}
+        line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    g.close()
+
+
 # ---------------------------------------------------------------------------- advection (config 3, headline)
 def build_grid(dccrg_amd, rank, size, base, R, uid):
     nx, ny, nz = base, base, base * size
@@ -534,7 +609,8 @@ def main():
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
-    fn = {"advection": advection_main, "gol": gol_main, "gol_amr": gol_amr_main, "poisson": poisson_main,
+    fn = {"advection": advection_main, "advection_adapt": advection_adapt_main, "gol": gol_main,
+          "gol_amr": gol_amr_main, "poisson": poisson_main,
           "scalability": scalability_main}[a.workload]
     fn(a, dccrg_amd, torch, dist, rank, world, uid)
     if world > 1:

@@ -1053,7 +1053,7 @@ int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 2449-2459: only local cells
 		if (map_level(g.m, cell) >= g.R) return 0;                      // 2474-2477: no-op at max level
-		g.refine_requests.push_back(cell);
+		g.refine_requests.insert(cell);
 		return 0;
 	});
 }
@@ -1070,14 +1070,14 @@ int dccrgx_unrefine_completely(dccrgx_grid* gp, uint64_t cell) {
 		if (map_level(g.m, cell) == 0) return 0;
 		uint64_t sib[8];
 		map_siblings(g.m, cell, sib);
-		auto has = [](const std::vector<uint64_t>& v, uint64_t x) { return std::find(v.begin(), v.end(), x) != v.end(); };
+		auto has = [](const std::unordered_set<uint64_t>& v, uint64_t x) { return v.count(x) > 0; };
 		for (uint64_t s : sib) {  // 2596-2607, sibling by sibling
 			if (lookup_owner(g, s) < 0) return DCCRGX_ENOTFOUND;  // the sibling has children
 			if (has(g.refine_requests, s) || has(g.dont_unrefine_cells, s)) return 0;
 		}
 		for (uint64_t s : sib)
 			if (has(g.unrefine_requests, s)) return 0;  // 2636-2641
-		g.unrefine_requests.push_back(cell);
+		g.unrefine_requests.insert(cell);
 		return 0;
 	});
 }
@@ -1093,12 +1093,9 @@ int dccrgx_dont_unrefine(dccrgx_grid* gp, uint64_t cell) {
 		uint64_t sib[8];
 		map_siblings(g.m, cell, sib);
 		for (uint64_t s : sib)
-			if (std::find(g.dont_unrefine_cells.begin(), g.dont_unrefine_cells.end(), s) != g.dont_unrefine_cells.end())
-				return 0;
-		for (uint64_t s : sib)
-			g.unrefine_requests.erase(std::remove(g.unrefine_requests.begin(), g.unrefine_requests.end(), s),
-			                          g.unrefine_requests.end());
-		g.dont_unrefine_cells.push_back(cell);
+			if (g.dont_unrefine_cells.count(s)) return 0;
+		for (uint64_t s : sib) g.unrefine_requests.erase(s);
+		g.dont_unrefine_cells.insert(cell);
 		return 0;
 	});
 }
@@ -1111,9 +1108,8 @@ int dccrgx_dont_refine(dccrgx_grid* gp, uint64_t cell) {
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
 		if (map_level(g.m, cell) >= g.R) return 0;
-		g.refine_requests.erase(std::remove(g.refine_requests.begin(), g.refine_requests.end(), cell),
-		                        g.refine_requests.end());
-		g.dont_refine_cells.push_back(cell);
+		g.refine_requests.erase(cell);
+		g.dont_refine_cells.insert(cell);
 		return 0;
 	});
 }
@@ -1787,41 +1783,64 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		            diff_threshold, unrefine_sensitivity, band.p, g.s_comp);
 		const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
 		const auto& ids = slot_ids_host(g);
-		std::map<uint64_t, std::vector<size_t>> fam;  // parent -> local members (slots)
-		std::vector<uint64_t> ref, keep, unref;
+		// families: the local members of a parent are consecutive slots on
+		// Morton-ordered meshes (a run of 8 is a whole family); shorter runs
+		// (a family split between the inner and outer runs, or with members
+		// elsewhere) are merged by parent
+		uint64_t nref = 0, nkeep = 0, nunref = 0;
+		auto decide = [&](const size_t* mem, size_t k) {
+			size_t first2 = n, first1 = n;
+			for (size_t i = 0; i < k; i++) {
+				if (b[mem[i]] == 2 && first2 == n) first2 = mem[i];
+				if (b[mem[i]] == 1 && first1 == n) first1 = mem[i];
+			}
+			if (first2 != n || first1 != n) {  // dont_unrefine (2679-2733) of a local leaf, level > 0
+				g.dont_unrefine_cells.insert(ids[first2 != n ? first2 : first1]);
+				nkeep++;
+			} else if (k == 8) {  // the whole family is local: every sibling a leaf here
+				g.unrefine_requests.insert(ids[mem[0]]);
+				nunref++;
+			} else if (dccrgx_unrefine_completely(gp, ids[mem[0]]) == DCCRGX_OK) {
+				nunref++;
+			}
+		};
+		std::unordered_map<uint64_t, std::vector<size_t>> partial;
+		std::vector<size_t> run;
+		uint64_t run_parent = error_cell;
+		auto flush = [&] {
+			if (run.empty()) return;
+			if (run.size() == 8) decide(run.data(), 8);
+			else {
+				auto& v = partial[run_parent];
+				v.insert(v.end(), run.begin(), run.end());
+			}
+			run.clear();
+		};
 		for (size_t s = 0; s < n; s++) {
 			const int lvl = map_level(g.m, ids[s]);
-			if (b[s] == 2 && lvl < g.R) ref.push_back(ids[s]);
-			if (lvl > 0) fam[map_parent(g.m, ids[s])].push_back(s);
-		}
-		for (const auto& kv : fam) {
-			bool any2 = false, any1 = false;
-			size_t first1 = 0;
-			for (size_t s : kv.second) {
-				any2 = any2 || b[s] == 2;
-				if (b[s] == 1 && !any1) {
-					any1 = true;
-					first1 = s;
-				}
+			if (b[s] == 2 && lvl < g.R) {
+				g.refine_requests.insert(ids[s]);  // 2434-2520: a local leaf below the maximum level
+				nref++;
 			}
-			if (any2) {
-				for (size_t s : kv.second)
-					if (b[s] == 2) {
-						keep.push_back(ids[s]);
-						break;
-					}
-			} else if (any1) {
-				keep.push_back(ids[first1]);
-			} else {
-				for (size_t s : kv.second) unref.push_back(ids[s]);
+			if (lvl == 0) {
+				flush();
+				run_parent = error_cell;
+				continue;
 			}
+			const uint64_t p = map_parent(g.m, ids[s]);
+			if (p != run_parent) {
+				flush();
+				run_parent = p;
+			}
+			run.push_back(s);
 		}
-		for (uint64_t c : ref)
-			if (dccrgx_refine_completely(gp, c) == DCCRGX_OK && counts) counts[0]++;
-		for (uint64_t c : keep)
-			if (dccrgx_dont_unrefine(gp, c) == DCCRGX_OK && counts) counts[1]++;
-		for (uint64_t c : unref)
-			if (dccrgx_unrefine_completely(gp, c) == DCCRGX_OK && counts) counts[2]++;
+		flush();
+		for (auto& kv : partial) decide(kv.second.data(), kv.second.size());
+		if (counts) {
+			counts[0] = nref;
+			counts[1] = nkeep;
+			counts[2] = nunref;
+		}
 		return 0;
 	});
 }

@@ -9,6 +9,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/dccrgx.h"
@@ -271,10 +272,10 @@ struct Grid {
 	std::unordered_map<uint64_t, int> pins;  // local cells pinned to a process (pin 5832-5909)
 	std::unordered_map<uint64_t, double> weights;  // set_cell_weight (6210), cleared by balance_load
 	std::string lb_method = "RCB";                 // set_load_balancing_method (8223); default 7082
-	std::vector<uint64_t> refine_requests;
-	std::vector<uint64_t> unrefine_requests;    // unrefine_completely 2560 (one sibling per family)
-	std::vector<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
-	std::vector<uint64_t> dont_refine_cells;    // dont_refine 2744
+	std::unordered_set<uint64_t> refine_requests;      // refine_completely 2434
+	std::unordered_set<uint64_t> unrefine_requests;    // unrefine_completely 2560 (one sibling per family)
+	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
+	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
 	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;

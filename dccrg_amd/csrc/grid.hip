@@ -410,11 +410,12 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	for (auto& f : g.fields) f.removed.release();
 	g.removed_ids_h.clear();
 
-	std::vector<uint64_t> D = union_sorted(comm_allgather_u64(g, sorted_unique(g.dont_refine_cells)));
+	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
+	std::vector<uint64_t> D = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_refine_cells))));
 	g.dont_refine_cells.clear();
 	if (!D.empty()) close_set(g, D, true);
 	std::vector<uint64_t> mine;
-	for (uint64_t c : sorted_unique(g.refine_requests))
+	for (uint64_t c : sorted_unique(vec(g.refine_requests)))
 		if (!sorted_contains(D, c)) mine.push_back(c);
 	g.refine_requests.clear();
 	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
@@ -425,7 +426,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
 	req_par = sorted_unique(req_par);
 	g.unrefine_requests.clear();
-	const std::vector<uint64_t> DU = union_sorted(comm_allgather_u64(g, sorted_unique(g.dont_unrefine_cells)));
+	const std::vector<uint64_t> DU = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_unrefine_cells))));
 	g.dont_unrefine_cells.clear();
 	std::vector<uint64_t> cand;
 	for (uint64_t p : req_par) {

@@ -326,9 +326,11 @@ __global__ void po_jacobi_copy_kernel(PoArrays a, size_t n, const PoScalars* st)
 // order -> red[0..K); then (scalar != 0, one GPU) the reference's control
 // flow of that point of the iteration, or (scalar == 0) nothing: with
 // several GPUs the sums are all-reduced first and po_scalar_kernel follows
+constexpr int RB = 1024;  // threads of the second stage
+
 template <int K>
-__global__ void po_reduce_kernel(const double* __restrict__ part, unsigned nb, double* red, PoScalars* st,
-                                 PoParams prm, int stage, int scalar);
+__global__ __launch_bounds__(RB) void po_reduce_kernel(const double* __restrict__ part, unsigned nb, double* red,
+                                                       PoScalars* st, PoParams prm, int stage, int scalar);
 
 __device__ void po_scalar(PoScalars* st, const double* red, const PoParams& prm, int stage) {
 	switch (stage) {
@@ -391,24 +393,38 @@ __device__ void po_scalar(PoScalars* st, const double* red, const PoParams& prm,
 	}
 }
 
+// one block of RB threads: thread t sums partials t, t + RB, ... into four
+// independent accumulators (their loads in flight together), then wave
+// shuffles and the 16 wave sums in order - a fixed order for any run
 template <int K>
-__global__ void po_reduce_kernel(const double* __restrict__ part, unsigned nb, double* red, PoScalars* st,
-                                 PoParams prm, int stage, int scalar) {
-	__shared__ double sh[K][BS];
+__global__ __launch_bounds__(RB) void po_reduce_kernel(const double* __restrict__ part, unsigned nb, double* red,
+                                                       PoScalars* st, PoParams prm, int stage, int scalar) {
+#pragma clang fp contract(off)
+	__shared__ double sh[K][RB / 64];
 	double v[K];
-	for (int k = 0; k < K; k++) v[k] = 0;
-	for (unsigned i = threadIdx.x; i < nb; i += BS)
-		for (int k = 0; k < K; k++) v[k] += part[K * i + k];
-	for (int k = 0; k < K; k++) sh[k][threadIdx.x] = v[k];
-	__syncthreads();
-	for (int w = BS / 2; w > 0; w >>= 1) {
-		if (int(threadIdx.x) < w)
-			for (int k = 0; k < K; k++) sh[k][threadIdx.x] += sh[k][threadIdx.x + w];
-		__syncthreads();
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+		unsigned i = threadIdx.x;
+		for (; i + 3 * RB < nb; i += 4 * RB) {
+			a0 += part[K * i + k];
+			a1 += part[K * (i + RB) + k];
+			a2 += part[K * (i + 2 * RB) + k];
+			a3 += part[K * (i + 3 * RB) + k];
+		}
+		for (; i < nb; i += RB) a0 += part[K * i + k];
+		v[k] = (a0 + a1) + (a2 + a3);
+		for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_down(v[k], o, 64);
 	}
+	const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	if (lane == 0)
+#pragma unroll
+		for (int k = 0; k < K; k++) sh[k][w] = v[k];
+	__syncthreads();
 	if (threadIdx.x == 0) {
 		double r[2] = {0, 0};
-		for (int k = 0; k < K; k++) r[k] = sh[k][0];
+		for (int k = 0; k < K; k++)
+			for (int i = 0; i < RB / 64; i++) r[k] += sh[k][i];
 		for (int k = 0; k < K; k++) red[k] = r[k];
 		if (scalar) po_scalar(st, r, prm, stage);
 	}
@@ -455,8 +471,8 @@ void k_po_phase(int phase, const PoArrays& a, size_t n, const PoParams& prm, con
 
 void k_po_reduce(int k, const double* part, unsigned nb, double* red, PoScalars* st, const PoParams& prm, int stage,
                  bool scalar, hipStream_t s) {
-	if (k == 1) po_reduce_kernel<1><<<1, BS, 0, s>>>(part, nb, red, st, prm, stage, scalar ? 1 : 0);
-	else po_reduce_kernel<2><<<1, BS, 0, s>>>(part, nb, red, st, prm, stage, scalar ? 1 : 0);
+	if (k == 1) po_reduce_kernel<1><<<1, RB, 0, s>>>(part, nb, red, st, prm, stage, scalar ? 1 : 0);
+	else po_reduce_kernel<2><<<1, RB, 0, s>>>(part, nb, red, st, prm, stage, scalar ? 1 : 0);
 	HIP_CHECK(hipGetLastError());
 }
 

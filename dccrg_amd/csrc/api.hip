@@ -1617,10 +1617,10 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 		DBuf<int> err;
 		err.alloc(1);
 		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		if (!g.gola.valid) k_gol_amr_tables(g.m, g.slot_ids.p, g.n_slots, g.n_local, g.gola, g.s_comp);
 		k_time_begin(g);
-		if (g.gol_l0p.n < g.n_slots) g.gol_l0p.alloc(g.n_slots);
-		k_gol_amr(phase, g.m, g.slot_ids.p, g.n_slots, g.gol_l0p.p, (uint32_t*)st.data.p, (uint64_t*)ls.data.p,
-		          g.nof_ptr.p, g.nof_slot.p, s0, s1, err.p, g.s_comp);
+		k_gol_amr(phase, g.gola, g.n_slots, (uint32_t*)st.data.p, (uint64_t*)ls.data.p, g.nof_ptr.p, g.nof_slot.p, s0,
+		          s1, err.p, g.s_comp);
 		k_time_end(g);
 		int h = 0;
 		HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));

@@ -241,6 +241,16 @@ struct Migration {
 // a box of whole z-planes of the uniform grid in slot order (slot0 first
 // slot, nz planes) and the slots of its z-1 / z+1 planes (-2: outside the
 // grid, -3: the box wraps onto itself periodically)
+// refined game of life per mesh: level-0 parent of every slot (bit 31 set
+// on level-0 leaves), the per-call packed (parent << 1 | alive), the groups
+// of slots sharing a refined level-0 parent (gptr / gslot) and the local
+// level-0 leaves
+struct GolAmrTables {
+	bool valid = false;
+	DBuf<uint32_t> l0, pack, gptr, gslot, lvl0;
+	size_t ng = 0, n_lvl0 = 0;
+};
+
 struct GolBox {
 	uint64_t slot0, nz;
 	int64_t lo, hi;
@@ -337,7 +347,7 @@ struct Grid {
 	// faces): the run is then swept by the untiled face-CSR kernel
 	DBuf<uint32_t> tmeta;
 	std::map<int, UserHood> uhoods;  // add_neighborhood ids
-	DBuf<uint64_t> gol_l0p;  // refined game of life: level-0 parent per slot (scratch)
+	GolAmrTables gola;  // refined game of life: per-mesh tables (gol_amr.hip)
 	// uniform game of life: the regions as plane boxes (gol_slab_plan), built lazily
 	bool gol_plan_valid = false, gol_plan_ok = false;
 	std::vector<GolBox> gol_inner, gol_outer;
@@ -530,9 +540,11 @@ void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 
 // --- launchers implemented in gol_amr.hip ----------------------------------
-void k_gol_amr(int phase, const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, uint64_t* l0p, uint32_t* state,
-               uint64_t* lst, const uint32_t* ptr, const int32_t* nslot, size_t s0, size_t s1, int* err,
-               hipStream_t s);
+// refined game of life (gol_amr.hip): per-mesh tables, then one phase
+void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, GolAmrTables& T,
+                      hipStream_t s);
+void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
+               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots

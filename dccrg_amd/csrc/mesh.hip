@@ -368,6 +368,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	g.index_h_valid = false;
 	g.po.valid = false;
 	g.gol_plan_valid = false;
+	g.gola.valid = false;
 	for (auto& kv : g.uhoods) kv.second.valid = false;
 }
 

@@ -103,6 +103,15 @@ _SIGS = {
     "dccrgx_get_cell_process": (C.c_int, [vp, vp, vp, sz, P(sz)]),
     "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
     "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),
+    "dccrgx_add_variable_field": (C.c_int, [vp, C.c_char_p, C.c_int, P(C.c_int)]),
+    "dccrgx_variable_field_sizes": (C.c_int, [vp, C.c_int, sz, sz, vp]),
+    "dccrgx_variable_field_resize": (C.c_int, [vp, C.c_int, sz, sz, vp]),
+    "dccrgx_variable_field_upload": (C.c_int, [vp, C.c_int, sz, sz, vp, sz]),
+    "dccrgx_variable_field_download": (C.c_int, [vp, C.c_int, sz, sz, vp, sz, P(sz)]),
+    "dccrgx_variable_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp), P(vp)]),
+    "dccrgx_removed_variable_field_download": (C.c_int, [vp, C.c_int, vp, vp, sz, P(sz)]),
+    "dccrgx_set_send_single_cells": (C.c_int, [vp, C.c_int]),
+    "dccrgx_get_send_single_cells": (C.c_int, [vp, P(C.c_int)]),
     "dccrgx_set_field_window": (C.c_int, [vp, C.c_int, sz, sz]),
     "dccrgx_field_device_ptr": (C.c_int, [vp, C.c_int, P(vp)]),
     "dccrgx_field_upload": (C.c_int, [vp, C.c_int, sz, sz, vp]),

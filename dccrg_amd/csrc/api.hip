@@ -335,6 +335,7 @@ struct Closer {
 
 static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const void* header, size_t header_bytes) {
 	DX_REQUIRE(g.initialized, "not initialized");
+	DX_REQUIRE(var_transfer_fields(g).empty(), "grid files hold fixed-size payloads only");
 	const std::vector<Field*> tf = transfer_fields(g);
 	size_t bpc = 0;
 	for (Field* f : tf) bpc += f->elem;
@@ -385,6 +386,7 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 
 static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t header_bytes) {
 	DX_REQUIRE(!g.initialized, "load_grid_data initializes the grid: call it instead of initialize");
+	DX_REQUIRE(var_transfer_fields(g).empty(), "grid files hold fixed-size payloads only");
 	const int fd = ::open(path, O_RDONLY);
 	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
 	Closer closer{fd};
@@ -1124,7 +1126,7 @@ int dccrgx_get_removed_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t*
 int dccrgx_removed_field_download(dccrgx_grid* gp, int fid, void* host, size_t cap_bytes) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		Field& f = field(g, fid);
+		Field& f = fixed_field(g, fid);
 		const size_t bytes = g.removed_ids_h.size() * f.elem;
 		DX_REQUIRE(cap_bytes >= bytes, "buffer too small for the removed cells' payloads");
 		if (bytes) HIP_CHECK(hipMemcpy(host, f.removed.p, bytes, hipMemcpyDeviceToHost));
@@ -1136,7 +1138,7 @@ int dccrgx_removed_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(ptr, "null pointer");
-		*ptr = g.removed_ids_h.empty() ? nullptr : field(g, fid).removed.p;
+		*ptr = g.removed_ids_h.empty() ? nullptr : fixed_field(g, fid).removed.p;
 		return 0;
 	});
 }
@@ -1490,6 +1492,136 @@ int dccrgx_add_field(dccrgx_grid* gp, const char* name, size_t elem, int transfe
 	});
 }
 
+// ---- variable-size fields (tests/variable_data_size; varfield.hip) ----------
+int dccrgx_add_variable_field(dccrgx_grid* gp, const char* name, int transfer, int* fid) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(fid, "null pointer");
+		Field f;
+		f.name = name ? name : "";
+		f.var = true;
+		f.transfer = transfer != 0;
+		g.fields.push_back(std::move(f));
+		if (g.initialized) var_reset(g.fields.back(), g.n_slots, g.s_comp);
+		*fid = int(g.fields.size() - 1);
+		return 0;
+	});
+}
+
+static Field& var_field(Grid& g, int fid, size_t slot0, size_t n) {
+	Field& f = field(g, fid);
+	DX_REQUIRE(f.var, "not a variable-size field");
+	DX_REQUIRE(g.initialized, "not initialized");
+	DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+	return f;
+}
+
+int dccrgx_variable_field_sizes(dccrgx_grid* gp, int fid, size_t slot0, size_t n, uint64_t* sizes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = var_field(g, fid, slot0, n);
+		DX_REQUIRE(sizes || !n, "null pointer");
+		const std::vector<uint64_t> o = download(f.voff.p + slot0, n + 1, g.s_comp);
+		for (size_t i = 0; i < n; i++) sizes[i] = o[i + 1] - o[i];
+		return 0;
+	});
+}
+
+int dccrgx_variable_field_resize(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const uint64_t* sizes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = var_field(g, fid, slot0, n);
+		DX_REQUIRE(sizes || !n, "null pointer");
+		DBuf<uint64_t> all;
+		all.alloc(g.n_slots + 1);
+		var_sizes(f, nullptr, 0, g.n_slots, all.p, g.s_comp);
+		if (n) HIP_CHECK(hipMemcpyAsync(all.p + slot0, sizes, n * 8, hipMemcpyHostToDevice, g.s_comp));
+		var_resize(f, g.n_slots, all.p, g.s_comp);
+		return 0;
+	});
+}
+
+int dccrgx_variable_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const void* bytes, size_t nbytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = var_field(g, fid, slot0, n);
+		uint64_t a = 0, b = 0;
+		HIP_CHECK(hipMemcpyAsync(&a, f.voff.p + slot0, 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipMemcpyAsync(&b, f.voff.p + slot0 + n, 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		DX_REQUIRE(nbytes == b - a, "byte count differs from the cells' sizes (resize them first)");
+		if (nbytes) HIP_CHECK(hipMemcpy(f.data.p + a, bytes, nbytes, hipMemcpyHostToDevice));
+		return 0;
+	});
+}
+
+int dccrgx_variable_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_t n, void* bytes, size_t cap,
+                                   size_t* nbytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = var_field(g, fid, slot0, n);
+		uint64_t a = 0, b = 0;
+		HIP_CHECK(hipMemcpyAsync(&a, f.voff.p + slot0, 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipMemcpyAsync(&b, f.voff.p + slot0 + n, 8, hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		if (nbytes) *nbytes = size_t(b - a);
+		if (b - a > cap) return DCCRGX_ERANGE;
+		if (b > a) HIP_CHECK(hipMemcpy(bytes, f.data.p + a, b - a, hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+int dccrgx_variable_field_device_ptr(dccrgx_grid* gp, int fid, void** data, const uint64_t** offsets) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = var_field(g, fid, 0, 0);
+		if (data) *data = f.data.p;
+		if (offsets) *offsets = f.voff.p;
+		return 0;
+	});
+}
+
+int dccrgx_removed_variable_field_download(dccrgx_grid* gp, int fid, uint64_t* sizes, void* bytes, size_t cap,
+                                           size_t* nbytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& f = field(g, fid);
+		DX_REQUIRE(f.var, "not a variable-size field");
+		const size_t n = g.removed_ids_h.size();
+		if (!n || !f.rm_off.p) {
+			if (nbytes) *nbytes = 0;
+			return 0;
+		}
+		const std::vector<uint64_t> o = download(f.rm_off.p, n + 1, g.s_comp);
+		if (nbytes) *nbytes = size_t(o[n]);
+		if (sizes)
+			for (size_t i = 0; i < n; i++) sizes[i] = o[i + 1] - o[i];
+		if (o[n] > cap) return DCCRGX_ERANGE;
+		if (o[n] && bytes) HIP_CHECK(hipMemcpy(bytes, f.removed.p, o[n], hipMemcpyDeviceToHost));
+		return 0;
+	});
+}
+
+// set_send_single_cells 6677 / get_send_single_cells 6684: accepted and
+// reported; the wire message is always one per peer and field (message
+// boundaries carry no data here, so the received payloads are the same)
+int dccrgx_set_send_single_cells(dccrgx_grid* gp, int on) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.send_single_cells = on != 0;
+		return 0;
+	});
+}
+
+int dccrgx_get_send_single_cells(dccrgx_grid* gp, int* on) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(on, "null pointer");
+		*on = g.send_single_cells ? 1 : 0;
+		return 0;
+	});
+}
+
 int dccrgx_set_field_transfer(dccrgx_grid* gp, int fid, int transfer) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
@@ -1501,7 +1633,7 @@ int dccrgx_set_field_transfer(dccrgx_grid* gp, int fid, int transfer) {
 int dccrgx_set_field_window(dccrgx_grid* gp, int fid, size_t offset, size_t bytes) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		Field& f = field(g, fid);
+		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(offset + bytes <= f.elem && bytes > 0, "window outside the element");
 		f.win_off = offset;
 		f.win_len = bytes;
@@ -1512,7 +1644,7 @@ int dccrgx_set_field_window(dccrgx_grid* gp, int fid, size_t offset, size_t byte
 int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		*ptr = field(g, fid).data.p;
+		*ptr = fixed_field(g, fid).data.p;
 		return 0;
 	});
 }
@@ -1520,7 +1652,7 @@ int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const void* host) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		Field& f = field(g, fid);
+		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		if (n) HIP_CHECK(hipMemcpy(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice));
@@ -1531,7 +1663,7 @@ int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const 
 int dccrgx_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_t n, void* host) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		Field& f = field(g, fid);
+		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		if (n) HIP_CHECK(hipMemcpy(host, f.data.p + slot0 * f.elem, n * f.elem, hipMemcpyDeviceToHost));
@@ -1617,9 +1749,11 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 		DBuf<int> err;
 		err.alloc(1);
 		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
-		if (!g.gola.valid) k_gol_amr_tables(g.m, g.slot_ids.p, g.n_slots, g.n_local, g.gola, g.s_comp);
+		if (!g.gola.valid)
+			k_gol_amr_tables(g.m, g.slot_ids.p, g.n_slots, g.n_local, g.hood_len, g.nof_ptr.p, g.nof_slot.p, g.gola,
+			                 g.s_comp);
 		k_time_begin(g);
-		k_gol_amr(phase, g.gola, g.n_slots, (uint32_t*)st.data.p, (uint64_t*)ls.data.p, g.nof_ptr.p, g.nof_slot.p, s0,
+		k_gol_amr(phase, g.gola, g.n_slots, g.n_local, (uint32_t*)st.data.p, (uint64_t*)ls.data.p, g.nof_ptr.p, g.nof_slot.p, s0,
 		          s1, err.p, g.s_comp);
 		k_time_end(g);
 		int h = 0;

@@ -8,6 +8,8 @@ namespace dccrgx {
 
 std::vector<Field*> transfer_fields(Grid& g);
 Field& field(Grid& g, int fid);
+Field& fixed_field(Grid& g, int fid);  // EINVAL for a variable-size field
+std::vector<Field*> var_transfer_fields(Grid& g);
 void ensure_scratch(Grid& g, Field& f);
 void commit(Grid& g, Field& f);
 void region_range(const Grid& g, int region, size_t& s0, size_t& s1);

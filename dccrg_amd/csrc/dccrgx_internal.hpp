@@ -126,6 +126,11 @@ struct Field {
 	// payloads of the cells removed by the last stop_refining whose parent is
 	// local (unrefined_cell_data 7250), in the order of Grid::removed_ids_h
 	DBuf<uint8_t> removed;
+	// variable-size payloads (varfield.hip): elem == 0, `data` is a byte pool
+	// and slot s owns [voff[s], voff[s + 1]); the removed store likewise
+	// (rm_off, one entry per removed cell + 1)
+	bool var = false;
+	DBuf<uint64_t> voff, rm_off;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
@@ -225,6 +230,15 @@ struct Mesh {
 	}
 };
 
+// Gathered variable-size payloads of the cells of a send list (sizes on the
+// device and the host, concatenated bytes) and what arrived for a receive
+// list (varfield.hip, grid.hip)
+struct VarMsg {
+	DBuf<uint64_t> ssz, rsz;
+	DBuf<uint8_t> sbytes, rbytes;
+	std::vector<uint64_t> hs;
+};
+
 // A balance_load in progress (initialize_balance_load 3746 / continue 3899 /
 // finish 3942): per peer the cells leaving / arriving (ascending id), the
 // payloads of every field packed peer by peer (per peer: field 0 of every
@@ -236,6 +250,7 @@ struct Migration {
 	std::vector<uint64_t> in_pinned;        // arriving cells that stay pinned here
 	DBuf<uint8_t> sendbuf, recvbuf;
 	size_t bytes_per_cell = 0;
+	std::vector<VarMsg> var;  // per variable-size field (field order)
 };
 
 // a box of whole z-planes of the uniform grid in slot order (slot0 first
@@ -245,10 +260,20 @@ struct Migration {
 // on level-0 leaves), the per-call packed (parent << 1 | alive), the groups
 // of slots sharing a refined level-0 parent (gptr / gslot) and the local
 // level-0 leaves
+// Mask path (neighborhood length <= 1, small enough grids): every neighbor's
+// level-0 parent is one of the 27 level-0 cells around the row's own, so a
+// neighbor entry carries that position (code 0..26, 13 = the own parent)
+// next to its slot (ent = slot | code << 27) and the distinct live parents
+// of a leaf are a 27-bit mask (mask, per slot); l0c = packed level-0
+// coordinates (x | y << bx | z << (bx + by)) of every slot
 struct GolAmrTables {
 	bool valid = false;
 	DBuf<uint32_t> l0, pack, gptr, gslot, lvl0;
 	size_t ng = 0, n_lvl0 = 0;
+	bool mask_path = false;
+	DBuf<uint32_t> l0c, ent, mask, val;  // val: one byte per entry (4 per word)
+	size_t n_ent = 0;
+	uint32_t bx = 0, by = 0, lx = 0, ly = 0, lz = 0;
 };
 
 struct GolBox {
@@ -266,6 +291,7 @@ struct Grid {
 	hipStream_t s_comp = nullptr, s_comm = nullptr;
 	hipEvent_t ev_comp = nullptr, ev_halo = nullptr;
 	bool halo_in_flight = false;
+	bool send_single_cells = false;  // set_send_single_cells (6677), reported only
 
 	// setup (dccrg.hpp:8120-8230)
 	uint64_t len[3] = {1, 1, 1};
@@ -539,11 +565,29 @@ void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const doub
 void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 
+// --- variable-size fields (varfield.hip) ----------------------------------
+uint64_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, size_t n, hipStream_t s);  // returns total
+void var_reset(Field& f, size_t n_slots, hipStream_t s);  // every slot empty
+uint64_t var_total(const Field& f, size_t n_slots, hipStream_t s);
+// sizes of slots[i] (slots != nullptr) or of slot0 + i, into out (device)
+void var_sizes(const Field& f, const int32_t* slots, size_t slot0, size_t n, uint64_t* out, hipStream_t s);
+// new sizes for every slot (device): each keeps its first min(old, new) bytes, the rest zero
+void var_resize(Field& f, size_t n_slots, const uint64_t* new_sizes, hipStream_t s);
+// the payloads of slots[0..n): sizes and concatenated bytes; returns the byte total
+size_t var_gather(const Field& f, const int32_t* slots, size_t n, DBuf<uint64_t>& sizes, DBuf<uint8_t>& bytes,
+                  hipStream_t s);
+// payloads into slots[0..n) (sizes and concatenated bytes on the device); returns the byte total
+uint64_t var_place(Field& f, size_t n_slots, const int32_t* slots, size_t n, const uint64_t* sizes,
+                   const uint8_t* bytes, hipStream_t s);
+// after a rebuild: cells that stayed local keep their payload, every other slot is empty
+void var_remap(Field& f, const uint64_t* old_ids, size_t n_old_local, const DevMesh& newM, size_t new_n_slots,
+               hipStream_t s);
+
 // --- launchers implemented in gol_amr.hip ----------------------------------
 // refined game of life (gol_amr.hip): per-mesh tables, then one phase
-void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, GolAmrTables& T,
-                      hipStream_t s);
-void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
+void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, unsigned hood_len,
+                      const uint32_t* ptr, const int32_t* nslot, GolAmrTables& T, hipStream_t s);
+void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------

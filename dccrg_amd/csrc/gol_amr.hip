@@ -40,7 +40,9 @@ namespace {
 constexpr int kList = 8;  // data[1..8]
 constexpr uint32_t kLevel0 = 0x80000000u;  // mesh table: the slot is a level-0 leaf
 
-__device__ __forceinline__ bool list_insert(uint64_t (&l)[kList], int& n, uint64_t v) {
+// the list in registers as 32-bit level-0 ids (< 2^31, checked when the
+// tables are built): half the compares of the reference's uint64_t entries
+__device__ __forceinline__ bool list_insert(uint32_t (&l)[kList], int& n, uint32_t v) {
 #pragma unroll
 	for (int i = 0; i < kList; i++)
 		if (i < n && l[i] == v) return true;
@@ -87,49 +89,89 @@ __global__ void group_fill_kernel(const uint64_t* __restrict__ keys, size_t n, c
 
 // per call: (level-0 parent << 1) | alive of every slot, one 4-byte gather
 // per neighbor entry in the collect walk
-__global__ void pack_kernel(const uint32_t* __restrict__ l0, const uint32_t* __restrict__ state, size_t n,
+__global__ void gol_amr_pack_kernel(const uint32_t* __restrict__ l0, const uint32_t* __restrict__ state, size_t n,
                             uint32_t* __restrict__ pack) {
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x)
 		pack[s] = ((l0[s] & ~kLevel0) << 1) | (state[s] ? 1u : 0u);
 }
 
-// collect (solve.hpp:46-110): the neighbor rows are walked K entries ahead,
-// so K independent gathers are in flight per thread
-template <int K>
-__global__ void gol_amr_collect_kernel(const uint32_t* __restrict__ pack, uint64_t* __restrict__ lst,
-                                       const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nslot, size_t s0,
-                                       size_t s1, int* __restrict__ err) {
-	const size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x;
-	if (s >= s1) return;
+// collect (solve.hpp:46-110), one block per 256 consecutive rows: the
+// block's neighbor entries (one contiguous run of the CSR) are read coalesced
+// and their packed (level-0 parent, alive) values gathered eight per thread
+// in flight into LDS; then every thread walks its own row from LDS (entries
+// past the LDS window, in blocks with very long rows, are gathered directly).
+// Entries without a slot hold kNoSlot and are skipped like same-parent ones.
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
+// XCD-contiguous block order: hardware block b runs on XCD b % 8, so XCD x
+// gets the x-th eighth of the logical blocks and the rows neighboring its
+// rows (whose packed values it gathers) are fetched into its own L2 once,
+// not into all eight (gridDim.x is a multiple of 8)
+__device__ __forceinline__ uint32_t xcd_block() {
+	return (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+}
+__host__ __device__ constexpr unsigned xcd_grid(size_t blocks) { return unsigned((blocks + 7) / 8 * 8); }
+constexpr int kCollectRows = 256;
+constexpr uint32_t kCollectLds = 8192;  // packed entries staged per block (32 KB)
+
+__device__ __forceinline__ uint32_t gather_pack(const uint32_t* __restrict__ pack, int32_t ns) {
+	return ns >= 0 ? pack[ns] : kNoSlot;
+}
+
+__global__ __launch_bounds__(kCollectRows) void gol_amr_collect_kernel(const uint32_t* __restrict__ pack,
+                                                                      uint64_t* __restrict__ lst,
+                                                                      const uint32_t* __restrict__ ptr,
+                                                                      const int32_t* __restrict__ nslot, size_t s0,
+                                                                      size_t s1, int* __restrict__ err) {
+	__shared__ uint32_t sp[kCollectLds];
+	const uint32_t tid = threadIdx.x;
+	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
+	if (r0 >= s1) return;  // block-uniform (the grid is rounded up to whole XCD shares)
+	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
+	const uint32_t E0 = ptr[r0], E1 = ptr[r1];
+	const uint32_t nE = E1 - E0 < kCollectLds ? E1 - E0 : kCollectLds;
+	// stage: 8 coalesced index loads, then their 8 gathers, per thread and round
+	for (uint32_t b = 0; b < nE; b += 8 * kCollectRows) {
+		int32_t ns[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const uint32_t j = b + uint32_t(k) * kCollectRows + tid;
+			ns[k] = j < nE ? nslot[E0 + j] : -1;
+		}
+		uint32_t v[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++) v[k] = gather_pack(pack, ns[k]);
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const uint32_t j = b + uint32_t(k) * kCollectRows + tid;
+			if (j < nE) sp[j] = v[k];
+		}
+	}
+	__syncthreads();
+	const size_t s = r0 + tid;
+	if (s >= r1) return;
 	const uint32_t parent = pack[s] >> 1;
-	uint64_t l[kList];
+	uint32_t l[kList];
 #pragma unroll
-	for (int i = 0; i < kList; i++) l[i] = error_cell;
+	for (int i = 0; i < kList; i++) l[i] = 0;
 	int n = 0;
-	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j += K) {
-		uint32_t pk[K];
+	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++) {
+		const uint32_t pk = j - E0 < nE ? sp[j - E0] : gather_pack(pack, nslot[j]);
+		if (pk == kNoSlot) continue;
+		const uint32_t q = pk >> 1;
+		if (q == parent) continue;
+		if (!(pk & 1u)) {
+			bool seen = false;
 #pragma unroll
-		for (int k = 0; k < K; k++) {
-			const int32_t ns = j + k < e ? nslot[j + k] : -1;
-			pk[k] = ns >= 0 ? pack[ns] : (parent << 1);
+			for (int i = 0; i < kList; i++) seen |= (i < n && l[i] == q);
+			if (seen) atomicOr(err, 2);
+			continue;
 		}
-#pragma unroll
-		for (int k = 0; k < K; k++) {
-			const uint32_t q = pk[k] >> 1;
-			if (q == parent) continue;  // also the padding past the row
-			if (!(pk[k] & 1u)) {
-				bool seen = false;
-#pragma unroll
-				for (int i = 0; i < kList; i++) seen |= (i < n && l[i] == uint64_t(q));
-				if (seen) atomicOr(err, 2);
-				continue;
-			}
-			if (!list_insert(l, n, uint64_t(q))) atomicOr(err, 1);
-		}
+		if (!list_insert(l, n, q)) atomicOr(err, 1);
 	}
 	uint64_t* o = lst + s * kList;
 #pragma unroll
-	for (int i = 0; i < kList; i++) o[i] = l[i];
+	for (int i = 0; i < kList; i++) o[i] = l[i];  // error_cell (0) padded
 }
 
 __device__ __forceinline__ void gol_rule(uint32_t* state, size_t s, int n) {
@@ -160,31 +202,256 @@ __global__ void gol_amr_spread_groups_kernel(const uint32_t* __restrict__ gptr, 
                                              const uint32_t* __restrict__ gslot, uint32_t* __restrict__ state,
                                              const uint64_t* __restrict__ lst, size_t s0, size_t s1,
                                              int* __restrict__ err) {
-	for (size_t gi = blockIdx.x * size_t(blockDim.x) + threadIdx.x; gi < ng; gi += size_t(gridDim.x) * blockDim.x) {
-		const uint32_t b = gptr[gi], e = gptr[gi + 1];
-		bool any = false;
-		for (uint32_t j = b; j < e; j++) any |= gslot[j] >= s0 && gslot[j] < s1;
-		if (!any) continue;
-		uint64_t l[kList];
-		int n = 0;
-		for (uint32_t j = b; j < e; j++) {
-			const uint64_t* nl = lst + size_t(gslot[j]) * kList;
-			for (int i = 0; i < kList; i++) {
-				const uint64_t v = nl[i];
-				if (v == error_cell) break;
-				if (!list_insert(l, n, v)) atomicOr(err, 1);
-			}
+	const size_t gi = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	if (gi >= ng) return;
+	const uint32_t b = gptr[gi], e = gptr[gi + 1];
+	bool any = false;
+	for (uint32_t j = b; j < e; j++) any |= gslot[j] >= s0 && gslot[j] < s1;
+	if (!any) return;
+	uint32_t l[kList];
+	int n = 0;
+	for (uint32_t j = b; j < e; j++) {
+		// a sibling's whole list in four 16-byte loads, then merged
+		const ulonglong2* q = reinterpret_cast<const ulonglong2*>(lst + size_t(gslot[j]) * kList);
+		uint64_t v[kList];
+#pragma unroll
+		for (int i = 0; i < kList / 2; i++) {
+			const ulonglong2 t = q[i];
+			v[2 * i] = t.x;
+			v[2 * i + 1] = t.y;
 		}
-		for (uint32_t j = b; j < e; j++)
-			if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
+		bool end = false;
+#pragma unroll
+		for (int i = 0; i < kList; i++) {
+			end |= v[i] == error_cell;
+			if (!end && !list_insert(l, n, uint32_t(v[i]))) atomicOr(err, 1);
+		}
 	}
+	for (uint32_t j = b; j < e; j++)
+		if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
+}
+
+// ---- mask path -------------------------------------------------------------
+struct L0Geom {
+	uint32_t lx, ly, lz, bx, by;
+};
+
+__device__ __forceinline__ void l0_unpack(uint32_t c, const L0Geom& G, int& x, int& y, int& z) {
+	x = int(c & ((1u << G.bx) - 1u));
+	y = int((c >> G.bx) & ((1u << G.by) - 1u));
+	z = int(c >> (G.bx + G.by));
+}
+
+// offset of level-0 coordinate q from p along an axis of length L, in
+// [-1, 1] for a neighbor's parent (a periodic wrap undone); 2 if not
+__device__ __forceinline__ int l0_rel(int q, int p, int L) {
+	int d = q - p;
+	if (d > 1) d -= L;
+	else if (d < -1) d += L;
+	return d >= -1 && d <= 1 ? d : 2;
+}
+
+__global__ void mask_l0c_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, size_t n, L0Geom G,
+                                uint32_t* __restrict__ l0c) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t i = map_level0_parent(m, slot_ids[s]) - 1;
+		const uint64_t x = i % G.lx, y = (i / G.lx) % G.ly, z = i / (uint64_t(G.lx) * G.ly);
+		l0c[s] = uint32_t(x) | (uint32_t(y) << G.bx) | (uint32_t(z) << (G.bx + G.by));
+	}
+}
+
+// per neighbor entry: slot | code << 27 (code = 9 (dz+1) + 3 (dy+1) + dx+1 of
+// the neighbor's level-0 parent from the row's), kEntNone without a slot
+constexpr uint32_t kEntNone = 0xffffffffu;
+__global__ void mask_ent_kernel(const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nslot, size_t rows,
+                                const uint32_t* __restrict__ l0c, L0Geom G, uint32_t* __restrict__ ent,
+                                int* __restrict__ bad) {
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < rows; r += size_t(gridDim.x) * blockDim.x) {
+		int px, py, pz;
+		l0_unpack(l0c[r], G, px, py, pz);
+		for (uint32_t j = ptr[r], e = ptr[r + 1]; j < e; j++) {
+			const int32_t ns = nslot[j];
+			if (ns < 0) {
+				ent[j] = kEntNone;
+				continue;
+			}
+			int qx, qy, qz;
+			l0_unpack(l0c[ns], G, qx, qy, qz);
+			const int dx = l0_rel(qx, px, int(G.lx)), dy = l0_rel(qy, py, int(G.ly)), dz = l0_rel(qz, pz, int(G.lz));
+			if (dx == 2 || dy == 2 || dz == 2) {
+				*bad = 1;
+				ent[j] = kEntNone;
+				continue;
+			}
+			ent[j] = uint32_t(ns) | (uint32_t(9 * (dz + 1) + 3 * (dy + 1) + dx + 1) << 27);
+		}
+	}
+}
+
+// the level-0 id at code c from the level-0 cell at (px, py, pz)
+__device__ __forceinline__ uint64_t l0_id_at(uint32_t c, int px, int py, int pz, const L0Geom& G) {
+	int x = px + int(c % 3u) - 1, y = py + int((c / 3u) % 3u) - 1, z = pz + int(c / 9u) - 1;
+	x += x < 0 ? int(G.lx) : (x >= int(G.lx) ? -int(G.lx) : 0);
+	y += y < 0 ? int(G.ly) : (y >= int(G.ly) ? -int(G.ly) : 0);
+	z += z < 0 ? int(G.lz) : (z >= int(G.lz) ? -int(G.lz) : 0);
+	return 1 + uint64_t(x) + uint64_t(y) * G.lx + uint64_t(z) * G.lx * G.ly;
+}
+
+// collect (solve.hpp:46-110) on the mask path, in two passes.
+// Pass 1, over the neighbor entries of the rows: one byte per entry, code |
+// alive << 5 (31: no slot); four entries per thread (one 16-byte index load,
+// four state gathers, one 4-byte store), so the gathers of the whole grid are
+// in flight together instead of behind each row's walk.
+__global__ void gol_amr_values_kernel(const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent,
+                                      const uint32_t* __restrict__ ptr, size_t s0, size_t s1,
+                                      uint32_t* __restrict__ val) {
+	const uint32_t w0 = ptr[s0] >> 2, w1 = (ptr[s1] + 3) >> 2;
+	const uint32_t step = gridDim.x * blockDim.x;
+	// two words (eight gathers) in flight per thread
+	for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += 2 * step) {
+		const bool two = w + step < w1;
+		const uint4 ea = reinterpret_cast<const uint4*>(ent)[w];
+		const uint4 eb = two ? reinterpret_cast<const uint4*>(ent)[w + step] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
+		const uint32_t q[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
+		uint32_t st[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++) st[k] = q[k] == kEntNone ? 0u : state[q[k] & 0x7ffffffu];
+		uint32_t out[2] = {0, 0};
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
+			out[k >> 2] |= v << (8 * (k & 3));
+		}
+		val[w] = out[0];
+		if (two) val[w + step] = out[1];
+	}
+}
+
+// Pass 2, one thread per row: the block's entry bytes staged into LDS with
+// coalesced 4-byte loads; the row walk tests and sets bits instead of
+// comparing ids and appends a parent to the reference's list (data[1..8],
+// first-seen order) only when its bit is new
+__global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
+    const uint8_t* __restrict__ val, const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ l0c, L0Geom G,
+    uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0, size_t s1, int* __restrict__ err) {
+	constexpr uint32_t cap = 8192;  // bytes of entry values staged per block
+	__shared__ uint32_t sp32[cap / 4];
+	const uint32_t tid = threadIdx.x;
+	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
+	if (r0 >= s1) return;  // block-uniform
+	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
+	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
+	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
+	const uint32_t* val32 = reinterpret_cast<const uint32_t*>(val) + (E0 >> 2);
+	for (uint32_t w = tid; w < (nB + 3) / 4; w += kCollectRows) sp32[w] = val32[w];
+	__syncthreads();
+	const size_t s = r0 + tid;
+	if (s >= r1) return;
+	uint32_t mask = 0, l[kList];
+#pragma unroll
+	for (int i = 0; i < kList; i++) l[i] = 13;
+	int n = 0;
+	auto visit = [&](uint32_t v) {
+		const uint32_t c = v & 31u;
+		if (c == 31u || c == 13u) return;  // no slot / the own level-0 parent
+		const uint32_t bit = 1u << c;
+		if (v & 32u) {
+			if (!(mask & bit)) {
+				mask |= bit;
+				if (n == kList) {
+					atomicOr(err, 1);
+				} else {
+#pragma unroll
+					for (int i = 0; i < kList; i++)
+						if (i == n) l[i] = c;
+					n++;
+				}
+			}
+		} else if (mask & bit) {
+			atomicOr(err, 2);
+		}
+	};
+	// the row's entry bytes a 4-byte word at a time (E0 is word aligned)
+	const uint32_t* gval32 = reinterpret_cast<const uint32_t*>(val);
+	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e;) {
+		const uint32_t word = j - E0 < nB ? sp32[(j - E0) >> 2] : gval32[j >> 2];
+		const uint32_t b0 = j & 3u, b1 = e - j < 4u - b0 ? b0 + (e - j) : 4u;
+		for (uint32_t b = b0; b < b1; b++) visit((word >> (8 * b)) & 0xffu);
+		j += b1 - b0;
+	}
+	int px, py, pz;
+	l0_unpack(l0c[s], G, px, py, pz);
+	uint64_t out[kList];
+#pragma unroll
+	for (int i = 0; i < kList; i++) out[i] = i < n ? l0_id_at(l[i], px, py, pz, G) : error_cell;
+	ulonglong2* o = reinterpret_cast<ulonglong2*>(lst + s * kList);
+#pragma unroll
+	for (int i = 0; i < kList / 2; i++) o[i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+	mask_out[s] = mask;
+}
+
+__global__ void gol_amr_spread0_mask_kernel(const uint32_t* __restrict__ lvl0, size_t n0, uint32_t* __restrict__ state,
+                                            const uint32_t* __restrict__ mask, size_t s0, size_t s1) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n0; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t s = lvl0[i];
+		if (s < s0 || s >= s1) continue;
+		gol_rule(state, s, __popc(mask[s]));
+	}
+}
+
+// spread + rule of one refined level-0 cell's leaves: the union of the
+// siblings' parents is the OR of their masks (a sibling held as a remote
+// copy contributes its received list, turned into bits)
+__global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ gptr, size_t ng,
+                                                  const uint32_t* __restrict__ gslot, uint32_t* __restrict__ state,
+                                                  const uint32_t* __restrict__ mask, const uint64_t* __restrict__ lst,
+                                                  const uint32_t* __restrict__ l0c, L0Geom G, size_t n_local,
+                                                  size_t s0, size_t s1, int* __restrict__ err) {
+	const size_t gi = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	if (gi >= ng) return;
+	const uint32_t b = gptr[gi], e = gptr[gi + 1];
+	bool any = false;
+	uint32_t u = 0;
+	for (uint32_t j = b; j < e; j++) {
+		const uint32_t gs = gslot[j];
+		any |= gs >= s0 && gs < s1;
+		if (gs < n_local) {
+			u |= mask[gs];
+			continue;
+		}
+		int px, py, pz;
+		l0_unpack(l0c[gs], G, px, py, pz);
+		for (int i = 0; i < kList; i++) {
+			const uint64_t id = lst[size_t(gs) * kList + i];
+			if (id == error_cell) break;
+			const uint64_t k = id - 1;
+			const int qx = int(k % G.lx), qy = int((k / G.lx) % G.ly), qz = int(k / (uint64_t(G.lx) * G.ly));
+			const int dx = l0_rel(qx, px, int(G.lx)), dy = l0_rel(qy, py, int(G.ly)), dz = l0_rel(qz, pz, int(G.lz));
+			if (dx == 2 || dy == 2 || dz == 2) {
+				atomicOr(err, 4);
+				continue;
+			}
+			u |= 1u << (9 * (dz + 1) + 3 * (dy + 1) + dx + 1);
+		}
+	}
+	if (!any) return;
+	const int n = __popc(u);
+	if (n > kList) atomicOr(err, 1);
+	for (uint32_t j = b; j < e; j++)
+		if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
 }
 
 }  // namespace
 
-void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, GolAmrTables& T,
-                      hipStream_t s) {
-	DX_REQUIRE(m.first[1] - 1 <= 0x7fffffffull && n_slots <= 0xffffffffull,
+static uint32_t bits_for(uint64_t len) {
+	uint32_t b = 0;
+	while ((uint64_t(1) << b) < len) b++;
+	return b;
+}
+
+void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, unsigned hood_len,
+                      const uint32_t* ptr, const int32_t* nslot, GolAmrTables& T, hipStream_t s) {
+	DX_REQUIRE(m.first[1] - 1 < 0x7fffffffull && n_slots <= 0xffffffffull,
 	           "refined game of life: level-0 ids must fit 31 bits");
 	T.l0.alloc(n_slots + 1);
 	T.pack.alloc(n_slots + 1);
@@ -229,24 +496,79 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 	HIP_CHECK(hipStreamSynchronize(s));
 	T.ng = ng;
 	T.n_lvl0 = size_t(h[1]);
+
+	// mask path: neighborhood length <= 1, slots < 2^27, packed level-0 coordinates in 31 bits
+	const uint32_t bx = bits_for(m.len[0]), by = bits_for(m.len[1]), bz = bits_for(m.len[2]);
+	T.mask_path = false;
+	T.l0c.release();
+	T.ent.release();
+	T.mask.release();
+	if (hood_len <= 1 && n_slots < (size_t(1) << 27) && bx + by + bz <= 31) {
+		const L0Geom G{uint32_t(m.len[0]), uint32_t(m.len[1]), uint32_t(m.len[2]), bx, by};
+		T.bx = bx;
+		T.by = by;
+		T.lx = G.lx;
+		T.ly = G.ly;
+		T.lz = G.lz;
+		T.l0c.alloc(n_slots + 1);
+		T.mask.alloc(n_slots + 1);
+		uint32_t total = 0;
+		if (n_local) HIP_CHECK(hipMemcpyAsync(&total, ptr + n_local, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		T.ent.alloc(size_t(total) + 4);  // whole 16-byte words for the values pass
+		T.val.alloc(size_t(total) / 4 + 2);
+		T.n_ent = total;
+		HIP_CHECK(hipMemsetAsync(T.ent.p, 0xff, T.ent.n * 4, s));  // padding = no slot
+		DBuf<int> bad;
+		bad.alloc(1);
+		HIP_CHECK(hipMemsetAsync(bad.p, 0, 4, s));
+		if (n_slots) {
+			mask_l0c_kernel<<<grid_for(n_slots, 256), 256, 0, s>>>(m, slot_ids, n_slots, G, T.l0c.p);
+			HIP_CHECK(hipGetLastError());
+		}
+		if (n_local) {
+			mask_ent_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(ptr, nslot, n_local, T.l0c.p, G, T.ent.p, bad.p);
+			HIP_CHECK(hipGetLastError());
+		}
+		int hb = 0;
+		HIP_CHECK(hipMemcpyAsync(&hb, bad.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		T.mask_path = hb == 0;
+	}
 	T.valid = true;
 }
 
-void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
+void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s) {
 	if (s1 <= s0) return;
-	if (phase == 0) {
-		pack_kernel<<<grid_for(n_slots, 256), 256, 0, s>>>(T.l0.p, state, n_slots, T.pack.p);
+	if (T.mask_path) {
+		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
+		if (phase == 0) {
+			gol_amr_values_kernel<<<grid_for(T.n_ent / 4 + 1, 256, 256u * 64u), 256, 0, s>>>(state, T.ent.p, ptr, s0, s1,
+			                                                                               T.val.p);
+			gol_amr_collect_mask_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
+			    reinterpret_cast<const uint8_t*>(T.val.p), ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, err);
+		} else {
+			if (T.n_lvl0)
+				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,
+				                                                                   s0, s1);
+			if (T.ng)
+				gol_amr_spread_groups_mask_kernel<<<xcd_grid((T.ng + 255) / 256), 256, 0, s>>>(
+				    T.gptr.p, T.ng, T.gslot.p, state, T.mask.p, lst, T.l0c.p, G, n_local, s0, s1, err);
+		}
 		HIP_CHECK(hipGetLastError());
-		// eight neighbor rows gathered ahead (round 1: 3.02 / 2.25 / 2.20 ms
-		// per step with one / four / eight)
-		gol_amr_collect_kernel<8><<<unsigned((s1 - s0 + 255) / 256), 256, 0, s>>>(T.pack.p, lst, ptr, nslot, s0, s1,
-		                                                                         err);
+		return;
+	}
+	if (phase == 0) {
+		gol_amr_pack_kernel<<<grid_for(n_slots, 256), 256, 0, s>>>(T.l0.p, state, n_slots, T.pack.p);
+		HIP_CHECK(hipGetLastError());
+		gol_amr_collect_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
+		    T.pack.p, lst, ptr, nslot, s0, s1, err);
 	} else {
 		if (T.n_lvl0)
 			gol_amr_spread0_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, lst, s0, s1);
 		if (T.ng)
-			gol_amr_spread_groups_kernel<<<grid_for(T.ng, 256), 256, 0, s>>>(T.gptr.p, T.ng, T.gslot.p, state, lst, s0,
+			gol_amr_spread_groups_kernel<<<xcd_grid((T.ng + 255) / 256), 256, 0, s>>>(T.gptr.p, T.ng, T.gslot.p, state, lst, s0,
 			                                                                 s1, err);
 	}
 	HIP_CHECK(hipGetLastError());

@@ -20,9 +20,79 @@ std::vector<Field*> transfer_fields(Grid& g) {
 	return tf;
 }
 
+// the fixed-size / variable-size ones among them
+static std::vector<Field*> fixed_transfer_fields(Grid& g) {
+	std::vector<Field*> tf;
+	for (auto& f : g.fields)
+		if (f.transfer && !f.var) tf.push_back(&f);
+	return tf;
+}
+
+std::vector<Field*> var_transfer_fields(Grid& g) {
+	std::vector<Field*> tf;
+	for (auto& f : g.fields)
+		if (f.transfer && f.var) tf.push_back(&f);
+	return tf;
+}
+
+// --------------------------------------------------------------------------- variable-size payloads
+// Per peer (ascending) the runs of a transfer: cells [soff, soff + sn) of the
+// send list and [roff, roff + rn) of the receive list.
+struct PeerRuns {
+	std::vector<int> peer;
+	std::vector<size_t> soff, sn, roff, rn;
+	void add(int p, size_t so, size_t ns, size_t ro, size_t nr) {
+		peer.push_back(p);
+		soff.push_back(so);
+		sn.push_back(ns);
+		roff.push_back(ro);
+		rn.push_back(nr);
+	}
+};
+
+static void var_pack(const Field& f, const int32_t* slots, size_t n, VarMsg& M, hipStream_t s) {
+	var_gather(f, slots, n, M.ssz, M.sbytes, s);
+	M.hs = download(M.ssz.p, n, s);
+}
+
+// the two exchanges of a variable-size transfer: the sizes (their counts are
+// known to both sides), then the bytes (known from the sizes)
+static void var_transfer(Grid& g, VarMsg& M, const PeerRuns& R, size_t n_recv, hipStream_t s) {
+	M.rsz.alloc(n_recv + 1);
+	std::vector<DevMsg> m1;
+	for (size_t i = 0; i < R.peer.size(); i++)
+		if (R.sn[i] || R.rn[i])
+			m1.push_back(DevMsg{R.peer[i], reinterpret_cast<const uint8_t*>(M.ssz.p + R.soff[i]), R.sn[i] * 8,
+			                    reinterpret_cast<uint8_t*>(M.rsz.p + R.roff[i]), R.rn[i] * 8});
+	comm_device_transfer(g, m1, s);
+	HIP_CHECK(hipStreamSynchronize(s));
+	const std::vector<uint64_t> hr = download(M.rsz.p, n_recv, s);
+	auto sum = [](const std::vector<uint64_t>& v, size_t a, size_t b) {
+		uint64_t t = 0;
+		for (size_t i = a; i < b; i++) t += v[i];
+		return t;
+	};
+	const uint64_t rtotal = sum(hr, 0, n_recv);
+	M.rbytes.alloc(rtotal + 1);
+	std::vector<DevMsg> m2;
+	for (size_t i = 0; i < R.peer.size(); i++) {
+		const uint64_t sbo = sum(M.hs, 0, R.soff[i]), sbl = sum(M.hs, R.soff[i], R.soff[i] + R.sn[i]);
+		const uint64_t rbo = sum(hr, 0, R.roff[i]), rbl = sum(hr, R.roff[i], R.roff[i] + R.rn[i]);
+		if (sbl || rbl) m2.push_back(DevMsg{R.peer[i], M.sbytes.p + sbo, sbl, M.rbytes.p + rbo, rbl});
+	}
+	comm_device_transfer(g, m2, s);
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
 Field& field(Grid& g, int fid) {
 	DX_REQUIRE(fid >= 0 && size_t(fid) < g.fields.size(), "invalid field id");
 	return g.fields[size_t(fid)];
+}
+
+Field& fixed_field(Grid& g, int fid) {
+	Field& f = field(g, fid);
+	DX_REQUIRE(!f.var, "a variable-size field has no fixed element layout (use the dccrgx_variable_field_* calls)");
+	return f;
 }
 
 void ensure_scratch(Grid& g, Field& f) {
@@ -120,9 +190,30 @@ static size_t off_of(const std::map<int, size_t>& m, int p) {
 // start the exchange of a plan on s_comm (after the work queued on s_comp);
 // `direct`: the plan's receive slots of a peer are one contiguous run of
 // halo slots, so full-element fields are received in place
+static void var_halo(Grid& g, HaloPlan& H, hipStream_t s) {
+	const std::vector<Field*> vf = var_transfer_fields(g);
+	if (vf.empty()) return;
+	PeerRuns R;
+	for (int p : H.peers()) R.add(p, off_of(H.send_off, p), count_of(H.send_ids, p), off_of(H.recv_off, p), count_of(H.recv_ids, p));
+	for (Field* f : vf) {
+		VarMsg M;
+		var_pack(*f, H.send_slots.p, H.n_send, M, s);
+		var_transfer(g, M, R, H.n_recv, s);
+		var_place(*f, g.n_slots, H.recv_slots.p, H.n_recv, M.rsz.p, M.rbytes.p, s);
+	}
+}
+
 static void plan_start(Grid& g, HaloPlan& H, bool direct) {
-	const std::vector<Field*> tf = transfer_fields(g);
-	if (tf.empty()) return;
+	if (transfer_fields(g).empty()) return;
+	const std::vector<Field*> tf = fixed_transfer_fields(g);
+	if (tf.empty()) {
+		// variable-size payloads only: synchronous (their byte counts travel first)
+		HIP_CHECK(hipEventRecord(g.ev_comp, g.s_comp));
+		HIP_CHECK(hipStreamWaitEvent(g.s_comm, g.ev_comp, 0));
+		var_halo(g, H, g.s_comm);
+		HIP_CHECK(hipEventRecord(g.ev_halo, g.s_comm));
+		return;
+	}
 	const PlanLayout L = plan_layout(H, tf);
 	HIP_CHECK(hipEventRecord(g.ev_comp, g.s_comp));
 	HIP_CHECK(hipStreamWaitEvent(g.s_comm, g.ev_comp, 0));
@@ -192,6 +283,7 @@ static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 			        tf[k]->data.p, s);
 		HIP_CHECK(hipStreamSynchronize(s));
 	}
+	var_halo(g, H, s);
 	HIP_CHECK(hipEventRecord(g.ev_halo, s));
 }
 
@@ -300,9 +392,15 @@ void uhood_halo(Grid& g, int id) {
 }
 
 // the explicit transport of one plan (dccrgx_halo_pack / _place)
+static void no_var_transfer(Grid& g, const char* what) {
+	DX_REQUIRE(var_transfer_fields(g).empty(),
+	           std::string(what) + ": variable-size fields move only with the library's own transport");
+}
+
 size_t halo_pack_peer(Grid& g, int hood, int peer, uint8_t* buf, size_t cap) {
+	no_var_transfer(g, "halo_pack");
 	HaloPlan& H = plan_of(g, hood);
-	const std::vector<Field*> tf = transfer_fields(g);
+	const std::vector<Field*> tf = fixed_transfer_fields(g);
 	const PlanLayout L = plan_layout(H, tf);
 	const size_t ns = count_of(H.send_ids, peer), so = off_of(H.send_off, peer);
 	DX_REQUIRE(cap >= ns * L.bpc, "buffer too small for the halo message");
@@ -318,8 +416,9 @@ size_t halo_pack_peer(Grid& g, int hood, int peer, uint8_t* buf, size_t cap) {
 }
 
 void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t bytes) {
+	no_var_transfer(g, "halo_place");
 	HaloPlan& H = plan_of(g, hood);
-	const std::vector<Field*> tf = transfer_fields(g);
+	const std::vector<Field*> tf = fixed_transfer_fields(g);
 	const PlanLayout L = plan_layout(H, tf);
 	const size_t nr = count_of(H.recv_ids, peer), ro = off_of(H.recv_off, peer);
 	DX_REQUIRE(bytes == nr * L.bpc, "halo message has the wrong size");
@@ -336,8 +435,9 @@ void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t byt
 }
 
 void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb) {
+	no_var_transfer(g, "halo_message_size");
 	HaloPlan& H = plan_of(g, hood);
-	const PlanLayout L = plan_layout(H, transfer_fields(g));
+	const PlanLayout L = plan_layout(H, fixed_transfer_fields(g));
 	sb = count_of(H.send_ids, peer) * L.bpc;
 	rb = count_of(H.recv_ids, peer) * L.bpc;
 }
@@ -407,7 +507,10 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (g.size > 1) comm_require(g, "stop_refining");
 	const int nh = int(g.hood.size() / 3);
 	hipStream_t s = g.s_comp;
-	for (auto& f : g.fields) f.removed.release();
+	for (auto& f : g.fields) {
+		f.removed.release();
+		f.rm_off.release();
+	}
 	g.removed_ids_h.clear();
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
@@ -496,10 +599,13 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		return k;
 	}();
 	const size_t n_rm = keep_ids.size() + n_recv;
-	if (n_rm || !send_ids.empty()) {
+	// every rank takes part when any family merges (the host transport's
+	// exchanges are collective)
+	if (!F.empty()) {
 		// removed store order: the kept children ascending, then per source
 		// process (ascending rank) its children ascending
 		for (auto& f : g.fields) {
+			if (f.var) continue;
 			f.removed.alloc(n_rm * f.elem + 1);
 			if (!keep_ids.empty()) {
 				const DBuf<int32_t> sl = slots_of(g, keep_ids);
@@ -526,6 +632,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			const DBuf<int32_t> sl = slots_of(g, kv.second);
 			size_t o = soff[i++];
 			for (auto& f : g.fields) {
+				if (f.var) continue;
 				k_pack(f.data.p, f.elem, 0, f.elem, sl.p, kv.second.size(), sbuf.p + o, s);
 				o += kv.second.size() * f.elem;
 			}
@@ -554,6 +661,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		for (auto& kv : recv_ids) {
 			size_t o = roff[j++];
 			for (auto& f : g.fields) {
+				if (f.var) continue;
 				HIP_CHECK(hipMemcpyAsync(f.removed.p + at * f.elem, rbuf.p + o, kv.second.size() * f.elem,
 				                         hipMemcpyDeviceToDevice, s));
 				o += kv.second.size() * f.elem;
@@ -561,6 +669,41 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			at += kv.second.size();
 		}
 		HIP_CHECK(hipStreamSynchronize(s));
+		// variable-size payloads: the kept children's, then the received ones
+		if (std::any_of(g.fields.begin(), g.fields.end(), [](const Field& f) { return f.var; })) {
+			std::vector<uint64_t> out_all;
+			PeerRuns R;
+			size_t so2 = 0, ro2 = 0;
+			for (int p = 0; p < g.size; p++) {
+				if (p == g.rank) continue;
+				const size_t ns = count_of(send_ids, p), nr = count_of(recv_ids, p);
+				if (ns) out_all.insert(out_all.end(), send_ids[p].begin(), send_ids[p].end());
+				R.add(p, so2, ns, ro2, nr);
+				so2 += ns;
+				ro2 += nr;
+			}
+			const DBuf<int32_t> osl = slots_of(g, out_all);
+			const DBuf<int32_t> ksl = slots_of(g, keep_ids);
+			for (auto& f : g.fields) {
+				if (!f.var) continue;
+				VarMsg K, X;
+				var_pack(f, ksl.p, keep_ids.size(), K, s);
+				var_pack(f, osl.p, out_all.size(), X, s);
+				if (g.size > 1) var_transfer(g, X, R, ro2, s);
+				const size_t nk = keep_ids.size();
+				DBuf<uint64_t> sizes;
+				sizes.alloc(n_rm + 1);
+				if (nk) HIP_CHECK(hipMemcpyAsync(sizes.p, K.ssz.p, nk * 8, hipMemcpyDeviceToDevice, s));
+				if (ro2) HIP_CHECK(hipMemcpyAsync(sizes.p + nk, X.rsz.p, ro2 * 8, hipMemcpyDeviceToDevice, s));
+				f.rm_off.alloc(n_rm + 1);
+				const uint64_t tot = scan_exclusive_u64(sizes.p, f.rm_off.p, n_rm, s);
+				const uint64_t kb = std::accumulate(K.hs.begin(), K.hs.end(), uint64_t(0));
+				f.removed.alloc(tot + 1);
+				if (kb) HIP_CHECK(hipMemcpyAsync(f.removed.p, K.sbytes.p, kb, hipMemcpyDeviceToDevice, s));
+				if (tot > kb) HIP_CHECK(hipMemcpyAsync(f.removed.p + kb, X.rbytes.p, tot - kb, hipMemcpyDeviceToDevice, s));
+				HIP_CHECK(hipStreamSynchronize(s));
+			}
+		}
 	}
 
 	Mesh known, nm;
@@ -623,7 +766,10 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 	}
 	g.weights.clear();
 	g.removed_ids_h.clear();  // unrefined_cell_data (3811)
-	for (auto& f : g.fields) f.removed.release();
+	for (auto& f : g.fields) {
+		f.removed.release();
+		f.rm_off.release();
+	}
 	if (n) {
 		std::vector<int32_t> own(n);
 		lookup_batch(g, cells, n, own.data(), nullptr);
@@ -669,12 +815,37 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 		const DBuf<int32_t> sl = slots_of(g, kv.second);
 		size_t o = M.out_off[kv.first];
 		for (auto& f : g.fields) {
+			if (f.var) continue;
 			k_pack(f.data.p, f.elem, 0, f.elem, sl.p, kv.second.size(), M.sendbuf.p + o, g.s_comp);
 			o += kv.second.size() * f.elem;
 		}
 	}
+	// variable-size payloads of the leaving cells (peer by peer, ascending id)
+	std::vector<uint64_t> leaving;
+	for (auto& kv : M.out) leaving.insert(leaving.end(), kv.second.begin(), kv.second.end());
+	const DBuf<int32_t> lsl = slots_of(g, leaving);
+	for (auto& f : g.fields) {
+		if (!f.var) continue;
+		M.var.emplace_back();
+		var_pack(f, lsl.p, leaving.size(), M.var.back(), g.s_comp);
+	}
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	M.active = true;
+}
+
+// the runs of a migration's leaving / arriving cells per peer
+static PeerRuns migration_runs(const Grid& g, const Migration& M, size_t& n_in) {
+	PeerRuns R;
+	size_t so = 0, ro = 0;
+	for (int p = 0; p < g.size; p++) {
+		if (p == g.rank) continue;
+		const size_t ns = count_of(M.out, p), nr = count_of(M.in, p);
+		R.add(p, so, ns, ro, nr);
+		so += ns;
+		ro += nr;
+	}
+	n_in = ro;
+	return R;
 }
 
 // continue_balance_load (3899-3934): the payloads move
@@ -690,6 +861,9 @@ void continue_balance_load_impl(Grid& g) {
 		}
 		comm_device_transfer(g, msgs, g.s_comp);
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		size_t n_in = 0;
+		const PeerRuns R = migration_runs(g, M, n_in);
+		for (VarMsg& vm : M.var) var_transfer(g, vm, R, n_in, g.s_comp);
 	}
 	M.transferred = true;
 }
@@ -734,8 +908,18 @@ void finish_balance_load_impl(Grid& g) {
 		const DBuf<int32_t> sl = slots_of(g, kv.second);
 		size_t o = M.in_off[kv.first];
 		for (auto& f : g.fields) {
+			if (f.var) continue;
 			k_place(M.recvbuf.p + o, f.elem, 0, f.elem, sl.p, kv.second.size(), f.data.p, s);
 			o += kv.second.size() * f.elem;
+		}
+	}
+	if (!arrived.empty() && !M.var.empty()) {
+		const DBuf<int32_t> asl = slots_of(g, arrived);
+		size_t k = 0;
+		for (auto& f : g.fields) {
+			if (!f.var) continue;
+			VarMsg& vm = M.var[k++];
+			var_place(f, g.n_slots, asl.p, arrived.size(), vm.rsz.p, vm.rbytes.p, s);
 		}
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
@@ -746,6 +930,7 @@ void finish_balance_load_impl(Grid& g) {
 void migration_message_size(Grid& g, int peer, size_t& sb, size_t& rb) {
 	const Migration& M = g.mig;
 	DX_REQUIRE(M.active, "no balance_load in progress");
+	DX_REQUIRE(M.var.empty(), "migration messages: variable-size fields move only with continue_balance_load");
 	sb = count_of(M.out, peer) * M.bytes_per_cell;
 	rb = count_of(M.in, peer) * M.bytes_per_cell;
 }

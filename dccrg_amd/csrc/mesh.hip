@@ -350,6 +350,10 @@ void rebuild(Grid& g, Mesh& nm) {
 	// 6. carry field payloads over
 	const DevMesh odm = old.dev(m.last);
 	for (auto& f : g.fields) {
+		if (f.var) {  // children and new copies start empty (the reference default-constructs them)
+			var_remap(f, old_slot_ids.p, old_slot_ids.p ? old_n_local : 0, dm, g.n_slots, s);
+			continue;
+		}
 		DBuf<uint8_t> nd;
 		nd.alloc(g.n_slots * f.elem);
 		if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));

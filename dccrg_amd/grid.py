@@ -69,6 +69,71 @@ class Field:
         check(lib().dccrgx_set_field_window(self.grid.h, self.id, int(offset), int(nbytes)))
 
 
+class VariableField:
+    """A payload of a different number of bytes per cell (a Cell_Data whose
+    get_mpi_datatype describes e.g. a std::vector, tests/variable_data_size):
+    one byte pool over all slots.  Values are lists of numpy arrays of
+    ``dtype`` (one per cell); the halo, migrations and removed-cell payloads
+    carry each cell's bytes and its size."""
+
+    def __init__(self, grid, fid, name, dtype, transfer):
+        self.grid, self.id, self.name, self.dtype, self.transfer = grid, fid, name, np.dtype(dtype), transfer
+
+    def sizes(self, slot0=0, n=None):
+        """Byte sizes of the cells at slots [slot0, slot0 + n)."""
+        if n is None:
+            n = self.grid.n_slots - slot0
+        out = np.empty(n, np.uint64)
+        check(lib().dccrgx_variable_field_sizes(self.grid.h, self.id, slot0, n, _ptr(out)))
+        return out
+
+    def resize(self, counts, slot0=0):
+        """Element counts of the cells from slot0 on (Cell_Data::...resize):
+        each keeps its leading bytes, new bytes are zero."""
+        b = np.ascontiguousarray(np.asarray(counts, np.uint64) * np.uint64(self.dtype.itemsize))
+        check(lib().dccrgx_variable_field_resize(self.grid.h, self.id, slot0, b.size, _ptr(b)))
+
+    def set(self, values, slot0=0):
+        """One array per cell from slot0 on; the cells take their sizes."""
+        arrs = [np.ascontiguousarray(v, self.dtype) for v in values]
+        self.resize([a.size for a in arrs], slot0)
+        raw = np.concatenate([a.view(np.uint8) for a in arrs]) if arrs else np.zeros(0, np.uint8)
+        raw = np.ascontiguousarray(raw)
+        check(lib().dccrgx_variable_field_upload(self.grid.h, self.id, slot0, len(arrs), _ptr(raw), raw.nbytes))
+
+    def get(self, slot0=0, n=None):
+        if n is None:
+            n = self.grid.n_slots - slot0
+        sz = self.sizes(slot0, n)
+        raw = np.empty(int(sz.sum()), np.uint8)
+        got = C.c_size_t()
+        check(lib().dccrgx_variable_field_download(self.grid.h, self.id, slot0, n, _ptr(raw), raw.nbytes,
+                                                     C.byref(got)))
+        return _split(raw, sz, self.dtype)
+
+    def get_removed(self):
+        """Payloads of the cells removed by the last stop_refining whose
+        parent is local (order of Dccrg.get_removed_cells(sorted=False))."""
+        n = len(self.grid.get_removed_cells(sorted=False))
+        sz = np.zeros(n + 1, np.uint64)
+        total = C.c_size_t()
+        rc = lib().dccrgx_removed_variable_field_download(self.grid.h, self.id, _ptr(sz), None, 0, C.byref(total))
+        if rc != ERANGE:
+            check(rc)
+        raw = np.empty(total.value, np.uint8)
+        check(lib().dccrgx_removed_variable_field_download(self.grid.h, self.id, _ptr(sz), _ptr(raw), raw.nbytes,
+                                                           C.byref(total)))
+        return _split(raw, sz[:n], self.dtype)
+
+
+def _split(raw, sizes, dtype):
+    out, o = [], 0
+    for b in sizes.tolist():
+        out.append(raw[o:o + int(b)].view(dtype).copy())
+        o += int(b)
+    return out
+
+
 class TorchExchange:
     """Host transport over torch.distributed point-to-point (gloo): the
     exchange primitive of include/dccrgx.h (dccrgx_exchange_fn)."""
@@ -607,6 +672,23 @@ class Dccrg:
         f = Field(self, fid.value, name, dt, transfer)
         self.fields[name] = f
         return f
+
+    def add_variable_field(self, name, dtype, transfer=True):
+        """A payload whose size differs per cell (tests/variable_data_size)."""
+        fid = C.c_int()
+        check(lib().dccrgx_add_variable_field(self.h, name.encode(), int(transfer), C.byref(fid)))
+        f = VariableField(self, fid.value, name, dtype, transfer)
+        self.fields[name] = f
+        return f
+
+    def set_send_single_cells(self, on):  # 6677
+        check(lib().dccrgx_set_send_single_cells(self.h, int(bool(on))))
+        return self
+
+    def get_send_single_cells(self):  # 6684
+        v = C.c_int()
+        check(lib().dccrgx_get_send_single_cells(self.h, C.byref(v)))
+        return bool(v.value)
 
     # ---- halo -------------------------------------------------------------------
     def update_copies_of_remote_neighbors(self, hood=None):

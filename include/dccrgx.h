@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 4 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 5 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -278,6 +278,45 @@ int dccrgx_field_device_ptr(dccrgx_grid* g, int field_id, void** ptr);
 /* host <-> device copies of whole slot ranges [slot0, slot0+n) */
 int dccrgx_field_upload(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const void* host);
 int dccrgx_field_download(dccrgx_grid* g, int field_id, size_t slot0, size_t n, void* host);
+
+/* ---- variable-size payloads (a Cell_Data whose get_mpi_datatype describes
+ * a different number of bytes per cell, e.g. a std::vector member:
+ * tests/variable_data_size/variable_data_size.cpp, variable_neighbour_data.cpp;
+ * dccrg_get_cell_datatype.hpp:40-340).  One byte pool over all slots; a new
+ * field, new children and new remote copies start empty (the reference
+ * default-constructs them).  The halo, migrations (continue_balance_load)
+ * and the removed-cell store move every cell's size with its bytes, so a
+ * receiver takes the sender's sizes (the reference needs the receiver to
+ * size its copies first, variable_neighbour_data.cpp:95-102, 133-145; done
+ * that way the bytes are the same).  Grid files and the explicit halo /
+ * migration message calls (dccrgx_halo_*, dccrgx_migration_*) refuse them
+ * (DCCRGX_EINVAL); the fixed-field calls (dccrgx_field_*) refuse a variable
+ * field. */
+int dccrgx_add_variable_field(dccrgx_grid* g, const char* name, int transfer, int* field_id);
+/* byte sizes of slots [slot0, slot0 + n) */
+int dccrgx_variable_field_sizes(dccrgx_grid* g, int field_id, size_t slot0, size_t n, uint64_t* sizes);
+/* new byte sizes of slots [slot0, slot0 + n): each cell keeps its first
+ * min(old, new) bytes, new bytes are zero (std::vector::resize) */
+int dccrgx_variable_field_resize(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const uint64_t* sizes);
+/* the concatenated bytes of slots [slot0, slot0 + n); upload needs exactly
+ * their current total, download sets *nbytes (DCCRGX_ERANGE when cap is short) */
+int dccrgx_variable_field_upload(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const void* bytes,
+                                 size_t nbytes);
+int dccrgx_variable_field_download(dccrgx_grid* g, int field_id, size_t slot0, size_t n, void* bytes, size_t cap,
+                                   size_t* nbytes);
+/* device pool and the n_slots + 1 byte offsets (slot s: [off[s], off[s+1])) */
+int dccrgx_variable_field_device_ptr(dccrgx_grid* g, int field_id, void** data, const uint64_t** offsets);
+/* the removed cells' payloads (order of dccrgx_get_removed_cells): sizes
+ * (one per removed cell, may be NULL) and concatenated bytes */
+int dccrgx_removed_variable_field_download(dccrgx_grid* g, int field_id, uint64_t* sizes, void* bytes, size_t cap,
+                                           size_t* nbytes);
+/* set_send_single_cells 6677 / get_send_single_cells 6684: one message per
+ * cell (tag = position + 1) instead of one per process.  Accepted and
+ * reported; the library always sends one message per peer and field, which
+ * carries the same bytes in the same order (message boundaries hold no data
+ * here), so the received payloads are identical. */
+int dccrgx_set_send_single_cells(dccrgx_grid* g, int on);
+int dccrgx_get_send_single_cells(dccrgx_grid* g, int* on);
 
 /* ---- halo (update_copies_of_remote_neighbors 966-1000 and its split form
  * start_remote_neighbor_copy_updates 5010, wait_* 5267-5367) ------------- */

@@ -825,10 +825,9 @@ static uint64_t level0_parent(const Mapping& m, uint64_t cell) {  // dccrg_mappi
 	return m.from_indices(m.indices(cell), 0);
 }
 
-static void gol_amr_step(const Grid& g, std::unordered_map<uint64_t, GolAmrData>& data) {
-	std::vector<uint64_t> cells;
-	for (const auto& cp : g.cell_process) cells.push_back(cp.first);
-	std::sort(cells.begin(), cells.end());
+// the collect loop of get_live_neighbors (solve.hpp:45-109)
+static void gol_amr_collect(const Grid& g, std::unordered_map<uint64_t, GolAmrData>& data,
+                            const std::vector<uint64_t>& cells) {
 	for (const uint64_t cell : cells) {
 		GolAmrData& cd = data.at(cell);
 		for (size_t i = 1; i < cd.size(); i++) cd[i] = 0;
@@ -854,6 +853,13 @@ static void gol_amr_step(const Grid& g, std::unordered_map<uint64_t, GolAmrData>
 			}
 		}
 	}
+}
+
+static void gol_amr_step(const Grid& g, std::unordered_map<uint64_t, GolAmrData>& data) {
+	std::vector<uint64_t> cells;
+	for (const auto& cp : g.cell_process) cells.push_back(cp.first);
+	std::sort(cells.begin(), cells.end());
+	gol_amr_collect(g, data, cells);
 	for (const uint64_t cell : cells) {
 		const uint64_t cp = level0_parent(g.m, cell);
 		GolAmrData& cd = data.at(cell);
@@ -1550,6 +1556,20 @@ int or_gola_steps(void* hp, int steps) {
 	OR_TRY({
 		auto* h = static_cast<OracleHandle*>(hp);
 		for (int s = 0; s < steps; s++) gol_amr_step(h->g, h->gola);
+		return 0;
+	})
+}
+
+// only the collect loop; then the lists data[1..8] of the cells (8 per id)
+int or_gola_collect(void* hp, const uint64_t* ids, uint64_t* lists, size_t n) {
+	OR_TRY({
+		auto* h = static_cast<OracleHandle*>(hp);
+		std::vector<uint64_t> cells;
+		for (const auto& cp : h->g.cell_process) cells.push_back(cp.first);
+		std::sort(cells.begin(), cells.end());
+		gol_amr_collect(h->g, h->gola, cells);
+		for (size_t i = 0; i < n; i++)
+			for (int k = 0; k < 8; k++) lists[8 * i + size_t(k)] = h->gola.at(ids[i])[size_t(k) + 1];
 		return 0;
 	})
 }

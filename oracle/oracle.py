@@ -73,6 +73,7 @@ def lib():
     L.or_gola_set.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
     L.or_gola_steps.argtypes = [C.c_void_p, C.c_int]
     L.or_gola_get.argtypes = [C.c_void_p, u64p, u32p, C.c_size_t]
+    L.or_gola_collect.argtypes = [C.c_void_p, u64p, u64p, C.c_size_t]
     L.or_set_geometry.argtypes = [C.c_void_p, f64p, f64p]
     L.or_geometry_batch.argtypes = [C.c_void_p, u64p, C.c_size_t, f64p, f64p]
     L.or_adv_initialize.argtypes = [C.c_void_p]
@@ -282,6 +283,13 @@ class Grid:
         ids = np.ascontiguousarray(ids, np.uint64)
         out = np.empty(ids.size, np.uint32)
         self._chk(lib().or_gola_get(self.h, ids, out, ids.size))
+        return out
+
+    def gola_collect(self, ids):
+        """Only the collect loop (solve.hpp:45-109); the cells' lists data[1..8]."""
+        ids = np.ascontiguousarray(ids, np.uint64)
+        out = np.empty((ids.size, 8), np.uint64)
+        self._chk(lib().or_gola_collect(self.h, ids, out, ids.size))
         return out
 
     # -- advection ---------------------------------------------------------

@@ -72,6 +72,30 @@ def test_refined_game_matches_oracle(gpu, length, periodic, frac, seed, density,
     g.close()
 
 
+@pytest.mark.parametrize("length,periodic,frac,seed,density", [
+    ((15, 15, 1), (False, False, False), 0.5, 0, 0.3),
+    ((24, 20, 1), (True, True, False), 0.5, 9, 0.3),
+    ((9, 8, 7), (True, True, True), 0.4, 2, 0.05),
+    ((2, 2, 3), (True, True, True), 0.5, 3, 0.3),
+])
+def test_collected_lists_match_oracle(gpu, length, periodic, frac, seed, density):
+    """The lists data[1..8] after the collect loop, entry for entry (level-0
+    parents of live neighbors in first-seen order, error_cell padded)."""
+    o = refined_oracle(length, periodic, frac, seed)
+    g, st, ls = product_on(o, length, periodic)
+    n0 = length[0] * length[1] * length[2]
+    rng = np.random.default_rng(seed + 7)
+    live0 = {int(c) for c in np.nonzero(rng.random(n0) < density)[0] + 1}
+    slots = g.slot_ids()[: g.n_local]
+    a0, _ = states_by_parent(o, slots, live0)
+    st.set(a0)
+    o.gola_set(slots, a0)
+    g.gol_amr_collect(st, ls)
+    got = ls.get(0, g.n_local).reshape(-1, 8)
+    assert np.array_equal(got, o.gola_collect(slots))
+    g.close()
+
+
 def test_unrefined2d_differential_through_product(gpu):
     """unrefined2d.cpp:104-240 with the product on both sides: the refined
     grid (random half of the cells refined, children inherit the state)

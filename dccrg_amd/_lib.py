@@ -86,6 +86,7 @@ _SIGS = {
     "dccrgx_set_cell_weight": (C.c_int, [vp, u64, C.c_double]),
     "dccrgx_get_cell_weight": (C.c_double, [vp, u64]),
     "dccrgx_continue_balance_load": (C.c_int, [vp]),
+    "dccrgx_get_migration_cells": (C.c_int, [vp, C.c_int, C.c_int, vp, sz, P(sz)]),
     "dccrgx_finish_balance_load": (C.c_int, [vp]),
     "dccrgx_migration_message_size": (C.c_int, [vp, C.c_int, P(sz), P(sz)]),
     "dccrgx_migration_pack": (C.c_int, [vp, C.c_int, vp, sz]),

@@ -1602,6 +1602,22 @@ int dccrgx_removed_variable_field_download(dccrgx_grid* gp, int fid, uint64_t* s
 	});
 }
 
+// cells_to_send / cells_to_receive while a balance_load is in progress
+// (initialize_balance_load fills them with the migration lists, 3746-3884)
+int dccrgx_get_migration_cells(dccrgx_grid* gp, int peer, int incoming, uint64_t* ids, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.mig.active, "no balance_load in progress");
+		const auto& m = incoming ? g.mig.in : g.mig.out;
+		const auto it = m.find(peer);
+		const size_t k = it == m.end() ? 0 : it->second.size();
+		if (n) *n = k;
+		if (k > cap) return DCCRGX_ERANGE;
+		for (size_t i = 0; i < k; i++) ids[i] = it->second[i];
+		return 0;
+	});
+}
+
 // set_send_single_cells 6677 / get_send_single_cells 6684: accepted and
 // reported; the wire message is always one per peer and field (message
 // boundaries carry no data here, so the received payloads are the same)

@@ -106,6 +106,67 @@ std::tuple<void*, int, MPI_Datatype> call_datatype(T& c, ...) {
 	return std::make_tuple((void*)&c, int(sizeof(T)), MPI_BYTE);
 }
 
+// the datatype of one cell for a transfer (the five-argument member gets the
+// cell, the processes and the direction, dccrg_get_cell_datatype.hpp:68-340)
+template <class T>
+auto cell_datatype(T& c, uint64_t, int, int, bool, int, int) -> decltype(c.get_mpi_datatype()) {
+	return c.get_mpi_datatype();
+}
+template <class T>
+auto cell_datatype(T& c, uint64_t cell, int sender, int receiver, bool receiving, int hood, long)
+    -> decltype(c.get_mpi_datatype(uint64_t(0), 0, 0, false, 0)) {
+	return c.get_mpi_datatype(cell, sender, receiver, receiving, hood);
+}
+
+template <class T>
+std::tuple<void*, int, MPI_Datatype> cell_datatype(T& c, uint64_t, int, int, bool, int, ...) {
+	return std::make_tuple((void*)&c, int(sizeof(T)), MPI_BYTE);
+}
+
+inline bool is_named_datatype(MPI_Datatype t) {
+	int ni = 0, na = 0, nd = 0, comb = 0;
+	MPI_Type_get_envelope(t, &ni, &na, &nd, &comb);
+	return comb == MPI_COMBINER_NAMED;
+}
+
+// a Cell_Data that is not trivially copyable (e.g. std::vector members,
+// tests/variable_data_size) is serialized with MPI_Pack over the datatype
+// it describes and lives on the device as a variable-size field
+template <class T>
+void pack_cell(T& c, uint64_t cell, int sender, int receiver, int hood, MPI_Comm comm, std::vector<char>& out) {
+	auto dt = cell_datatype(c, cell, sender, receiver, false, hood, 0);
+	MPI_Datatype t = std::get<2>(dt);
+	const bool named = is_named_datatype(t);
+	if (!named) MPI_Type_commit(&t);
+	int bound = 0;
+	MPI_Pack_size(std::get<1>(dt), t, comm, &bound);
+	const size_t at = out.size();
+	out.resize(at + size_t(bound));
+	int pos = 0;
+	if (bound) MPI_Pack(std::get<0>(dt), std::get<1>(dt), t, out.data() + at, bound, &pos, comm);
+	out.resize(at + size_t(pos));
+	if (!named) MPI_Type_free(&t);
+}
+
+template <class T>
+void unpack_cell(T& c, uint64_t cell, int sender, int receiver, int hood, MPI_Comm comm, const char* in, size_t bytes) {
+	auto dt = cell_datatype(c, cell, sender, receiver, true, hood, 0);
+	MPI_Datatype t = std::get<2>(dt);
+	const bool named = is_named_datatype(t);
+	if (!named) MPI_Type_commit(&t);
+	int need = 0;
+	MPI_Pack_size(std::get<1>(dt), t, comm, &need);
+	if (size_t(need) < bytes) {
+		if (!named) MPI_Type_free(&t);
+		throw std::runtime_error("dccrg: received " + std::to_string(bytes) + " bytes for cell " + std::to_string(cell) +
+		                         " whose datatype holds " + std::to_string(need) + " (size its data first)");
+	}
+	int pos = 0;
+	if (bytes)
+		MPI_Unpack(const_cast<char*>(in), int(bytes), &pos, std::get<0>(dt), std::get<1>(dt), t, comm);
+	if (!named) MPI_Type_free(&t);
+}
+
 // the halo window [offset, offset + bytes) of a Cell_Data: one contiguous
 // run inside the object (a non-contiguous or out-of-object datatype sends
 // the whole object)
@@ -308,8 +369,10 @@ class Dccrg;
 
 template <class Cell_Data, class Geometry, class... Additional_Cell_Items, class... Additional_Neighbor_Items>
 class Dccrg<Cell_Data, Geometry, std::tuple<Additional_Cell_Items...>, std::tuple<Additional_Neighbor_Items...>> {
-	static_assert(std::is_trivially_copyable<Cell_Data>::value,
-	              "Cell_Data is mirrored on the GPU: it must be trivially copyable");
+	// a trivially copyable Cell_Data is mirrored byte for byte in a device
+	// field; any other one (std::vector members, tests/variable_data_size) is
+	// serialized over its get_mpi_datatype into a variable-size device field
+	static constexpr bool serialized_ = !std::is_trivially_copyable<Cell_Data>::value;
 
 public:
 	using cell_data_type = Cell_Data;
@@ -435,6 +498,10 @@ public:
 		});
 	}
 	Cell_Data* operator[](const uint64_t cell) const {  // 756: local cells, remote copies, removed cells (764)
+		if (balancing_) {  // cells arriving in the balance_load in progress (3855)
+			const auto it = pending_.find(cell);
+			if (it != pending_.end()) return const_cast<Cell_Data*>(&it->second);
+		}
 		int64_t s = -1;
 		if (g_) dccrgx_get_slots(g_, &cell, 1, &s);
 		if (s >= 0 && size_t(s) < host_.size()) return const_cast<Cell_Data*>(&host_[size_t(s)]);
@@ -584,14 +651,23 @@ public:
 		upload_local();
 		size_t n = 0;
 		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
-		refresh();
+		std::unordered_map<uint64_t, Cell_Data> gone;
+		refresh(&gone);
 		// removed cells' payloads on the parent's process (unrefined_cell_data 7250)
 		removed_ids_ = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_removed_cells(g_, o, c, k); });
-		removed_.assign(removed_ids_.size(), Cell_Data{});
+		removed_.clear();
+		removed_.resize(removed_ids_.size());
 		removed_index_.clear();
 		for (size_t i = 0; i < removed_ids_.size(); i++) removed_index_[removed_ids_[i]] = i;
-		if (!removed_.empty())
-			detail::check(dccrgx_removed_field_download(g_, payload_, removed_.data(), removed_.size() * sizeof(Cell_Data)));
+		if (serialized_) {
+			// the removed children that were local here keep their objects
+			for (size_t i = 0; i < removed_ids_.size(); i++) {
+				auto it = gone.find(removed_ids_[i]);
+				if (it != gone.end()) removed_[i] = std::move(it->second);
+			}
+		} else if (!removed_.empty()) {
+			removed_download(removed_.data(), removed_.size() * sizeof(Cell_Data));
+		}
 		auto out = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
 		if (sorted) std::sort(out.begin(), out.end());
 		return out;
@@ -608,22 +684,25 @@ public:
 	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
 	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
 	Dccrg& balance_load(const bool use_zoltan = true) {
-		clear_removed();
-		upload_local();
-		detail::check(dccrgx_balance_load(g_, use_zoltan ? 1 : 0));
-		refresh();
+		initialize_balance_load(use_zoltan);
+		continue_balance_load();
+		finish_balance_load();
 		return *this;
 	}
-	// split form (3746, 3899, 3942): the payloads move in continue
+	// split form (3746, 3899, 3942): the payloads move in continue; in
+	// between, get_cells_to_receive() lists the arriving cells and
+	// operator[] gives their (default-constructed) data, which a program
+	// with variable-size data sizes before continue (variable_data_size.cpp:83-95)
 	void initialize_balance_load(const bool use_zoltan) {
 		clear_removed();
 		upload_local();
 		detail::check(dccrgx_initialize_balance_load(g_, use_zoltan ? 1 : 0, nullptr, nullptr, 0));
+		begin_balancing();
 	}
 	void continue_balance_load() { detail::check(dccrgx_continue_balance_load(g_)); }
 	void finish_balance_load() {
 		detail::check(dccrgx_finish_balance_load(g_));
-		refresh();
+		end_balancing();
 	}
 	// 6210 / 6244
 	bool set_cell_weight(const uint64_t cell, const double weight) {
@@ -635,15 +714,21 @@ public:
 		clear_removed();
 		upload_local();
 		std::vector<int32_t> p(processes.begin(), processes.end());
-		detail::check(dccrgx_balance_load_to(g_, cells_out.data(), p.data(), cells_out.size()));
-		refresh();
+		detail::check(dccrgx_initialize_balance_load(g_, 0, cells_out.data(), p.data(), cells_out.size()));
+		begin_balancing();
+		continue_balance_load();
+		finish_balance_load();
 		return *this;
 	}
+	// allocate_copies_of_remote_neighbors (1054-1074): the copies exist (default
+	// constructed) after every structural change
+	void allocate_copies_of_remote_neighbors(const int = default_neighborhood_id) {}
 
 	// ---- grid files (1089, 1742) --------------------------------------------------------
 	// the header is raw bytes (the reference takes (void*, count, MPI_Datatype))
 	bool save_grid_data(const std::string& name, const uint64_t offset, const void* header = nullptr,
 	                    const size_t header_bytes = 0) {
+		if (serialized_) return false;  // files of fixed-size payloads only
 		upload_local();
 		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
 	}
@@ -682,7 +767,7 @@ private:
 	// tests/test_gpu_facade.py)
 	void dump_cells(const char* when) const {
 		const char* base = std::getenv("DCCRGX_DUMP_CELLS");
-		if (!base || !g_) return;
+		if (!base || !g_ || serialized_) return;
 		const std::string path = std::string(base) + "." + when + "." + std::to_string(rank_);
 		std::vector<std::pair<uint64_t, size_t>> c;
 		for (size_t s = 0; s < n_local_ && s < slot_ids_.size(); s++) c.push_back({slot_ids_[s], s});
@@ -727,6 +812,10 @@ private:
 		geometry_rw.set(geometry_rw.get_params_or_default());
 	}
 	void add_payload_field() {
+		if constexpr (serialized_) {
+			detail::check(dccrgx_add_variable_field(g_, "Cell_Data", 1, &payload_));
+			return;
+		}
 		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
 		const auto w = detail::datatype_window<Cell_Data>();
 		detail::check(dccrgx_set_field_window(g_, payload_, w.first, w.second));
@@ -749,20 +838,60 @@ private:
 			dump_cells("initial");
 		}
 	}
+	// serialized Cell_Data: slots [s0, s0 + n) packed into the device field
+	void pack_range(size_t s0, size_t n) {
+		std::vector<char> bytes;
+		std::vector<uint64_t> sizes(n);
+		for (size_t i = 0; i < n; i++) {
+			const size_t at = bytes.size();
+			detail::pack_cell(host_[s0 + i], slot_ids_[s0 + i], rank_, rank_, default_neighborhood_id, comm_, bytes);
+			sizes[i] = bytes.size() - at;
+		}
+		if (!n) return;
+		detail::check(dccrgx_variable_field_resize(g_, payload_, s0, n, sizes.data()));
+		detail::check(dccrgx_variable_field_upload(g_, payload_, s0, n, bytes.data(), bytes.size()));
+	}
+	// ... and back (receiving side: the objects' own datatypes decide the layout)
+	void unpack_slot(size_t s, int sender) {
+		uint64_t sz = 0;
+		detail::check(dccrgx_variable_field_sizes(g_, payload_, s, 1, &sz));
+		std::vector<char> bytes(size_t(sz) + 1);
+		size_t got = 0;
+		detail::check(dccrgx_variable_field_download(g_, payload_, s, 1, bytes.data(), bytes.size(), &got));
+		detail::unpack_cell(host_[s], slot_ids_[s], sender, rank_, default_neighborhood_id, comm_, bytes.data(), got);
+	}
 	void upload_local() {
 		const size_t nl = std::min(n_local_, host_.size());
+		if constexpr (serialized_) {
+			pack_range(0, nl);
+			return;
+		}
 		if (nl) detail::check(dccrgx_field_upload(g_, payload_, 0, nl, host_.data()));
 	}
 	void upload_all() {
+		if constexpr (serialized_) {
+			pack_range(0, host_.size());
+			return;
+		}
 		if (!host_.empty()) detail::check(dccrgx_field_upload(g_, payload_, 0, host_.size(), host_.data()));
 	}
 	void download_all() {
+		if constexpr (serialized_) {
+			for (size_t s = 0; s < host_.size(); s++) unpack_slot(s, s < n_local_ ? rank_ : dccrgx_get_process(g_, slot_ids_[s]));
+			return;
+		}
 		if (!host_.empty()) detail::check(dccrgx_field_download(g_, payload_, 0, host_.size(), host_.data()));
 	}
 	// received bytes into the host copies of remote neighbors
 	void download_remote() {
 		const size_t nr = host_.size() - n_local_;
 		if (!nr) return;
+		if constexpr (serialized_) {
+			size_t nrecv = 0;
+			detail::check(dccrgx_get_counts(g_, nullptr, nullptr, &nrecv, nullptr));
+			for (size_t s = n_local_; s < n_local_ + nrecv; s++) unpack_slot(s, dccrgx_get_process(g_, slot_ids_[s]));
+			return;
+		}
 		std::vector<Cell_Data> tmp(nr);
 		detail::check(dccrgx_field_download(g_, payload_, n_local_, nr, tmp.data()));
 		for (size_t i = 0; i < nr; i++)
@@ -771,14 +900,86 @@ private:
 	}
 
 	// after a structural change: slots, host payloads, items, caches
-	void refresh() {
+	void refresh(std::unordered_map<uint64_t, Cell_Data>* gone = nullptr) {
 		size_t ns = 0;
 		detail::check(dccrgx_get_counts(g_, nullptr, nullptr, nullptr, &ns));
+		const size_t old_nl = n_local_;
 		n_local_ = n_local();
+		std::vector<uint64_t> old_ids = std::move(slot_ids_);
 		slot_ids_ = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_slot_ids(g_, o, c, n); });
-		host_.assign(ns, Cell_Data{});
-		download_all();
+		if constexpr (serialized_) {
+			// the host objects are the data: a local cell keeps its object,
+			// arrivals take the objects sized during the balance, new cells and
+			// every remote copy start default-constructed (the reference clears
+			// remote_neighbors at a balance and at a refinement, 3807, 10124)
+			std::unordered_map<uint64_t, Cell_Data> old;
+			for (size_t s = 0; s < old_ids.size() && s < host_.size() && s < old_nl; s++)
+				old.emplace(old_ids[s], std::move(host_[s]));
+			host_.clear();
+			host_.resize(ns);
+			arrived_.clear();
+			for (size_t s = 0; s < ns; s++) {
+				const uint64_t id = slot_ids_[s];
+				auto it = old.find(id);
+				if (it != old.end() && s < n_local_) {
+					host_[s] = std::move(it->second);
+					old.erase(it);
+					continue;
+				}
+				auto pt = pending_.find(id);
+				if (pt != pending_.end() && s < n_local_) {
+					host_[s] = std::move(pt->second);
+					arrived_.push_back(s);
+					continue;
+				}
+				if (s < n_local_) arrived_.push_back(s);
+			}
+			if (gone) *gone = std::move(old);
+		} else {
+			(void)old_nl;
+			(void)gone;
+			host_.assign(ns, Cell_Data{});
+			download_all();
+		}
 		refresh_items();
+	}
+
+	// initialize_balance_load done: the migration lists and the arriving cells' objects
+	void begin_balancing() {
+		balancing_ = true;
+		pending_.clear();
+		bal_send_.clear();
+		bal_recv_.clear();
+		for (int p = 0; p < size_; p++) {
+			if (p == rank_) continue;
+			for (int in = 0; in < 2; in++) {
+				const auto v = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) {
+					return dccrgx_get_migration_cells(g_, p, in, o, c, n);
+				});
+				if (v.empty()) continue;
+				auto& dst = (in ? bal_recv_ : bal_send_)[p];
+				for (size_t i = 0; i < v.size(); i++) {
+					dst.push_back({v[i], int(i + 1)});
+					if (in) pending_[v[i]];
+				}
+			}
+		}
+	}
+	void end_balancing() {
+		balancing_ = false;
+		refresh();
+		pending_.clear();
+		bal_send_.clear();
+		bal_recv_.clear();
+		if constexpr (serialized_) {
+			// the arrived cells' bytes into their objects (sized by the program
+			// between initialize_ and continue_balance_load, as in the reference)
+			for (size_t s : arrived_) unpack_slot(s, dccrgx_get_process(g_, slot_ids_[s]));
+		}
+		arrived_.clear();
+	}
+	void removed_download(Cell_Data* out, size_t bytes) {
+		if constexpr (!serialized_) detail::check(dccrgx_removed_field_download(g_, payload_, out, bytes));
 	}
 
 	void refresh_items() {
@@ -963,6 +1164,7 @@ private:
 
 	using list_map = std::unordered_map<int, std::vector<std::pair<uint64_t, int>>>;
 	const list_map& lists_for(int hood, bool receive) const {
+		if (balancing_) return receive ? bal_recv_ : bal_send_;  // the migration lists (3746-3884)
 		auto& cache = receive ? recv_maps_ : send_maps_;
 		auto it = cache.find(hood);
 		if (it != cache.end()) return it->second;
@@ -1027,6 +1229,11 @@ private:
 	std::unordered_map<uint64_t, size_t> removed_index_;
 	std::vector<uint64_t> slot_ids_;
 	std::vector<Cell_Data> host_;
+	// a balance_load in progress: migration lists and the arriving cells' objects
+	bool balancing_ = false;
+	list_map bal_send_, bal_recv_;
+	std::unordered_map<uint64_t, Cell_Data> pending_;
+	std::vector<size_t> arrived_;  // serialized Cell_Data: local slots whose bytes came from elsewhere
 	std::vector<Cells_Item> cells_rw;
 	std::vector<Neighbors_Item> neighbors_rw;
 	std::array<Iterator_Storage<Cells_Item>, 5> ranges_{};

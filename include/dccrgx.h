@@ -258,6 +258,10 @@ int dccrgx_get_load_balancing_method(dccrgx_grid* g, char* out, size_t cap);
 int dccrgx_set_cell_weight(dccrgx_grid* g, uint64_t cell, double weight);
 double dccrgx_get_cell_weight(dccrgx_grid* g, uint64_t cell);
 int dccrgx_continue_balance_load(dccrgx_grid* g);
+/* between initialize_ and finish_balance_load: the cells leaving to
+ * (incoming = 0) or arriving from (incoming = 1) `peer`, ascending (the
+ * reference's cells_to_send / cells_to_receive during a balance, 3746-3884) */
+int dccrgx_get_migration_cells(dccrgx_grid* g, int peer, int incoming, uint64_t* ids, size_t cap, size_t* n);
 int dccrgx_finish_balance_load(dccrgx_grid* g);
 /* Explicit migration transport (instead of continue_balance_load): the
  * message to / from `peer` = for every field in field order, the payload of

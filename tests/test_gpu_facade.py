@@ -84,3 +84,55 @@ def test_config1_driver_matches_oracle(gpu, P):
     o.gol_set(ids, alive0(ids))
     o.gol_steps(30)
     assert int(m.group(3)) == int(o.gol_get(ids).sum())
+
+
+CELL_LINE = re.compile(r"Cell (\d+) data \(on process (\d+)\): ([-\d .e+]*)")
+
+
+def _cell_lines(out):
+    rows = []
+    for m in CELL_LINE.finditer(out):
+        vals = [float(v) for v in m.group(3).split()]
+        rows.append((int(m.group(1)), int(m.group(2)), vals))
+    return rows
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_reference_variable_data_size(gpu, P):
+    """tests/variable_data_size/variable_data_size.cpp compiled against the
+    facade (include lines only): cell c holds c values c, c+1, ...; the
+    program sizes the arriving cells between initialize_ and
+    continue_balance_load and prints every cell before and after the
+    balance.  Both prints must show every cell once with its own values."""
+    rows = _cell_lines(mpirun("ref_variable_data_size", P))
+    assert len(rows) == 6, rows
+    for phase in (rows[:3], rows[3:]):
+        assert sorted(c for c, _, _ in phase) == [1, 2, 3]
+        for c, _, vals in phase:
+            assert vals == [float(c + i) for i in range(c)]
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_reference_variable_neighbour_data(gpu, P):
+    """tests/variable_data_size/variable_neighbour_data.cpp against the
+    facade: variables1 of every cell and variables2 of its neighbors
+    (cell.neighbors_of) through a derived-datatype halo, twice around
+    balances; in the last print the halo carries variables1 only, so a
+    remote neighbor's variables2 is its freshly sized zeros."""
+    out = mpirun("ref_variable_neighbour_data", P)
+    rows = _cell_lines(out)
+    assert len(rows) == 9, rows
+    nbrs = {1: [2], 2: [1, 3], 3: [2]}
+    for k, phase in enumerate((rows[:3], rows[3:6], rows[6:])):
+        assert sorted(c for c, _, _ in phase) == [1, 2, 3]
+        for c, _, vals in phase:
+            assert vals[:c] == [float(c + i) for i in range(c)]
+            rest = vals[c:]
+            for n in nbrs[c]:
+                part, rest = rest[:n], rest[n:]
+                own = [float(-(n + i)) for i in range(n)]
+                if k < 2:
+                    assert part == own, (k, c, n, vals)
+                else:
+                    assert part == own or part == [0.0] * n, (k, c, n, vals)
+            assert rest == []

@@ -664,10 +664,91 @@ def sc_iterators(rank, world):
     return {"invariants": bool(ok)}
 
 
+def var_payload(cell):
+    """tests/variable_data_size: a cell's own number of values (here 1 + id % 5)."""
+    c = int(cell)
+    return np.array([c * 1000.0 + i for i in range(1 + c % 5)], np.float64)
+
+
+def sc_variable(rank, world):
+    """Variable-size payloads (tests/variable_data_size/variable_data_size.cpp,
+    variable_neighbour_data.cpp) through the library's own transport: every
+    remote copy receives its cell's values (sizes travel with them), a field
+    left out of the transfer keeps empty copies, payloads follow migrations
+    (a third of the cells move on), new children start empty, removed
+    children's payloads reach their parent's process; send_single_cells
+    on / off gives the same copies."""
+    length, R, per, hood = (6, 5, 4), 1, (True, False, False), 1
+    g = _grid(length, R, per, hood)
+    v2 = g.add_variable_field("variables2", np.float64, True)
+    v1 = g.add_variable_field("variables1", np.int32, False)
+    fx = g.add_field("val", np.uint32)
+    res = {}
+
+    def fill():
+        sl = g.slot_ids()[: g.n_local]
+        v2.set([var_payload(c) for c in sl])
+        v1.set([np.arange(int(c) % 3, dtype=np.int32) for c in sl])
+        fx.set(val(sl))
+
+    def copies_ok():
+        g.update_copies_of_remote_neighbors()
+        sl = g.slot_ids()
+        nl, nr = g.n_local, len(g.remote_cells())
+        got = v2.get(nl, nr)
+        ok = all(np.array_equal(a, var_payload(c)) for a, c in zip(got, sl[nl:nl + nr]))
+        ok = ok and all(a.size == 0 for a in v1.get(nl, nr))
+        ok = ok and np.array_equal(fx.get(nl, nr), val(sl[nl:nl + nr]))
+        ok = ok and all(np.array_equal(a, var_payload(c)) for a, c in zip(v2.get(0, nl), sl[:nl]))
+        return bool(ok and nr > 0)
+
+    fill()
+    res["halo"] = copies_ok()
+    g.set_send_single_cells(True)
+    res["single_flag"] = g.get_send_single_cells()
+    res["halo_single"] = copies_ok()
+    g.set_send_single_cells(False)
+    # migration: a third of the local cells to the next rank
+    loc = g.local_cells()
+    mv = loc[loc % np.uint64(3) == 0]
+    g.balance_load_to(mv, np.full(mv.size, (rank + 1) % world, np.int32))
+    sl = g.slot_ids()[: g.n_local]
+    res["migrated"] = bool(all(np.array_equal(a, var_payload(c)) for a, c in zip(v2.get(0, g.n_local), sl)))
+    res["moved_in"] = any(_gather(bool(set(sl.tolist()) - set(loc.tolist()))))
+    res["halo_after"] = copies_ok()
+    # refine some cells: children empty; then merge them back: removed payloads
+    fill()
+    for c in g.local_cells():
+        if int(c) % 4 == 1:
+            g.refine_completely(int(c))
+    new = g.stop_refining()
+    pos = {int(c): i for i, c in enumerate(g.slot_ids()[: g.n_local])}
+    vals = v2.get(0, g.n_local)
+    res["children_empty"] = bool(new.size > 0 and all(vals[pos[int(c)]].size == 0 for c in new))
+    fill()
+    for c in g.local_cells():
+        if g.get_refinement_level(int(c)) == 1:
+            g.unrefine_completely(int(c))
+    g.stop_refining()
+    got = g.get_removed_cells()
+    rem = v2.get_removed()
+    res["removed"] = bool(all(np.array_equal(a, var_payload(c)) for a, c in zip(rem, got)))
+    res["merged"] = any(_gather(bool(got.size)))
+    # merged parents start empty (default-constructed, dccrg.hpp:10475)
+    parents = set(g.mapping_batch(got)["parent"].tolist()) if got.size else set()
+    pos = {int(c): i for i, c in enumerate(g.slot_ids()[: g.n_local])}
+    vals = v2.get(0, g.n_local)
+    res["parents_empty"] = bool(all(vals[pos[p]].size == 0 for p in parents))
+    fill()
+    res["halo_final"] = copies_ok()
+    g.close()
+    return res
+
+
 SCENARIOS = {
     2: ["sc_config1", "sc_gol_explicit", "sc_rcb"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
-        "sc_rcb", "sc_unrefine", "sc_advection_adapt"],
+        "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable"],
 }
 
 
@@ -776,3 +857,11 @@ def test_save_grid_data_three_ranks(transport_results):
 
 def test_iterators_test1_invariants(transport_results):
     _check(transport_results, "sc_iterators", ["invariants"])
+
+
+def test_variable_size_payloads(transport_results):
+    _check(transport_results, "sc_variable", ["halo", "single_flag", "halo_single", "migrated", "halo_after",
+                                              "children_empty", "removed", "parents_empty",
+                                              "halo_final"])
+    assert any(o["moved_in"] for _, o in transport_results["sc_variable"].values())
+    assert any(o["merged"] for _, o in transport_results["sc_variable"].values())

@@ -83,6 +83,19 @@ struct Center {
 template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry>;
 template class dccrg::Dccrg<Cell>;
 template class dccrg::Dccrg<Cell, dccrg::Cartesian_Geometry, std::tuple<Center>, std::tuple<Is_Local>>;
+// a variable-size Cell_Data (tests/variable_data_size): the serialized mode
+struct Var {
+	std::vector<double> v;
+	std::tuple<void*, int, MPI_Datatype> get_mpi_datatype() { return std::make_tuple(v.data(), int(v.size()), MPI_DOUBLE); }
+};
+struct Var5 {
+	std::vector<int> a;
+	std::tuple<void*, int, MPI_Datatype> get_mpi_datatype(uint64_t, int, int, bool, int) {
+		return std::make_tuple(a.data(), int(a.size()), MPI_INT);
+	}
+};
+template class dccrg::Dccrg<Var>;
+template class dccrg::Dccrg<Var5, dccrg::Cartesian_Geometry>;
 int main() { return 0; }
 ''')
     r = cxx(src, tmp_path / "inst")

@@ -124,9 +124,23 @@ def line_base(metric, value, world, a, ms, dtype, data, config, scaling="weak"):
             "dtype": dtype, "data": data, "config": config}
 
 
+# Rehearsal of the N > 1 path on one GPU (DCCRG_BENCH_TRANSPORT=host): every
+# rank on cuda:0, a gloo group, and the library's host exchange instead of
+# RCCL (which needs one GPU per rank).  Same timing, reductions and JSON; the
+# numbers measure the host transport, not xGMI.
+HOST_TRANSPORT = "host"
+
+
+def make_grid(mod, rank, world, uid):
+    if uid == HOST_TRANSPORT:
+        return mod.Dccrg(rank, world, 0, exchange=mod.grid.TorchExchange())
+    return mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+
+
 def reduce_stats(torch, dist, world, vals):
     """(max over ranks, sum over ranks) of a list of floats."""
-    t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+    dev = "cpu" if world > 1 and dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world == 1:
         return [float(x) for x in t], [float(x) for x in t]
     mx, sm = t.clone(), t.clone()
@@ -158,7 +172,7 @@ def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """BASELINE config 2: game of life 1024 x 1024 x 64 (x N, z slabs),
     26-point stencil, uint32 state (algorithmic 8 B per cell-update)."""
     nx, ny, nz = 1024, 1024, 64 * world
-    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g = make_grid(dccrgx_mod, rank, world, uid)
     g.set_initial_length((nx, ny, nz)).set_neighborhood_length(1).set_maximum_refinement_level(0).initialize()
     st = g.add_field("is_alive", np.uint32)
     st.set(alive_rule(g.slot_ids()[: g.n_local]))
@@ -265,7 +279,7 @@ def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
 
     n = a.base
     L0 = (2 * math.pi / n, math.pi / n, 8 * math.pi / n)
-    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g = make_grid(dccrgx_mod, rank, world, uid)
     g.set_initial_length((n, n, n * world)).set_neighborhood_length(0).set_maximum_refinement_level(2)
     g.set_periodic(True, True, True).initialize()
     g.set_geometry((0, 0, 0), L0)
@@ -330,7 +344,7 @@ def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     shifted by half a rank (every rank exports its first half to the
     previous rank; at N = 1 nothing moves and the time is the rebuild)."""
     nx, ny, nzr = 1024, 1024, 128
-    g = dccrgx_mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g = make_grid(dccrgx_mod, rank, world, uid)
     g.set_initial_length((nx, ny, nzr * world)).set_neighborhood_length(1).set_maximum_refinement_level(0)
     g.initialize()
     st = g.add_field("is_alive", np.uint32)
@@ -481,7 +495,7 @@ def advection_adapt_main(a, dccrg_amd, torch, dist, rank, world, uid):
 # ---------------------------------------------------------------------------- advection (config 3, headline)
 def build_grid(dccrg_amd, rank, size, base, R, uid):
     nx, ny, nz = base, base, base * size
-    g = dccrg_amd.Dccrg(rank, size, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    g = make_grid(dccrg_amd, rank, size, uid)
     g.set_initial_length((nx, ny, nz)).set_neighborhood_length(0).set_maximum_refinement_level(R)
     g.set_periodic(True, True, False).initialize()
     g.set_geometry((0.0, 0.0, 0.0), (1.0 / nx, 1.0 / ny, 1.0 / nx))
@@ -599,13 +613,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
+    host = world > 1 and os.environ.get("DCCRG_BENCH_TRANSPORT") == HOST_TRANSPORT
+    torch.cuda.set_device(0 if host else local)
+    if host:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     import dccrg_amd
 
-    uid = None
-    if world > 1:
+    uid = HOST_TRANSPORT if host else None
+    if world > 1 and not host:
         obj = [dccrg_amd.Dccrg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]

@@ -32,16 +32,7 @@ def layout(ids, base, R, T=512):
     lvl, ind, clen, key = lvl[order], ind[order].astype(np.int64), clen[order], key[order]
     n = ids.size
     k = ind[:, 0] | ind[:, 1] | ind[:, 2]
-    al = np.where(k == 0, 63, 0)
-    kk = k.copy()
-    tz = np.zeros(n, np.int64)
-    for b in range(40):
-        m = (kk & 1) == 0
-        m &= k != 0
-        tz += m & ((kk >> 0) & 1 == 0)
-        kk = np.where(m, kk >> 1, kk)
-        # stop counting once a one is reached
-    # exact ctz
+    # alignment = trailing zeros of x | y | z (align_kernel)
     tz = np.zeros(n, np.int64)
     kk = k.copy()
     alive = k != 0
@@ -135,6 +126,10 @@ def main():
             mixed += 1
     print("general tiles with mixed levels:", mixed)
     np.savez("/tmp/tile_layout.npz", starts=L["starts"], reason=reason, lvl=L["lvl"], ind=L["ind"])
+    st = L["starts"]
+    for r in (1, 0x30):
+        t = np.nonzero(reason == r)[0]
+        print(f"reason {r:#x}: boxes by level", np.bincount(L["lvl"][st[t]], minlength=R + 1))
 
 
 if __name__ == "__main__":

@@ -257,7 +257,7 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS if ach else None,
                         "traffic": measured_traffic("gol_amr", nl, per_cell * nl, 1),
-                        "kernel": "gol_amr_values + gol_amr_collect_mask + gol_amr_spread0_mask + gol_amr_spread_groups_mask", "alg_bytes_per_leaf": per_cell,
+                        "kernel": "gol_amr_collect_mask + gol_amr_spread0_mask + gol_amr_spread_groups_mask", "alg_bytes_per_leaf": per_cell,
                         "alg_bytes_per_step": per_cell * nl,
                         "logical_bytes_per_leaf": logical,
                         "logical_GB_per_s": logical * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None,

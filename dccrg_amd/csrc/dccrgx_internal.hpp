@@ -271,7 +271,7 @@ struct GolAmrTables {
 	DBuf<uint32_t> l0, pack, gptr, gslot, lvl0;
 	size_t ng = 0, n_lvl0 = 0;
 	bool mask_path = false;
-	DBuf<uint32_t> l0c, ent, mask, val;  // val: one byte per entry (4 per word)
+	DBuf<uint32_t> l0c, ent, mask;
 	size_t n_ent = 0;
 	uint32_t bx = 0, by = 0, lx = 0, ly = 0, lz = 0;
 };

@@ -288,30 +288,40 @@ __global__ void mask_ent_kernel(const uint32_t* __restrict__ ptr, const int32_t*
 	}
 }
 
-// the level-0 id at code c from the level-0 cell at (px, py, pz)
-__device__ __forceinline__ uint64_t l0_id_at(uint32_t c, int px, int py, int pz, const L0Geom& G) {
-	int x = px + int(c % 3u) - 1, y = py + int((c / 3u) % 3u) - 1, z = pz + int(c / 9u) - 1;
-	x += x < 0 ? int(G.lx) : (x >= int(G.lx) ? -int(G.lx) : 0);
-	y += y < 0 ? int(G.ly) : (y >= int(G.ly) ? -int(G.ly) : 0);
-	z += z < 0 ? int(G.lz) : (z >= int(G.lz) ? -int(G.lz) : 0);
-	return 1 + uint64_t(x) + uint64_t(y) * G.lx + uint64_t(z) * G.lx * G.ly;
+// collect (solve.hpp:46-110) on the mask path, one block per 256 consecutive
+// rows.  Phase 1, over the block's neighbor entries (one contiguous run of
+// the CSR): one byte per entry, code | alive << 5 (31: no slot), built from
+// the entry's (slot, code) word and a gather of the neighbor's state, four
+// entries per 16-byte index load and eight gathers in flight per thread,
+// written straight into LDS.  Phase 2, one thread per row: the row walk
+// tests and sets bits instead of comparing ids and appends a parent to the
+// reference's list (data[1..8], first-seen order) only when its bit is new.
+// Entries past the LDS window (blocks with very long rows) are built where
+// they are walked.
+__device__ __forceinline__ uint32_t mask_entry_byte(uint32_t q, const uint32_t* __restrict__ state) {
+	if (q == kEntNone) return 31u;
+	return (q >> 27) | (state[q & 0x7ffffffu] ? 32u : 0u);
 }
 
-// collect (solve.hpp:46-110) on the mask path, in two passes.
-// Pass 1, over the neighbor entries of the rows: one byte per entry, code |
-// alive << 5 (31: no slot); four entries per thread (one 16-byte index load,
-// four state gathers, one 4-byte store), so the gathers of the whole grid are
-// in flight together instead of behind each row's walk.
-__global__ void gol_amr_values_kernel(const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent,
-                                      const uint32_t* __restrict__ ptr, size_t s0, size_t s1,
-                                      uint32_t* __restrict__ val) {
-	const uint32_t w0 = ptr[s0] >> 2, w1 = (ptr[s1] + 3) >> 2;
-	const uint32_t step = gridDim.x * blockDim.x;
-	// two words (eight gathers) in flight per thread
-	for (uint32_t w = w0 + blockIdx.x * blockDim.x + threadIdx.x; w < w1; w += 2 * step) {
-		const bool two = w + step < w1;
-		const uint4 ea = reinterpret_cast<const uint4*>(ent)[w];
-		const uint4 eb = two ? reinterpret_cast<const uint4*>(ent)[w + step] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
+__global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
+    const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ ptr,
+    const uint32_t* __restrict__ l0c, L0Geom G, uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0,
+    size_t s1, int* __restrict__ err) {
+	constexpr uint32_t cap = 8192;  // entry bytes staged per block
+	__shared__ uint32_t sp32[cap / 4];
+	const uint32_t tid = threadIdx.x;
+	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
+	if (r0 >= s1) return;  // block-uniform
+	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
+	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
+	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
+	const uint32_t nw = (nB + 3) / 4;
+	const uint4* ent4 = reinterpret_cast<const uint4*>(ent) + (E0 >> 2);
+	// phase 1: two index words (eight state gathers) in flight per thread
+	for (uint32_t w = tid; w < nw; w += 2 * kCollectRows) {
+		const bool two = w + kCollectRows < nw;
+		const uint4 ea = ent4[w];
+		const uint4 eb = two ? ent4[w + kCollectRows] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
 		const uint32_t q[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
 		uint32_t st[8];
 #pragma unroll
@@ -322,28 +332,9 @@ __global__ void gol_amr_values_kernel(const uint32_t* __restrict__ state, const 
 			const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
 			out[k >> 2] |= v << (8 * (k & 3));
 		}
-		val[w] = out[0];
-		if (two) val[w + step] = out[1];
+		sp32[w] = out[0];
+		if (two) sp32[w + kCollectRows] = out[1];
 	}
-}
-
-// Pass 2, one thread per row: the block's entry bytes staged into LDS with
-// coalesced 4-byte loads; the row walk tests and sets bits instead of
-// comparing ids and appends a parent to the reference's list (data[1..8],
-// first-seen order) only when its bit is new
-__global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
-    const uint8_t* __restrict__ val, const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ l0c, L0Geom G,
-    uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0, size_t s1, int* __restrict__ err) {
-	constexpr uint32_t cap = 8192;  // bytes of entry values staged per block
-	__shared__ uint32_t sp32[cap / 4];
-	const uint32_t tid = threadIdx.x;
-	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
-	if (r0 >= s1) return;  // block-uniform
-	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
-	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
-	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
-	const uint32_t* val32 = reinterpret_cast<const uint32_t*>(val) + (E0 >> 2);
-	for (uint32_t w = tid; w < (nB + 3) / 4; w += kCollectRows) sp32[w] = val32[w];
 	__syncthreads();
 	const size_t s = r0 + tid;
 	if (s >= r1) return;
@@ -372,18 +363,32 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 		}
 	};
 	// the row's entry bytes a 4-byte word at a time (E0 is word aligned)
-	const uint32_t* gval32 = reinterpret_cast<const uint32_t*>(val);
 	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e;) {
-		const uint32_t word = j - E0 < nB ? sp32[(j - E0) >> 2] : gval32[j >> 2];
 		const uint32_t b0 = j & 3u, b1 = e - j < 4u - b0 ? b0 + (e - j) : 4u;
-		for (uint32_t b = b0; b < b1; b++) visit((word >> (8 * b)) & 0xffu);
+		if (j - E0 < nB) {
+			const uint32_t word = sp32[(j - E0) >> 2];
+			for (uint32_t b = b0; b < b1; b++) visit((word >> (8 * b)) & 0xffu);
+		} else {
+			for (uint32_t b = b0; b < b1; b++) visit(mask_entry_byte(ent[(j & ~3u) + b], state));
+		}
 		j += b1 - b0;
 	}
+	// level-0 ids of the listed positions: the row's three wrapped x, y, z
+	// coordinates once, then per entry 1 + x + y lx + z lx ly
 	int px, py, pz;
 	l0_unpack(l0c[s], G, px, py, pz);
+	auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
+	const uint64_t lxy = uint64_t(G.lx) * G.ly;
+	const uint64_t X[3] = {uint64_t(wrap(px - 1, int(G.lx))) + 1, uint64_t(px) + 1, uint64_t(wrap(px + 1, int(G.lx))) + 1};
+	const uint64_t Y[3] = {uint64_t(wrap(py - 1, int(G.ly))) * G.lx, uint64_t(py) * G.lx,
+	                       uint64_t(wrap(py + 1, int(G.ly))) * G.lx};
+	const uint64_t Z[3] = {uint64_t(wrap(pz - 1, int(G.lz))) * lxy, uint64_t(pz) * lxy, uint64_t(wrap(pz + 1, int(G.lz))) * lxy};
 	uint64_t out[kList];
 #pragma unroll
-	for (int i = 0; i < kList; i++) out[i] = i < n ? l0_id_at(l[i], px, py, pz, G) : error_cell;
+	for (int i = 0; i < kList; i++) {
+		const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
+		out[i] = i < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
+	}
 	ulonglong2* o = reinterpret_cast<ulonglong2*>(lst + s * kList);
 #pragma unroll
 	for (int i = 0; i < kList / 2; i++) o[i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
@@ -516,7 +521,6 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		if (n_local) HIP_CHECK(hipMemcpyAsync(&total, ptr + n_local, 4, hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		T.ent.alloc(size_t(total) + 4);  // whole 16-byte words for the values pass
-		T.val.alloc(size_t(total) / 4 + 2);
 		T.n_ent = total;
 		HIP_CHECK(hipMemsetAsync(T.ent.p, 0xff, T.ent.n * 4, s));  // padding = no slot
 		DBuf<int> bad;
@@ -544,10 +548,8 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 	if (T.mask_path) {
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
-			gol_amr_values_kernel<<<grid_for(T.n_ent / 4 + 1, 256, 256u * 64u), 256, 0, s>>>(state, T.ent.p, ptr, s0, s1,
-			                                                                               T.val.p);
 			gol_amr_collect_mask_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
-			    reinterpret_cast<const uint8_t*>(T.val.p), ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, err);
+			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, err);
 		} else {
 			if (T.n_lvl0)
 				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,

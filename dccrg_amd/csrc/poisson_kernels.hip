@@ -242,12 +242,25 @@ __global__ void po_phase_b_kernel(PoArrays a, size_t n, const PoScalars* st, dou
 			const double r0 = a.r0[s] - alpha * a.ap0[s];
 			a.r0[s] = r0;
 			double ap1 = a.sf[s] * a.p1[s];
+			// as in po_apply_row: the six face entries, then the same-size /
+			// coarser neighbors' factors (reversed direction) and p1 values
+			// gathered together, then the ordered sum
+			int32_t ev[6];
+			double fv[6], pv[6];
+#pragma unroll
+			for (int dir = 0; dir < 6; dir++) ev[dir] = a.ell[6 * s + dir];
+#pragma unroll
 			for (int dir = 0; dir < 6; dir++) {
-				const int32_t e = a.ell[6 * s + dir];
+				fv[dir] = ev[dir] >= 0 ? a.f[dir ^ 1][ev[dir]] : 0.0;
+				pv[dir] = ev[dir] >= 0 ? a.p1[ev[dir]] : 0.0;
+			}
+#pragma unroll
+			for (int dir = 0; dir < 6; dir++) {
+				const int32_t e = ev[dir];
 				if (e == -1) continue;
 				const double* __restrict__ fo = a.f[dir ^ 1];  // neighbor's factor, reversed direction
 				if (e >= 0) {
-					ap1 += fo[e] * a.p1[e];
+					ap1 += fv[dir] * pv[dir];
 				} else {
 					const size_t k = size_t(-2 - e);
 					for (int j = 0; j < 4; j++) {

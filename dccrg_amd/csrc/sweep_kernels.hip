@@ -46,15 +46,50 @@ __global__ void place_bytes_kernel(const uint8_t* __restrict__ in, size_t elem, 
 }
 
 // ---------------------------------------------------------------------------
-// Game of life over the iterator neighbor list (deduplicated neighbors_of).
-__global__ void gol_csr_kernel(const uint32_t* __restrict__ state, uint32_t* __restrict__ out,
-                               const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nb, size_t s0, size_t s1) {
-	for (size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < s1; s += size_t(gridDim.x) * blockDim.x) {
-		uint32_t cnt = 0;
-		for (uint32_t e = ptr[s]; e < ptr[s + 1]; e++) cnt += state[nb[e]] > 0 ? 1u : 0u;
-		const uint32_t cur = state[s];
-		out[s] = cnt == 3 ? 1u : (cnt == 2 ? cur : 0u);
+// Game of life over the iterator neighbor list (deduplicated neighbors_of),
+// for refined meshes and partitions the structured kernel cannot take.  One
+// block per 256 consecutive rows: phase 1 reads the block's entries (one
+// contiguous run of the CSR) coalesced, four per thread and word, and
+// gathers their states eight in flight per thread into one LDS byte each;
+// phase 2 sums each row from LDS (rows past the LDS window gather directly).
+// Blocks are dealt XCD-contiguously (block b runs on XCD b % 8), so the rows
+// whose states a block gathers were loaded into the same L2.
+constexpr int kGolRows = 256;
+__global__ __launch_bounds__(kGolRows) void gol_csr_kernel(const uint32_t* __restrict__ state,
+                                                         uint32_t* __restrict__ out, const uint32_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ nb, size_t s0, size_t s1) {
+	constexpr uint32_t cap = 8192;  // entry bytes staged per block
+	__shared__ uint32_t sp32[cap / 4];
+	const uint32_t tid = threadIdx.x;
+	const uint32_t lb = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+	const size_t r0 = s0 + size_t(lb) * kGolRows;
+	if (r0 >= s1) return;  // block-uniform
+	const size_t r1 = r0 + kGolRows < s1 ? r0 + kGolRows : s1;
+	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
+	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
+	const uint32_t nw = (nB + 3) / 4;
+	for (uint32_t w = tid; w < nw; w += 2 * kGolRows) {
+		int32_t q[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			const uint32_t e = E0 + 4 * (w + (k >> 2) * kGolRows) + (k & 3);
+			q[k] = e >= E0 + 4 * nw || e >= E1 ? -1 : nb[e];
+		}
+		uint32_t v[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++) v[k] = q[k] >= 0 && state[q[k]] > 0 ? 1u : 0u;
+		sp32[w] = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+		if (w + kGolRows < nw) sp32[w + kGolRows] = v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24);
 	}
+	__syncthreads();
+	const size_t s = r0 + tid;
+	if (s >= r1) return;
+	const uint8_t* sp8 = reinterpret_cast<const uint8_t*>(sp32);
+	uint32_t cnt = 0;
+	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e; j++)
+		cnt += j - E0 < nB ? sp8[j - E0] : (state[nb[j]] > 0 ? 1u : 0u);
+	const uint32_t cur = state[s];
+	out[s] = cnt == 3 ? 1u : (cnt == 2 ? cur : 0u);
 }
 
 // Uniform 26-point game of life (nx a multiple of 256): a lane owns 4 consecutive x (16-B loads and
@@ -710,7 +745,8 @@ void k_place(const uint8_t* in, size_t elem, size_t off, size_t len, const int32
 void k_gol_csr(const uint32_t* state, uint32_t* out, const uint32_t* it_ptr, const int32_t* it_slot, size_t s0,
                size_t s1, hipStream_t s) {
 	if (s1 <= s0) return;
-	gol_csr_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(state, out, it_ptr, it_slot, s0, s1);
+	const size_t nb = (s1 - s0 + kGolRows - 1) / kGolRows;
+	gol_csr_kernel<<<unsigned((nb + 7) / 8 * 8), kGolRows, 0, s>>>(state, out, it_ptr, it_slot, s0, s1);
 	HIP_CHECK(hipGetLastError());
 }
 

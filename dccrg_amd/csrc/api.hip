@@ -1945,7 +1945,14 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 				if (b[mem[i]] == 1 && first1 == n) first1 = mem[i];
 			}
 			if (first2 != n || first1 != n) {  // dont_unrefine (2679-2733) of a local leaf, level > 0
-				g.dont_unrefine_cells.insert(ids[first2 != n ? first2 : first1]);
+				// it can only cancel an unrefine request of this family: one from
+				// another process (a family split across processes, k < 8) or one
+				// made earlier here; a whole local family without a pending request
+				// needs no mark (the outcome of stop_refining is the same)
+				bool pending = k < 8;
+				for (size_t i = 0; i < k && !pending && !g.unrefine_requests.empty(); i++)
+					pending = g.unrefine_requests.count(ids[mem[i]]) != 0;
+				if (pending) g.dont_unrefine_cells.insert(ids[first2 != n ? first2 : first1]);
 				nkeep++;
 			} else if (k == 8) {  // the whole family is local: every sibling a leaf here
 				g.unrefine_requests.insert(ids[mem[0]]);

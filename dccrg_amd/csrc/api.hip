@@ -1931,68 +1931,93 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		band.alloc(n + 1);
 		k_adv_bands(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p, n, diff_increase,
 		            diff_threshold, unrefine_sensitivity, band.p, g.s_comp);
-		const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
-		const auto& ids = slot_ids_host(g);
+		uint64_t nref = 0, nkeep = 0, nunref = 0;
+		// decide one family from its local members (bands bb, ids ii, k of
+		// them): dont_unrefine (2679-2733) when any member is kept or refined,
+		// else unrefine it
+		auto decide = [&](const uint8_t* bb, const uint64_t* ii, size_t k) {
+			size_t first2 = k, first1 = k;
+			for (size_t i = 0; i < k; i++) {
+				if (bb[i] == 2 && first2 == k) first2 = i;
+				if (bb[i] == 1 && first1 == k) first1 = i;
+			}
+			if (first2 != k || first1 != k) {
+				// the mark can only cancel an unrefine request of this family: one
+				// from another process (a family split across processes, k < 8)
+				// or one made earlier here; a whole local family without a pending
+				// request needs no mark (the outcome of stop_refining is the same)
+				bool pending = k < 8;
+				for (size_t i = 0; i < k && !pending && !g.unrefine_requests.empty(); i++)
+					pending = g.unrefine_requests.count(ii[i]) != 0;
+				if (pending) g.dont_unrefine_cells.insert(ii[first2 != k ? first2 : first1]);
+				nkeep++;
+			} else if (k == 8) {  // the whole family is local: every sibling a leaf here
+				g.unrefine_requests.insert(ii[0]);
+				nunref++;
+			} else if (dccrgx_unrefine_completely(gp, ii[0]) == DCCRGX_OK) {
+				nunref++;
+			}
+		};
 		// families: the local members of a parent are consecutive slots on
 		// Morton-ordered meshes (a run of 8 is a whole family); shorter runs
 		// (a family split between the inner and outer runs, or with members
 		// elsewhere) are merged by parent
-		uint64_t nref = 0, nkeep = 0, nunref = 0;
-		auto decide = [&](const size_t* mem, size_t k) {
-			size_t first2 = n, first1 = n;
-			for (size_t i = 0; i < k; i++) {
-				if (b[mem[i]] == 2 && first2 == n) first2 = mem[i];
-				if (b[mem[i]] == 1 && first1 == n) first1 = mem[i];
-			}
-			if (first2 != n || first1 != n) {  // dont_unrefine (2679-2733) of a local leaf, level > 0
-				// it can only cancel an unrefine request of this family: one from
-				// another process (a family split across processes, k < 8) or one
-				// made earlier here; a whole local family without a pending request
-				// needs no mark (the outcome of stop_refining is the same)
-				bool pending = k < 8;
-				for (size_t i = 0; i < k && !pending && !g.unrefine_requests.empty(); i++)
-					pending = g.unrefine_requests.count(ids[mem[i]]) != 0;
-				if (pending) g.dont_unrefine_cells.insert(ids[first2 != n ? first2 : first1]);
-				nkeep++;
-			} else if (k == 8) {  // the whole family is local: every sibling a leaf here
-				g.unrefine_requests.insert(ids[mem[0]]);
-				nunref++;
-			} else if (dccrgx_unrefine_completely(gp, ids[mem[0]]) == DCCRGX_OK) {
-				nunref++;
-			}
+		std::unordered_map<uint64_t, std::pair<std::vector<uint8_t>, std::vector<uint64_t>>> partial;
+		auto add_partial = [&](uint64_t parent, uint8_t band_v, uint64_t id) {
+			auto& pr = partial[parent];
+			pr.first.push_back(band_v);
+			pr.second.push_back(id);
 		};
-		std::unordered_map<uint64_t, std::vector<size_t>> partial;
-		std::vector<size_t> run;
-		uint64_t run_parent = error_cell;
-		auto flush = [&] {
-			if (run.empty()) return;
-			if (run.size() == 8) decide(run.data(), 8);
-			else {
-				auto& v = partial[run_parent];
-				v.insert(v.end(), run.begin(), run.end());
+		if (g.unrefine_requests.empty()) {
+			// on the device: refine requests, whole-family decisions, partial runs
+			const AdvRequests q = k_adv_requests(g.m, g.slot_ids.p, band.p, n, g.s_comp);
+			g.refine_requests.insert(q.refine.begin(), q.refine.end());  // 2434-2520
+			nref = q.refine.size();
+			nkeep = q.kept;
+			g.unrefine_requests.insert(q.unrefine.begin(), q.unrefine.end());
+			nunref = q.unrefine.size();
+			size_t at = 0;
+			for (size_t r = 0; r < q.part_slot.size(); r++) {
+				const uint64_t parent = map_parent(g.m, q.part_ids[at]);
+				for (uint32_t j = 0; j < q.part_len[r]; j++, at++) add_partial(parent, q.part_bands[at], q.part_ids[at]);
 			}
-			run.clear();
-		};
-		for (size_t s = 0; s < n; s++) {
-			const int lvl = map_level(g.m, ids[s]);
-			if (b[s] == 2 && lvl < g.R) {
-				g.refine_requests.insert(ids[s]);  // 2434-2520: a local leaf below the maximum level
-				nref++;
+		} else {
+			// unrefine requests pending from before: the same walk on the host
+			const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
+			const auto& ids = slot_ids_host(g);
+			std::vector<uint8_t> rb;
+			std::vector<uint64_t> ri;
+			uint64_t run_parent = error_cell;
+			auto flush = [&] {
+				if (ri.empty()) return;
+				if (ri.size() == 8) decide(rb.data(), ri.data(), 8);
+				else
+					for (size_t i = 0; i < ri.size(); i++) add_partial(run_parent, rb[i], ri[i]);
+				rb.clear();
+				ri.clear();
+			};
+			for (size_t s = 0; s < n; s++) {
+				const int lvl = map_level(g.m, ids[s]);
+				if (b[s] == 2 && lvl < g.R) {
+					g.refine_requests.insert(ids[s]);  // 2434-2520: a local leaf below the maximum level
+					nref++;
+				}
+				if (lvl == 0) {
+					flush();
+					run_parent = error_cell;
+					continue;
+				}
+				const uint64_t p = map_parent(g.m, ids[s]);
+				if (p != run_parent) {
+					flush();
+					run_parent = p;
+				}
+				rb.push_back(b[s]);
+				ri.push_back(ids[s]);
 			}
-			if (lvl == 0) {
-				flush();
-				run_parent = error_cell;
-				continue;
-			}
-			const uint64_t p = map_parent(g.m, ids[s]);
-			if (p != run_parent) {
-				flush();
-				run_parent = p;
-			}
-			run.push_back(s);
+			flush();
 		}
-		flush();
-		for (auto& kv : partial) decide(kv.second.data(), kv.second.size());
+		for (auto& kv : partial) decide(kv.second.first.data(), kv.second.second.data(), kv.second.first.size());
 		if (counts) {
 			counts[0] = nref;
 			counts[1] = nkeep;
@@ -2018,31 +2043,32 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		double* f[7];
 		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
 		// merged parents: the store order of the removed children -> per
-		// parent its eight children in ascending id
+		// parent its eight children in ascending id (children grouped by a
+		// sort on the parent, the parents' slots from the device table)
 		const auto& rm = g.removed_ids_h;
-		std::map<uint64_t, std::array<int32_t, 8>> par;
-		for (size_t i = 0; i < rm.size(); i++) {
-			const uint64_t p = map_parent(g.m, rm[i]);
-			uint64_t ch[8];
-			map_all_children(g.m, p, ch);
-			auto it = par.find(p);
-			if (it == par.end()) {
-				std::array<int32_t, 8> a;
-				a.fill(-1);
-				it = par.emplace(p, a).first;
+		if (!rm.empty()) {
+			std::vector<std::pair<uint64_t, uint32_t>> pc(rm.size());
+			for (size_t i = 0; i < rm.size(); i++) pc[i] = {map_parent(g.m, rm[i]), uint32_t(i)};
+			std::sort(pc.begin(), pc.end());
+			std::vector<uint64_t> parents;
+			std::vector<int32_t> cidx;
+			for (size_t a = 0; a < pc.size();) {
+				size_t b = a;
+				while (b < pc.size() && pc[b].first == pc[a].first) b++;
+				uint64_t ch[8];
+				map_all_children(g.m, pc[a].first, ch);
+				int32_t c8[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+				for (size_t j = a; j < b; j++)
+					for (int k = 0; k < 8; k++)
+						if (ch[k] == rm[pc[j].second]) c8[k] = int32_t(pc[j].second);
+				for (int32_t v : c8) DX_REQUIRE(v >= 0, "a removed child's payload is missing");
+				parents.push_back(pc[a].first);
+				cidx.insert(cidx.end(), c8, c8 + 8);
+				a = b;
 			}
-			for (int k = 0; k < 8; k++)
-				if (ch[k] == rm[i]) it->second[size_t(k)] = int32_t(i);
-		}
-		if (!par.empty()) {
-			std::vector<int32_t> pslot, cidx;
-			for (const auto& kv : par) {
-				const int64_t sl = lookup_slot(g, kv.first);
-				DX_REQUIRE(sl >= 0 && size_t(sl) < g.n_local, "merged parent is not local");
-				for (int32_t v : kv.second) DX_REQUIRE(v >= 0, "a removed child's payload is missing");
-				pslot.push_back(int32_t(sl));
-				cidx.insert(cidx.end(), kv.second.begin(), kv.second.end());
-			}
+			std::vector<int32_t> pslot(parents.size());
+			lookup_batch(g, parents.data(), parents.size(), nullptr, pslot.data());
+			for (int32_t sl : pslot) DX_REQUIRE(sl >= 0 && size_t(sl) < g.n_local, "merged parent is not local");
 			DBuf<int32_t> dp, dc;
 			upload(dp, pslot, s);
 			upload(dc, cidx, s);

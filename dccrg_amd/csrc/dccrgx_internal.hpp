@@ -555,6 +555,19 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face
                         uint64_t* out, hipStream_t s);
 // adaptation of tests/advection/adapter.hpp: per local cell band (2 refine,
 // 1 keep, 0 unrefine), merged parents' densities, velocity + length reset
+// check_for_adaptation's requests computed on the device (sweep_kernels.hip
+// adv_requests_kernel): refine ids, unrefine ids of whole local families,
+// the number of kept whole families, and the partial runs (first slot,
+// length, members' ids and bands) for the host to merge by parent
+struct AdvRequests {
+	std::vector<uint64_t> refine, unrefine;
+	size_t kept = 0;
+	std::vector<size_t> part_slot;
+	std::vector<uint32_t> part_len;
+	std::vector<uint64_t> part_ids;
+	std::vector<uint8_t> part_bands;
+};
+AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint8_t* band, size_t n, hipStream_t s);
 void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                  const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
                  double unrefine_sensitivity, uint8_t* band, hipStream_t s);

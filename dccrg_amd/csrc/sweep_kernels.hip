@@ -677,6 +677,47 @@ __global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const
 	}
 }
 
+// the requests check_for_adaptation issues from the bands (adapter.hpp:
+// 124-176), per local slot on Morton-ordered slots: a refine request for a
+// band-2 leaf below the maximum level; per family (a run of consecutive slots
+// with one parent, level > 0) headed at this slot: all 8 members here -> kept
+// when any member's band is >= 1, else one unrefine request; fewer -> the
+// run goes to the host, which merges the runs of a parent (families split
+// between runs or processes).  Lists are appended through counters
+// cnt[0] refines, cnt[1] unrefines, cnt[2] kept families, cnt[3] partial runs.
+__global__ void adv_requests_kernel(MapCtx m, const uint64_t* __restrict__ ids, const uint8_t* __restrict__ band,
+                                    size_t n, uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
+                                    uint32_t* __restrict__ part, unsigned long long* __restrict__ cnt) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[s];
+		const int lvl = map_level(m, id);
+		if (band[s] == 2 && lvl < int(m.R)) ref[atomicAdd(&cnt[0], 1ull)] = id;
+		if (lvl == 0) continue;
+		const uint64_t p = map_parent(m, id);
+		if (s > 0 && map_level(m, ids[s - 1]) > 0 && map_parent(m, ids[s - 1]) == p) continue;  // not a run head
+		uint32_t k = 1;
+		bool keep = band[s] >= 1;
+		while (k < 8 && s + k < n) {
+			const uint64_t c = ids[s + k];
+			if (map_level(m, c) == 0 || map_parent(m, c) != p) break;
+			keep = keep || band[s + k] >= 1;
+			k++;
+		}
+		if (k < 8) part[atomicAdd(&cnt[3], 1ull)] = uint32_t(s) | (k << 28);
+		else if (keep) atomicAdd(&cnt[2], 1ull);
+		else unref[atomicAdd(&cnt[1], 1ull)] = id;
+	}
+}
+
+__global__ void gather_ids_bands_kernel(const uint64_t* __restrict__ ids, const uint8_t* __restrict__ band,
+                                        const uint32_t* __restrict__ at, size_t n, uint64_t* __restrict__ oid,
+                                        uint8_t* __restrict__ ob) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		oid[i] = ids[at[i]];
+		ob[i] = band[at[i]];
+	}
+}
+
 // adapt_grid (adapter.hpp:260-290): a merged parent's density is the sum of
 // its removed children's densities / 8 (children in ascending id)
 __global__ void adv_parent_density_kernel(double* __restrict__ rho, const int32_t* __restrict__ parent_slot,
@@ -827,6 +868,56 @@ void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t
 	if (!np) return;
 	adv_parent_density_kernel<<<grid_for(np, 256), 256, 0, s>>>(rho, parent_slot, child_idx, removed_rho, np);
 	HIP_CHECK(hipGetLastError());
+}
+
+static void k_gather_ids_bands(const uint64_t* ids, const uint8_t* band, const uint32_t* at, size_t n, uint64_t* oid,
+                               uint8_t* ob, hipStream_t s) {
+	gather_ids_bands_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, band, at, n, oid, ob);
+	HIP_CHECK(hipGetLastError());
+}
+
+AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint8_t* band, size_t n, hipStream_t s) {
+	AdvRequests out;
+	if (!n) return out;
+	DX_REQUIRE(n < (size_t(1) << 28), "too many local cells for the request runs");
+	DBuf<uint64_t> ref, unref;
+	DBuf<uint32_t> part;
+	DBuf<unsigned long long> cnt;
+	ref.alloc(n);
+	unref.alloc(n / 8 + 1);
+	part.alloc(n);
+	cnt.alloc(4);
+	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
+	adv_requests_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, slot_ids, band, n, ref.p, unref.p, part.p, cnt.p);
+	HIP_CHECK(hipGetLastError());
+	unsigned long long h[4];
+	HIP_CHECK(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	out.refine = download(ref.p, size_t(h[0]), s);
+	out.unrefine = download(unref.p, size_t(h[1]), s);
+	out.kept = size_t(h[2]);
+	const std::vector<uint32_t> runs = download(part.p, size_t(h[3]), s);
+	// the partial runs' members: ids and bands
+	for (uint32_t r : runs) {
+		const size_t s0 = r & ((1u << 28) - 1u), k = r >> 28;
+		out.part_slot.push_back(s0);
+		out.part_len.push_back(uint32_t(k));
+	}
+	if (!runs.empty()) {
+		std::vector<uint32_t> mem;
+		for (size_t i = 0; i < out.part_slot.size(); i++)
+			for (uint32_t j = 0; j < out.part_len[i]; j++) mem.push_back(uint32_t(out.part_slot[i] + j));
+		DBuf<uint32_t> dm;
+		upload(dm, mem, s);
+		DBuf<uint64_t> gid;
+		DBuf<uint8_t> gb;
+		gid.alloc(mem.size());
+		gb.alloc(mem.size());
+		k_gather_ids_bands(slot_ids, band, dm.p, mem.size(), gid.p, gb.p, s);
+		out.part_ids = download(gid.p, mem.size(), s);
+		out.part_bands = download(gb.p, mem.size(), s);
+	}
+	return out;
 }
 
 void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],

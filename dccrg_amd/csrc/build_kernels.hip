@@ -825,18 +825,18 @@ void sort_u64(uint64_t* keys, size_t n, hipStream_t s) {
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 
-size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s) {
+size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	if (n == 0) return 0;
 	DBuf<uint64_t> tmp;
 	tmp.alloc(n);
 	DBuf<unsigned long long> nsel;
 	nsel.alloc(1);
 	size_t b1 = 0, b2 = 0;
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, end_bit, s));
 	HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, b2, tmp.p, keys, nsel.p, n, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(std::max(b1, b2));
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, end_bit, s));
 	HIP_CHECK(hipcub::DeviceSelect::Unique(temp.p, b2, tmp.p, keys, nsel.p, n, s));
 	return read_counter(nsel, s);
 }

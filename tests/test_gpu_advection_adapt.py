@@ -56,3 +56,41 @@ def test_adaptive_advection_matches_oracle(gpu, base, R, steps):
     for k, col in ((1, 1), (2, 2), (4, 6), (5, 7), (6, 8)):
         assert np.array_equal(f[k].get(0, g.n_local), exp[:, col])  # velocities and lengths bitwise
     g.close()
+
+
+def test_check_with_pending_unrefine_matches_device_decisions(gpu):
+    """check_for_adaptation decides on the device unless unrefine requests
+    are already pending; then it walks the slots on the host.  Two identical
+    grids step together, the second with an unrefine request of one level-2
+    family issued before every check: whatever the check decides for that
+    family (keep: its dont_unrefine mark cancels the request; unrefine: the
+    same family twice), both grids must adapt identically - so the host walk
+    and the device decisions agree."""
+    base, R, steps = (16, 16, 1), 2, 12
+    grids = []
+    for _ in range(2):
+        g, f = gpu_grid(base, R)
+        prerefine(g, f, R)
+        grids.append((g, f))
+    di = 0.025 / R
+    issued = 0
+    for step in range(steps):
+        dt = 0.5 * grids[0][0].advection_max_time_step(grids[0][1])
+        out = []
+        for k, (g, f) in enumerate(grids):
+            g.advection_step(f, dt)
+            if k == 1:
+                cells = g.local_cells()
+                lvl2 = [int(c) for c in cells[::97] if g.get_refinement_level(int(c)) == R]
+                if lvl2:
+                    g.unrefine_completely(lvl2[0])
+                    issued += 1
+            g.advection_check_adaptation(f[0], di)
+            g.advection_commit(f[0])
+            out.append(g.advection_adapt(f))
+        assert out[0] == out[1], step
+        assert np.array_equal(grids[0][0].local_cells(), grids[1][0].local_cells()), step
+        assert np.array_equal(grids[0][1][0].get(0, grids[0][0].n_local), grids[1][1][0].get(0, grids[1][0].n_local))
+    assert issued > 0
+    for g, _ in grids:
+        g.close()

@@ -1968,7 +1968,7 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			pr.first.push_back(band_v);
 			pr.second.push_back(id);
 		};
-		if (g.unrefine_requests.empty()) {
+		if (g.unrefine_requests.empty() && n < (size_t(1) << 28)) {
 			// on the device: refine requests, whole-family decisions, partial runs
 			const AdvRequests q = k_adv_requests(g.m, g.slot_ids.p, band.p, n, g.s_comp);
 			g.refine_requests.insert(q.refine.begin(), q.refine.end());  // 2434-2520
@@ -1982,7 +1982,8 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 				for (uint32_t j = 0; j < q.part_len[r]; j++, at++) add_partial(parent, q.part_bands[at], q.part_ids[at]);
 			}
 		} else {
-			// unrefine requests pending from before: the same walk on the host
+			// unrefine requests pending from before (or more local cells than
+			// the device runs encode): the same walk on the host
 			const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
 			const auto& ids = slot_ids_host(g);
 			std::vector<uint8_t> rb;

@@ -307,7 +307,10 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
     const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ ptr,
     const uint32_t* __restrict__ l0c, L0Geom G, uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0,
     size_t s1, int* __restrict__ err) {
-	constexpr uint32_t cap = 8192;  // entry bytes staged per block
+	// entry bytes staged per block; after the walks the same 16 KB hold the
+	// block's lists (256 rows x 64 B) for a coalesced store
+	constexpr uint32_t cap = 16384;
+	static_assert(cap >= kCollectRows * kList * 8, "LDS too small for the lists");
 	__shared__ uint32_t sp32[cap / 4];
 	const uint32_t tid = threadIdx.x;
 	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	}
 	__syncthreads();
 	const size_t s = r0 + tid;
-	if (s >= r1) return;
+	const bool act = s < r1;
 	uint32_t mask = 0, l[kList];
 #pragma unroll
 	for (int i = 0; i < kList; i++) l[i] = 13;
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 		}
 	};
 	// the row's entry bytes a 4-byte word at a time (E0 is word aligned)
-	for (uint32_t j = ptr[s], e = ptr[s + 1]; j < e;) {
+	for (uint32_t j = act ? ptr[s] : 0, e = act ? ptr[s + 1] : 0; j < e;) {
 		const uint32_t b0 = j & 3u, b1 = e - j < 4u - b0 ? b0 + (e - j) : 4u;
 		if (j - E0 < nB) {
 			const uint32_t word = sp32[(j - E0) >> 2];
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	// level-0 ids of the listed positions: the row's three wrapped x, y, z
 	// coordinates once, then per entry 1 + x + y lx + z lx ly
 	int px, py, pz;
-	l0_unpack(l0c[s], G, px, py, pz);
+	l0_unpack(act ? l0c[s] : 0u, G, px, py, pz);
 	auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
 	const uint64_t lxy = uint64_t(G.lx) * G.ly;
 	const uint64_t X[3] = {uint64_t(wrap(px - 1, int(G.lx))) + 1, uint64_t(px) + 1, uint64_t(wrap(px + 1, int(G.lx))) + 1};
@@ -389,10 +392,18 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 		const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
 		out[i] = i < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
 	}
-	ulonglong2* o = reinterpret_cast<ulonglong2*>(lst + s * kList);
+	// the lists through LDS: each row's 64 B at its place, then the block's
+	// rows stored as one contiguous run, 16 B per lane and instruction
+	__syncthreads();  // every walk done: the staged entry bytes are free
+	ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
+	if (act)
 #pragma unroll
-	for (int i = 0; i < kList / 2; i++) o[i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
-	mask_out[s] = mask;
+		for (int i = 0; i < kList / 2; i++) so[tid * (kList / 2) + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+	__syncthreads();
+	ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + r0 * kList);
+	const uint32_t n16 = uint32_t(r1 - r0) * (kList / 2);
+	for (uint32_t k = tid; k < n16; k += kCollectRows) dst[k] = so[k];
+	if (act) mask_out[s] = mask;
 }
 
 __global__ void gol_amr_spread0_mask_kernel(const uint32_t* __restrict__ lvl0, size_t n0, uint32_t* __restrict__ state,

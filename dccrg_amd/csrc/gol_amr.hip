@@ -417,43 +417,54 @@ __global__ void gol_amr_spread0_mask_kernel(const uint32_t* __restrict__ lvl0, s
 
 // spread + rule of one refined level-0 cell's leaves: the union of the
 // siblings' parents is the OR of their masks (a sibling held as a remote
-// copy contributes its received list, turned into bits)
+// copy contributes its received list, turned into bits).  Eight lanes per
+// group, one member each (a group of more members loops in steps of eight):
+// the members' slots and masks are loaded side by side, OR-ed by shuffles.
+__device__ __forceinline__ uint32_t remote_mask(const uint64_t* __restrict__ lst, const uint32_t* __restrict__ l0c,
+                                                const L0Geom& G, uint32_t gs, int* __restrict__ err) {
+	int px, py, pz;
+	l0_unpack(l0c[gs], G, px, py, pz);
+	uint32_t u = 0;
+	for (int i = 0; i < kList; i++) {
+		const uint64_t id = lst[size_t(gs) * kList + i];
+		if (id == error_cell) break;
+		const uint64_t k = id - 1;
+		const int qx = int(k % G.lx), qy = int((k / G.lx) % G.ly), qz = int(k / (uint64_t(G.lx) * G.ly));
+		const int dx = l0_rel(qx, px, int(G.lx)), dy = l0_rel(qy, py, int(G.ly)), dz = l0_rel(qz, pz, int(G.lz));
+		if (dx == 2 || dy == 2 || dz == 2) {
+			atomicOr(err, 4);
+			continue;
+		}
+		u |= 1u << (9 * (dz + 1) + 3 * (dy + 1) + dx + 1);
+	}
+	return u;
+}
+
 __global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ gptr, size_t ng,
                                                   const uint32_t* __restrict__ gslot, uint32_t* __restrict__ state,
                                                   const uint32_t* __restrict__ mask, const uint64_t* __restrict__ lst,
                                                   const uint32_t* __restrict__ l0c, L0Geom G, size_t n_local,
                                                   size_t s0, size_t s1, int* __restrict__ err) {
-	const size_t gi = size_t(xcd_block()) * blockDim.x + threadIdx.x;
-	if (gi >= ng) return;
-	const uint32_t b = gptr[gi], e = gptr[gi + 1];
-	bool any = false;
-	uint32_t u = 0;
-	for (uint32_t j = b; j < e; j++) {
+	const size_t t = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	const size_t gi = t >> 3;
+	const uint32_t m = uint32_t(t & 7u);
+	const bool live_group = gi < ng;  // lanes of one group share a wave (8 | 64): no early exit
+	const uint32_t b = live_group ? gptr[gi] : 0u, e = live_group ? gptr[gi + 1] : 0u;
+	uint32_t u = 0, any = 0;
+	for (uint32_t j = b + m; j < e; j += 8) {
 		const uint32_t gs = gslot[j];
-		any |= gs >= s0 && gs < s1;
-		if (gs < n_local) {
-			u |= mask[gs];
-			continue;
-		}
-		int px, py, pz;
-		l0_unpack(l0c[gs], G, px, py, pz);
-		for (int i = 0; i < kList; i++) {
-			const uint64_t id = lst[size_t(gs) * kList + i];
-			if (id == error_cell) break;
-			const uint64_t k = id - 1;
-			const int qx = int(k % G.lx), qy = int((k / G.lx) % G.ly), qz = int(k / (uint64_t(G.lx) * G.ly));
-			const int dx = l0_rel(qx, px, int(G.lx)), dy = l0_rel(qy, py, int(G.ly)), dz = l0_rel(qz, pz, int(G.lz));
-			if (dx == 2 || dy == 2 || dz == 2) {
-				atomicOr(err, 4);
-				continue;
-			}
-			u |= 1u << (9 * (dz + 1) + 3 * (dy + 1) + dx + 1);
-		}
+		any |= (gs >= s0 && gs < s1) ? 1u : 0u;
+		u |= gs < n_local ? mask[gs] : remote_mask(lst, l0c, G, gs, err);
+	}
+#pragma unroll
+	for (int o = 1; o < 8; o <<= 1) {
+		u |= __shfl_xor(u, o, 8);
+		any |= __shfl_xor(any, o, 8);
 	}
 	if (!any) return;
 	const int n = __popc(u);
-	if (n > kList) atomicOr(err, 1);
-	for (uint32_t j = b; j < e; j++)
+	if (n > kList && m == 0) atomicOr(err, 1);
+	for (uint32_t j = b + m; j < e; j += 8)
 		if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
 }
 
@@ -566,7 +577,7 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,
 				                                                                   s0, s1);
 			if (T.ng)
-				gol_amr_spread_groups_mask_kernel<<<xcd_grid((T.ng + 255) / 256), 256, 0, s>>>(
+				gol_amr_spread_groups_mask_kernel<<<xcd_grid((8 * T.ng + 255) / 256), 256, 0, s>>>(
 				    T.gptr.p, T.ng, T.gslot.p, state, T.mask.p, lst, T.l0c.p, G, n_local, s0, s1, err);
 		}
 		HIP_CHECK(hipGetLastError());

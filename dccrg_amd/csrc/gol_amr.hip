@@ -309,8 +309,11 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
     size_t s1, int* __restrict__ err) {
 	// entry bytes staged per block; after the walks the same 16 KB hold the
 	// block's lists (256 rows x 64 B) for a coalesced store
-	constexpr uint32_t cap = 16384;
-	static_assert(cap >= kCollectRows * kList * 8, "LDS too small for the lists");
+	// (the lists at a row stride of 80 B: five 16-B slots, conflict-free
+	// 16-B stores across a 16-lane group)
+	constexpr uint32_t kRowSlots = kList / 2 + 1;
+	constexpr uint32_t cap = kCollectRows * kRowSlots * 16;
+	static_assert(cap >= 8192, "LDS too small for the entry bytes");
 	__shared__ uint32_t sp32[cap / 4];
 	const uint32_t tid = threadIdx.x;
 	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
@@ -398,11 +401,11 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
 	if (act)
 #pragma unroll
-		for (int i = 0; i < kList / 2; i++) so[tid * (kList / 2) + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+		for (int i = 0; i < kList / 2; i++) so[tid * kRowSlots + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
 	__syncthreads();
 	ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + r0 * kList);
 	const uint32_t n16 = uint32_t(r1 - r0) * (kList / 2);
-	for (uint32_t k = tid; k < n16; k += kCollectRows) dst[k] = so[k];
+	for (uint32_t k = tid; k < n16; k += kCollectRows) dst[k] = so[(k / (kList / 2)) * kRowSlots + k % (kList / 2)];
 	if (act) mask_out[s] = mask;
 }
 

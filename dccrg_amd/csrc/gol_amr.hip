@@ -396,7 +396,8 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 		out[i] = i < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
 	}
 	// the lists through LDS: each row's 64 B at its place, then the block's
-	// rows stored as one contiguous run, 16 B per lane and instruction
+	// rows stored as one contiguous run, 16 B per lane and instruction,
+	// non-temporal (paired A/B: 0.713 -> 0.693 ms per step)
 	__syncthreads();  // every walk done: the staged entry bytes are free
 	ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
 	if (act)
@@ -405,7 +406,12 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	__syncthreads();
 	ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + r0 * kList);
 	const uint32_t n16 = uint32_t(r1 - r0) * (kList / 2);
-	for (uint32_t k = tid; k < n16; k += kCollectRows) dst[k] = so[(k / (kList / 2)) * kRowSlots + k % (kList / 2)];
+	for (uint32_t k = tid; k < n16; k += kCollectRows) {
+		typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+		const ulonglong2 v = so[(k / (kList / 2)) * kRowSlots + k % (kList / 2)];
+		const u2v w = {v.x, v.y};
+		__builtin_nontemporal_store(w, reinterpret_cast<u2v*>(dst + k));
+	}
 	if (act) mask_out[s] = mask;
 }
 

@@ -397,11 +397,14 @@ def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                          "synthetic: seeded alive(id) rule, p=0.2",
                          {"workload": f"tests/scalability 1024x1024x{nzr * world} uniform, neighborhood 1, "
                                       "block partition (z slabs), game of life on the 4-B payload",
-                          "cells_total": int(sm[1]), "parallelism": f"domain decomposition x{world}"})
+                          "cells_total": int(sm[1]), "cells_rank0": int(n),
+                          "parallelism": f"domain decomposition x{world}"})
         ach = 8.0 * n * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
-                            "kernel": "gol_structured_v3 (plane boxes)", "kernel_ms_per_step": kms / a.steps}
+                            "frac": ach / PEAK_HBM_GBS if ach else None,
+                            "traffic": measured_traffic("scalability", n, 8 * n, world),
+                            "kernel": "gol_structured_v3 (plane boxes)", "alg_bytes_per_step": 8 * n,
+                            "kernel_ms_per_step": kms / a.steps}
         halo = {"ms_per_exchange_4B": mx[3] * 1e3, "ms_per_exchange_1B": mx[4] * 1e3,
                 "send_cells_max_rank": mx[6], "peers_rank0": peers}
         if world > 1 and mx[3] > 0:

@@ -527,9 +527,12 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		               nf = meta[tt].nf;
 		if (tid < n) {
 			load7(ts + tid, c);
-			row[0] = tell[3 * (ts + tid)];
-			row[1] = tell[3 * (ts + tid) + 1];
-			row[2] = tell[3 * (ts + tid) + 2];
+			// the tile's face codes, ext list and finer pairs are read once per
+			// sweep: non-temporal, so they do not evict the field lines other
+			// tiles re-read (paired A/B on config 3: 0.1915 -> 0.1865 ms/sweep)
+			row[0] = __builtin_nontemporal_load(tell + 3 * (ts + tid));
+			row[1] = __builtin_nontemporal_load(tell + 3 * (ts + tid) + 1);
+			row[2] = __builtin_nontemporal_load(tell + 3 * (ts + tid) + 2);
 		}
 		// ext = slot | axis mask << 29: density and lengths, and only the
 		// velocity components along the axes its faces cross
@@ -540,11 +543,11 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
 			v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
 		};
-		if (tid < ne) load5(ext[e0 + tid], xa);
-		if (tid + T < ne) load5(ext[e0 + tid + T], xb);
+		if (tid < ne) load5(__builtin_nontemporal_load(ext + e0 + tid), xa);
+		if (tid + T < ne) load5(__builtin_nontemporal_load(ext + e0 + tid + T), xb);
 		if (tid < nf) {
-			fq[0] = tfine[2 * (fb + tid)];
-			fq[1] = tfine[2 * (fb + tid) + 1];
+			fq[0] = __builtin_nontemporal_load(tfine + 2 * (fb + tid));
+			fq[1] = __builtin_nontemporal_load(tfine + 2 * (fb + tid) + 1);
 		}
 	};
 	load(t);

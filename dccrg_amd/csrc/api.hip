@@ -203,17 +203,13 @@ static void po_reduce(Grid& g, int k, unsigned nb, const PoParams& prm, int stag
 	const bool one = g.size == 1;
 	k_po_reduce(k, P.part.p, nb, P.red.p, P.st.p, prm, stage, one, g.s_comp);
 	if (one) return;
+	// MPI_Allreduce SUM (poisson_solve.hpp:349, 486, 684): the ranks' sums
+	// all-gathered and added in rank order on every rank (the same result
+	// over RCCL and the host exchange)
 	comm_require(g, "Poisson solve");
-	if (g.nccl && !g.xfn) {
-		NCCL_CHECK(ncclAllReduce(P.red.p, P.red.p, size_t(k), ncclFloat64, ncclSum, g.nccl, g.s_comp));
-	} else {
-		double h[2] = {0, 0};
-		HIP_CHECK(hipMemcpyAsync(h, P.red.p, size_t(k) * 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
-		comm_allreduce_f64(g, h, k, 0);
-		HIP_CHECK(hipMemcpyAsync(P.red.p, h, size_t(k) * 8, hipMemcpyHostToDevice, g.s_comp));
-	}
-	k_po_scalar(P.red.p, P.st.p, prm, stage, g.s_comp);
+	P.gath.reserve(size_t(g.size) * 2);
+	comm_allgather_dev(g, P.red.p, size_t(k) * 8, reinterpret_cast<uint8_t*>(P.gath.p), g.s_comp);
+	k_po_scalar(P.gath.p, g.size, k, P.st.p, prm, stage, g.s_comp);
 }
 
 static PoScalars po_read_scalars(Grid& g) {

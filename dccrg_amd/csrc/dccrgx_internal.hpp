@@ -167,7 +167,7 @@ struct PoissonState {
 	int type = -1;             // int32 field: classification / final type
 	int p0 = -1, p1 = -1, r0 = -1, r1 = -1, ap0 = -1, best = -1, sf = -1, f[6] = {-1, -1, -1, -1, -1, -1};
 	DBuf<int32_t> ell, fine;
-	DBuf<double> part, red;
+	DBuf<double> part, red, gath;  // gath: P x 2 all-gathered per-rank sums
 	DBuf<PoScalars> st;
 	size_t n_cached = 0;       // local cells in cell_info
 };
@@ -415,7 +415,13 @@ struct DevMsg {
 	uint8_t* recv;
 	size_t recv_bytes;
 };
+// one grouped point-to-point round of device messages (the same message list
+// for every transport; see comm.hip)
 void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s);
+// every rank's `bytes` at `mine` into all[p * bytes] on the device (own slot included)
+void comm_allgather_dev(Grid& g, const void* mine, size_t bytes, uint8_t* all, hipStream_t s);
+// P x count values, rank-major, combined in rank order (op 0 sum, 1 min, 2 max)
+void rank_ordered_combine(const double* all, int P, int count, int op, double* out);
 void comm_require(const Grid& g, const char* what);
 
 // --- mesh.hip: knowledge, hash table, structures --------------------------------
@@ -612,6 +618,7 @@ void k_po_phase(int phase, const PoArrays& a, size_t n, const PoParams& prm, con
                 hipStream_t s);
 void k_po_reduce(int k, const double* part, unsigned nb, double* red, PoScalars* st, const PoParams& prm, int stage,
                  bool scalar, hipStream_t s);
-void k_po_scalar(const double* red, PoScalars* st, const PoParams& prm, int stage, hipStream_t s);
+// all: P x k all-gathered per-rank sums, combined in rank order
+void k_po_scalar(const double* all, int P, int k, PoScalars* st, const PoParams& prm, int stage, hipStream_t s);
 
 }  // namespace dccrgx

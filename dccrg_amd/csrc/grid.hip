@@ -219,70 +219,26 @@ static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 	HIP_CHECK(hipStreamWaitEvent(g.s_comm, g.ev_comp, 0));
 	hipStream_t s = g.s_comm;
 	pack_plan(H, tf, L, s);
-	const std::vector<int> peers = H.peers();
-	if (g.nccl && !g.xfn) {
-		NCCL_CHECK(ncclGroupStart());
-		for (int p : peers) {
-			const size_t ns = count_of(H.send_ids, p), nr = count_of(H.recv_ids, p);
-			const size_t so = off_of(H.send_off, p), ro = off_of(H.recv_off, p);
-			for (size_t k = 0; k < tf.size(); k++) {
-				Field* f = tf[k];
-				if (ns)
-					NCCL_CHECK(ncclSend(H.sendbuf.p + L.sfo[k] + so * f->win_len, ns * f->win_len, ncclUint8, p, g.nccl, s));
-				if (nr) {
-					uint8_t* dst = direct && f->full_window() ? f->data.p + (g.n_local + ro) * f->elem
-					                                          : H.recvbuf.p + L.rfo[k] + ro * f->win_len;
-					NCCL_CHECK(ncclRecv(dst, nr * f->win_len, ncclUint8, p, g.nccl, s));
-				}
-			}
+	// one message per peer and field (field order): the send slice of the
+	// packed buffer, received straight into the peer's run of halo slots for
+	// a whole-element field of a direct plan, else into the receive buffer
+	// and placed; the same list for RCCL and the host exchange
+	std::vector<DevMsg> msgs;
+	for (int p : H.peers()) {
+		const size_t ns = count_of(H.send_ids, p), nr = count_of(H.recv_ids, p);
+		const size_t so = off_of(H.send_off, p), ro = off_of(H.recv_off, p);
+		for (size_t k = 0; k < tf.size(); k++) {
+			Field* f = tf[k];
+			uint8_t* dst = direct && f->full_window() ? f->data.p + (g.n_local + ro) * f->elem
+			                                          : H.recvbuf.p + L.rfo[k] + ro * f->win_len;
+			msgs.push_back({p, H.sendbuf.p + L.sfo[k] + so * f->win_len, ns * f->win_len, dst, nr * f->win_len});
 		}
-		NCCL_CHECK(ncclGroupEnd());
-		for (size_t k = 0; k < tf.size(); k++)
-			if (!(direct && tf[k]->full_window()))
-				k_place(H.recvbuf.p + L.rfo[k], tf[k]->elem, tf[k]->win_off, tf[k]->win_len, H.recv_slots.p, H.n_recv,
-				        tf[k]->data.p, s);
-	} else {
-		// host exchange: the per-peer messages through the host
-		HIP_CHECK(hipStreamSynchronize(s));
-		std::vector<std::vector<uint8_t>> msg(size_t(g.size)), in(size_t(g.size));
-		for (int p : peers) {
-			const size_t ns = count_of(H.send_ids, p), so = off_of(H.send_off, p);
-			std::vector<uint8_t>& m = msg[size_t(p)];
-			m.resize(ns * L.bpc);
-			size_t o = 0;
-			for (size_t k = 0; k < tf.size(); k++) {
-				const size_t b = ns * tf[k]->win_len;
-				if (b) HIP_CHECK(hipMemcpy(m.data() + o, H.sendbuf.p + L.sfo[k] + so * tf[k]->win_len, b, hipMemcpyDeviceToHost));
-				o += b;
-			}
-			in[size_t(p)].resize(count_of(H.recv_ids, p) * L.bpc);
-		}
-		std::vector<const void*> sp(size_t(g.size), nullptr);
-		std::vector<void*> rp(size_t(g.size), nullptr);
-		std::vector<size_t> sb(size_t(g.size), 0), rb(size_t(g.size), 0);
-		for (int p = 0; p < g.size; p++) {
-			sp[size_t(p)] = msg[size_t(p)].data();
-			sb[size_t(p)] = msg[size_t(p)].size();
-			rp[size_t(p)] = in[size_t(p)].data();
-			rb[size_t(p)] = in[size_t(p)].size();
-		}
-		DX_REQUIRE(g.xfn(g.xctx, sp.data(), sb.data(), rp.data(), rb.data()) == 0, "exchange function failed");
-		for (int p : peers) {
-			const size_t nr = count_of(H.recv_ids, p), ro = off_of(H.recv_off, p);
-			size_t o = 0;
-			for (size_t k = 0; k < tf.size(); k++) {
-				const size_t b = nr * tf[k]->win_len;
-				if (b)
-					HIP_CHECK(hipMemcpyAsync(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, in[size_t(p)].data() + o, b,
-					                         hipMemcpyHostToDevice, s));
-				o += b;
-			}
-		}
-		for (size_t k = 0; k < tf.size(); k++)
+	}
+	comm_device_transfer(g, msgs, s);
+	for (size_t k = 0; k < tf.size(); k++)
+		if (!(direct && tf[k]->full_window()))
 			k_place(H.recvbuf.p + L.rfo[k], tf[k]->elem, tf[k]->win_off, tf[k]->win_len, H.recv_slots.p, H.n_recv,
 			        tf[k]->data.p, s);
-		HIP_CHECK(hipStreamSynchronize(s));
-	}
 	var_halo(g, H, s);
 	HIP_CHECK(hipEventRecord(g.ev_halo, s));
 }

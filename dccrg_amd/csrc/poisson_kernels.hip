@@ -443,8 +443,18 @@ __global__ __launch_bounds__(RB) void po_reduce_kernel(const double* __restrict_
 	}
 }
 
-__global__ void po_scalar_kernel(const double* red, PoScalars* st, PoParams prm, int stage) {
-	if (threadIdx.x == 0 && blockIdx.x == 0) po_scalar(st, red, prm, stage);
+// all = P x k per-rank sums (rank-major, all-gathered): the global sums
+// combined in rank order, as every rank does, then the scalar step
+__global__ void po_scalar_kernel(const double* all, int P, int k, PoScalars* st, PoParams prm, int stage) {
+#pragma clang fp contract(off)
+	if (threadIdx.x != 0 || blockIdx.x != 0) return;
+	double r[2] = {0, 0};
+	for (int j = 0; j < k; j++) {
+		double acc = all[j];
+		for (int p = 1; p < P; p++) acc += all[p * k + j];
+		r[j] = acc;
+	}
+	po_scalar(st, r, prm, stage);
 }
 
 inline unsigned po_blocks(size_t n) {
@@ -489,8 +499,8 @@ void k_po_reduce(int k, const double* part, unsigned nb, double* red, PoScalars*
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_po_scalar(const double* red, PoScalars* st, const PoParams& prm, int stage, hipStream_t s) {
-	po_scalar_kernel<<<1, 64, 0, s>>>(red, st, prm, stage);
+void k_po_scalar(const double* all, int P, int k, PoScalars* st, const PoParams& prm, int stage, hipStream_t s) {
+	po_scalar_kernel<<<1, 64, 0, s>>>(all, P, k, st, prm, stage);
 	HIP_CHECK(hipGetLastError());
 }
 

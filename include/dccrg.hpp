@@ -485,7 +485,20 @@ public:
 	int get_comm_size() const { return size_; }
 	unsigned int get_neighborhood_length() const { return hood_; }
 	int get_maximum_refinement_level() const { return mapping_rw.get_maximum_refinement_level(); }
+	int get_refinement_level(const uint64_t cell) const { return mapping_rw.get_refinement_level(cell); }  // 1050
 	MPI_Comm get_communicator() const { return comm_; }
+	// 4157-4190: the parent if it exists as a cell of the grid, else the cell
+	// itself if it exists, else error_cell (existence as known to this rank:
+	// its own and ghost leaves)
+	uint64_t get_parent(const uint64_t cell) const {
+		const int l = mapping_rw.get_refinement_level(cell);
+		if (l < 0) return error_cell;
+		const bool cell_exists = dccrgx_get_process(g_, cell) >= 0;
+		if (l == 0) return cell_exists ? cell : error_cell;
+		const uint64_t parent = mapping_rw.get_parent(cell);
+		if (dccrgx_get_process(g_, parent) >= 0) return parent;
+		return cell_exists ? cell : error_cell;
+	}
 
 	// ---- queries ----------------------------------------------------------------
 	// get_cells (651-739) with is_neighbor_type_match (2946-3053)
@@ -505,6 +518,8 @@ public:
 		int64_t s = -1;
 		if (g_) dccrgx_get_slots(g_, &cell, 1, &s);
 		if (s >= 0 && size_t(s) < host_.size()) return const_cast<Cell_Data*>(&host_[size_t(s)]);
+		const auto rf = refined_.find(cell);  // refined_cell_data (762)
+		if (rf != refined_.end()) return const_cast<Cell_Data*>(&rf->second);
 		const auto it = removed_index_.find(cell);
 		if (it != removed_index_.end()) return const_cast<Cell_Data*>(&removed_[it->second]);
 		return nullptr;
@@ -601,6 +616,7 @@ public:
 	// ---- halo (966-1000, 5010-5367) -------------------------------------------------
 	bool update_copies_of_remote_neighbors(const int neighborhood_id = default_neighborhood_id) {
 		dump_initial();
+		sync_window();
 		upload_local();
 		if (dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) != DCCRGX_OK) return false;
 		download_remote();
@@ -609,6 +625,7 @@ public:
 	bool start_remote_neighbor_copy_updates(const int neighborhood_id = default_neighborhood_id) {
 		if (neighborhood_id != default_neighborhood_id) return update_copies_of_remote_neighbors(neighborhood_id);
 		dump_initial();
+		sync_window();
 		upload_local();
 		return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK;
 	}
@@ -652,7 +669,13 @@ public:
 		size_t n = 0;
 		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
 		std::unordered_map<uint64_t, Cell_Data> gone;
+		// the local cells before the change, for the refined parents' data
+		std::unordered_map<uint64_t, Cell_Data> before;
+		if constexpr (!serialized_)
+			for (size_t s = 0; s < n_local_ && s < slot_ids_.size() && s < host_.size(); s++)
+				before.emplace(slot_ids_[s], host_[s]);
 		refresh(&gone);
+		if constexpr (serialized_) before = gone;
 		// removed cells' payloads on the parent's process (unrefined_cell_data 7250)
 		removed_ids_ = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_removed_cells(g_, o, c, k); });
 		removed_.clear();
@@ -669,8 +692,22 @@ public:
 			removed_download(removed_.data(), removed_.size() * sizeof(Cell_Data));
 		}
 		auto out = detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+		// refined_cell_data (10215-10219): the refined local parents' data
+		// stay reachable through operator[] until the next structural change
+		refined_.clear();
+		for (const uint64_t c : out) {
+			const uint64_t p = mapping_rw.get_parent(c);
+			if (refined_.count(p)) continue;
+			auto it = before.find(p);
+			if (it != before.end()) refined_.emplace(p, it->second);
+		}
 		if (sorted) std::sort(out.begin(), out.end());
 		return out;
+	}
+	// 5504
+	Dccrg& clear_refined_unrefined_data() {
+		clear_removed();
+		return *this;
 	}
 	// 3497: cells removed by the last stop_refining whose parent is local
 	std::vector<uint64_t> get_removed_cells(const bool sorted = false) const {
@@ -821,6 +858,18 @@ private:
 		detail::check(dccrgx_set_field_window(g_, payload_, w.first, w.second));
 		window_ = w;
 	}
+	// the reference asks get_mpi_datatype at every transfer, so the bytes a
+	// halo moves may change between calls (tests/advection/cell.hpp:47-55,
+	// Cell::transfer_all_data): re-read the window before each exchange
+	void sync_window() {
+		if constexpr (!serialized_) {
+			const auto w = detail::datatype_window<Cell_Data>();
+			if (w != window_) {
+				detail::check(dccrgx_set_field_window(g_, payload_, w.first, w.second));
+				window_ = w;
+			}
+		}
+	}
 
 	size_t n_local() const {
 		size_t ni = 0, no = 0;
@@ -828,6 +877,7 @@ private:
 		return ni + no;
 	}
 	void clear_removed() {
+		refined_.clear();
 		removed_ids_.clear();
 		removed_.clear();
 		removed_index_.clear();
@@ -1225,6 +1275,7 @@ private:
 	size_t n_local_ = 0;
 	bool dumped_initial_ = false;
 	std::vector<uint64_t> removed_ids_;
+	std::unordered_map<uint64_t, Cell_Data> refined_;
 	std::vector<Cell_Data> removed_;
 	std::unordered_map<uint64_t, size_t> removed_index_;
 	std::vector<uint64_t> slot_ids_;

@@ -745,10 +745,125 @@ def sc_variable(rank, world):
     return res
 
 
+def _poisson_mesh(n, world, balance):
+    """poisson3d.cpp:141-192 on n^3: periodic, (2 pi, pi, 8 pi) / n level-0
+    cells, balance_load() before refining (children stay with their parent,
+    170-171), then two rounds of refining the cells touching (pi, pi/2, 4 pi)
+    on every rank.  Returns the grid and the gathered leaves."""
+    from poisson_cases import center_refine_select, poisson3d_lengths
+
+    g = _grid((n, n, n), 2, (True, True, True), 0)
+    g.set_geometry((0, 0, 0), poisson3d_lengths(n))
+    if balance:
+        g.balance_load()
+    for _ in range(2):
+        ids = g.local_cells()
+        c, L = g.geometry(ids)
+        for i in ids[center_refine_select(c, L)]:
+            g.refine_completely(int(i))
+        g.stop_refining()
+    return g, np.sort(np.concatenate(_gather(g.local_cells())))
+
+
+def _poisson_oracle(n):
+    from oracle import oracle as O
+    from poisson_cases import center_refine_select, poisson3d_lengths
+
+    o = O.Grid((n, n, n), 2, (True, True, True), 0, 1)
+    o.set_geometry((0, 0, 0), poisson3d_lengths(n))
+    for _ in range(2):
+        ids, _ = o.cells()
+        c, L = o.geometry(ids)
+        for i in ids[center_refine_select(c, L)]:
+            o.refine_completely(int(i))
+        o.stop_refining()
+    return o
+
+
+def _poisson_setup(g):
+    from poisson_cases import poisson3d_solution
+
+    slots = g.slot_ids()[: g.n_local]
+    c, _ = g.geometry(slots)
+    rhs = g.fields["rhs"] if "rhs" in g.fields else g.add_field("rhs", np.float64, False)
+    sol = g.fields["solution"] if "solution" in g.fields else g.add_field("solution", np.float64, False)
+    rhs.set(-(81.0 / 16.0) * poisson3d_solution(c))
+    sol.set(np.zeros(slots.size))
+    return slots
+
+
+PO_STATE = ("solution", "best_solution", "p0", "p1", "r0", "r1", "A_dot_p0")
+
+
+def sc_poisson(rank, world):
+    """BASELINE config 4's multi-rank path (poisson_solve.hpp:251-522): per
+    iteration the p0 / p1 halo (284) and the global sums (349, 486) across
+    real processes, boundary-spanning face factors (cache_system_info
+    827-971) - on the poisson3d mesh at 16^3 refined twice, 1 / 5 / 20 fixed
+    iterations against the one-rank oracle at test_gpu_poisson.py's
+    tolerances, and the poisson3d.cpp:227 known answer (norm < 0.35 after
+    the default solve) on its own 8^3 mesh."""
+    import dccrg_amd
+    from oracle import oracle as O
+    from poisson_cases import level0_avg_norm, poisson3d_lengths
+
+    res = {}
+    g, leaves = _poisson_mesh(16, world, balance=True)
+    o = _poisson_oracle(16)
+    oid, _ = o.cells()
+    res["mesh"] = bool(np.array_equal(oid, leaves))
+    res["spans_ranks"] = g.counts["outer"] > 0 and len(g.remote_cells()) > 0
+    for iters, tol in ((1, 1e-13), (5, 1e-11), (20, 1e-8)):
+        slots = _poisson_setup(g)
+        it, resid = dccrg_amd.Poisson_Solve(iters, iters).solve(slots, g)
+        mine = {nm: dict(zip(slots.tolist(), (g.fields["solution"] if nm == "solution" else
+                                             dccrg_amd.Poisson_Solve.field(g, nm)).get(0, slots.size).tolist()))
+                for nm in PO_STATE}
+        allst = _gather(mine)
+        ok = True
+        if rank == 0:
+            from poisson_cases import poisson3d_solution
+
+            c, _ = o.geometry(oid)
+            o.po_set(oid, -(81.0 / 16.0) * poisson3d_solution(c), np.zeros(oid.size), np.zeros(oid.size, np.int32))
+            oit, ores = o.po_solve(max_iterations=iters, min_iterations=iters)
+            ok = it == oit == iters and abs(resid - ores) <= 1e-10 * abs(ores)
+            exp = o.po_get(oid)
+            for nm in PO_STATE:
+                d = {}
+                for part in allst:
+                    d.update(part[nm])
+                got = np.array([d[int(i)] for i in oid])
+                e = exp[:, O.Grid.PO_FIELDS.index(nm)]
+                t = 1e-12 if nm in ("solution", "best_solution") else tol
+                ok = ok and float(np.max(np.abs(got - e))) <= t * max(float(np.max(np.abs(e))), 1e-300)
+        # every rank ends with the same residual and iteration count (the
+        # global sums are identical on all ranks)
+        ok = ok and len({(i, r) for i, r in _gather((it, resid))}) == 1
+        res[f"iters_{iters}"] = bool(ok)
+    g.close()
+    # poisson3d.cpp:194-227: the default solver to convergence, PASSED iff norm < 0.35
+    g, leaves = _poisson_mesh(8, world, balance=True)
+    slots = _poisson_setup(g)
+    it, _ = dccrg_amd.Poisson_Solve().solve(slots, g)
+    sol = _gather(dict(zip(slots.tolist(), g.fields["solution"].get(0, slots.size).tolist())))
+    res["kat"] = True
+    if rank == 0:
+        d = {}
+        for part in sol:
+            d.update(part)
+        c, L = _poisson_oracle(8).geometry(leaves)
+        norm = level0_avg_norm(leaves, np.array([d[int(i)] for i in leaves]), c, L, 8, poisson3d_lengths(8))
+        res["kat"] = bool(norm < 0.35)
+        res["norm"] = norm
+    g.close()
+    return res
+
+
 SCENARIOS = {
-    2: ["sc_config1", "sc_gol_explicit", "sc_rcb"],
+    2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
-        "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable"],
+        "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable", "sc_poisson"],
 }
 
 
@@ -849,6 +964,11 @@ def test_unrefine_across_ranks(transport_results):
 
 def test_advection_adapt_across_ranks(transport_results):
     _check(transport_results, "sc_advection_adapt", ["mesh", "bitwise", "mesh_migrate", "bitwise_migrate"])
+
+
+def test_poisson_distributed(transport_results):
+    """Config 4 across 2 and 3 real processes (sc_poisson runs at both)."""
+    _check(transport_results, "sc_poisson", ["mesh", "spans_ranks", "iters_1", "iters_5", "iters_20", "kat"])
 
 
 def test_save_grid_data_three_ranks(transport_results):

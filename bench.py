@@ -42,7 +42,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--base", type=int, default=128, help="level-0 cells per dimension per GPU")
+    p.add_argument("--base", type=int, default=None,
+                   help="level-0 cells per dimension per GPU (default 128; poisson 256)")
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -87,10 +88,18 @@ def cpu_baseline(workload, seconds):
         outs.append(json.loads(o.strip().splitlines()[-1]))
     total = sum(r["cells"] * r["steps"] / r["seconds"] for r in outs)
     per_core = [r["cells"] * r["steps"] / r["seconds"] for r in outs]
+    nproc = os.cpu_count() or cores
     return dict(value=total, unit="cell-updates/s", cores=cores, kind="port",
                 sample=f"oracle restatement ({outs[0]['sample']}, {outs[0]['cells']} cells) x {cores} processes, "
                        f"~{seconds:.0f} s each; per core {min(per_core):.3g}-{max(per_core):.3g} cell-updates/s",
-                nproc=os.cpu_count(), affinity=avail, cpu_model=cpu_model())
+                cores_note=f"{cores} = this GPU's share of the host (the GPU box allots {CPU_SHARE} cores per GPU; "
+                           f"its worker pools are capped there), not all {nproc} cores: each process is one MPI "
+                           "rank on a per-rank subdomain (the advection sample is config 3 / 256 ranks in size)",
+                per_core_mean=total / cores,
+                extrapolated_all_cores={"value": total / cores * nproc, "cores": nproc,
+                                        "how": "per-core mean x all host cores (assumes linear scaling; "
+                                               "not measured)"},
+                nproc=nproc, affinity=avail, cpu_model=cpu_model())
 
 
 def measured_traffic(workload, cells, alg_bytes, world):
@@ -214,13 +223,13 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
     halo between them is a no-op).
 
-    Roofline bytes per leaf and step (SURVEY §8(d) CSR / AMR form): state
-    read + written (8 B), the neighbor CSR (4 B per neighbors_of entry + 4 B
-    row pointer) walked by each of the two phases, and the reference's 72-B
-    payload (Cell_Data::data, array<uint64_t, 9>) written by the collect and
-    read by the spread: 8 + 2 (4 k + 4) + 2 x 72.  The per-gather count
-    (every neighbor's parent and state, the siblings' lists) is reported
-    beside it as `logical_bytes_per_leaf`, not as HBM traffic."""
+    Roofline bytes per leaf and step: the minimum any implementation moves
+    from HBM - the leaf's state (4 B), its neighbors_of row (4 B per entry +
+    4 B row pointer) and the collected list it writes (data[1..8], 64 B):
+    4 + (4 k + 4) + 64, at or below the PMC-measured traffic.  The
+    per-gather count (every neighbor's parent and state, the siblings'
+    lists) is reported beside it as `logical_bytes_per_leaf`, not as HBM
+    traffic."""
     n = 2048
     g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
     g.set_maximum_refinement_level(1).initialize()
@@ -246,7 +255,12 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     nl = g.n_local
     kbar = g.neighbor_entries("of") / nl
     f1 = float(np.mean(lvl == 1))
-    per_cell = 8 + 2 * (4 * kbar + 4) + 2 * 72
+    # minimal bytes per leaf and step: its state read once (4 B), its
+    # neighbors_of row walked once (4 B per entry + 4 B row pointer) and the
+    # collected list written (data[1..8], 64 B); the state gathers and the
+    # siblings' masks are L2 re-reads.  (Round 2 charged 8 + 2(4k+4) + 2 x 72,
+    # which exceeded the PMC-measured traffic.)
+    per_cell = 4 + (4 * kbar + 4) + 64
     logical = (2 * 16) + (8 + 8 + kbar * 16 + 64) + (16 + 8 + 64 + f1 * (kbar * 12 + 7 * 64) + 4)
     ach = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
@@ -270,7 +284,7 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
 # ---------------------------------------------------------------------------- Poisson (config 4)
 def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """BASELINE config 4: Poisson BiCG (tests/poisson/poisson3d.cpp) on a
-    128^3-base grid per GPU (cell lengths 2pi/128, pi/128, 8pi/128), periodic,
+    256^3-base grid per GPU (cell lengths 2pi/n, pi/n, 8pi/n), periodic,
     refined twice around (pi, pi/2, 4pi); one step = one BiCG iteration over
     every solve cell (min = max = steps iterations, as SURVEY §8(d)).  The
     timed kernels of an iteration run from its first phase to its last, the
@@ -610,6 +624,10 @@ def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
 
 def main():
     a = parse()
+    if a.base is None:
+        # Poisson at 256^3 per GPU: one phase's working set (~1.5 GB) is far
+        # above the 256 MiB Infinity Cache, so its rate is an HBM rate
+        a.base = 256 if a.workload == "poisson" else 128
     import torch
     import torch.distributed as dist
 

@@ -10,7 +10,9 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdccrgx.so")
+# DCCRGX_LIB: another in-tree build of the same library (a paired A/B of two
+# builds, dccrg_amd/build.py `out=`); the default is the product build
+LIB_PATH = os.path.join(HERE, os.path.basename(os.environ.get("DCCRGX_LIB", "libdccrgx.so")))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "dccrgx.h")
 
 _lib = None

@@ -27,15 +27,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, out=None, defines=()):
+    """Compile every source and link OUT.  `out` / `defines` build an
+    experiment variant next to it (e.g. libdccrgx_b.so with -DNAME=1) for a
+    paired A/B; the product always loads OUT."""
+    if out is None and not force and not _stale():
         return OUT
+    out = out or OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
     procs = []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.replace(".hip", ".o"))
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj,
+        obj = obj.replace(".o", f".{os.path.basename(out)}.o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"] + [f"-D{d}" for d in defines] + [
+               "-c", os.path.join(CSRC, src), "-o", obj,
                "-Wall", "-Wno-unused-function", "-Wno-unused-parameter", "-Wno-pass-failed"]
         if verbose:
             print(" ".join(cmd))
@@ -44,14 +50,14 @@ def build(force=False, verbose=False):
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [
         "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     for o in objs:
         os.remove(o)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":

@@ -1390,6 +1390,10 @@ int dccrgx_set_cell_weight(dccrgx_grid* gp, uint64_t cell, double weight) {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 6225-6235: local leaves only
+		// the native partitioner cuts on fixed-point weights: a negative or
+		// non-finite weight has no meaning there
+		DX_REQUIRE(std::isfinite(weight) && weight >= 0 && weight * 65536.0 < 9.2e18,
+		           "cell weight must be finite and non-negative");
 		g.weights[cell] = weight;
 		return 0;
 	});

@@ -517,7 +517,13 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			g.weights.erase(w);
 			for (uint64_t c : ch) g.weights[c] = wv;
 		}
-		g.pins.erase(S[i]);
+		// children inherit their parent's pin (10239-10251)
+		auto pn = g.pins.find(S[i]);
+		if (pn != g.pins.end()) {
+			const int pv = pn->second;
+			g.pins.erase(pn);
+			for (uint64_t c : ch) g.pins[c] = pv;
+		}
 	}
 	std::sort(created.begin(), created.end());
 

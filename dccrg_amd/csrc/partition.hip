@@ -145,6 +145,7 @@ void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& 
 	uint64_t cmax = 0;
 	for (int d = 0; d < 3; d++) cmax = std::max(cmax, 2 * g.m.glen[d]);
 	DX_REQUIRE(bits_for(cmax) + id_bits <= 64, "grid too large for the partitioner's 64-bit keys");
+	DX_REQUIRE(cmax < (uint64_t(1) << 32), "grid too large for the partitioner's 32-bit centers");
 
 	DBuf<uint32_t> c2;
 	DBuf<int32_t> lo, hi;

@@ -131,7 +131,11 @@ inline bool is_named_datatype(MPI_Datatype t) {
 
 // a Cell_Data that is not trivially copyable (e.g. std::vector members,
 // tests/variable_data_size) is serialized with MPI_Pack over the datatype
-// it describes and lives on the device as a variable-size field
+// it describes and lives on the device as a variable-size field.  Limit: a
+// cell is packed once, with sender == receiver == this rank, and that one
+// byte string goes to every peer (the reference asks get_mpi_datatype per
+// destination); a Cell_Data whose datatype depends on the peer is not
+// supported.
 template <class T>
 void pack_cell(T& c, uint64_t cell, int sender, int receiver, int hood, MPI_Comm comm, std::vector<char>& out) {
 	auto dt = cell_datatype(c, cell, sender, receiver, false, hood, 0);
@@ -162,8 +166,19 @@ void unpack_cell(T& c, uint64_t cell, int sender, int receiver, int hood, MPI_Co
 		                         " whose datatype holds " + std::to_string(need) + " (size its data first)");
 	}
 	int pos = 0;
-	if (bytes)
+	if (bytes && size_t(need) > bytes) {
+		// a shorter message than the receiving datatype describes: the
+		// reference's MPI_Irecv fills only the bytes that arrived and leaves the
+		// rest of the object as it was, so the object's own packed bytes are
+		// overlaid with what arrived and unpacked whole
+		std::vector<char> full(static_cast<size_t>(need));
+		int at = 0;
+		MPI_Pack(std::get<0>(dt), std::get<1>(dt), t, full.data(), need, &at, comm);
+		std::memcpy(full.data(), in, bytes);
+		MPI_Unpack(full.data(), at, &pos, std::get<0>(dt), std::get<1>(dt), t, comm);
+	} else if (bytes) {
 		MPI_Unpack(const_cast<char*>(in), int(bytes), &pos, std::get<0>(dt), std::get<1>(dt), t, comm);
+	}
 	if (!named) MPI_Type_free(&t);
 }
 

@@ -3,6 +3,9 @@
 # expects dccrg_amd/libdccrgx_base.so and dccrg_amd/libdccrgx_nt.so (the two
 # variants, built here beforehand); prints ms/step, kernel ms/step, roofline frac.
 cd "${GRAFT_REPO_ROOT:-.}"
+# the library built from the committed sources is restored whatever happens
+cp dccrg_amd/libdccrgx.so /tmp/libdccrgx_orig.so || exit 1
+trap 'cp /tmp/libdccrgx_orig.so dccrg_amd/libdccrgx.so' EXIT
 WL=${1:-"gol scalability"}
 ROUNDS=${2:-2}
 for round in $(seq "$ROUNDS"); do
@@ -13,4 +16,3 @@ for v in base nt; do
   done
 done
 done
-cp dccrg_amd/libdccrgx_nt.so dccrg_amd/libdccrgx.so

@@ -2,7 +2,9 @@
 // in an exception guard and returns a status code.
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -513,6 +515,43 @@ static void gol_step_impl(Grid& g, Field& f, int region) {
 	}
 	k_time_end(g);
 }
+
+#if DCCRGX_ALLOC_SKEW
+unsigned alloc_skew_next() {
+	static unsigned k = 0;
+	return (k++ * 7u) % 31u + 1u;
+}
+void alloc_skew_note(const void* raw, size_t bytes, size_t skew) {
+	if (bytes >= (size_t(64) << 20))
+		std::fprintf(stderr, "[skew] base %p (mod 2 MiB %zu) bytes %zu skew %zu\n", raw,
+		             size_t(reinterpret_cast<uintptr_t>(raw) & ((size_t(2) << 20) - 1)), bytes, skew);
+}
+#endif
+
+#if DCCRGX_PHASE_TIMING
+namespace {
+struct PhaseTable {
+	std::map<std::string, std::pair<double, long>> t;
+	~PhaseTable() {
+		for (auto& kv : t)
+			std::fprintf(stderr, "[phase] %-28s %10.3f ms total %7ld calls %9.3f ms/call\n", kv.first.c_str(),
+			             kv.second.first * 1e3, kv.second.second, kv.second.first * 1e3 / double(kv.second.second));
+	}
+};
+PhaseTable& phase_table() {
+	static PhaseTable pt;
+	return pt;
+}
+}  // namespace
+double PhaseScope::now() {
+	return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void phase_add(const char* name, double seconds) {
+	auto& e = phase_table().t[name];
+	e.first += seconds;
+	e.second += 1;
+}
+#endif
 
 }  // namespace dccrgx
 
@@ -1791,12 +1830,15 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		size_t s0, s1;
 		region_range(g, region, s0, s1);
 		if (s1 <= s0) return 0;
+		DX_LAPS(g.s_comp);
 		ensure_tiles(g);
+		DX_LAP("step.0_ensure_tiles");
 		k_time_begin(g);
 		// tiles never straddle the inner / outer runs
 		if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
 		if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
 		k_time_end(g);
+		DX_LAP("step.1_sweep");
 		return 0;
 	});
 }
@@ -1925,12 +1967,15 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
 		if (counts) counts[0] = counts[1] = counts[2] = 0;
 		if (g.R == 0) return 0;  // 61-63
+		DX_LAPS(g.s_comp);
 		ensure_face(g);
+		DX_LAP("chk.0_face");
 		const size_t n = g.n_local;
 		DBuf<uint8_t> band;
 		band.alloc(n + 1);
 		k_adv_bands(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p, n, diff_increase,
 		            diff_threshold, unrefine_sensitivity, band.p, g.s_comp);
+		DX_LAP("chk.1_bands");
 		uint64_t nref = 0, nkeep = 0, nunref = 0;
 		// decide one family from its local members (bands bb, ids ii, k of
 		// them): dont_unrefine (2679-2733) when any member is kept or refined,
@@ -2018,7 +2063,9 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			}
 			flush();
 		}
+		DX_LAP("chk.2_requests");
 		for (auto& kv : partial) decide(kv.second.first.data(), kv.second.second.data(), kv.second.first.size());
+		DX_LAP("chk.3_partial_families");
 		if (counts) {
 			counts[0] = nref;
 			counts[1] = nkeep;
@@ -2039,7 +2086,9 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		DX_REQUIRE(g.initialized, "not initialized");
 		const double* cf[7];
 		adv_fields(g, fids, cf);
+		DX_LAPS(g.s_comp);
 		g.last_new_cells = stop_refining_impl(g);
+		DX_LAP("adapt.1_stop_refining");
 		hipStream_t s = g.s_comp;
 		double* f[7];
 		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
@@ -2075,8 +2124,10 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 			upload(dc, cidx, s);
 			k_adv_parent_density(f[0], dp.p, dc.p, (const double*)field(g, fids[0]).removed.p, pslot.size(), s);
 		}
+		DX_LAP("adapt.2_parents");
 		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
 		HIP_CHECK(hipStreamSynchronize(s));
+		DX_LAP("adapt.3_reset");
 		// transfer_all_data: every field of the seven in this halo
 		bool saved[7];
 		for (int k = 0; k < 7; k++) {
@@ -2092,6 +2143,7 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 			throw;
 		}
 		for (int k = 0; k < 7; k++) field(g, fids[k]).transfer = saved[k];
+		DX_LAP("adapt.4_halo");
 		if (out) {
 			out[0] = g.last_new_cells.size();
 			out[1] = rm.size();

@@ -45,38 +45,106 @@ struct Error : std::runtime_error {
 		if (!(cond)) throw ::dccrgx::Error(DCCRGX_EINVAL, std::string(msg)); \
 	} while (0)
 
+// Host phase timing of an analysis build (-DDCCRGX_PHASE_TIMING=1, never the
+// product build): DX_PHASE("name", stream) times the enclosing scope, the
+// stream drained at its end; the totals go to stderr at exit.
+#if DCCRGX_PHASE_TIMING
+void phase_add(const char* name, double seconds);
+struct PhaseScope {
+	const char* name;
+	hipStream_t s;
+	double t0;
+	static double now();
+	PhaseScope(const char* n, hipStream_t st) : name(n), s(st), t0(now()) {}
+	~PhaseScope() {
+		(void)hipStreamSynchronize(s);
+		phase_add(name, now() - t0);
+	}
+};
+// laps: DX_LAPS(stream) starts a lap clock in this scope, DX_LAP("name")
+// books the time since the previous lap (stream drained) under name
+struct PhaseLaps {
+	hipStream_t s;
+	double t;
+	explicit PhaseLaps(hipStream_t st) : s(st), t(PhaseScope::now()) {}
+	void lap(const char* name) {
+		(void)hipStreamSynchronize(s);
+		const double n = PhaseScope::now();
+		phase_add(name, n - t);
+		t = n;
+	}
+};
+#define DX_PHASE_CAT2(a, b) a##b
+#define DX_PHASE_CAT(a, b) DX_PHASE_CAT2(a, b)
+#define DX_PHASE(name, s) ::dccrgx::PhaseScope DX_PHASE_CAT(dx_phase_, __LINE__)(name, s)
+#define DX_LAPS(s) ::dccrgx::PhaseLaps dx_laps_(s)
+#define DX_LAP(name) dx_laps_.lap(name)
+#else
+#define DX_PHASE(name, s) \
+	do {                  \
+	} while (0)
+#define DX_LAPS(s) \
+	do {           \
+	} while (0)
+#define DX_LAP(name) \
+	do {             \
+	} while (0)
+#endif
+
 // Owning device buffer.
+#if DCCRGX_ALLOC_SKEW
+// experiment build: large buffers start at a per-allocation skew (a multiple
+// of 256 B) past the allocator's base, so equal-index elements of different
+// arrays do not share L2 set alignment
+unsigned alloc_skew_next();
+void alloc_skew_note(const void* raw, size_t bytes, size_t skew);
+#endif
 template <class T>
 struct DBuf {
 	T* p = nullptr;
 	size_t n = 0;
+	void* raw = nullptr;
 	DBuf() = default;
 	DBuf(const DBuf&) = delete;
 	DBuf& operator=(const DBuf&) = delete;
-	DBuf(DBuf&& o) noexcept : p(o.p), n(o.n) {
+	DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), raw(o.raw) {
 		o.p = nullptr;
 		o.n = 0;
+		o.raw = nullptr;
 	}
 	DBuf& operator=(DBuf&& o) noexcept {
 		if (this != &o) {
 			release();
 			p = o.p;
 			n = o.n;
+			raw = o.raw;
 			o.p = nullptr;
 			o.n = 0;
+			o.raw = nullptr;
 		}
 		return *this;
 	}
 	~DBuf() { release(); }
 	void release() {
-		if (p) (void)hipFree(p);
+		if (raw) (void)hipFree(raw);
 		p = nullptr;
 		n = 0;
+		raw = nullptr;
 	}
 	void alloc(size_t count) {
 		if (count == n && p) return;
 		release();
-		if (count) HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+		if (count) {
+			size_t skew = 0;
+#if DCCRGX_ALLOC_SKEW
+			if (count * sizeof(T) >= (size_t(1) << 20)) skew = size_t(alloc_skew_next()) * 4352u;
+#endif
+			HIP_CHECK(hipMalloc(&raw, count * sizeof(T) + skew));
+#if DCCRGX_ALLOC_SKEW
+			if (skew) alloc_skew_note(raw, count * sizeof(T), skew);
+#endif
+			p = reinterpret_cast<T*>(static_cast<char*>(raw) + skew);
+		}
 		n = count;
 	}
 	// grow-only (keeps the allocation when it is large enough)
@@ -86,6 +154,7 @@ struct DBuf {
 	void swap(DBuf& o) {
 		std::swap(p, o.p);
 		std::swap(n, o.n);
+		std::swap(raw, o.raw);
 	}
 };
 

@@ -463,6 +463,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (g.size > 1) comm_require(g, "stop_refining");
 	const int nh = int(g.hood.size() / 3);
 	hipStream_t s = g.s_comp;
+	DX_LAPS(s);
 	for (auto& f : g.fields) {
 		f.removed.release();
 		f.rm_off.release();
@@ -473,12 +474,14 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	std::vector<uint64_t> D = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_refine_cells))));
 	g.dont_refine_cells.clear();
 	if (!D.empty()) close_set(g, D, true);
+	DX_LAP("sr.1_override_refines");
 	std::vector<uint64_t> mine;
 	for (uint64_t c : sorted_unique(vec(g.refine_requests)))
 		if (!sorted_contains(D, c)) mine.push_back(c);
 	g.refine_requests.clear();
 	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
 	if (!S.empty()) close_set(g, S, false);
+	DX_LAP("sr.2_induce_refines");
 
 	// unrefines: one family per requested parent
 	std::vector<uint64_t> req_par;
@@ -500,6 +503,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	for (size_t i = 0; i < cand.size(); i++)
 		if (ok[i]) fmine.push_back(cand[i]);
 	const std::vector<uint64_t> F = union_sorted(comm_allgather_u64(g, fmine));
+	DX_LAP("sr.3_override_unrefines");
 	if (S.empty() && F.empty()) return {};
 
 	// local refined cells -> the new local cells; weights follow (6199-6200)
@@ -526,6 +530,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		}
 	}
 	std::sort(created.begin(), created.end());
+	DX_LAP("sr.4_created");
 
 	// merged families: the children's payloads to the parent's new process
 	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
@@ -668,12 +673,15 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		}
 	}
 
+	DX_LAP("sr.5_removed_payloads");
 	Mesh known, nm;
 	mesh_materialize(g, known);
 	nm.implicit = false;
 	nm.bp = known.bp;
 	k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s);
+	DX_LAP("sr.6_apply");
 	rebuild(g, nm);
+	DX_LAP("sr.7_rebuild");
 	return created;
 }
 
@@ -916,10 +924,11 @@ void migration_place_peer(Grid& g, int peer, const uint8_t* buf, size_t bytes) {
 
 // --------------------------------------------------------------------------- game of life, slab planes
 // The structured 26-point sweep needs the cells of a box in raster order.
-// On the initial level-0 grid with the block partition, a rank whose block is
-// whole z-planes holds its planes in slot order [inner planes | outer planes]
-// and receives each neighbor plane as one contiguous run of halo slots, so
-// every region is a set of boxes whose z-1 / z+1 planes are other runs.
+// On a uniform level-0 grid whose ranks hold whole z-planes (the block
+// partition, or any repartition into z-planes) a rank holds its planes in
+// slot order [inner planes | outer planes] and receives each neighbor plane as
+// one contiguous run of halo slots, so every region is a set of boxes whose
+// z-1 / z+1 planes are other runs.
 static int64_t plane_slot(Grid& g, int64_t z) {
 	const int64_t nz = int64_t(g.len[2]);
 	if (z < 0 || z >= nz) {
@@ -938,50 +947,45 @@ bool gol_slab_plan(Grid& g, std::vector<GolBox>& inner, std::vector<GolBox>& out
 	outer.clear();
 	if (g.R != 0 || g.hood_len != 1 || g.len[0] % 256 != 0) return false;
 	const uint64_t plane = g.len[0] * g.len[1];
-	uint64_t f = 0, c = 0;
-	if (g.mesh.implicit) {
-		g.mesh.bp.range(uint64_t(g.rank), f, c);
-	} else {
-		// an explicit uniform mesh (e.g. after a repartition): the own cells
-		// must be one contiguous id range
-		const auto& sid = slot_ids_host(g);
-		if (!g.n_local) return false;
-		const auto mm = std::minmax_element(sid.begin(), sid.begin() + ptrdiff_t(g.n_local));
-		f = *mm.first;
-		c = g.n_local;
-		if (*mm.second - f + 1 != c) return false;
-	}
-	if (c == 0 || (f - 1) % plane != 0 || c % plane != 0) return false;
-	const int64_t z0 = int64_t((f - 1) / plane), z1 = z0 + int64_t(c / plane);
-	if (g.size == 1 && g.n_outer == 0 && g.n_slots == g.n_local) {
-		inner.push_back(GolBox{0, uint64_t(z1 - z0), -3, -3});  // -3: the kernel's own periodic wrap
+	const int64_t nz = int64_t(g.len[2]);
+	if (!g.n_local || g.n_local % plane != 0) return false;
+	if (g.size == 1 && g.n_outer == 0 && g.n_slots == g.n_local && g.n_local == plane * uint64_t(nz)) {
+		inner.push_back(GolBox{0, uint64_t(nz), -3, -3});  // -3: the kernel's own periodic wrap
 		return true;
 	}
-	std::vector<int64_t> sl(size_t(z1 - z0 + 2));
-	for (int64_t z = z0 - 1; z <= z1; z++) {
-		sl[size_t(z - z0 + 1)] = plane_slot(g, z);
-		if (sl[size_t(z - z0 + 1)] == -1) return false;
+	// the own cells must be whole planes, each one run of local slots of one
+	// class (inner or outer); any number of z runs (e.g. a rank holding two
+	// slabs after a repartition)
+	std::vector<int64_t> own(size_t(nz), -1);
+	uint64_t owned = 0;
+	for (int64_t z = 0; z < nz; z++) {
+		const int64_t s0 = plane_slot(g, z);
+		if (s0 < 0 || uint64_t(s0) + plane > g.n_local) continue;
+		if ((uint64_t(s0) < g.n_inner) != (uint64_t(s0) + plane - 1 < g.n_inner)) return false;
+		own[size_t(z)] = s0;
+		owned++;
 	}
-	auto slot = [&](int64_t z) { return sl[size_t(z - z0 + 1)]; };
-	// inner planes: a run of planes stored contiguously from slot 0
-	int64_t zi0 = -1, zi1 = -1;
-	for (int64_t z = z0; z < z1; z++) {
-		const int64_t s = slot(z);
-		if (size_t(s) < g.n_inner) {
-			if (zi0 < 0) zi0 = z;
-			zi1 = z + 1;
+	if (owned * plane != g.n_local) return false;
+	auto slot = [&](int64_t z) -> int64_t {
+		return (z >= 0 && z < nz && own[size_t(z)] >= 0) ? own[size_t(z)] : plane_slot(g, z);
+	};
+	// boxes: runs of inner planes consecutive in z and in slots; every outer
+	// plane alone; z-1 / z+1 of a box: another run (local or halo) or nothing
+	for (int64_t z = 0; z < nz;) {
+		if (own[size_t(z)] < 0) {
+			z++;
+			continue;
 		}
+		const bool in = uint64_t(own[size_t(z)]) < g.n_inner;
+		int64_t e = z + 1;
+		while (in && e < nz && own[size_t(e)] >= 0 && uint64_t(own[size_t(e)]) < g.n_inner &&
+		       own[size_t(e)] == own[size_t(e - 1)] + int64_t(plane))
+			e++;
+		const int64_t lo = slot(z - 1), hi = slot(e);
+		if (lo == -1 || hi == -1) return false;  // a neighbor plane not held as one run
+		(in ? inner : outer).push_back(GolBox{uint64_t(own[size_t(z)]), uint64_t(e - z), lo, hi});
+		z = e;
 	}
-	if (zi0 >= 0) {
-		if (slot(zi0) != 0 || uint64_t(zi1 - zi0) * plane != g.n_inner) return false;
-		for (int64_t z = zi0; z < zi1; z++)
-			if (slot(z) != int64_t(uint64_t(z - zi0) * plane)) return false;
-		inner.push_back(GolBox{0, uint64_t(zi1 - zi0), slot(zi0 - 1), slot(zi1)});
-	} else if (g.n_inner) {
-		return false;
-	}
-	for (int64_t z = z0; z < z1; z++)
-		if (size_t(slot(z)) >= g.n_inner) outer.push_back(GolBox{uint64_t(slot(z)), 1, slot(z - 1), slot(z + 1)});
 	return true;
 }
 

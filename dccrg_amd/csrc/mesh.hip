@@ -195,6 +195,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	hipStream_t s = g.s_comp;
 	const MapCtx& m = g.m;
 	const int nh = int(g.hood.size() / 3);
+	DX_LAPS(s);
 
 	DBuf<uint64_t> old_slot_ids;
 	old_slot_ids.swap(g.slot_ids);
@@ -231,6 +232,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	}
 	const size_t nl = g.n_local;
 	DevMesh dm = g.dm();  // implicit: no table yet (owners by formula)
+	DX_LAP("rb.1_local");
 
 	// 2. inner / outer classification (update_remote_neighbor_info 8992-9095)
 	DBuf<uint32_t> flag, scan;
@@ -254,6 +256,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
 	}
 
+	DX_LAP("rb.2_classify_sort");
 	// 3. neighbor lists of outer cells -> send / receive lists (8590-8752)
 	HaloPlan& H = g.halo;
 	H.send_ids.clear();
@@ -300,6 +303,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		g.extra_remote = extra;
 	}
 	g.peers = H.peers();
+	DX_LAP("rb.3_lists");
 
 	// 4. slots: local | halo (per peer, ascending) | remote neighbors_to-only
 	std::vector<uint64_t> halo;
@@ -328,6 +332,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		upload(H.recv_slots, rs, s);
 	}
 
+	DX_LAP("rb.4_slots_hash");
 	// 5. send slots (ascending id per peer = wire order)
 	std::vector<uint64_t> sids;
 	H.send_off.clear();
@@ -347,6 +352,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		DX_REQUIRE(herr == 0, "internal error: slot of a local, halo or send cell missing from the mesh table");
 	}
 
+	DX_LAP("rb.5_send_slots");
 	// 6. carry field payloads over
 	const DevMesh odm = old.dev(m.last);
 	for (auto& f : g.fields) {
@@ -365,6 +371,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		f.scratch.release();
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
+	DX_LAP("rb.6_carry_fields");
 	g.csr_valid = false;
 	g.face_valid = false;
 	g.tiles_valid = false;
@@ -421,6 +428,7 @@ void ensure_csr(Grid& g) {
 void ensure_face(Grid& g) {
 	if (g.face_valid) return;
 	hipStream_t s = g.s_comp;
+	DX_PHASE("face.build", s);
 	const size_t nl = g.n_local;
 	const DevMesh dm = g.dm();
 	DBuf<uint32_t> cnt;
@@ -446,6 +454,7 @@ void ensure_face(Grid& g) {
 void ensure_tiles(Grid& g) {
 	ensure_face(g);
 	if (g.tiles_valid) return;
+	DX_LAPS(g.s_comp);
 	const int T = g.tile;
 	const TileBuild tb = k_build_tiles(g.face_ptr.p, g.face_ent.p, g.slot_ids.p, g.m, g.morton_slots, g.n_inner,
 	                                   g.n_local, T, g.tstart, g.tell, g.ext_ptr, g.ext, g.ext_pk, g.fine_base, g.tfine,
@@ -454,8 +463,10 @@ void ensure_tiles(Grid& g) {
 	g.n_tiles_outer = tb.n_tiles_outer;
 	g.max_ext = tb.max_ext;
 	g.total_ext = tb.total_ext;
+	DX_LAP("tiles.1_build");
 	k_classify_tiles(g.m, g.tstart.p, g.n_tiles_inner, g.n_tiles_outer, g.slot_ids.p, g.face_ell.p, g.tlists, g.tnb,
 	                 g.tregmeta, g.tcount, g.s_comp);
+	DX_LAP("tiles.2_classify");
 	// records of the irregular tiles for the pipelined tile kernel
 	const size_t nt = g.n_tiles_inner + g.n_tiles_outer, ni = g.tcount[2] + g.tcount[3];
 	const auto ts = download(g.tstart.p, nt + 1, g.s_comp);
@@ -481,6 +492,7 @@ void ensure_tiles(Grid& g) {
 	g.tmeta.release();
 	if (fits && ni) upload(g.tmeta, rec, g.s_comp);
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	DX_LAP("tiles.3_meta");
 	g.tiles_valid = true;
 }
 

@@ -318,12 +318,6 @@ static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, ui
 	}
 }
 
-__global__ void tile_first_ids_kernel(const uint32_t* __restrict__ tstart, const uint64_t* __restrict__ slot_ids,
-                                      size_t nt, uint64_t* __restrict__ out) {
-	for (size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x; t < nt; t += size_t(gridDim.x) * blockDim.x)
-		out[t] = slot_ids[tstart[t]];
-}
-
 __global__ void pack_ext_kernel(const uint32_t* __restrict__ ext, const uint32_t* __restrict__ ax, size_t m,
                                 uint32_t* __restrict__ out) {
 	for (size_t k = blockIdx.x * size_t(blockDim.x) + threadIdx.x; k < m; k += size_t(gridDim.x) * blockDim.x)
@@ -460,39 +454,6 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 		const int run = t < n_tiles_inner ? 0 : 1;
 		(h[t] == 1u ? reg[run] : irr[run]).push_back(uint32_t(t));
 	}
-#if DCCRGX_TILE_ORDER
-	{
-		// sweep order of the regular tiles: 8x8x8 super-cubes of tiles in
-		// Morton order, each swept as eight 8x8 planes of tiles along z, so the
-		// tiles in flight on an XCD at once are one plane (x / y faces shared
-		// between concurrent tiles) and consecutive planes share z faces
-		DBuf<uint64_t> fid;
-		fid.alloc(nt);
-		tile_first_ids_kernel<<<grid_for(nt, 256), 256, 0, s>>>(tstart, slot_ids, nt, fid.p);
-		HIP_CHECK(hipGetLastError());
-		const std::vector<uint64_t> first = download(fid.p, nt, s);
-		auto spread = [](uint64_t v) {
-			uint64_t o = 0;
-			for (int b = 0; b < 16; b++) o |= ((v >> b) & 1ull) << (3 * b);
-			return o;
-		};
-		auto key = [&](uint32_t t) -> uint64_t {
-			uint64_t c[3];
-			const int L = map_indices(m, first[t], c[0], c[1], c[2]);
-			const uint64_t E = uint64_t(8) << (m.R - L);
-			uint64_t tc[3];
-			for (int d = 0; d < 3; d++) tc[d] = c[d] / E;
-			const uint64_t sc = spread(tc[0] >> 3) | (spread(tc[1] >> 3) << 1) | (spread(tc[2] >> 3) << 2);
-			return (uint64_t(L) << 58) | (sc << 9) | ((tc[2] & 7) << 6) | ((tc[1] & 7) << 3) | (tc[0] & 7);
-		};
-		for (int run = 0; run < 2; run++) {
-			std::vector<std::pair<uint64_t, uint32_t>> kv;
-			for (uint32_t t : reg[run]) kv.push_back({key(t), t});
-			std::stable_sort(kv.begin(), kv.end(), [](auto& a, auto& b) { return a.first < b.first; });
-			for (size_t i = 0; i < kv.size(); i++) reg[run][i] = kv[i].second;
-		}
-	}
-#endif
 	std::vector<uint32_t> all;
 	for (auto* v : {&reg[0], &reg[1], &irr[0], &irr[1]}) all.insert(all.end(), v->begin(), v->end());
 	counts[0] = reg[0].size();

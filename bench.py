@@ -484,6 +484,9 @@ def advection_adapt_main(a, dccrg_amd, torch, dist, rank, world, uid):
     st = {"cells": 0, "created": 0, "removed": 0, "step": 0, "t_check": 0.0, "t_adapt": 0.0}
     for _ in range(a.warmup):
         step(st)
+    reset = getattr(dccrg_amd.lib(), "dccrgx_phase_reset", None)  # phase-timing analysis builds only
+    if reset is not None:
+        reset()
     st.update(cells=0, created=0, removed=0, t_check=0.0, t_adapt=0.0)
     el, kms, kn = timed(g, torch, dist, world, lambda: step(st), a.steps)
     mx, sm = reduce_stats(torch, dist, world, [el, float(st["cells"]), kms, float(st["created"]),

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdccrgx.so")
 SOURCES = ["api.hip", "grid.hip", "mesh.hip", "comm.hip", "partition.hip", "build_kernels.hip", "tile_build.hip", "sweep_kernels.hip",
-           "poisson_kernels.hip", "gol_amr.hip", "varfield.hip"]
+           "poisson_kernels.hip", "gol_amr.hip", "varfield.hip", "pool.hip"]
 HEADERS = ["dccrgx_internal.hpp", "dccrgx_grid.hpp", "dccrgx_mapping.hpp", "dccrgx_mesh.hpp", "dccrgx_neighbors.hpp"]
 ARCH = os.environ.get("DCCRGX_ARCH", "gfx950")
 

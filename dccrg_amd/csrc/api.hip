@@ -516,17 +516,6 @@ static void gol_step_impl(Grid& g, Field& f, int region) {
 	k_time_end(g);
 }
 
-#if DCCRGX_ALLOC_SKEW
-unsigned alloc_skew_next() {
-	static unsigned k = 0;
-	return (k++ * 7u) % 31u + 1u;
-}
-void alloc_skew_note(const void* raw, size_t bytes, size_t skew) {
-	if (bytes >= (size_t(64) << 20))
-		std::fprintf(stderr, "[skew] base %p (mod 2 MiB %zu) bytes %zu skew %zu\n", raw,
-		             size_t(reinterpret_cast<uintptr_t>(raw) & ((size_t(2) << 20) - 1)), bytes, skew);
-}
-#endif
 
 #if DCCRGX_PHASE_TIMING
 namespace {
@@ -551,6 +540,7 @@ void phase_add(const char* name, double seconds) {
 	e.first += seconds;
 	e.second += 1;
 }
+void phase_reset() { phase_table().t.clear(); }
 #endif
 
 }  // namespace dccrgx
@@ -585,6 +575,11 @@ static dccrgx_grid* new_grid(int rank, int size, int device) {
 }
 
 extern "C" {
+
+#if DCCRGX_PHASE_TIMING
+// analysis build only: forget the phase totals so far (e.g. after a warm-up)
+void dccrgx_phase_reset(void) { phase_reset(); }
+#endif
 
 const char* dccrgx_last_error(void) { return g_last_error.c_str(); }
 int dccrgx_abi_version(void) { return DCCRGX_ABI_VERSION; }
@@ -1084,10 +1079,18 @@ int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* n
 	});
 }
 
+static void flush_bulk_requests(Grid& g) {
+	g.refine_requests.insert(g.refine_bulk.begin(), g.refine_bulk.end());
+	g.unrefine_requests.insert(g.unrefine_bulk.begin(), g.unrefine_bulk.end());
+	g.refine_bulk.clear();
+	g.unrefine_bulk.clear();
+}
+
 int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
+		flush_bulk_requests(g);
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 2449-2459: only local cells
 		if (map_level(g.m, cell) >= g.R) return 0;                      // 2474-2477: no-op at max level
 		g.refine_requests.insert(cell);
@@ -1105,6 +1108,7 @@ int dccrgx_unrefine_completely(dccrgx_grid* gp, uint64_t cell) {
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
 		if (map_level(g.m, cell) == 0) return 0;
+		flush_bulk_requests(g);
 		uint64_t sib[8];
 		map_siblings(g.m, cell, sib);
 		auto has = [](const std::unordered_set<uint64_t>& v, uint64_t x) { return v.count(x) > 0; };
@@ -1127,6 +1131,7 @@ int dccrgx_dont_unrefine(dccrgx_grid* gp, uint64_t cell) {
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
 		if (map_level(g.m, cell) == 0) return 0;
+		flush_bulk_requests(g);
 		uint64_t sib[8];
 		map_siblings(g.m, cell, sib);
 		for (uint64_t s : sib)
@@ -1145,6 +1150,7 @@ int dccrgx_dont_refine(dccrgx_grid* gp, uint64_t cell) {
 		DX_REQUIRE(g.initialized, "not initialized");
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;
 		if (map_level(g.m, cell) >= g.R) return 0;
+		flush_bulk_requests(g);
 		g.refine_requests.erase(cell);
 		g.dont_refine_cells.insert(cell);
 		return 0;
@@ -2013,13 +2019,15 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			pr.first.push_back(band_v);
 			pr.second.push_back(id);
 		};
+		flush_bulk_requests(g);
 		if (g.unrefine_requests.empty() && n < (size_t(1) << 28)) {
 			// on the device: refine requests, whole-family decisions, partial runs
 			const AdvRequests q = k_adv_requests(g.m, g.slot_ids.p, band.p, n, g.s_comp);
-			g.refine_requests.insert(q.refine.begin(), q.refine.end());  // 2434-2520
+			// 2434-2520 (bulk lists: no set hashing of ~20 K ids per step)
+			g.refine_bulk.insert(g.refine_bulk.end(), q.refine.begin(), q.refine.end());
 			nref = q.refine.size();
 			nkeep = q.kept;
-			g.unrefine_requests.insert(q.unrefine.begin(), q.unrefine.end());
+			g.unrefine_bulk.insert(g.unrefine_bulk.end(), q.unrefine.begin(), q.unrefine.end());
 			nunref = q.unrefine.size();
 			size_t at = 0;
 			for (size_t r = 0; r < q.part_slot.size(); r++) {
@@ -2092,38 +2100,10 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		hipStream_t s = g.s_comp;
 		double* f[7];
 		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
-		// merged parents: the store order of the removed children -> per
-		// parent its eight children in ascending id (children grouped by a
-		// sort on the parent, the parents' slots from the device table)
+		// merged parents (adapter.hpp:260-290): the removed children grouped by
+		// parent on the device, each parent's mean of its eight children
 		const auto& rm = g.removed_ids_h;
-		if (!rm.empty()) {
-			std::vector<std::pair<uint64_t, uint32_t>> pc(rm.size());
-			for (size_t i = 0; i < rm.size(); i++) pc[i] = {map_parent(g.m, rm[i]), uint32_t(i)};
-			std::sort(pc.begin(), pc.end());
-			std::vector<uint64_t> parents;
-			std::vector<int32_t> cidx;
-			for (size_t a = 0; a < pc.size();) {
-				size_t b = a;
-				while (b < pc.size() && pc[b].first == pc[a].first) b++;
-				uint64_t ch[8];
-				map_all_children(g.m, pc[a].first, ch);
-				int32_t c8[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-				for (size_t j = a; j < b; j++)
-					for (int k = 0; k < 8; k++)
-						if (ch[k] == rm[pc[j].second]) c8[k] = int32_t(pc[j].second);
-				for (int32_t v : c8) DX_REQUIRE(v >= 0, "a removed child's payload is missing");
-				parents.push_back(pc[a].first);
-				cidx.insert(cidx.end(), c8, c8 + 8);
-				a = b;
-			}
-			std::vector<int32_t> pslot(parents.size());
-			lookup_batch(g, parents.data(), parents.size(), nullptr, pslot.data());
-			for (int32_t sl : pslot) DX_REQUIRE(sl >= 0 && size_t(sl) < g.n_local, "merged parent is not local");
-			DBuf<int32_t> dp, dc;
-			upload(dp, pslot, s);
-			upload(dc, cidx, s);
-			k_adv_parent_density(f[0], dp.p, dc.p, (const double*)field(g, fids[0]).removed.p, pslot.size(), s);
-		}
+		k_adv_merge_parents(g.m, g.dm(), g.n_local, rm, f[0], (const double*)field(g, fids[0]).removed.p, s);
 		DX_LAP("adapt.2_parents");
 		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
 		HIP_CHECK(hipStreamSynchronize(s));

@@ -404,25 +404,37 @@ __global__ void face_lists_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 	}
 }
 
-__global__ void remap_field_kernel(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, DevMesh newM,
-                                   uint8_t* new_data, size_t elem) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n_old; i += size_t(gridDim.x) * blockDim.x) {
-		const int32_t s = dm_slot(newM, old_ids[i]);
-		if (s < 0) continue;
-		for (size_t b = 0; b < elem; b++) new_data[size_t(s) * elem + b] = old_data[i * elem + b];
+// where each slot of a rebuilt mesh takes its payload from (rebuild step 6):
+// the old local slot of the same cell, else (a new local cell absent from the
+// old mesh: a refined cell's child) the old slot of its parent, else nothing
+__global__ void carry_src_kernel(const uint64_t* __restrict__ slot_ids, size_t n_slots, size_t nl, MapCtx m,
+                                 DevMesh oldM, size_t old_n_local, int32_t* __restrict__ src) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n_slots; s += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = slot_ids[s];
+		const int32_t o = dm_slot(oldM, id);
+		int32_t r = -1;
+		if (o >= 0) {
+			if (size_t(o) < old_n_local) r = o;
+		} else if (s < nl) {
+			const uint64_t p = map_parent(m, id);
+			if (p != error_cell && p != id) r = dm_slot(oldM, p);
+		}
+		src[s] = r;
 	}
 }
 
-__global__ void parent_fill_kernel(uint8_t* data, const uint64_t* slot_ids, size_t n, MapCtx m, const uint8_t* old_data,
-                                   DevMesh oldM, size_t elem) {
-	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
-		const uint64_t id = slot_ids[s];
-		if (dm_slot(oldM, id) >= 0) continue;
-		const uint64_t p = map_parent(m, id);
-		if (p == error_cell || p == id) continue;
-		const int32_t ps = dm_slot(oldM, p);
-		if (ps < 0) continue;
-		for (size_t b = 0; b < elem; b++) data[s * elem + b] = old_data[size_t(ps) * elem + b];
+template <class T>
+__global__ void gather_rows_kernel(const T* __restrict__ old, const int32_t* __restrict__ src, size_t n,
+                                   T* __restrict__ out) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x)
+		if (src[s] >= 0) out[s] = old[src[s]];
+}
+
+__global__ void gather_bytes_kernel(const uint8_t* __restrict__ old, const int32_t* __restrict__ src, size_t n,
+                                    size_t elem, uint8_t* __restrict__ out) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * elem; i += size_t(gridDim.x) * blockDim.x) {
+		const size_t s = i / elem;
+		if (src[s] >= 0) out[i] = old[size_t(src[s]) * elem + (i - s * elem)];
 	}
 }
 
@@ -881,19 +893,26 @@ void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, s
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_remap_field(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const DevMesh& newM,
-                   uint8_t* new_data, size_t elem, hipStream_t s) {
-	if (!n_old) return;
-	remap_field_kernel<<<grid_for(n_old, 256), 256, 0, s>>>(old_data, old_ids, n_old, newM, new_data, elem);
+void k_carry_src(const uint64_t* slot_ids, size_t n_slots, size_t nl, const MapCtx& m, const DevMesh& oldM,
+                 size_t old_n_local, int32_t* src, hipStream_t s) {
+	if (!n_slots) return;
+	carry_src_kernel<<<grid_for(n_slots, 256), 256, 0, s>>>(slot_ids, n_slots, nl, m, oldM, old_n_local, src);
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const MapCtx& m, const uint8_t* old_data,
-                   const DevMesh& oldM, size_t elem, hipStream_t s) {
-	if (!n) return;
-	parent_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(data, slot_ids, n, m, old_data, oldM, elem);
+void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t elem, uint8_t* out, hipStream_t s) {
+	if (!n || !elem) return;
+	if (elem == 4)
+		gather_rows_kernel<uint32_t><<<grid_for(n, 256), 256, 0, s>>>((const uint32_t*)old_data, src, n, (uint32_t*)out);
+	else if (elem == 8)
+		gather_rows_kernel<uint64_t><<<grid_for(n, 256), 256, 0, s>>>((const uint64_t*)old_data, src, n, (uint64_t*)out);
+	else if (elem == 16)
+		gather_rows_kernel<uint4><<<grid_for(n, 256), 256, 0, s>>>((const uint4*)old_data, src, n, (uint4*)out);
+	else
+		gather_bytes_kernel<<<grid_for(n * elem, 256), 256, 0, s>>>(old_data, src, n, elem, out);
 	HIP_CHECK(hipGetLastError());
 }
+
 
 size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s) {
 	if (!nrows) return 0;

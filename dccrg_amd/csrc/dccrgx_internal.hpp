@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <stdexcept>
@@ -50,6 +51,7 @@ struct Error : std::runtime_error {
 // stream drained at its end; the totals go to stderr at exit.
 #if DCCRGX_PHASE_TIMING
 void phase_add(const char* name, double seconds);
+void phase_reset();
 struct PhaseScope {
 	const char* name;
 	hipStream_t s;
@@ -91,26 +93,39 @@ struct PhaseLaps {
 	} while (0)
 #endif
 
-// Owning device buffer.
-#if DCCRGX_ALLOC_SKEW
-// experiment build: large buffers start at a per-allocation skew (a multiple
-// of 256 B) past the allocator's base, so equal-index elements of different
-// arrays do not share L2 set alignment
-unsigned alloc_skew_next();
-void alloc_skew_note(const void* raw, size_t bytes, size_t skew);
-#endif
+// Owning device buffer.  Buffers of 1 MiB and more start at a rotating skew
+// (1..31 x 4352 B, a multiple of 256 B) past the allocator's 2-MiB-aligned
+// base, so the same element index of different field arrays does not fall on
+// the same DRAM channel / L2 set alignment: paired A/B on config 3 (three
+// boxes) 0.1893 / 0.1884 / 0.1904 -> 0.1870 / 0.1864 / 0.1866 ms per sweep.
+inline unsigned alloc_skew_next() {
+	static std::atomic<unsigned> k{0};
+	return (k.fetch_add(1u) * 7u) % 31u + 1u;
+}
+// Device memory of every DBuf comes from a process-wide caching pool
+// (pool.hip): a released block is kept and handed to a later allocation of a
+// similar size instead of hipFree (which drains the whole device: ~0.08 ms per
+// call, ~2.5 K calls in 20 adaptive steps of config 3).  A block released
+// while work that uses it may still be queued is only reused after a device
+// synchronisation, the same ordering hipFree gave.  `bytes` is the block's
+// capacity (what pool_free must be given back).
+void* pool_alloc(size_t bytes, size_t& capacity);
+void pool_free(void* raw, size_t capacity);
+
 template <class T>
 struct DBuf {
 	T* p = nullptr;
 	size_t n = 0;
 	void* raw = nullptr;
+	size_t cap = 0;
 	DBuf() = default;
 	DBuf(const DBuf&) = delete;
 	DBuf& operator=(const DBuf&) = delete;
-	DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), raw(o.raw) {
+	DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), raw(o.raw), cap(o.cap) {
 		o.p = nullptr;
 		o.n = 0;
 		o.raw = nullptr;
+		o.cap = 0;
 	}
 	DBuf& operator=(DBuf&& o) noexcept {
 		if (this != &o) {
@@ -118,31 +133,28 @@ struct DBuf {
 			p = o.p;
 			n = o.n;
 			raw = o.raw;
+			cap = o.cap;
 			o.p = nullptr;
 			o.n = 0;
 			o.raw = nullptr;
+			o.cap = 0;
 		}
 		return *this;
 	}
 	~DBuf() { release(); }
 	void release() {
-		if (raw) (void)hipFree(raw);
+		if (raw) pool_free(raw, cap);
 		p = nullptr;
 		n = 0;
 		raw = nullptr;
+		cap = 0;
 	}
 	void alloc(size_t count) {
 		if (count == n && p) return;
 		release();
 		if (count) {
-			size_t skew = 0;
-#if DCCRGX_ALLOC_SKEW
-			if (count * sizeof(T) >= (size_t(1) << 20)) skew = size_t(alloc_skew_next()) * 4352u;
-#endif
-			HIP_CHECK(hipMalloc(&raw, count * sizeof(T) + skew));
-#if DCCRGX_ALLOC_SKEW
-			if (skew) alloc_skew_note(raw, count * sizeof(T), skew);
-#endif
+			const size_t skew = count * sizeof(T) >= (size_t(1) << 20) ? size_t(alloc_skew_next()) * 4352u : 0;
+			raw = pool_alloc(count * sizeof(T) + skew, cap);
 			p = reinterpret_cast<T*>(static_cast<char*>(raw) + skew);
 		}
 		n = count;
@@ -155,6 +167,7 @@ struct DBuf {
 		std::swap(p, o.p);
 		std::swap(n, o.n);
 		std::swap(raw, o.raw);
+		std::swap(cap, o.cap);
 	}
 };
 
@@ -379,6 +392,10 @@ struct Grid {
 	std::string lb_method = "RCB";                 // set_load_balancing_method (8223); default 7082
 	std::unordered_set<uint64_t> refine_requests;      // refine_completely 2434
 	std::unordered_set<uint64_t> unrefine_requests;    // unrefine_completely 2560 (one sibling per family)
+	// requests made in bulk by the device check_for_adaptation: plain lists,
+	// merged into the sets above by flush_bulk_requests() before any call
+	// that consults the sets, and read directly by stop_refining
+	std::vector<uint64_t> refine_bulk, unrefine_bulk;
 	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
 	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
 	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)
@@ -563,10 +580,9 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
                       int pass, hipStream_t s);
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
                   const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s);
-void k_remap_field(const uint8_t* old_data, const uint64_t* old_ids, size_t n_old, const DevMesh& newM,
-                   uint8_t* new_data, size_t elem, hipStream_t s);
-void k_parent_fill(uint8_t* data, const uint64_t* slot_ids, size_t n, const MapCtx& m, const uint8_t* old_data,
-                   const DevMesh& oldM, size_t elem, hipStream_t s);
+void k_carry_src(const uint64_t* slot_ids, size_t n_slots, size_t nl, const MapCtx& m, const DevMesh& oldM,
+                 size_t old_n_local, int32_t* src, hipStream_t s);
+void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t elem, uint8_t* out, hipStream_t s);
 // ghost region: the level-0 cells within `radius` of the level-0 parent of a
 // local cell that are not wholly owned here (sorted, unique)
 std::vector<uint64_t> k_ghost_level0(const MapCtx& m, const DevMesh& M, int rank, const uint64_t* local, size_t n,
@@ -646,6 +662,8 @@ AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint
 void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                  const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
                  double unrefine_sensitivity, uint8_t* band, hipStream_t s);
+void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
+                         double* rho, const double* removed_rho, hipStream_t s);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
                           size_t np, hipStream_t s);
 void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],

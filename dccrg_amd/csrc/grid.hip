@@ -476,9 +476,15 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (!D.empty()) close_set(g, D, true);
 	DX_LAP("sr.1_override_refines");
 	std::vector<uint64_t> mine;
-	for (uint64_t c : sorted_unique(vec(g.refine_requests)))
-		if (!sorted_contains(D, c)) mine.push_back(c);
+	{
+		std::vector<uint64_t> rq = vec(g.refine_requests);
+		rq.insert(rq.end(), g.refine_bulk.begin(), g.refine_bulk.end());
+		rq = sorted_unique(std::move(rq));
+		if (D.empty()) mine = std::move(rq);
+		else std::set_difference(rq.begin(), rq.end(), D.begin(), D.end(), std::back_inserter(mine));
+	}
 	g.refine_requests.clear();
+	g.refine_bulk.clear();
 	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
 	if (!S.empty()) close_set(g, S, false);
 	DX_LAP("sr.2_induce_refines");
@@ -486,18 +492,22 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	// unrefines: one family per requested parent
 	std::vector<uint64_t> req_par;
 	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
+	for (uint64_t c : g.unrefine_bulk) req_par.push_back(map_parent(g.m, c));
 	req_par = sorted_unique(req_par);
 	g.unrefine_requests.clear();
+	g.unrefine_bulk.clear();
 	const std::vector<uint64_t> DU = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_unrefine_cells))));
 	g.dont_unrefine_cells.clear();
+	// a family is a candidate unless one of its children is refined or marked
+	// dont_unrefine: the requested parents minus the parents of S and of DU
+	std::vector<uint64_t> blocked;
+	blocked.reserve(S.size() + DU.size());
+	for (const std::vector<uint64_t>* v : {static_cast<const std::vector<uint64_t>*>(&S), &DU})
+		for (uint64_t c : *v)
+			if (map_level(g.m, c) > 0) blocked.push_back(map_parent(g.m, c));
+	blocked = sorted_unique(std::move(blocked));
 	std::vector<uint64_t> cand;
-	for (uint64_t p : req_par) {
-		uint64_t ch[8];
-		map_all_children(g.m, p, ch);
-		bool ok = true;
-		for (uint64_t c : ch) ok = ok && !sorted_contains(S, c) && !sorted_contains(DU, c);
-		if (ok) cand.push_back(p);
-	}
+	std::set_difference(req_par.begin(), req_par.end(), blocked.begin(), blocked.end(), std::back_inserter(cand));
 	const std::vector<uint8_t> ok = k_unrefine_check(g.m, g.d_hood.p, nh, g.dm(), cand, S, s);
 	std::vector<uint64_t> fmine;
 	for (size_t i = 0; i < cand.size(); i++)

@@ -353,8 +353,14 @@ void rebuild(Grid& g, Mesh& nm) {
 	}
 
 	DX_LAP("rb.5_send_slots");
-	// 6. carry field payloads over
+	// 6. carry field payloads over: one source slot per new slot (one pair of
+	// hash lookups for all fields), then one gather per field
 	const DevMesh odm = old.dev(m.last);
+	DBuf<int32_t> src;
+	if (old_slot_ids.p && std::any_of(g.fields.begin(), g.fields.end(), [](const Field& f) { return !f.var; })) {
+		src.alloc(g.n_slots + 1);
+		k_carry_src(g.slot_ids.p, g.n_slots, nl, m, odm, old_n_local, src.p, s);
+	}
 	for (auto& f : g.fields) {
 		if (f.var) {  // children and new copies start empty (the reference default-constructs them)
 			var_remap(f, old_slot_ids.p, old_slot_ids.p ? old_n_local : 0, dm, g.n_slots, s);
@@ -363,10 +369,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		DBuf<uint8_t> nd;
 		nd.alloc(g.n_slots * f.elem);
 		if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
-		if (f.data.p && old_slot_ids.p) {
-			k_remap_field(f.data.p, old_slot_ids.p, old_n_local, dm, nd.p, f.elem, s);
-			k_parent_fill(nd.p, g.slot_ids.p, nl, m, f.data.p, odm, f.elem, s);
-		}
+		if (f.data.p && old_slot_ids.p) k_gather_rows(f.data.p, src.p, g.n_slots, f.elem, nd.p, s);
 		f.data.swap(nd);
 		f.scratch.release();
 	}

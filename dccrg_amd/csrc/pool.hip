@@ -1,0 +1,129 @@
+// Process-wide caching pool of device memory behind every DBuf
+// (dccrgx_internal.hpp).  hipFree synchronises the whole device and unmaps
+// the block (~0.08 ms a call; an adaptive advection step of config 3 made
+// ~120 of them), so released blocks are kept and handed to later requests of
+// a similar size.
+//
+// Ordering: a block released while queued work may still use it goes to
+// `pending`; it becomes reusable only after a device synchronisation, done on
+// demand when a request finds no ready block but a pending one - the same
+// guarantee hipFree gave, paid once for every block pending at that moment.
+#include <map>
+#include <mutex>
+
+#include "dccrgx_internal.hpp"
+
+namespace dccrgx {
+
+namespace {
+
+constexpr size_t kMaxHeld = size_t(16) << 30;  // cached bytes kept at most (the rest is hipFree'd)
+constexpr size_t kBig = size_t(1) << 20;
+
+struct Pool {
+	std::mutex mu;
+	std::multimap<size_t, void*> ready;    // reusable now
+	std::multimap<size_t, void*> pending;  // released, reusable after a device synchronisation
+	size_t held = 0;                       // bytes in ready + pending
+};
+
+// never destroyed: blocks outlive static destruction and go with the process
+Pool& pool() {
+	static Pool* p = new Pool();
+	return *p;
+}
+
+// size classes: powers of two up to 1 MiB, 2-MiB multiples above
+size_t size_class(size_t b) {
+	if (b <= kBig) {
+		size_t r = 256;
+		while (r < b) r <<= 1;
+		return r;
+	}
+	const size_t g = size_t(2) << 20;
+	return (b + g - 1) / g * g;
+}
+
+// a block of at least `want` bytes and at most a quarter more (exact class
+// for small blocks)
+bool take(Pool& P, std::multimap<size_t, void*>& m, size_t want, void*& out, size_t& cap) {
+	auto it = m.lower_bound(want);
+	if (it == m.end()) return false;
+	if (want <= kBig ? it->first != want : it->first > want + want / 4) return false;
+	out = it->second;
+	cap = it->first;
+	P.held -= cap;
+	m.erase(it);
+	return true;
+}
+
+void retire_pending(Pool& P) {
+#if DCCRGX_PHASE_TIMING
+	const double t0 = PhaseScope::now();
+	HIP_CHECK(hipDeviceSynchronize());
+	phase_add("pool.sync", PhaseScope::now() - t0);
+#else
+	HIP_CHECK(hipDeviceSynchronize());
+#endif
+	P.ready.insert(P.pending.begin(), P.pending.end());
+	P.pending.clear();
+}
+
+void free_all(Pool& P) {
+	(void)hipDeviceSynchronize();
+	for (auto* m : {&P.ready, &P.pending}) {
+		for (auto& kv : *m) (void)hipFree(kv.second);
+		m->clear();
+	}
+	P.held = 0;
+}
+
+}  // namespace
+
+void* pool_alloc(size_t bytes, size_t& cap) {
+	const size_t want = size_class(bytes);
+	Pool& P = pool();
+	std::lock_guard<std::mutex> lock(P.mu);
+	void* out = nullptr;
+	if (take(P, P.ready, want, out, cap)) return out;
+	{
+		auto it = P.pending.lower_bound(want);
+		if (it != P.pending.end() && (want <= kBig ? it->first == want : it->first <= want + want / 4)) {
+			retire_pending(P);
+			if (take(P, P.ready, want, out, cap)) return out;
+		}
+	}
+#if DCCRGX_PHASE_TIMING
+	const double t0 = PhaseScope::now();
+	hipError_t e = hipMalloc(&out, want);
+	phase_add("pool.hipMalloc", PhaseScope::now() - t0);
+#else
+	hipError_t e = hipMalloc(&out, want);
+#endif
+	if (e != hipSuccess) {  // out of memory: give the cached blocks back and retry once
+		(void)hipGetLastError();
+		free_all(P);
+		e = hipMalloc(&out, want);
+	}
+	if (e != hipSuccess) {
+		(void)hipGetLastError();
+		throw Error(DCCRGX_EHIP, "device allocation of " + std::to_string(want) + " bytes failed: " +
+		                             hipGetErrorString(e));
+	}
+	cap = want;
+	return out;
+}
+
+void pool_free(void* raw, size_t cap) {
+	if (!raw) return;
+	Pool& P = pool();
+	std::lock_guard<std::mutex> lock(P.mu);
+	if (P.held + cap > kMaxHeld) {
+		(void)hipFree(raw);
+		return;
+	}
+	P.pending.insert({cap, raw});
+	P.held += cap;
+}
+
+}  // namespace dccrgx

@@ -495,8 +495,9 @@ struct TileMeta {
 
 template <int MINW>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
-    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, const uint32_t* __restrict__ ext,
-    const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta, uint32_t ntiles, uint32_t ecap, double dt) {
+    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, uint32_t tplane,
+    const uint32_t* __restrict__ ext, const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta,
+    uint32_t ntiles, uint32_t ecap, double dt) {
 #pragma clang fp contract(off)
 	constexpr uint32_t T = 512;
 	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
@@ -530,9 +531,11 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			// the tile's face codes, ext list and finer pairs are read once per
 			// sweep: non-temporal, so they do not evict the field lines other
 			// tiles re-read (paired A/B on config 3: 0.1915 -> 0.1865 ms/sweep)
-			row[0] = __builtin_nontemporal_load(tell + 3 * (ts + tid));
-			row[1] = __builtin_nontemporal_load(tell + 3 * (ts + tid) + 1);
-			row[2] = __builtin_nontemporal_load(tell + 3 * (ts + tid) + 2);
+			// (three planes of codes: one coalesced 4-B load per plane; the
+			// interleaved 12-B records cost ~20 us per sweep on config 3)
+			row[0] = __builtin_nontemporal_load(tell + (ts + tid));
+			row[1] = __builtin_nontemporal_load(tell + tplane + (ts + tid));
+			row[2] = __builtin_nontemporal_load(tell + 2 * tplane + (ts + tid));
 		}
 		// ext = slot | axis mask << 29: density and lengths, and only the
 		// velocity components along the axes its faces cross
@@ -546,8 +549,10 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		if (tid < ne) load5(__builtin_nontemporal_load(ext + e0 + tid), xa);
 		if (tid + T < ne) load5(__builtin_nontemporal_load(ext + e0 + tid + T), xb);
 		if (tid < nf) {
-			fq[0] = __builtin_nontemporal_load(tfine + 2 * (fb + tid));
-			fq[1] = __builtin_nontemporal_load(tfine + 2 * (fb + tid) + 1);
+			typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+			const u2v q = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(tfine) + (fb + tid));
+			fq[0] = q.x;
+			fq[1] = q.y;
 		}
 	};
 	load(t);
@@ -741,6 +746,46 @@ __global__ void adv_parent_density_kernel(double* __restrict__ rho, const int32_
 	}
 }
 
+// merged families on the device: the parent of every removed child, and
+// (after the parents are sorted and deduplicated) each child's place in its
+// parent's row of eight, in map_all_children order (= ascending id)
+__global__ void removed_parents_kernel(MapCtx m, const uint64_t* __restrict__ rm, size_t n, uint64_t* __restrict__ par) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		par[i] = map_parent(m, rm[i]);
+}
+
+__global__ void removed_rows_kernel(MapCtx m, const uint64_t* __restrict__ rm, size_t n,
+                                    const uint64_t* __restrict__ parents, size_t np, int32_t* __restrict__ cidx,
+                                    int* __restrict__ err) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t x, y, z;
+		const int l = map_indices(m, rm[i], x, y, z);
+		const uint64_t p = map_parent(m, rm[i]);
+		size_t lo = 0, hi = np;
+		while (lo < hi) {
+			const size_t mid = (lo + hi) / 2;
+			if (parents[mid] < p) lo = mid + 1;
+			else hi = mid;
+		}
+		if (l <= 0 || lo >= np || parents[lo] != p) {
+			atomicOr(err, 1);
+			continue;
+		}
+		const uint64_t o = uint64_t(1) << (m.R - l);  // the child's length in indices
+		const int k = int((x / o) & 1u) | int(((y / o) & 1u) << 1) | int(((z / o) & 1u) << 2);
+		cidx[8 * lo + size_t(k)] = int32_t(i);
+	}
+}
+
+__global__ void check_rows_kernel(const int32_t* __restrict__ cidx, const int32_t* __restrict__ pslot, size_t np,
+                                  size_t n_local, int* __restrict__ err) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < np; i += size_t(gridDim.x) * blockDim.x) {
+		if (pslot[i] < 0 || size_t(pslot[i]) >= n_local) atomicOr(err, 2);
+		for (int k = 0; k < 8; k++)
+			if (cidx[8 * i + k] < 0) atomicOr(err, 4);
+	}
+}
+
 // adapt_grid (adapter.hpp:294-305): velocity (solve.hpp:336-342) and lengths
 // (Cartesian_Geometry get_center / get_length, dccrg_cartesian_geometry.hpp:
 // 282-362) of every local cell
@@ -853,7 +898,8 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 		const uint32_t ecap = uint32_t(g.max_ext);
 		const size_t lds = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
-		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, g.ext_pk.p, g.tfine.p, meta,
+		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1), g.ext_pk.p,
+		                                                    g.tfine.p, meta,
 		                                                    uint32_t(n_irr), ecap, dt);
 		HIP_CHECK(hipGetLastError());
 	}
@@ -871,6 +917,39 @@ void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, c
 	adv_bands_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, face_ptr, face_ent, slot_ids, n, diff_increase,
 	                                                  diff_threshold, unrefine_sensitivity, band);
 	HIP_CHECK(hipGetLastError());
+}
+
+// adapt_grid's merged parents (adapter.hpp:260-290) from the removed store's
+// ids `rm` (store order): parents grouped, their eight children in ascending
+// id, the parents' local slots, then the mean density
+void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
+                         double* rho, const double* removed_rho, hipStream_t s) {
+	if (rm.empty()) return;
+	const size_t n = rm.size();
+	DBuf<uint64_t> d_rm, par;
+	upload(d_rm, rm, s);
+	par.alloc(n);
+	removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, d_rm.p, n, par.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t np = sort_unique_u64(par.p, n, s);
+	DX_REQUIRE(np * 8 == n, "a merged family's removed children are incomplete");
+	DBuf<int32_t> cidx, pslot;
+	DBuf<int> err;
+	cidx.alloc(8 * np);
+	pslot.alloc(np);
+	err.alloc(1);
+	HIP_CHECK(hipMemsetAsync(cidx.p, 0xff, 8 * np * sizeof(int32_t), s));
+	HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), s));
+	removed_rows_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, d_rm.p, n, par.p, np, cidx.p, err.p);
+	HIP_CHECK(hipGetLastError());
+	k_lookup_slots(par.p, np, dm, pslot.p, err.p, s);  // a missing parent sets err too
+	check_rows_kernel<<<grid_for(np, 256), 256, 0, s>>>(cidx.p, pslot.p, np, n_local, err.p);
+	HIP_CHECK(hipGetLastError());
+	int h = 0;
+	HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(h == 0, "merged parent is not local or a removed child's payload is missing");
+	k_adv_parent_density(rho, pslot.p, cidx.p, removed_rho, np, s);
 }
 
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,

@@ -161,9 +161,12 @@ __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restr
 			}
 			e = k;
 		}
-		tell[3 * size_t(r)] = code[0] | (code[1] << 16);
-		tell[3 * size_t(r) + 1] = code[2] | (code[3] << 16);
-		tell[3 * size_t(r) + 2] = code[4] | (code[5] << 16);
+		// three planes of n_local + 1 words (x, y, z pairs of codes), so the
+		// sweep reads each plane with one coalesced load per cell
+		const size_t pl = size_t(tg.n_local) + 1;
+		tell[size_t(r)] = code[0] | (code[1] << 16);
+		tell[pl + size_t(r)] = code[2] | (code[3] << 16);
+		tell[2 * pl + size_t(r)] = code[4] | (code[5] << 16);
 	}
 }
 
@@ -318,10 +321,135 @@ static void cut_run(const std::vector<uint8_t>& al, uint32_t r0, uint32_t r1, ui
 	}
 }
 
+// The greedy cut of cut_run on the device.  next[a] = the start of the tile
+// after one starting at slot a of its run [r0, r1): r1 when the rest fits one
+// tile, else the best-aligned slot in [a + lo, a + T], the latest on ties -
+// for every slot at once (one block per 256 slots, their windows staged in
+// LDS).  The tile starts are then the chain 0, next[0], next[next[0]], ...
+// (through the inner run's end into the outer run), listed by pointer
+// jumping: next^64 by six doublings, the anchors next^(64 i)(0) walked by one
+// thread, each anchor's 64 successors by one thread each.
+constexpr uint32_t kCutBlock = 256;
+constexpr uint32_t kCutMaxT = 4096;
+
+__global__ __launch_bounds__(kCutBlock) void cut_next_kernel(const uint8_t* __restrict__ al, uint32_t r0, uint32_t r1,
+                                                              uint32_t T, uint32_t lo, uint32_t* __restrict__ next) {
+	__shared__ uint8_t w[kCutBlock + kCutMaxT + 1];
+	const uint32_t a0 = r0 + blockIdx.x * kCutBlock;
+	if (a0 >= r1) return;  // block-uniform
+	const uint32_t span = kCutBlock + T + 1;
+	for (uint32_t i = threadIdx.x; i < span; i += kCutBlock) w[i] = a0 + i < r1 ? al[a0 + i] : 0;
+	__syncthreads();
+	const uint32_t a = a0 + threadIdx.x;
+	if (a >= r1) return;
+	if (r1 - a <= T) {
+		next[a] = r1;
+		return;
+	}
+	// key = alignment * 8192 + offset: the max is the best alignment, latest
+	uint32_t best = 0;
+	for (uint32_t o = lo; o <= T; o++) {
+		const uint32_t k = (uint32_t(w[threadIdx.x + o]) << 13) | o;
+		best = k > best ? k : best;
+	}
+	next[a] = a + (best & 8191u);
+}
+
+__global__ void jump_double_kernel(const uint32_t* __restrict__ in, size_t n, uint32_t* __restrict__ out) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		out[i] = in[in[i]];
+}
+
+// one thread: the anchors 0, J64[0], ... up to the terminal n
+__global__ void chain_anchors_kernel(const uint32_t* __restrict__ j64, uint32_t n, uint32_t* __restrict__ anchors,
+                                     uint32_t cap, uint32_t* __restrict__ count) {
+	if (blockIdx.x != 0 || threadIdx.x != 0) return;
+	uint32_t a = 0, k = 0;
+	while (k < cap) {
+		anchors[k++] = a;
+		if (a >= n) break;
+		a = j64[a];
+	}
+	*count = k;
+}
+
+// anchor i expands into starts[64 i .. 64 i + 63]; n marks the end
+__global__ void chain_expand_kernel(const uint32_t* __restrict__ next, const uint32_t* __restrict__ anchors,
+                                    const uint32_t* __restrict__ count, uint32_t n, uint32_t* __restrict__ starts) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= *count) return;
+	uint32_t a = anchors[i];
+	for (uint32_t j = 0; j < 64; j++) {
+		starts[size_t(i) * 64 + j] = a;
+		if (a >= n) break;
+		a = next[a];
+	}
+}
+
 __global__ void pack_ext_kernel(const uint32_t* __restrict__ ext, const uint32_t* __restrict__ ax, size_t m,
                                 uint32_t* __restrict__ out) {
 	for (size_t k = blockIdx.x * size_t(blockDim.x) + threadIdx.x; k < m; k += size_t(gridDim.x) * blockDim.x)
 		out[k] = ext[k] | (ax[k] << 29);
+}
+
+// cut_run over both runs on the device (see cut_next_kernel): the tile starts
+// of [0, n_inner) then [n_inner, n_local) into tstart (+ the end n_local);
+// returns the tile count, n_tiles_inner the inner run's
+static size_t device_cut(const DBuf<uint8_t>& al, size_t n_inner, size_t n_local, uint32_t T, DBuf<uint32_t>& tstart,
+                         size_t& n_tiles_inner, hipStream_t s) {
+	DX_REQUIRE(T <= kCutMaxT, "tile size out of range for the device cut");
+	const uint32_t n = uint32_t(n_local), lo = tile_lo(T);
+	DBuf<uint32_t> next, ja, jb;
+	next.alloc(size_t(n) + 1);
+	const uint32_t runs[3] = {0u, uint32_t(n_inner), n};
+	for (int r = 0; r < 2; r++) {
+		const uint32_t r0 = runs[r], r1 = runs[r + 1];
+		if (r1 > r0)
+			cut_next_kernel<<<(r1 - r0 + kCutBlock - 1) / kCutBlock, kCutBlock, 0, s>>>(al.p, r0, r1, T, lo, next.p);
+	}
+	HIP_CHECK(hipGetLastError());
+	HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(next.p + n), int(n), 1, s));  // terminal: next[n] = n
+	// J64 = next^64
+	ja.alloc(size_t(n) + 1);
+	jb.alloc(size_t(n) + 1);
+	const uint32_t* src = next.p;
+	DBuf<uint32_t>* dst = &ja;
+	for (int k = 0; k < 6; k++) {
+		jump_double_kernel<<<grid_for(size_t(n) + 1, 256), 256, 0, s>>>(src, size_t(n) + 1, dst->p);
+		HIP_CHECK(hipGetLastError());
+		src = dst->p;
+		dst = dst == &ja ? &jb : &ja;
+	}
+	// every tile but a run's last has at least lo slots: at most n / lo + 2
+	// starts, + the terminal
+	const uint32_t cap_anchor = uint32_t((size_t(n) / lo + 4) / 64 + 4);
+	DBuf<uint32_t> anchors, cnt, starts;
+	anchors.alloc(cap_anchor);
+	cnt.alloc(1);
+	chain_anchors_kernel<<<1, 64, 0, s>>>(src, n, anchors.p, cap_anchor, cnt.p);
+	HIP_CHECK(hipGetLastError());
+	starts.alloc(size_t(cap_anchor) * 64);
+	HIP_CHECK(hipMemsetAsync(starts.p, 0xff, starts.n * 4, s));
+	chain_expand_kernel<<<(cap_anchor + 63) / 64, 64, 0, s>>>(next.p, anchors.p, cnt.p, n, starts.p);
+	HIP_CHECK(hipGetLastError());
+	uint32_t na = 0;
+	HIP_CHECK(hipMemcpyAsync(&na, cnt.p, 4, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	DX_REQUIRE(na >= 1 && na < cap_anchor, "internal error: tile chain longer than its bound");
+	// the starts before the terminal: the sequence is increasing, so the
+	// count of each run is a count of values below its end
+	const std::vector<uint32_t> h = download(starts.p, size_t(na) * 64, s);
+	size_t ntiles = 0, ni = 0;
+	while (ntiles < h.size() && h[ntiles] < n) {
+		ni += h[ntiles] < n_inner;
+		ntiles++;
+	}
+	n_tiles_inner = ni;
+	tstart.alloc(ntiles + 1);
+	if (ntiles) HIP_CHECK(hipMemcpyAsync(tstart.p, starts.p, ntiles * 4, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(tstart.p + ntiles), int(n), 1, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	return ntiles;
 }
 
 TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& mc,
@@ -332,24 +460,30 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	DX_REQUIRE(n_local < (size_t(1) << 29), "too many local cells for 29-bit tile slots");
 	TileBuild out{};
 	const uint32_t T = uint32_t(tile);
-	std::vector<uint8_t> al;
+	DX_LAPS(s);
+	DBuf<uint8_t> dal;
 	if (morton && n_local) {
-		DBuf<uint8_t> dal;
 		dal.alloc(n_local);
 		align_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(mc, slot_ids, uint32_t(n_local), dal.p);
 		HIP_CHECK(hipGetLastError());
-		al = download(dal.p, n_local, s);
 	}
-	std::vector<uint32_t> hts;
-	cut_run(al, 0, uint32_t(n_inner), T, hts);
-	out.n_tiles_inner = hts.size();
-	cut_run(al, uint32_t(n_inner), uint32_t(n_local), T, hts);
-	out.n_tiles_outer = hts.size() - out.n_tiles_inner;
-	const size_t ntiles = hts.size();
-	hts.push_back(uint32_t(n_local));
-	tstart.alloc(ntiles + 1);
-	HIP_CHECK(hipMemcpyAsync(tstart.p, hts.data(), (ntiles + 1) * 4, hipMemcpyHostToDevice, s));
+	DX_LAP("tb.1_align");
+	size_t ntiles = 0;
+	if (morton && n_local) {
+		ntiles = device_cut(dal, n_inner, n_local, T, tstart, out.n_tiles_inner, s);
+		out.n_tiles_outer = ntiles - out.n_tiles_inner;
+	} else {
+		std::vector<uint32_t> hts;
+		cut_run({}, 0, uint32_t(n_inner), T, hts);
+		out.n_tiles_inner = hts.size();
+		cut_run({}, uint32_t(n_inner), uint32_t(n_local), T, hts);
+		out.n_tiles_outer = hts.size() - out.n_tiles_inner;
+		ntiles = hts.size();
+		hts.push_back(uint32_t(n_local));
+		upload(tstart, hts, s);
+	}
 	TileGeom tg{tstart.p, uint32_t(ntiles), uint32_t(n_local)};
+	DX_LAP("tb.2_cut");
 	tell.alloc(3 * n_local + 3);
 	ext_ptr.alloc(ntiles + 1);
 	fine_base.alloc(ntiles + 1);
@@ -388,6 +522,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		m0 = size_t(h);
 	}
 	all.release();
+	DX_LAP("tb.3_ext_keys_select");
 	int end_bit = 32;
 	while (end_bit < 64 && (uint64_t(ntiles) >> (end_bit - 32)) != 0) end_bit++;
 	const size_t m = sort_unique_u64(keys.p, m0, s, end_bit);
@@ -399,6 +534,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	out.total_ext = m;
 	for (size_t t = 0; t < ntiles; t++) out.max_ext = std::max<size_t>(out.max_ext, hptr[t + 1] - hptr[t]);
 	DX_REQUIRE(size_t(T) + out.max_ext < 0x8000u, "tile too large for 16-bit local indices");
+	DX_LAP("tb.4_sort_ranges");
 
 	// 4: finer faces
 	DBuf<uint32_t> cnt, fine_idx;
@@ -411,6 +547,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	fine_base_kernel<<<grid_for(ntiles, 256), 256, 0, s>>>(tg, fine_idx.p, fine_base.p);
 	HIP_CHECK(hipGetLastError());
 
+	DX_LAP("tb.5_fine");
 	// 5: tile-local rows
 	DBuf<int> err;
 	err.alloc(1);
@@ -429,6 +566,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
+	DX_LAP("tb.6_tile_rows");
 	return out;
 }
 

@@ -21,7 +21,8 @@ for round in $(seq "$ROUNDS"); do
     python -c "import json; d=json.loads(open('gpurun_out/${TAG}_${v}_$round.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$v', '$WL', round(d['ms_per_step'],4), round(r['kernel_ms_per_step'],4), round(r['frac'],3), r.get('kernels_ms', ''))"
   done
 done
-[ "$PMC" = "1" ] || exit 0
+# pmc: 0 none, 1 kernel stats + PMC passes, 2 kernel stats only
+[ "$PMC" = "0" ] && exit 0
 for v in $VARS; do
   DCCRGX_LIB=libdccrgx_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof_$v -o run \
       --output-format csv -- python -u bench.py --workload $WL --steps 20 --warmup 2 --no-cpu-baseline \
@@ -30,9 +31,12 @@ for v in $VARS; do
 import csv, glob, sys
 tag, v = sys.argv[1], sys.argv[2]
 for f in glob.glob(f"gpurun_out/{tag}_prof_{v}/**/*kernel_stats.csv", recursive=True):
-    for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))[:6]:
+    for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"])):
+        if "advection" not in r["Name"] and "gol" not in r["Name"] and "po_" not in r["Name"]:
+            continue
         print(v, f'{r["Name"][:70]:70s} calls={r["Calls"]:>5s} avg_us={float(r["AverageNs"]) / 1e3:8.1f}')
 EOF
+  [ "$PMC" = "2" ] && continue
   for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
     n=$(echo $c | cut -d' ' -f1)
     DCCRGX_LIB=libdccrgx_$v.so timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "${KREGEX:-advection}" \

@@ -5,6 +5,8 @@ The flux through a face is evaluated with the reference's expression and
 operand order on both sides (no contraction), so the only difference is the
 order in which a cell's face fluxes are summed (gather here, hash-ordered
 scatter in the reference)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -197,3 +199,25 @@ def test_parity_grid_four_rank_slabs_bitwise(gpu):
         assert np.array_equal(g.fields["density"].get(0, g.n_local), np.array([final[int(c)] for c in sl]))
     for g in gs + [ref]:
         g.close()
+
+
+@pytest.mark.parametrize("base,R", [((32, 32, 8), 2), ((24, 16, 6), 2), ((40, 24, 4), 1)])
+def test_tile_cut_matches_restatement(gpu, base, R):
+    """The device tile cut (tile_build.hip device_cut: greedy best-aligned
+    cuts by pointer jumping) and the regular / general classification equal
+    the host restatement scripts/tile_stats.py on the same leaf set."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import tile_stats
+
+    g, f = gpu_grid(base, R)
+    prerefine(g, f, R)
+    lay = g.advection_layout()
+    leaves = np.sort(g.local_cells())
+    L = tile_stats.layout(leaves, base, R, 512)
+    reason = tile_stats.classify(L, base, R)
+    assert lay["tiles"] == reason.size
+    assert lay["regular_tiles"] == int(np.sum(reason == 1))
+    assert lay["regular_cells"] == 512 * lay["regular_tiles"]
+    g.close()

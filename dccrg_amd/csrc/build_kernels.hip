@@ -824,6 +824,20 @@ void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_
 	slots = download(v2.p, n, s);
 }
 
+// a host list sorted (and deduplicated): by the device radix sort above a few
+// thousand ids (std::sort of 200 K ids takes 5-15 ms on the host), else here
+void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s) {
+	if (v.size() < 8192) {
+		std::sort(v.begin(), v.end());
+		if (unique) v.erase(std::unique(v.begin(), v.end()), v.end());
+		return;
+	}
+	DBuf<uint64_t> d;
+	upload(d, v, s);
+	const size_t n = unique ? sort_unique_u64(d.p, v.size(), s) : (sort_u64(d.p, v.size(), s), v.size());
+	v = download(d.p, n, s);
+}
+
 void sort_u64(uint64_t* keys, size_t n, hipStream_t s) {
 	if (n < 2) return;
 	DBuf<uint64_t> tmp;

@@ -564,6 +564,7 @@ size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uin
                       size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s);
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit = 64);  // in place; keys < 2^end_bit
 void sort_u64(uint64_t* keys, size_t n, hipStream_t s);           // in place
+void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s);  // host list, device radix sort when large
 // (id, slot) of every slot sorted by id
 void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
                          hipStream_t s);

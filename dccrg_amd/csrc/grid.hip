@@ -399,19 +399,17 @@ void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb) {
 }
 
 // --------------------------------------------------------------------------- refinement
-static std::vector<uint64_t> union_sorted(const std::vector<std::vector<uint64_t>>& all) {
+static std::vector<uint64_t> union_sorted(Grid& g, const std::vector<std::vector<uint64_t>>& all) {
 	std::vector<uint64_t> u;
 	for (const auto& v : all) u.insert(u.end(), v.begin(), v.end());
-	std::sort(u.begin(), u.end());
-	u.erase(std::unique(u.begin(), u.end()), u.end());
+	host_sort_u64(u, true, g.s_comp);
 	return u;
 }
 
 static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids);
 
-static std::vector<uint64_t> sorted_unique(std::vector<uint64_t> v) {
-	std::sort(v.begin(), v.end());
-	v.erase(std::unique(v.begin(), v.end()), v.end());
+static std::vector<uint64_t> sorted_unique(Grid& g, std::vector<uint64_t> v) {
+	host_sort_u64(v, true, g.s_comp);
 	return v;
 }
 
@@ -430,7 +428,7 @@ static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
 		    k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp, finer);
 		std::vector<uint64_t> mine_new;
 		std::set_difference(found.begin(), found.end(), S.begin(), S.end(), std::back_inserter(mine_new));
-		const std::vector<uint64_t> all = union_sorted(comm_allgather_u64(g, mine_new));
+		const std::vector<uint64_t> all = union_sorted(g, comm_allgather_u64(g, mine_new));
 		fresh.clear();
 		std::set_difference(all.begin(), all.end(), S.begin(), S.end(), std::back_inserter(fresh));
 		if (fresh.empty()) break;
@@ -471,7 +469,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	g.removed_ids_h.clear();
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
-	std::vector<uint64_t> D = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_refine_cells))));
+	std::vector<uint64_t> D = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_refine_cells))));
 	g.dont_refine_cells.clear();
 	if (!D.empty()) close_set(g, D, true);
 	DX_LAP("sr.1_override_refines");
@@ -479,13 +477,13 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	{
 		std::vector<uint64_t> rq = vec(g.refine_requests);
 		rq.insert(rq.end(), g.refine_bulk.begin(), g.refine_bulk.end());
-		rq = sorted_unique(std::move(rq));
+		rq = sorted_unique(g, std::move(rq));
 		if (D.empty()) mine = std::move(rq);
 		else std::set_difference(rq.begin(), rq.end(), D.begin(), D.end(), std::back_inserter(mine));
 	}
 	g.refine_requests.clear();
 	g.refine_bulk.clear();
-	std::vector<uint64_t> S = union_sorted(comm_allgather_u64(g, mine));
+	std::vector<uint64_t> S = union_sorted(g, comm_allgather_u64(g, mine));
 	if (!S.empty()) close_set(g, S, false);
 	DX_LAP("sr.2_induce_refines");
 
@@ -493,10 +491,10 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	std::vector<uint64_t> req_par;
 	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
 	for (uint64_t c : g.unrefine_bulk) req_par.push_back(map_parent(g.m, c));
-	req_par = sorted_unique(req_par);
+	req_par = sorted_unique(g, req_par);
 	g.unrefine_requests.clear();
 	g.unrefine_bulk.clear();
-	const std::vector<uint64_t> DU = union_sorted(comm_allgather_u64(g, sorted_unique(vec(g.dont_unrefine_cells))));
+	const std::vector<uint64_t> DU = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_unrefine_cells))));
 	g.dont_unrefine_cells.clear();
 	// a family is a candidate unless one of its children is refined or marked
 	// dont_unrefine: the requested parents minus the parents of S and of DU
@@ -505,14 +503,14 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	for (const std::vector<uint64_t>* v : {static_cast<const std::vector<uint64_t>*>(&S), &DU})
 		for (uint64_t c : *v)
 			if (map_level(g.m, c) > 0) blocked.push_back(map_parent(g.m, c));
-	blocked = sorted_unique(std::move(blocked));
+	blocked = sorted_unique(g, std::move(blocked));
 	std::vector<uint64_t> cand;
 	std::set_difference(req_par.begin(), req_par.end(), blocked.begin(), blocked.end(), std::back_inserter(cand));
 	const std::vector<uint8_t> ok = k_unrefine_check(g.m, g.d_hood.p, nh, g.dm(), cand, S, s);
 	std::vector<uint64_t> fmine;
 	for (size_t i = 0; i < cand.size(); i++)
 		if (ok[i]) fmine.push_back(cand[i]);
-	const std::vector<uint64_t> F = union_sorted(comm_allgather_u64(g, fmine));
+	const std::vector<uint64_t> F = union_sorted(g, comm_allgather_u64(g, fmine));
 	DX_LAP("sr.3_override_unrefines");
 	if (S.empty() && F.empty()) return {};
 
@@ -539,7 +537,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			for (uint64_t c : ch) g.pins[c] = pv;
 		}
 	}
-	std::sort(created.begin(), created.end());
+	host_sort_u64(created, false, s);
 	DX_LAP("sr.4_created");
 
 	// merged families: the children's payloads to the parent's new process
@@ -566,7 +564,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		}
 		for (auto* mp : {&send_ids, &recv_ids})
 			for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
-		std::sort(keep_ids.begin(), keep_ids.end());
+		host_sort_u64(keep_ids, false, s);
 	}
 	size_t bpc = 0;
 	for (auto& f : g.fields) bpc += f.elem;

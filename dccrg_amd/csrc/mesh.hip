@@ -205,7 +205,15 @@ void rebuild(Grid& g, Mesh& nm) {
 	Mesh& M = g.mesh;
 	M.tab.release();
 
-	// 1. own leaves, ascending
+	// slot order: Morton order of the min corner on refined grids (step 2)
+	int order = g.slot_order;
+	if (order < 0) order = g.R > 0 ? 1 : 0;
+	bool fits = true;
+	for (int d = 0; d < 3; d++) fits = fits && m.glen[d] <= (uint64_t(1) << 21);
+	g.morton_slots = order == 1 && fits;
+
+	// 1. own leaves, ascending (in any order when the Morton sort of step 2
+	// decides the slot order)
 	DBuf<uint64_t> d_local;
 	if (M.implicit) {
 		uint64_t f, c;
@@ -228,7 +236,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		g.n_local = size_t(hn);
-		sort_u64(d_local.p, g.n_local, s);
+		if (!g.morton_slots) sort_u64(d_local.p, g.n_local, s);
 	}
 	const size_t nl = g.n_local;
 	DevMesh dm = g.dm();  // implicit: no table yet (owners by formula)
@@ -246,11 +254,6 @@ void rebuild(Grid& g, Mesh& nm) {
 	local_slots.alloc(nl + 1);
 	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
 	d_local.release();
-	int order = g.slot_order;
-	if (order < 0) order = g.R > 0 ? 1 : 0;
-	bool fits = true;
-	for (int d = 0; d < 3; d++) fits = fits && m.glen[d] <= (uint64_t(1) << 21);
-	g.morton_slots = order == 1 && fits;
 	if (g.morton_slots) {
 		k_morton_sort(m, local_slots.p, g.n_inner, s);
 		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);

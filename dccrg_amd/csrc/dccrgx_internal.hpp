@@ -187,6 +187,30 @@ inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
 	return h;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// Stream compaction: every lane of a FULL wave (no lane may have exited)
+// reserves `c` consecutive output positions from *ctr; one atomic per wave.
+// Appending one element per lane per atomic (even wave-aggregated, which the
+// compiler already does) serialises on the counter's address: ~140 K wave
+// atomics take ~1.5 ms for 8.87 M elements, so callers give each lane a run
+// of elements (kAppendRun) and reserve once for all of them.
+constexpr int kAppendRun = 16;
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* ctr, unsigned c) {
+	const int lane = int(threadIdx.x & 63u);
+	unsigned incl = c;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const unsigned v = __shfl_up(incl, d, 64);
+		if (lane >= d) incl += v;
+	}
+	const unsigned total = __shfl(incl, 63, 64);
+	unsigned long long base = 0;
+	if (lane == 63 && total) base = atomicAdd(ctr, static_cast<unsigned long long>(total));
+	base = __shfl(base, 63, 64);
+	return base + (incl - c);
+}
+#endif
+
 inline unsigned grid_for(size_t n, unsigned per_block, unsigned cap = 256u * 32u) {
 	size_t g = (n + per_block - 1) / per_block;
 	if (g > cap) g = cap;

@@ -701,8 +701,17 @@ __global__ void flag_slots_kernel(const int32_t* slots, size_t n, uint8_t* flag)
 
 __global__ void keep_unflagged_kernel(const uint64_t* ids, const uint8_t* flag, size_t n, uint64_t* out,
                                       unsigned long long* counter) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		if (!flag[i]) out[atomicAdd(counter, 1ull)] = ids[i];
+	// each lane a run of kAppendRun ids, one counter atomic per wave
+	const size_t i0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kAppendRun;
+	unsigned c = 0;
+	for (int k = 0; k < kAppendRun; k++)
+		if (i0 + k < n && !flag[i0 + k]) c++;
+	unsigned long long at = wave_reserve(counter, c);
+	for (int k = 0; k < kAppendRun && c; k++)
+		if (i0 + k < n && !flag[i0 + k]) {
+			out[at++] = ids[i0 + k];
+			c--;
+		}
 }
 
 static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids) {
@@ -870,7 +879,8 @@ void finish_balance_load_impl(Grid& g) {
 	ctr.alloc(1);
 	HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
 	if (nl) {
-		keep_unflagged_kernel<<<grid_for(nl, 256), 256, 0, s>>>(g.slot_ids.p, flag.p, nl, local.p, ctr.p);
+		keep_unflagged_kernel<<<unsigned((nl + 256 * kAppendRun - 1) / (256 * kAppendRun)), 256, 0, s>>>(
+		    g.slot_ids.p, flag.p, nl, local.p, ctr.p);
 		HIP_CHECK(hipGetLastError());
 	}
 	unsigned long long kept = 0;

@@ -13,11 +13,23 @@ namespace dccrgx {
 
 namespace {
 
+// the ids owned by `rank`: each lane a run of kAppendRun entries, one counter
+// atomic per wave (launch: select_owner_grid)
 __global__ void select_owner_kernel(const uint64_t* ids, const int32_t* own, size_t n, int rank, uint64_t* out,
                                     unsigned long long* counter) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		if (own[i] == rank) out[atomicAdd(counter, 1ull)] = ids[i];
+	const size_t i0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kAppendRun;
+	unsigned c = 0;
+	for (int k = 0; k < kAppendRun; k++)
+		if (i0 + k < n && own[i0 + k] == rank) c++;
+	unsigned long long at = wave_reserve(counter, c);
+	for (int k = 0; k < kAppendRun && c; k++)
+		if (i0 + k < n && own[i0 + k] == rank) {
+			out[at++] = ids[i0 + k];
+			c--;
+		}
 }
+
+unsigned select_owner_grid(size_t n) { return unsigned((n + size_t(256) * kAppendRun - 1) / (size_t(256) * kAppendRun)); }
 
 __global__ void fill_owner_kernel(int32_t* own, size_t n, int32_t v) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) own[i] = v;
@@ -228,7 +240,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		ctr.alloc(1);
 		HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
 		if (M.n_known) {
-			select_owner_kernel<<<grid_for(M.n_known, 256), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank, d_local.p,
+			select_owner_kernel<<<select_owner_grid(M.n_known), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank, d_local.p,
 			                                                              ctr.p);
 			HIP_CHECK(hipGetLastError());
 		}

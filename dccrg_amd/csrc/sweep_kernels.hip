@@ -703,13 +703,29 @@ __global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const
 __global__ void adv_requests_kernel(MapCtx m, const uint64_t* __restrict__ ids, const uint8_t* __restrict__ band,
                                     size_t n, uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
                                     uint32_t* __restrict__ part, unsigned long long* __restrict__ cnt) {
-	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+	// each lane a run of kRun slots: classify them, reserve its positions in
+	// the three lists with one atomic per wave and list, then write
+	constexpr int kRun = 8;
+	const size_t s0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kRun;
+	uint8_t what[kRun];  // bit 0 refine, 1 partial run head, 2 kept family head, 3 unrefine family head
+	uint8_t runk[kRun];
+	unsigned cr = 0, cp = 0, ck = 0, cu = 0;
+	for (int j = 0; j < kRun; j++) {
+		what[j] = 0;
+		runk[j] = 0;
+		const size_t s = s0 + j;
+		if (s >= n) continue;
 		const uint64_t id = ids[s];
 		const int lvl = map_level(m, id);
-		if (band[s] == 2 && lvl < int(m.R)) ref[atomicAdd(&cnt[0], 1ull)] = id;
+		if (band[s] == 2 && lvl < int(m.R)) {
+			what[j] |= 1;
+			cr++;
+		}
 		if (lvl == 0) continue;
+		// run head of a family: the first slot of a run of consecutive slots
+		// with one parent
 		const uint64_t p = map_parent(m, id);
-		if (s > 0 && map_level(m, ids[s - 1]) > 0 && map_parent(m, ids[s - 1]) == p) continue;  // not a run head
+		if (s > 0 && map_level(m, ids[s - 1]) > 0 && map_parent(m, ids[s - 1]) == p) continue;
 		uint32_t k = 1;
 		bool keep = band[s] >= 1;
 		while (k < 8 && s + k < n) {
@@ -718,9 +734,25 @@ __global__ void adv_requests_kernel(MapCtx m, const uint64_t* __restrict__ ids, 
 			keep = keep || band[s + k] >= 1;
 			k++;
 		}
-		if (k < 8) part[atomicAdd(&cnt[3], 1ull)] = uint32_t(s) | (k << 28);
-		else if (keep) atomicAdd(&cnt[2], 1ull);
-		else unref[atomicAdd(&cnt[1], 1ull)] = id;
+		runk[j] = uint8_t(k);
+		if (k < 8) {
+			what[j] |= 2;
+			cp++;
+		} else if (keep) {
+			what[j] |= 4;
+			ck++;
+		} else {
+			what[j] |= 8;
+			cu++;
+		}
+	}
+	unsigned long long ar = wave_reserve(&cnt[0], cr), ap = wave_reserve(&cnt[3], cp), au = wave_reserve(&cnt[1], cu);
+	(void)wave_reserve(&cnt[2], ck);
+	for (int j = 0; j < kRun; j++) {
+		const size_t s = s0 + j;
+		if (what[j] & 1) ref[ar++] = ids[s];
+		if (what[j] & 2) part[ap++] = uint32_t(s) | (uint32_t(runk[j]) << 28);
+		if (what[j] & 8) unref[au++] = ids[s];
 	}
 }
 
@@ -977,7 +1009,8 @@ AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint
 	part.alloc(n);
 	cnt.alloc(4);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
-	adv_requests_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, slot_ids, band, n, ref.p, unref.p, part.p, cnt.p);
+	adv_requests_kernel<<<unsigned((n + 256 * 8 - 1) / (256 * 8)), 256, 0, s>>>(m, slot_ids, band, n, ref.p, unref.p,
+	                                                                        part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	HIP_CHECK(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -84,6 +84,16 @@ DX_HD int map_indices(const MapCtx& m, uint64_t cell, uint64_t& x, uint64_t& y, 
 	uint64_t c = cell - m.first[l];
 	const int sh = m.R - l;
 	const uint64_t lx = m.len[0] << l, ly = m.len[1] << l;
+	if (((c | lx | ly) >> 32) == 0) {
+		// 32-bit division when the operands fit (exact, a fraction of the
+		// instructions of the 64-bit expansion on the device)
+		const uint32_t c32 = uint32_t(c), lx32 = uint32_t(lx), ly32 = uint32_t(ly);
+		const uint32_t q = c32 / lx32, q2 = q / ly32;
+		x = uint64_t(c32 - q * lx32) << sh;
+		y = uint64_t(q - q2 * ly32) << sh;
+		z = uint64_t(q2) << sh;
+		return l;
+	}
 	const uint64_t q = c / lx;
 	x = (c - q * lx) << sh;
 	const uint64_t q2 = q / ly;

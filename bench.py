@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--base", type=int, default=None,
-                   help="level-0 cells per dimension per GPU (default 128; poisson 256)")
+                   help="level-0 cells per dimension per GPU (default 128; poisson 384)")
     p.add_argument("--max-ref-lvl", type=int, default=2)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -284,11 +284,13 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
 # ---------------------------------------------------------------------------- Poisson (config 4)
 def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """BASELINE config 4: Poisson BiCG (tests/poisson/poisson3d.cpp) on a
-    256^3-base grid per GPU (cell lengths 2pi/n, pi/n, 8pi/n), periodic,
+    384^3-base grid per GPU (cell lengths 2pi/n, pi/n, 8pi/n), periodic,
     refined twice around (pi, pi/2, 4pi); one step = one BiCG iteration over
     every solve cell (min = max = steps iterations, as SURVEY §8(d)).  The
     timed kernels of an iteration run from its first phase to its last, the
-    two global reductions included."""
+    two global reductions included.  At 384^3 (56.6 M cells) every solver
+    vector is 453 MB, so no phase finds its operands in the 256 MiB Infinity
+    Cache beyond what the previous phase just wrote."""
     import math
 
     n = a.base
@@ -324,7 +326,9 @@ def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     it, resid = res["r"]
     n_solve = ids.size
     mx, sm = reduce_stats(torch, dist, world, [el, float(n_solve), kms])
-    per_cell = 272 + 48  # SURVEY §8(d) 3-phase minimum + the face table read by phases A and B
+    # SURVEY §8(d) 3-phase minimum (34 fp64 accesses) + the 24-B face table read by
+    # phases A and B; split per kernel in scripts/roofline_summary.py (A 112, B 160, C 48)
+    per_cell = 272 + 48
     ach = per_cell * n_solve * it / (kms / 1e3) / 1e9 if kms > 0 else None
     if rank == 0:
         line = line_base("cell-updates/s, Poisson BiCG iterations (BASELINE config 4)", sm[1] * it / mx[0], world, a,
@@ -630,7 +634,7 @@ def main():
     if a.base is None:
         # Poisson at 256^3 per GPU: one phase's working set (~1.5 GB) is far
         # above the 256 MiB Infinity Cache, so its rate is an HBM rate
-        a.base = 256 if a.workload == "poisson" else 128
+        a.base = 384 if a.workload == "poisson" else 128
     import torch
     import torch.distributed as dist
 

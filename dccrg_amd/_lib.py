@@ -98,6 +98,10 @@ _SIGS = {
     "dccrgx_halo_place": (C.c_int, [vp, C.c_int, C.c_int, vp, sz]),
     "dccrgx_save_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, vp, sz]),
     "dccrgx_load_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, sz]),
+    "dccrgx_start_loading_grid_data": (C.c_int, [vp, C.c_char_p, C.c_uint64, sz]),
+    "dccrgx_continue_loading_grid_data": (C.c_int, [vp, C.c_int, vp]),
+    "dccrgx_finish_loading_grid_data": (C.c_int, [vp]),
+    "dccrgx_grid_file_bytes_left": (C.c_int, [vp, vp]),
     "dccrgx_add_neighborhood": (C.c_int, [vp, C.c_int, vp, sz]),
     "dccrgx_remove_neighborhood": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_user_neighbors": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_int, vp, vp, sz, P(sz)]),

@@ -278,7 +278,8 @@ static PoScalars po_solve(Grid& g, const PoParams& prm, bool failsafe) {
 // cell (uint64 id, uint64 absolute byte offset of its data) rank by rank,
 // then the cell data in the same order.  A cell's data = the payload of
 // every transferred field, in field order (the reference writes what
-// get_mpi_datatype describes at save time).  Cells of a rank in ascending id
+// get_mpi_datatype describes at save time: a fixed-size field's window, a
+// variable-size field's bytes of the cell).  Cells of a rank in ascending id
 // (the reference: get_cells() order).  Every rank writes its own records with
 // pwrite at offsets derived from the all-gathered per-rank cell counts.
 static constexpr uint64_t kEndianCheck = 0x1234567890abcdefULL;
@@ -331,18 +332,40 @@ struct Closer {
 	~Closer() { ::close(fd); }
 };
 
+// The bytes a field adds to one cell's record: a fixed-size field the window
+// its get_mpi_datatype describes (the whole element by default), a
+// variable-size field the cell's own bytes (save_grid_data writes what each
+// cell's datatype describes, 1521-1540; padding is not written, 1529).
 static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const void* header, size_t header_bytes) {
 	DX_REQUIRE(g.initialized, "not initialized");
-	DX_REQUIRE(var_transfer_fields(g).empty(), "grid files hold fixed-size payloads only");
 	const std::vector<Field*> tf = transfer_fields(g);
-	size_t bpc = 0;
-	for (Field* f : tf) bpc += f->elem;
-	const auto cnt = comm_allgather_u64(g, {uint64_t(g.n_local)});
-	uint64_t total = 0, before = 0;
+	const size_t nl = g.n_local;
+	// the local slots' payloads on the host, and each cell's record length
+	std::vector<std::vector<uint8_t>> host(tf.size());
+	std::vector<std::vector<uint64_t>> voff(tf.size());
+	std::vector<uint64_t> rec(nl, 0);
+	for (size_t k = 0; k < tf.size(); k++) {
+		const Field* f = tf[k];
+		if (f->var) {
+			voff[k] = download(f->voff.p, nl + 1, g.s_comp);
+			host[k] = download(f->data.p + voff[k][0], voff[k][nl] - voff[k][0], g.s_comp);
+			for (size_t s = 0; s < nl; s++) rec[s] += voff[k][s + 1] - voff[k][s];
+		} else {
+			host[k] = download(f->data.p, nl * f->elem, g.s_comp);
+			for (size_t s = 0; s < nl; s++) rec[s] += f->win_len;
+		}
+	}
+	const uint64_t mine = std::accumulate(rec.begin(), rec.end(), uint64_t(0));
+	const auto cnt = comm_allgather_u64(g, {uint64_t(nl), mine});
+	uint64_t total = 0, before = 0, bytes_before = 0;
 	for (int p = 0; p < g.size; p++) {
-		const uint64_t c = cnt[size_t(p)].empty() ? 0 : cnt[size_t(p)][0];
-		if (p < g.rank) before += c;
-		total += c;
+		const auto& c = cnt[size_t(p)];
+		DX_REQUIRE(c.size() == 2, "grid file: inconsistent cell counts");
+		if (p < g.rank) {
+			before += c[0];
+			bytes_before += c[1];
+		}
+		total += c[0];
 	}
 	const int fd = ::open(path, O_CREAT | O_WRONLY, 0644);
 	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
@@ -357,37 +380,44 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 	off += block.size();
 	if (g.rank == 0) pwrite_all(fd, &total, 8, off);
 	off += 8;
-	const uint64_t list0 = off, data0 = off + 16 * total;
+	const uint64_t list0 = off, data0 = off + 16 * total + bytes_before;
 	// local cells ascending, with their slots
-	const size_t nl = g.n_local;
 	const auto& sid = slot_ids_host(g);
 	std::vector<uint32_t> order(nl);
 	std::iota(order.begin(), order.end(), 0u);
 	std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sid[a] < sid[b]; });
 	std::vector<uint64_t> list(2 * nl);
+	std::vector<uint8_t> data(mine);
+	uint64_t at = 0;
 	for (size_t i = 0; i < nl; i++) {
-		list[2 * i] = sid[order[i]];
-		list[2 * i + 1] = data0 + bpc * (before + i);
+		const size_t s = order[i];
+		list[2 * i] = sid[s];
+		list[2 * i + 1] = data0 + at;
+		for (size_t k = 0; k < tf.size(); k++) {
+			const Field* f = tf[k];
+			if (f->var) {
+				const uint64_t a = voff[k][s] - voff[k][0], n = voff[k][s + 1] - voff[k][s];
+				if (n) std::memcpy(&data[at], &host[k][a], n);
+				at += n;
+			} else {
+				if (f->win_len) std::memcpy(&data[at], &host[k][s * f->elem + f->win_off], f->win_len);
+				at += f->win_len;
+			}
+		}
 	}
 	if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
-	if (nl && bpc) {
-		std::vector<uint8_t> data(nl * bpc);
-		size_t fo = 0;
-		for (Field* f : tf) {
-			const std::vector<uint8_t> h = download(f->data.p, nl * f->elem, g.s_comp);
-			for (size_t i = 0; i < nl; i++) std::memcpy(&data[i * bpc + fo], &h[size_t(order[i]) * f->elem], f->elem);
-			fo += f->elem;
-		}
-		pwrite_all(fd, data.data(), data.size(), data0 + bpc * before);
-	}
+	if (mine) pwrite_all(fd, data.data(), data.size(), data0);
 }
 
-static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t header_bytes) {
+// start_loading_grid_data (1795-2083): the grid block and the cell list; every
+// local cell's record position, none of its payload
+static void start_load_impl(Grid& g, const char* path, uint64_t offset, size_t header_bytes) {
 	DX_REQUIRE(!g.initialized, "load_grid_data initializes the grid: call it instead of initialize");
-	DX_REQUIRE(var_transfer_fields(g).empty(), "grid files hold fixed-size payloads only");
 	const int fd = ::open(path, O_RDONLY);
 	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
 	Closer closer{fd};
+	const off_t file_end = ::lseek(fd, 0, SEEK_END);
+	DX_REQUIRE(file_end >= 0, "grid file size unknown");
 	uint64_t off = offset + header_bytes, endian = 0;
 	pread_all(fd, &endian, 8, off);
 	DX_REQUIRE(endian == kEndianCheck, "grid file endianness check failed");
@@ -424,17 +454,47 @@ static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t he
 	uint64_t total = 0;
 	pread_all(fd, &total, 8, off);
 	off += 8;
+	DX_REQUIRE(total <= (uint64_t(file_end) - off) / 16, "grid file truncated");
 	std::vector<uint64_t> list(2 * total);
 	if (total) pread_all(fd, list.data(), 16 * total, off);
-	std::vector<std::pair<uint64_t, uint64_t>> cells(total);
-	for (size_t i = 0; i < total; i++) cells[i] = {list[2 * i], list[2 * i + 1]};
+	const uint64_t data_start = off + 16 * total;
+	// a record ends where the next one starts, the last at the end of the
+	// file: in list order when the offsets never decrease along the list (the
+	// files save_grid_data writes, rank by rank, each rank's cells in the
+	// order of their data; empty records then stay empty), else in the order
+	// of the offsets
+	bool monotone = true;
+	for (size_t i = 0; i < total; i++) {
+		const uint64_t p = list[2 * i + 1];
+		DX_REQUIRE(p >= data_start && p <= uint64_t(file_end), "grid file: cell data out of range");
+		if (i && p < list[2 * i - 1]) monotone = false;
+	}
+	std::vector<uint64_t> starts(total);
+	for (size_t i = 0; i < total; i++) starts[i] = list[2 * i + 1];
+	std::sort(starts.begin(), starts.end());
+	struct Rec {
+		uint64_t id, pos, end;
+		bool operator<(const Rec& o) const { return id < o.id; }
+	};
+	std::vector<Rec> cells(total);
+	for (size_t i = 0; i < total; i++) {
+		const uint64_t p = list[2 * i + 1];
+		uint64_t e = uint64_t(file_end);
+		if (monotone) {
+			if (i + 1 < total) e = list[2 * i + 3];
+		} else {
+			auto nx = std::upper_bound(starts.begin(), starts.end(), p);
+			if (nx != starts.end()) e = *nx;
+		}
+		cells[i] = {list[2 * i], p, e};
+	}
 	std::sort(cells.begin(), cells.end());
 	// owners as load_cells (3647) produces them: the level-0 block
 	// partition (create_level_0_cells), refined cells inherit it
 	std::vector<uint64_t> ids(total);
 	std::vector<int32_t> own(total);
 	for (size_t i = 0; i < total; i++) {
-		ids[i] = cells[i].first;
+		ids[i] = cells[i].id;
 		DX_REQUIRE(i == 0 || ids[i] > ids[i - 1], "grid file lists a cell twice");
 		const uint64_t l0p = map_level0_parent(g.m, ids[i]);
 		DX_REQUIRE(l0p != error_cell, "grid file lists an invalid cell");
@@ -443,31 +503,114 @@ static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t he
 	Mesh nm;
 	mesh_from_global(g, nm, ids, own);
 	rebuild(g, nm);
-	// payloads of the local cells
-	const std::vector<Field*> tf = transfer_fields(g);
-	size_t bpc = 0;
-	for (Field* f : tf) bpc += f->elem;
 	const size_t nl = g.n_local;
-	if (!nl || !bpc) return;
 	const auto& sid = slot_ids_host(g);
-	std::vector<uint64_t> where(nl);
-	uint64_t lo = ~uint64_t(0), hi = 0;
+	g.load.pos.assign(nl, 0);
+	g.load.end.assign(nl, 0);
 	for (size_t i = 0; i < nl; i++) {
-		auto it = std::lower_bound(cells.begin(), cells.end(), std::make_pair(sid[i], uint64_t(0)));
-		DX_REQUIRE(it != cells.end() && it->first == sid[i], "local cell missing from grid file");
-		where[i] = it->second;
-		lo = std::min(lo, where[i]);
-		hi = std::max(hi, where[i] + bpc);
+		auto it = std::lower_bound(cells.begin(), cells.end(), Rec{sid[i], 0, 0});
+		DX_REQUIRE(it != cells.end() && it->id == sid[i], "local cell missing from grid file");
+		g.load.pos[i] = it->pos;
+		g.load.end[i] = it->end;
 	}
-	std::vector<uint8_t> raw(hi - lo);
-	pread_all(fd, raw.data(), raw.size(), lo);
-	size_t fo = 0;
-	for (Field* f : tf) {
-		std::vector<uint8_t> h(nl * f->elem);
-		for (size_t i = 0; i < nl; i++) std::memcpy(&h[i * f->elem], &raw[where[i] - lo + fo], f->elem);
-		HIP_CHECK(hipMemcpy(f->data.p, h.data(), h.size(), hipMemcpyHostToDevice));
-		fo += f->elem;
+	g.load.path = path;
+	g.load.active = true;
+}
+
+// continue_loading_grid_data (2112-2378): the next bytes of every local
+// cell's record into one field, from the cell's position on, which then
+// advances past them.  bytes[s]: the count for local slot s (a fixed-size
+// field: its window).  Reads coalesce records that lie close together.
+static void continue_load_impl(Grid& g, int fid, const uint64_t* sizes) {
+	DX_REQUIRE(g.load.active, "no grid file being loaded (start_loading_grid_data first)");
+	Field& f = field(g, fid);
+	const size_t nl = g.n_local;
+	DX_REQUIRE(g.load.pos.size() == nl, "the grid changed while loading a grid file");
+	DX_REQUIRE(!f.var || sizes || !nl, "a variable-size field needs the byte count of every local cell");
+	std::vector<uint64_t> bytes(nl);
+	for (size_t s = 0; s < nl; s++) {
+		bytes[s] = f.var ? sizes[s] : f.win_len;
+		DX_REQUIRE(bytes[s] <= g.load.end[s] - g.load.pos[s],
+		           "grid file: cell " + std::to_string(slot_ids_host(g)[s]) + " has fewer bytes left than requested");
 	}
+	const int fd = ::open(g.load.path.c_str(), O_RDONLY);
+	DX_REQUIRE(fd >= 0, "cannot open grid file " + g.load.path);
+	Closer closer{fd};
+	// slot order -> file order, then runs with gaps under 64 KiB read at once
+	std::vector<uint32_t> by_pos(nl);
+	std::iota(by_pos.begin(), by_pos.end(), 0u);
+	std::sort(by_pos.begin(), by_pos.end(), [&](uint32_t a, uint32_t b) { return g.load.pos[a] < g.load.pos[b]; });
+	std::vector<uint64_t> at(nl + 1, 0);  // the slot's bytes in `got` (slot order)
+	for (size_t s = 0; s < nl; s++) at[s + 1] = at[s] + bytes[s];
+	std::vector<uint8_t> got(at[nl]);
+	std::vector<uint8_t> run;
+	for (size_t i = 0; i < nl;) {
+		const uint64_t lo = g.load.pos[by_pos[i]];
+		uint64_t hi = lo + bytes[by_pos[i]];
+		size_t j = i + 1;
+		while (j < nl && g.load.pos[by_pos[j]] <= hi + 65536 && g.load.pos[by_pos[j]] - lo < (uint64_t(1) << 30)) {
+			hi = std::max(hi, g.load.pos[by_pos[j]] + bytes[by_pos[j]]);
+			j++;
+		}
+		if (hi > lo) {
+			run.resize(hi - lo);
+			pread_all(fd, run.data(), run.size(), lo);
+			for (size_t k = i; k < j; k++) {
+				const uint32_t s = by_pos[k];
+				if (bytes[s]) std::memcpy(&got[at[s]], &run[g.load.pos[s] - lo], bytes[s]);
+			}
+		}
+		i = j;
+	}
+	if (f.var) {
+		DBuf<uint64_t> all;
+		all.alloc(g.n_slots + 1);
+		var_sizes(f, nullptr, 0, g.n_slots, all.p, g.s_comp);
+		if (nl) HIP_CHECK(hipMemcpyAsync(all.p, bytes.data(), nl * 8, hipMemcpyHostToDevice, g.s_comp));
+		var_resize(f, g.n_slots, all.p, g.s_comp);
+		if (at[nl]) HIP_CHECK(hipMemcpy(f.data.p, got.data(), got.size(), hipMemcpyHostToDevice));
+	} else if (nl && f.win_len) {
+		// the window of every element; the rest of it keeps its bytes
+		std::vector<uint8_t> h = download(f.data.p, nl * f.elem, g.s_comp);
+		for (size_t s = 0; s < nl; s++) std::memcpy(&h[s * f.elem + f.win_off], &got[at[s]], f.win_len);
+		HIP_CHECK(hipMemcpy(f.data.p, h.data(), h.size(), hipMemcpyHostToDevice));
+	}
+	for (size_t s = 0; s < nl; s++) g.load.pos[s] += bytes[s];
+}
+
+// finish_loading_grid_data (2380-2400)
+static void finish_load_impl(Grid& g) {
+	g.load = Grid::FileLoad{};
+}
+
+// load_grid_data (1742-1790) = start, one continue over the transferred
+// fields in field order, finish.  A variable-size field takes what is left of
+// each record after the fixed-size fields that follow it, so at most one
+// variable-size field can be read this way (more need the split load with
+// the caller's byte counts, as the reference's multi-pass example
+// tests/restart/variable_cell_data.cpp does).
+static void load_grid_impl(Grid& g, const char* path, uint64_t offset, size_t header_bytes) {
+	DX_REQUIRE(var_transfer_fields(g).size() <= 1,
+	           "several variable-size fields: load with start / continue / finish_loading_grid_data");
+	start_load_impl(g, path, offset, header_bytes);
+	const std::vector<Field*> tf = transfer_fields(g);
+	for (size_t k = 0; k < tf.size(); k++) {
+		Field* f = tf[k];
+		if (!f->var) {
+			continue_load_impl(g, int(f - g.fields.data()), nullptr);
+			continue;
+		}
+		uint64_t after = 0;
+		for (size_t j = k + 1; j < tf.size(); j++) after += tf[j]->win_len;
+		std::vector<uint64_t> sz(g.n_local);
+		for (size_t s = 0; s < g.n_local; s++) {
+			const uint64_t left = g.load.end[s] - g.load.pos[s];
+			DX_REQUIRE(left >= after, "grid file: a cell's record is shorter than its fixed-size fields");
+			sz[s] = left - after;
+		}
+		continue_load_impl(g, int(f - g.fields.data()), sz.data());
+	}
+	finish_load_impl(g);
 }
 
 static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
@@ -1513,6 +1656,41 @@ int dccrgx_load_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, si
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		load_grid_impl(g, path, offset, header_bytes);
+		return 0;
+	});
+}
+
+int dccrgx_start_loading_grid_data(dccrgx_grid* gp, const char* path, uint64_t offset, size_t header_bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		start_load_impl(g, path, offset, header_bytes);
+		return 0;
+	});
+}
+
+int dccrgx_continue_loading_grid_data(dccrgx_grid* gp, int field_id, const uint64_t* sizes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		continue_load_impl(g, field_id, sizes);
+		return 0;
+	});
+}
+
+int dccrgx_finish_loading_grid_data(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.load.active, "no grid file being loaded");
+		finish_load_impl(g);
+		return 0;
+	});
+}
+
+int dccrgx_grid_file_bytes_left(dccrgx_grid* gp, uint64_t* bytes) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.load.active, "no grid file being loaded");
+		DX_REQUIRE(bytes || !g.n_local, "null pointer");
+		for (size_t s = 0; s < g.n_local; s++) bytes[s] = g.load.end[s] - g.load.pos[s];
 		return 0;
 	});
 }

@@ -420,6 +420,14 @@ struct Grid {
 	// merged into the sets above by flush_bulk_requests() before any call
 	// that consults the sets, and read directly by stop_refining
 	std::vector<uint64_t> refine_bulk, unrefine_bulk;
+	// a grid file being loaded in parts (start / continue / finish_loading_
+	// grid_data 1795-2400): per local slot the next unread byte of the cell's
+	// record and the record's end
+	struct FileLoad {
+		bool active = false;
+		std::string path;
+		std::vector<uint64_t> pos, end;
+	} load;
 	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
 	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
 	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)

@@ -19,8 +19,9 @@
 // fixed point (2^-16), every sum an integer: the result is a pure function of
 // the leaf set and the weights, bit-identical for any current distribution,
 // rank count of the input or summation order.  The ordered cut is a radix
-// select over 64-bit keys (center << id_bits | id), 8 bits per pass: one
-// device histogram per pass and group, summed over ranks.
+// select over the keys (center << id_bits | id; 64-bit when they fit, else
+// 128-bit), 8 bits per pass from the highest occupied byte: one device
+// histogram per pass and group, summed over ranks.
 #include <algorithm>
 
 #include "dccrgx_grid.hpp"
@@ -72,15 +73,20 @@ __global__ void rcb_bbox_kernel(const uint32_t* c2, const int32_t* lo, const int
 		if (sbox[k]) atomicMax(&box[k], sbox[k]);
 }
 
-__device__ __forceinline__ uint64_t rcb_key(const uint32_t* c2, const uint64_t* ids, size_t i, int axis, int id_bits) {
-	return (uint64_t(c2[3 * i + axis]) << id_bits) | ids[i];
+// K: uint64_t when center and id bits fit 64, else unsigned __int128 (a grid
+// at a refinement level near the id space's limit, set_maximum_refinement_
+// level(-1) on a small grid)
+template <class K>
+__device__ __forceinline__ K rcb_key(const uint32_t* c2, const uint64_t* ids, size_t i, int axis, int id_bits) {
+	return (K(c2[3 * i + axis]) << id_bits) | K(ids[i]);
 }
 
 // weight histogram of the next 8 key bits below `shift + 8` of the cells of
 // every active group whose key agrees with the group's prefix above them
+template <class K>
 __global__ void rcb_hist_kernel(const uint32_t* c2, const uint64_t* ids, const uint64_t* w, const int32_t* lo,
                                 const int32_t* hi, size_t n, const int32_t* group_of_lo, int G, const int32_t* axis,
-                                const uint64_t* prefix, int shift, int id_bits, unsigned long long* hist) {
+                                const K* prefix, int shift, bool first, int id_bits, unsigned long long* hist) {
 	extern __shared__ unsigned long long shist[];
 	const bool lds = G <= kMaxGroupsLds;
 	if (lds) {
@@ -90,8 +96,8 @@ __global__ void rcb_hist_kernel(const uint32_t* c2, const uint64_t* ids, const u
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		if (hi[i] - lo[i] < 2) continue;
 		const int gi = group_of_lo[lo[i]];
-		const uint64_t key = rcb_key(c2, ids, i, axis[gi], id_bits);
-		if (shift < 56 && (key >> (shift + 8)) != prefix[gi]) continue;
+		const K key = rcb_key<K>(c2, ids, i, axis[gi], id_bits);
+		if (!first && (key >> (shift + 8)) != prefix[gi]) continue;
 		const int b = int((key >> shift) & 0xff);
 		if (lds) atomicAdd(&shist[gi * kBins + b], (unsigned long long)w[i]);
 		else atomicAdd(&hist[gi * kBins + b], (unsigned long long)w[i]);
@@ -103,14 +109,15 @@ __global__ void rcb_hist_kernel(const uint32_t* c2, const uint64_t* ids, const u
 	}
 }
 
+template <class K>
 __global__ void rcb_assign_kernel(const uint32_t* c2, const uint64_t* ids, int32_t* lo, int32_t* hi, size_t n,
-                                  const int32_t* group_of_lo, const int32_t* axis, const uint64_t* cut, int id_bits) {
+                                  const int32_t* group_of_lo, const int32_t* axis, const K* cut, int id_bits) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const int32_t l = lo[i], h = hi[i];
 		if (h - l < 2) continue;
 		const int gi = group_of_lo[l];
 		const int32_t mid = l + (h - l) / 2;
-		if (rcb_key(c2, ids, i, axis[gi], id_bits) < cut[gi]) hi[i] = mid;
+		if (rcb_key<K>(c2, ids, i, axis[gi], id_bits) < cut[gi]) hi[i] = mid;
 		else lo[i] = mid;
 	}
 }
@@ -133,57 +140,20 @@ void allreduce_u64(Grid& g, std::vector<uint64_t>& v, bool max) {
 	}
 }
 
-}  // namespace
-
-void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& owners) {
-	DX_REQUIRE(g.initialized, "not initialized");
-	if (g.size > 1) comm_require(g, "balance_load");
+// the bisection levels: every group's cut by a radix select over the keys
+// (center << id_bits | id), 8 bits per pass from the highest occupied byte
+template <class K>
+void rcb_levels(Grid& g, size_t n, DBuf<uint32_t>& c2, DBuf<int32_t>& lo, DBuf<int32_t>& hi, DBuf<uint64_t>& w,
+                int id_bits, int key_bits) {
 	hipStream_t s = g.s_comp;
-	const size_t n = g.n_local;
 	const int P = g.size;
-	const int id_bits = bits_for(g.m.last);
-	uint64_t cmax = 0;
-	for (int d = 0; d < 3; d++) cmax = std::max(cmax, 2 * g.m.glen[d]);
-	DX_REQUIRE(bits_for(cmax) + id_bits <= 64, "grid too large for the partitioner's 64-bit keys");
-	DX_REQUIRE(cmax < (uint64_t(1) << 32), "grid too large for the partitioner's 32-bit centers");
-
-	DBuf<uint32_t> c2;
-	DBuf<int32_t> lo, hi;
-	DBuf<uint64_t> w;
-	c2.alloc(3 * n + 3);
-	lo.alloc(n + 1);
-	hi.alloc(n + 1);
-	w.alloc(n + 1);
-	if (n) {
-		rcb_init_kernel<<<grid_for(n, 256), 256, 0, s>>>(g.m, g.slot_ids.p, n, c2.p, lo.p, hi.p, w.p, P);
-		HIP_CHECK(hipGetLastError());
-	}
-	// user weights (set_cell_weight), fixed point
-	if (!g.weights.empty()) {
-		std::vector<int32_t> sl;
-		std::vector<uint64_t> wv;
-		for (const auto& kv : g.weights) {
-			const int64_t sidx = host_slot_of(g, kv.first);
-			if (sidx < 0 || size_t(sidx) >= n) continue;
-			sl.push_back(int32_t(sidx));
-			wv.push_back(uint64_t(std::llround(kv.second * kWeightOne)));
-		}
-		if (!sl.empty()) {
-			DBuf<int32_t> dsl;
-			DBuf<uint64_t> dwv;
-			upload(dsl, sl, s);
-			upload(dwv, wv, s);
-			rcb_set_weights_kernel<<<grid_for(sl.size(), 256), 256, 0, s>>>(dsl.p, dwv.p, sl.size(), w.p);
-			HIP_CHECK(hipGetLastError());
-		}
-	}
-
+	const int top = ((key_bits + 7) / 8) * 8 - 8;
 	// the process tree is known to every rank: groups of a level are the
 	// ranges of size > 1 produced by halving the previous level's ranges
 	std::vector<std::pair<int, int>> groups;
 	if (P > 1) groups.push_back({0, P});
 	DBuf<int32_t> d_group_of_lo, d_axis;
-	DBuf<uint64_t> d_prefix, d_cut;
+	DBuf<K> d_prefix, d_cut;
 	DBuf<unsigned int> d_box;
 	DBuf<unsigned long long> d_hist;
 	d_group_of_lo.alloc(size_t(P) + 1);
@@ -219,16 +189,17 @@ void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& 
 		upload(d_axis, axis, s);
 
 		// radix select of every group's cut key, 8 bits per pass, high first
-		std::vector<uint64_t> prefix(size_t(G), 0), target(size_t(G), 0);
+		std::vector<K> prefix(size_t(G), 0);
+		std::vector<uint64_t> target(size_t(G), 0);
 		d_hist.alloc(size_t(G) * kBins);
-		for (int shift = 56; shift >= 0; shift -= 8) {
+		for (int shift = top; shift >= 0; shift -= 8) {
 			upload(d_prefix, prefix, s);
 			HIP_CHECK(hipMemsetAsync(d_hist.p, 0, size_t(G) * kBins * 8, s));
 			if (n) {
 				const size_t lds = G <= kMaxGroupsLds ? size_t(G) * kBins * 8 : 0;
-				rcb_hist_kernel<<<grid_for(n, 256, 1024), 256, lds, s>>>(c2.p, g.slot_ids.p, w.p, lo.p, hi.p, n,
-				                                                        d_group_of_lo.p, G, d_axis.p, d_prefix.p,
-				                                                        shift, id_bits, d_hist.p);
+				rcb_hist_kernel<K><<<grid_for(n, 256, 1024), 256, lds, s>>>(c2.p, g.slot_ids.p, w.p, lo.p, hi.p, n,
+				                                                           d_group_of_lo.p, G, d_axis.p, d_prefix.p,
+				                                                           shift, shift == top, id_bits, d_hist.p);
 				HIP_CHECK(hipGetLastError());
 			}
 			std::vector<unsigned long long> h64 = download(d_hist.p, size_t(G) * kBins, s);
@@ -236,7 +207,7 @@ void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& 
 			allreduce_u64(g, hist, false);
 			for (int k = 0; k < G; k++) {
 				const uint64_t* hk = hist.data() + size_t(k) * kBins;
-				if (shift == 56) {  // the group's total weight -> its target
+				if (shift == top) {  // the group's total weight -> its target
 					unsigned __int128 W = 0;
 					for (int b = 0; b < kBins; b++) W += hk[b];
 					const int gp = groups[size_t(k)].second - groups[size_t(k)].first;
@@ -250,14 +221,14 @@ void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& 
 					cum += hk[b];
 				}
 				target[size_t(k)] -= cum;
-				prefix[size_t(k)] = (prefix[size_t(k)] << 8) | uint64_t(b);
+				prefix[size_t(k)] = (prefix[size_t(k)] << 8) | K(b);
 			}
 		}
 		// prefix now holds each group's cut key K: keys < K go to the lower half
 		upload(d_cut, prefix, s);
 		if (n) {
-			rcb_assign_kernel<<<grid_for(n, 256), 256, 0, s>>>(c2.p, g.slot_ids.p, lo.p, hi.p, n, d_group_of_lo.p,
-			                                                   d_axis.p, d_cut.p, id_bits);
+			rcb_assign_kernel<K><<<grid_for(n, 256), 256, 0, s>>>(c2.p, g.slot_ids.p, lo.p, hi.p, n, d_group_of_lo.p,
+			                                                      d_axis.p, d_cut.p, id_bits);
 			HIP_CHECK(hipGetLastError());
 		}
 		std::vector<std::pair<int, int>> next;
@@ -268,6 +239,55 @@ void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& 
 		}
 		groups.swap(next);
 	}
+}
+
+}  // namespace
+
+void rcb_partition(Grid& g, std::vector<uint64_t>& cells, std::vector<int32_t>& owners) {
+	DX_REQUIRE(g.initialized, "not initialized");
+	if (g.size > 1) comm_require(g, "balance_load");
+	hipStream_t s = g.s_comp;
+	const size_t n = g.n_local;
+	const int P = g.size;
+	const int id_bits = bits_for(g.m.last);
+	uint64_t cmax = 0;
+	for (int d = 0; d < 3; d++) cmax = std::max(cmax, 2 * g.m.glen[d]);
+	DX_REQUIRE(cmax < (uint64_t(1) << 32), "grid too large for the partitioner's 32-bit centers");
+
+	DBuf<uint32_t> c2;
+	DBuf<int32_t> lo, hi;
+	DBuf<uint64_t> w;
+	c2.alloc(3 * n + 3);
+	lo.alloc(n + 1);
+	hi.alloc(n + 1);
+	w.alloc(n + 1);
+	if (n) {
+		rcb_init_kernel<<<grid_for(n, 256), 256, 0, s>>>(g.m, g.slot_ids.p, n, c2.p, lo.p, hi.p, w.p, P);
+		HIP_CHECK(hipGetLastError());
+	}
+	// user weights (set_cell_weight), fixed point
+	if (!g.weights.empty()) {
+		std::vector<int32_t> sl;
+		std::vector<uint64_t> wv;
+		for (const auto& kv : g.weights) {
+			const int64_t sidx = host_slot_of(g, kv.first);
+			if (sidx < 0 || size_t(sidx) >= n) continue;
+			sl.push_back(int32_t(sidx));
+			wv.push_back(uint64_t(std::llround(kv.second * kWeightOne)));
+		}
+		if (!sl.empty()) {
+			DBuf<int32_t> dsl;
+			DBuf<uint64_t> dwv;
+			upload(dsl, sl, s);
+			upload(dwv, wv, s);
+			rcb_set_weights_kernel<<<grid_for(sl.size(), 256), 256, 0, s>>>(dsl.p, dwv.p, sl.size(), w.p);
+			HIP_CHECK(hipGetLastError());
+		}
+	}
+
+	const int key_bits = bits_for(cmax) + id_bits;
+	if (key_bits <= 64) rcb_levels<uint64_t>(g, n, c2, lo, hi, w, id_bits, key_bits);
+	else rcb_levels<unsigned __int128>(g, n, c2, lo, hi, w, id_bits, key_bits);
 	HIP_CHECK(hipStreamSynchronize(s));
 	// local cells ascending with their new owners
 	const std::vector<uint64_t> ids = download(g.slot_ids.p, n, s);

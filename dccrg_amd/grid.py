@@ -660,8 +660,38 @@ class Dccrg:
 
     def load_grid_data(self, path, offset=0, header_bytes=0):
         """Initializes this grid from a file written by save_grid_data (call
-        instead of initialize, after registering the same transferred fields)."""
+        instead of initialize, after registering the same transferred fields;
+        a variable-size field, at most one, takes the rest of each record)."""
         check(lib().dccrgx_load_grid_data(self.h, str(path).encode(), int(offset), int(header_bytes)))
+        return self
+
+    def start_loading_grid_data(self, path, offset=0, header_bytes=0):
+        """start_loading_grid_data (dccrg.hpp:1795): the grid and its cells
+        from the file, no payload; then continue_loading_grid_data per part
+        of the records, then finish_loading_grid_data."""
+        check(lib().dccrgx_start_loading_grid_data(self.h, str(path).encode(), int(offset), int(header_bytes)))
+        return self
+
+    def continue_loading_grid_data(self, field, counts=None):
+        """continue_loading_grid_data (2112): the next bytes of every local
+        cell's record into `field` - a fixed-size field its window, a
+        variable-size one `counts[s]` elements for local slot s."""
+        if isinstance(field, VariableField):
+            b = np.ascontiguousarray(np.asarray(counts, np.uint64) * np.uint64(field.dtype.itemsize))
+            if b.size != self.n_local:
+                raise ValueError("one element count per local cell")
+            check(lib().dccrgx_continue_loading_grid_data(self.h, field.id, _ptr(b)))
+        else:
+            check(lib().dccrgx_continue_loading_grid_data(self.h, field.id, None))
+        return self
+
+    def grid_file_bytes_left(self):
+        out = np.empty(self.n_local, np.uint64)
+        check(lib().dccrgx_grid_file_bytes_left(self.h, _ptr(out)))
+        return out
+
+    def finish_loading_grid_data(self):  # 2380
+        check(lib().dccrgx_finish_loading_grid_data(self.h))
         return self
 
     # ---- fields ---------------------------------------------------------------

@@ -735,6 +735,12 @@ public:
 	bool pin(const uint64_t cell) { return pin(cell, rank_); }
 	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
 	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
+	// 5952: unpin every local cell
+	bool unpin_local_cells() {
+		bool ok = true;
+		for (size_t s = 0; s < n_local_ && s < slot_ids_.size(); s++) ok = unpin(slot_ids_[s]) && ok;
+		return ok;
+	}
 	Dccrg& balance_load(const bool use_zoltan = true) {
 		initialize_balance_load(use_zoltan);
 		continue_balance_load();
@@ -776,26 +782,98 @@ public:
 	// constructed) after every structural change
 	void allocate_copies_of_remote_neighbors(const int = default_neighborhood_id) {}
 
-	// ---- grid files (1089, 1742) --------------------------------------------------------
-	// the header is raw bytes (the reference takes (void*, count, MPI_Datatype))
+	// ---- grid files (1089, 1742, 1795, 2112, 2380) --------------------------------------
+	// raw-byte header form
 	bool save_grid_data(const std::string& name, const uint64_t offset, const void* header = nullptr,
 	                    const size_t header_bytes = 0) {
-		if (serialized_) return false;  // files of fixed-size payloads only
 		upload_local();
 		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
+	}
+	// the reference's form: the header is (address, count, datatype), written
+	// by process 0 as MPI packs it (native layout, no padding)
+	bool save_grid_data(const std::string& name, const MPI_Offset offset, std::tuple<void*, int, MPI_Datatype> header) {
+		const std::vector<char> h = pack_header(header);
+		return save_grid_data(name, uint64_t(offset), h.data(), h.size());
 	}
 	// replaces initialize(): every setting comes from the file
 	bool load_grid_data(const std::string& name, const uint64_t offset, const MPI_Comm& comm,
 	                    const size_t header_bytes = 0) {
-		if (g_) throw std::invalid_argument("dccrg: already initialized");
-		create(comm);
-		add_payload_field();
-		if (dccrgx_load_grid_data(g_, name.c_str(), offset, header_bytes) != DCCRGX_OK) return false;
-		int R = 0;
-		detail::check(dccrgx_get_maximum_refinement_level(g_, &R));
-		max_ref_ = R;
-		refresh();
-		download_all();
+		if (!start_loading(name, offset, comm, header_bytes)) return false;
+		if (!continue_loading_grid_data()) return false;
+		return finish_loading_grid_data();
+	}
+	bool load_grid_data(const std::string& name, const MPI_Offset offset, std::tuple<void*, int, MPI_Datatype> header,
+	                    const MPI_Comm& comm, const char* const load_balancing_method = "RCB",
+	                    const uint64_t = 1, const uint64_t = ~uint64_t(0)) {
+		if (!start_loading_grid_data(name, offset, header, comm, load_balancing_method)) return false;
+		if (!continue_loading_grid_data()) return false;
+		return finish_loading_grid_data();
+	}
+	// start_loading_grid_data (1795): the grid, its cells and the header; the
+	// cells' data come with continue_loading_grid_data
+	bool start_loading_grid_data(const std::string& name, const MPI_Offset offset,
+	                             std::tuple<void*, int, MPI_Datatype> header, const MPI_Comm& comm,
+	                             const char* const load_balancing_method = "RCB", const uint64_t = 1,
+	                             const uint64_t = ~uint64_t(0)) {
+		const size_t hb = pack_header(header).size();
+		if (!start_loading(name, uint64_t(offset), comm, hb)) return false;
+		if (load_balancing_method) set_load_balancing_method(load_balancing_method);
+		if (hb) {
+			// the header as process 0 wrote it, into the caller's object
+			std::vector<char> h(hb);
+			std::FILE* f = std::fopen(name.c_str(), "rb");
+			const bool ok = f && std::fseek(f, long(offset), SEEK_SET) == 0 && std::fread(h.data(), 1, hb, f) == hb;
+			if (f) std::fclose(f);
+			if (!ok) return false;
+			MPI_Datatype t = std::get<2>(header);
+			int pos = 0;
+			MPI_Unpack(h.data(), int(hb), &pos, std::get<0>(header), std::get<1>(header), t, comm_);
+		}
+		return true;
+	}
+	// continue_loading_grid_data (2112): for every local cell the bytes its
+	// get_mpi_datatype describes now (receiving, from process -1), read from
+	// where the previous call stopped
+	bool continue_loading_grid_data() {
+		const size_t nl = n_local_;
+		if constexpr (serialized_) {
+			std::vector<uint64_t> sizes(nl);
+			for (size_t s = 0; s < nl; s++) {
+				auto dt = detail::cell_datatype(host_[s], slot_ids_[s], -1, rank_, true, -1, 0);
+				int sz = 0;
+				MPI_Type_size(std::get<2>(dt), &sz);
+				sizes[s] = uint64_t(std::get<1>(dt)) * uint64_t(sz);
+				if (!detail::is_named_datatype(std::get<2>(dt))) {
+					MPI_Datatype t = std::get<2>(dt);
+					MPI_Type_free(&t);
+				}
+			}
+			if (dccrgx_continue_loading_grid_data(g_, payload_, sizes.data()) != DCCRGX_OK) return false;
+			for (size_t s = 0; s < nl; s++) {
+				uint64_t sz = 0;
+				detail::check(dccrgx_variable_field_sizes(g_, payload_, s, 1, &sz));
+				std::vector<char> bytes(size_t(sz) + 1);
+				size_t got = 0;
+				detail::check(dccrgx_variable_field_download(g_, payload_, s, 1, bytes.data(), bytes.size(), &got));
+				detail::unpack_cell(host_[s], slot_ids_[s], -1, rank_, -1, comm_, bytes.data(), got);
+			}
+			return true;
+		}
+		sync_window();
+		if (dccrgx_continue_loading_grid_data(g_, payload_, nullptr) != DCCRGX_OK) return false;
+		if (nl) {
+			std::vector<Cell_Data> tmp(nl);
+			detail::check(dccrgx_field_download(g_, payload_, 0, nl, tmp.data()));
+			for (size_t s = 0; s < nl; s++)
+				std::memcpy(reinterpret_cast<char*>(&host_[s]) + window_.first,
+				            reinterpret_cast<const char*>(&tmp[s]) + window_.first, window_.second);
+		}
+		return true;
+	}
+	// finish_loading_grid_data (2380): the device payloads take the loaded objects
+	bool finish_loading_grid_data() {
+		if (dccrgx_finish_loading_grid_data(g_) != DCCRGX_OK) return false;
+		upload_local();
 		return true;
 	}
 
@@ -833,6 +911,32 @@ private:
 		}
 	}
 
+	std::vector<char> pack_header(std::tuple<void*, int, MPI_Datatype> header) const {
+		std::vector<char> out;
+		MPI_Datatype t = std::get<2>(header);
+		int sz = 0;
+		MPI_Type_size(t, &sz);
+		const size_t bytes = size_t(std::get<1>(header)) * size_t(sz);
+		if (!bytes) return out;
+		int bound = 0;
+		MPI_Pack_size(std::get<1>(header), t, comm_, &bound);
+		out.resize(size_t(bound));
+		int pos = 0;
+		MPI_Pack(std::get<0>(header), std::get<1>(header), t, out.data(), bound, &pos, comm_);
+		out.resize(size_t(pos));
+		return out;
+	}
+	bool start_loading(const std::string& name, const uint64_t offset, const MPI_Comm& comm, const size_t header_bytes) {
+		if (g_) throw std::invalid_argument("dccrg: already initialized");
+		create(comm);
+		add_payload_field();
+		if (dccrgx_start_loading_grid_data(g_, name.c_str(), offset, header_bytes) != DCCRGX_OK) return false;
+		int R = 0;
+		detail::check(dccrgx_get_maximum_refinement_level(g_, &R));
+		max_ref_ = R;
+		refresh();
+		return true;
+	}
 	void create(const MPI_Comm& comm) {
 		MPI_Comm_dup(comm, &comm_);
 		MPI_Comm_rank(comm_, &rank_);

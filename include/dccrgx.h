@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 5 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 6 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -216,14 +216,31 @@ int dccrgx_update_copies_of_remote_neighbors_hood(dccrgx_grid* g, int id);
 /* ---- grid files (save_grid_data 1089-1740, load_grid_data 1742-2425;
  * layout 1104-1120).  save: every rank calls it with the same arguments;
  * rank 0 writes the header bytes at `offset`, every rank its cells' records
- * and data (the payloads of the transferred fields, in field order).  load:
- * on a created, not yet initialized grid whose transferred fields are
+ * and data: per cell the payloads of the transferred fields in field order,
+ * a fixed-size field's window (dccrgx_set_field_window; what the cell's
+ * get_mpi_datatype describes) and a variable-size field's bytes of the cell.
+ * load: on a created, not yet initialized grid whose transferred fields are
  * registered as at save time; initializes the grid from the file (length,
  * refinement level, neighborhood length, periodicity, geometry), creates the
  * file's cells with the level-0 block partition inherited by children, and
- * reads the local cells' payloads. */
+ * reads the local cells' payloads; a variable-size field (at most one) takes
+ * the rest of each record after the fixed-size fields that follow it. */
 int dccrgx_save_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, const void* header, size_t header_bytes);
 int dccrgx_load_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, size_t header_bytes);
+/* the split load (start_loading_grid_data 1795, continue_loading_grid_data
+ * 2112, finish_loading_grid_data 2380), for records whose layout the caller
+ * learns from their first bytes (tests/restart/variable_cell_data.cpp):
+ * start initializes the grid and its cells as load does and reads no
+ * payload; each continue reads the next bytes of every local cell's record
+ * into one field and advances the cell's position past them - a fixed-size
+ * field its window (sizes NULL), a variable-size field sizes[s] bytes for
+ * local slot s (its cells take those sizes); a request beyond a record's end
+ * returns DCCRGX_EINVAL.  bytes_left: per local slot, the unread bytes of its
+ * record.  Nothing else may change the grid between start and finish. */
+int dccrgx_start_loading_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, size_t header_bytes);
+int dccrgx_continue_loading_grid_data(dccrgx_grid* g, int field_id, const uint64_t* sizes);
+int dccrgx_finish_loading_grid_data(dccrgx_grid* g);
+int dccrgx_grid_file_bytes_left(dccrgx_grid* g, uint64_t* bytes);
 
 /* ---- partition (pin 5832/5859, unpin 5909, balance_load 1024 and its
  * split form initialize_balance_load 3746 / continue_balance_load 3899 /

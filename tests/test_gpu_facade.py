@@ -136,3 +136,40 @@ def test_reference_variable_neighbour_data(gpu, P):
                 else:
                     assert part == own or part == [0.0] * n, (k, c, n, vals)
             assert rest == []
+
+
+@pytest.mark.parametrize("Ps,Pl", [(1, 1), (3, 2), (2, 3)])
+def test_variable_restart(gpu, tmp_path, Ps, Pl):
+    """Grid files of variable-size payloads through the facade, the scenario
+    of tests/restart/variable_cell_data.cpp (examples/variable_restart.cpp:
+    20 x 1 x 1 cells holding `id` ints behind a uint64 count, none when
+    id % 4 == 0).  Saved by Ps processes after the cells of every third one
+    moved on (an empty rank at Ps = 3), the file is the reference's layout
+    (save_grid_data 1089-1740: endianness word, grid block, cell list, then
+    each cell's bytes as its datatype describes them, no padding, back to
+    back); loaded by Pl processes in two passes (start / continue x2 /
+    finish_loading_grid_data), every cell holds its own data, also after a
+    balance moves the loaded payloads."""
+    import struct
+
+    path = tmp_path / "variable_cell_data.dc"
+    out = mpirun("variable_restart", Ps, ["save", path])
+    assert out.count("PASS") == Ps, out
+    raw = open(path, "rb").read()
+    assert struct.unpack_from("<Q", raw, 0)[0] == 0x1234567890ABCDEF
+    R = struct.unpack_from("<i", raw, 8 + 24)[0]
+    assert raw[8:8 + 87] == O.grid_block_bytes((20, 1, 1), R, 1, (False, False, False), (0, 0, 0), (1, 1, 1))
+    total = struct.unpack_from("<Q", raw, 95)[0]
+    assert total == 20
+    lst = np.frombuffer(raw, "<u8", 2 * total, 103).reshape(-1, 2)
+    assert sorted(lst[:, 0].tolist()) == list(range(1, 21))
+    pos = 103 + 16 * total
+    for cid, off in sorted(lst.tolist(), key=lambda r: r[1]):
+        n = cid if cid % 4 else 0
+        rec = struct.pack("<Q", n) + np.arange(n, dtype="<i4").tobytes()
+        assert off == pos and raw[off:off + len(rec)] == rec, cid
+        pos += len(rec)
+    assert pos == len(raw)
+    out = mpirun("variable_restart", Pl, ["load", path])
+    assert out.count("PASS") == Pl, out
+    assert sum(int(m) for m in re.findall(r"PASS \d+ (\d+)", out)) == 20

@@ -95,3 +95,117 @@ def test_load_rejects_bad_files(gpu, tmp_path):
         with pytest.raises(dccrg_amd.DccrgError, match="grid file"):
             h.load_grid_data(p)
         h.close()
+
+
+def _counts(ids):
+    """tests/restart/variable_cell_data.cpp's cells: id ints (0 .. id - 1) in
+    every cell whose id is not a multiple of 4, none in the others (here
+    modulo 23, so refined cells stay small)."""
+    return np.where(ids % 4 != 0, ids % 23, 0).astype(np.uint64)
+
+
+def _var_record(cid):
+    n = (cid % 23) if cid % 4 else 0
+    return (np.array([n], np.uint64).tobytes() + np.arange(n, dtype=np.int32).tobytes()
+            + np.array([cid * 0.5], np.float64).tobytes()[2:6])
+
+
+def _var_fields(g):
+    size = g.add_field("size", np.uint64)
+    data = g.add_variable_field("data", np.int32)
+    tail = g.add_field("tail", np.float64)
+    tail.set_window(2, 4)  # four bytes of each element (a datatype narrower than the object)
+    return size, data, tail
+
+
+def test_variable_payload_file_and_round_trip(gpu, tmp_path):
+    """save_grid_data of variable-size payloads (1521-1540: what each cell's
+    datatype describes, no padding): per cell the u64 count, its ints and a
+    4-byte window of an f64, byte for byte as the layout restatement; the
+    one-call load (one variable field: the rest of each record) and the split
+    load of tests/restart/variable_cell_data.cpp (the counts first, then the
+    ints sized from them: start / continue / finish_loading_grid_data 1795,
+    2112, 2380) both restore every payload."""
+    length, R = (5, 4, 3), 2
+    g, o = make_pair(length, R, (True, False, False), 1, 2, 0.25, 7)
+    g.set_geometry(*GEOM)
+    size, data, tail = _var_fields(g)
+    ids = g.slot_ids()[: g.n_local]
+    cnt = _counts(ids)
+    size.set(cnt)
+    data.set([np.arange(int(k), dtype=np.int32) for k in cnt])
+    tail.set(ids.astype(np.float64) * 0.5)
+    path = tmp_path / "var.dc"
+    g.save_grid_data(path, offset=8, header=b"hdr")
+    cells = g.local_cells()
+    exp = O.grid_file_bytes(O.grid_block_bytes(length, R, 1, (True, False, False), *GEOM), b"hdr", 8, [cells],
+                            _var_record)
+    assert open(path, "rb").read() == exp
+    assert cnt.sum() > 0 and (cnt == 0).any()
+
+    def check(h, sz, dt, tl):
+        hid = h.slot_ids()[: h.n_local]
+        assert np.array_equal(h.local_cells(), cells)
+        k = _counts(hid)
+        assert np.array_equal(sz.get(0, h.n_local), k)
+        got = dt.get(0, h.n_local)
+        assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32)) for a, n in zip(got, k))
+        want = np.zeros(h.n_local, np.float64)
+        wv, tv = want.view(np.uint8).reshape(-1, 8), (hid.astype(np.float64) * 0.5).view(np.uint8).reshape(-1, 8)
+        wv[:, 2:6] = tv[:, 2:6]
+        assert np.array_equal(tl.get(0, h.n_local).view(np.uint8), want.view(np.uint8))
+
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    f = _var_fields(h)
+    h.load_grid_data(path, offset=8, header_bytes=3)
+    check(h, *f)
+    h.close()
+
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    sz, dt, tl = _var_fields(h)
+    h.start_loading_grid_data(path, offset=8, header_bytes=3)
+    hid = h.slot_ids()[: h.n_local]
+    h.continue_loading_grid_data(sz)
+    k = sz.get(0, h.n_local)
+    assert np.array_equal(k, _counts(hid))
+    left = h.grid_file_bytes_left()
+    assert np.array_equal(left, 4 * k + 4)
+    # a request past a record's end is refused and moves nothing
+    with pytest.raises(dccrg_amd.DccrgError, match="fewer bytes left"):
+        h.continue_loading_grid_data(dt, k + 2)
+    h.continue_loading_grid_data(dt, k)
+    h.continue_loading_grid_data(tl)
+    assert np.all(h.grid_file_bytes_left() == 0)
+    h.finish_loading_grid_data()
+    check(h, sz, dt, tl)
+    with pytest.raises(dccrg_amd.DccrgError, match="no grid file"):
+        h.continue_loading_grid_data(tl)
+    g.close()
+    h.close()
+
+
+def test_variable_payload_file_empty_records(gpu, tmp_path):
+    """Records of zero bytes (a cell without data, no fixed-size field):
+    each cell still gets exactly its own bytes back."""
+    g, _ = make_pair((6, 1, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    data = g.add_variable_field("data", np.int32)
+    ids = g.slot_ids()[: g.n_local]
+    cnt = _counts(ids)
+    data.set([np.arange(int(k), dtype=np.int32) + 7 for k in cnt])
+    path = tmp_path / "empty.dc"
+    g.save_grid_data(path)
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    d = h.add_variable_field("data", np.int32)
+    h.load_grid_data(path)
+    hid = h.slot_ids()[: h.n_local]
+    got = d.get(0, h.n_local)
+    assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, _counts(hid)))
+    # two variable-size fields cannot be split without the caller's counts
+    h2 = dccrg_amd.Dccrg(0, 1, 0)
+    h2.add_variable_field("x", np.int32)
+    h2.add_variable_field("y", np.int32)
+    with pytest.raises(dccrg_amd.DccrgError, match="several variable-size"):
+        h2.load_grid_data(path)
+    g.close()
+    h.close()
+    h2.close()

@@ -16,6 +16,7 @@ life; advection bitwise against a one-rank run of the product, within
 import os
 import socket
 import sys
+import time
 import traceback
 
 import numpy as np
@@ -443,6 +444,8 @@ def sc_rcb(rank, world):
 
     length, R = (10, 8, 6), 1
     g = _grid(length, R, (True, False, False), 1)
+    if DEBUG_NOTES:
+        _progress(f"rank {rank} rcb start")
     loc = g.local_cells()
     for c in loc[::9]:
         g.refine_completely(int(c))
@@ -498,6 +501,28 @@ def sc_rcb(rank, world):
     before = g.local_cells()
     g.balance_load()
     res["none_keeps"] = bool(np.array_equal(before, g.local_cells())) and g.get_load_balancing_method() == "NONE"
+    g.close()
+    # a grid at the id space's deepest level (set_maximum_refinement_level(-1)
+    # on 20 x 1 x 1, tests/restart/variable_cell_data.cpp): center and id bits
+    # exceed 64, the select runs over 128-bit keys; same rule
+    g = _grid((20, 1, 1), -1, (False, False, False), 1)
+    Rd = g.get_maximum_refinement_level()
+    if DEBUG_NOTES:
+        _progress(f"rank {rank} deep grid R={Rd}")
+    for c in g.local_cells()[::3]:
+        g.refine_completely(int(c))
+    g.stop_refining()
+    if DEBUG_NOTES:
+        _progress(f"rank {rank} deep refined")
+    loc = g.local_cells()
+    c_part, p_part = g.make_new_partition()
+    if DEBUG_NOTES:
+        _progress(f"rank {rank} deep partition")
+    allc = np.sort(np.concatenate(_gather(loc)))
+    exp = RCB.rcb(allc, RCB.centers2(O.Mapping((20, 1, 1), Rd), allc), None, world)
+    exp_of = dict(zip(allc.tolist(), exp.tolist()))
+    res["deep_keys_eq_rule"] = bool(Rd > 16 and np.array_equal(c_part, np.sort(loc))
+                                    and all(exp_of[int(c)] == int(p) for c, p in zip(c_part, p_part)))
     g.close()
     return res
 
@@ -909,6 +934,19 @@ SCENARIOS = {
 }
 
 
+DEBUG_NOTES = bool(os.environ.get("DCCRGX_TEST_NOTES"))
+
+
+def _progress(msg):
+    """A progress line on stderr (seen with pytest -s) and, on a gpurun box,
+    in gpurun_out/test_progress.log (a long fixture stays visibly alive)."""
+    print(msg, file=sys.stderr, flush=True)
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root and os.path.isdir(os.path.join(root, "gpurun_out")):
+        with open(os.path.join(root, "gpurun_out", "test_progress.log"), "a") as f:
+            f.write(msg + "\n")
+
+
 def _worker(rank, world, port, q, names, tmpdir, module="test_gpu_transport"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -920,11 +958,16 @@ def _worker(rank, world, port, q, names, tmpdir, module="test_gpu_transport"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mod = sys.modules.get(module) or __import__(module)
     for name in names:
+        t0 = time.perf_counter()
         try:
             out = getattr(mod, name)(rank, world)
             q.put((name, rank, "ok", out))
+            kind = "ok"
         except Exception:
             q.put((name, rank, "error", traceback.format_exc()))
+            kind = "error"
+        if rank == 0:
+            _progress(f"[{module} world {world}] {name}: {kind} in {time.perf_counter() - t0:.1f} s")
         dist.barrier()
     dist.destroy_process_group()
 
@@ -943,6 +986,8 @@ def _run_group(world, tmpdir, names=None, module="test_gpu_transport"):
     for _ in range(world * len(names)):
         name, rank, kind, out = q.get(timeout=300)
         results.setdefault(name, {})[rank] = (kind, out)
+        if kind != "ok":
+            _progress(f"[{module} world {world}] {name} rank {rank} failed:\n{out}")
     for p in procs:
         p.join(timeout=60)
     return results
@@ -1000,6 +1045,7 @@ def test_pins_and_balance_load(transport_results):
 
 def test_rcb_partitioner(transport_results):
     _check(transport_results, "sc_rcb", ["weight_get", "partition_eq_rule", "final_eq_rule", "payload", "views",
+                                         "deep_keys_eq_rule",
                                          "weights_dropped", "inherit", "none_keeps"])
 
 

@@ -329,6 +329,20 @@ __device__ __forceinline__ double adv_face_g(int a, double cd, double clx, doubl
 	return (v >= 0 ? cd : n.d) * dt * v * min_area;
 }
 
+// Tile records (32 B) are read one tile ahead of their use by a vector load
+// (lanes 0..7 one word each) and made uniform with readlane.  A scalar load
+// issued that early would not help: the next LDS wait (lgkmcnt counts LDS and
+// scalar memory alike) would wait for it, exposing its latency once per tile;
+// the vector counter is in order, so waiting for the previous tile's fields
+// does not wait for the record loaded after them.
+__device__ __forceinline__ uint32_t tile_record_word(const void* meta, uint32_t tt, uint32_t lane) {
+	return lane < 8u ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(meta) + 8u * tt + lane) : 0u;
+}
+
+__device__ __forceinline__ uint32_t word_of(uint32_t v, int k) {
+	return uint32_t(__builtin_amdgcn_readlane(int(v), k));
+}
+
 // Static persistent schedule of the tile sweeps: block b runs on XCD b % 8
 // (measured: scripts/microbench/xcd_map.hip); XCD x sweeps the x-th eighth
 // of the tile list, its B blocks side by side (block j: tiles j, j + B, ...),
@@ -394,8 +408,16 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 	struct RegSet {
 		double c[7], e[4];
 	};
-	auto load = [&](uint32_t tt, RegSet& r) {
-		const uint32_t ts = meta[tt].ts;
+	// a tile record: its first slot, and the raw record words (lanes 0..7)
+	// whose neighbor-box starts are read with a wave-uniform readlane (a
+	// register array indexed by a run-time side would live in scratch)
+	struct RM {
+		uint32_t ts, rec;
+		__device__ __forceinline__ int32_t nst(uint32_t d) const { return int32_t(word_of(rec, int(1 + d))); }
+	};
+	auto unpack = [&](uint32_t v) { return RM{word_of(v, 0), v}; };
+	auto load = [&](const RM& mt, RegSet& r) {
+		const uint32_t ts = mt.ts;
 		const uint32_t o = (ts + tid) << 3;
 		r.c[0] = ldo(rho, o); r.c[1] = ldo(vx, o); r.c[2] = ldo(vy, o);
 		r.c[3] = ldo(vz, o); r.c[4] = ldo(lx, o); r.c[5] = ldo(ly, o);
@@ -406,7 +428,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			r.e[i] = 0;
 			if (row >= 30u) continue;
 			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
-			const int32_t st = meta[tt].nst[d];
+			const int32_t st = mt.nst(d);
 			if (st < 0) continue;
 			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
 			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
@@ -427,8 +449,8 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		}
 	};
 	// the staged tile tc from LDS
-	auto compute = [&](uint32_t tc) {
-		const uint32_t ts = meta[tc].ts;
+	auto compute = [&](const RM& mc) {
+		const uint32_t ts = mc.ts;
 		const double cd = shd[0][tid], clx = shd[4][tid], cly = shd[5][tid], clz = shd[6][tid];
 		const double cva[3] = {shd[1][tid], shd[2][tid], shd[3][tid]};
 		// pass 1: the +x, +y, +z face of every cell, once per face, branch-free
@@ -439,12 +461,12 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			const uint32_t li = lp[a];
 			const double g = adv_face_g(a, cd, clx, cly, clz, cva[a],
 			                            AdvNb{shd[0][li], shd[4][li], shd[5][li], shd[6][li], shd[1 + a][li]}, dt);
-			const bool has = l[a] < 7 || meta[tc].nst[2 * a + 1] >= 0;
+			const bool has = l[a] < 7 || mc.nst(2 * a + 1) >= 0;
 			shg[a][tid] = has ? g : 0.0;
 		}
 		// the tile's -a boundary faces (minus cell outside): 192 faces on
 		// waves 0..2, wave-uniform
-		if (w < 3 && meta[tc].nst[2 * w] >= 0) {
+		if (w < 3 && mc.nst(2 * w) >= 0) {
 			const uint32_t k = 512u + 64u * (2u * w) + lane;
 			const AdvNb self{shd[0][bcell], shd[4][bcell], shd[5][bcell], shd[6][bcell], shd[1 + w][bcell]};
 			double gmv;
@@ -462,24 +484,35 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 			q[a] -= 1;
 			double gm = 0;
 			if (l[a] > 0) gm = shg[a][m9(q[0] & 7u, q[1] & 7u, q[2] & 7u)];
-			else if (meta[tc].nst[2 * a] >= 0) gm = shm[a][fi[a]];
+			else if (mc.nst(2 * a) >= 0) gm = shm[a][fi[a]];
 			acc += gm;
 			acc += -shg[a][tid];
 		}
 		st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 	};
 	RegSet ra;
-	load(t, ra);
+	RM cur = unpack(tile_record_word(meta, t, lane));
+	uint32_t tn = tk.next(t);
+	load(cur, ra);
+	uint32_t rec = tn < t1 ? tile_record_word(meta, tn, lane) : 0u;  // tile tn's record
 	for (;;) {
 		__syncthreads();  // the previous tile's faces have been read from LDS
 		stage(ra);
 		__syncthreads();
-		const uint32_t tc = t, tn = tk.next(t);
 		const bool more = tn < t1;
-		if (more) load(tn, ra);  // the next tile's loads fly while this one is computed
-		compute(tc);
+		RM nxt = cur;
+		if (more) {
+			// the next tile's loads fly while this one is computed, then the
+			// record of the tile after it
+			nxt = unpack(rec);
+			load(nxt, ra);
+			const uint32_t tnn = tk.next(tn);
+			rec = tnn < t1 ? tile_record_word(meta, tnn, lane) : 0u;
+		}
+		compute(cur);
 		if (!more) break;
-		t = tn;
+		cur = nxt;
+		tn = tk.next(tn);
 	}
 }
 
@@ -523,9 +556,14 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
 		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
 	};
-	auto load = [&](uint32_t tt) {
-		const uint32_t ts = meta[tt].ts, n = meta[tt].n, e0 = meta[tt].e0, ne = meta[tt].ne, fb = meta[tt].fb,
-		               nf = meta[tt].nf;
+	const uint32_t lane = tid & 63u;
+	struct GM {
+		uint32_t ts, n, e0, ne, fb, nf;
+	};
+	auto unpack = [&](uint32_t v) { return GM{word_of(v, 0), word_of(v, 1), word_of(v, 2), word_of(v, 3), word_of(v, 4),
+	                                          word_of(v, 5)}; };
+	auto load = [&](const GM& mt) {
+		const uint32_t ts = mt.ts, n = mt.n, e0 = mt.e0, ne = mt.ne, fb = mt.fb, nf = mt.nf;
 		if (tid < n) {
 			load7(ts + tid, c);
 			// the tile's face codes, ext list and finer pairs are read once per
@@ -555,9 +593,12 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			fq[1] = q.y;
 		}
 	};
-	load(t);
+	GM cur = unpack(tile_record_word(meta, t, lane));
+	uint32_t tn = tk.next(t);
+	load(cur);
+	uint32_t rec = tn < t1 ? tile_record_word(meta, tn, lane) : 0u;  // tile tn's record
 	for (;;) {
-		const uint32_t n = meta[t].n, ne = meta[t].ne, nf = meta[t].nf, ts = meta[t].ts;
+		const uint32_t n = cur.n, ne = cur.ne, nf = cur.nf, ts = cur.ts;
 		__syncthreads();  // the previous tile's faces have been read from LDS
 		if (tid < n)
 #pragma unroll
@@ -574,9 +615,16 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		}
 		const uint32_t r0 = row[0], r1 = row[1], r2 = row[2];
 		__syncthreads();
-		const uint32_t tn = tk.next(t);
 		const bool more = tn < t1;
-		if (more) load(tn);  // the next tile's loads fly while this one is computed
+		GM nxt = cur;
+		if (more) {
+			// the next tile's loads fly while this one is computed, then the
+			// record of the tile after it
+			nxt = unpack(rec);
+			load(nxt);
+			const uint32_t tnn = tk.next(tn);
+			rec = tnn < t1 ? tile_record_word(meta, tnn, lane) : 0u;
+		}
 		if (tid < n) {
 			const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
 			             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
@@ -603,7 +651,8 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 		}
 		if (!more) break;
-		t = tn;
+		cur = nxt;
+		tn = tk.next(tn);
 	}
 }
 // max_time_step local part (solve.hpp:289-333): block minima

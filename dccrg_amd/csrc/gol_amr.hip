@@ -263,6 +263,9 @@ __global__ void mask_l0c_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids,
 // per neighbor entry: slot | code << 27 (code = 9 (dz+1) + 3 (dy+1) + dx+1 of
 // the neighbor's level-0 parent from the row's), kEntNone without a slot
 constexpr uint32_t kEntNone = 0xffffffffu;
+#ifndef DCCRGX_COLLECT_WORDS
+#define DCCRGX_COLLECT_WORDS 4
+#endif
 __global__ void mask_ent_kernel(const uint32_t* __restrict__ ptr, const int32_t* __restrict__ nslot, size_t rows,
                                 const uint32_t* __restrict__ l0c, L0Geom G, uint32_t* __restrict__ ent,
                                 int* __restrict__ bad) {
@@ -323,66 +326,85 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
 	const uint32_t nw = (nB + 3) / 4;
 	const uint4* ent4 = reinterpret_cast<const uint4*>(ent) + (E0 >> 2);
-	// phase 1: two index words (eight state gathers) in flight per thread
-	for (uint32_t w = tid; w < nw; w += 2 * kCollectRows) {
-		const bool two = w + kCollectRows < nw;
-		const uint4 ea = ent4[w];
-		const uint4 eb = two ? ent4[w + kCollectRows] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
-		const uint32_t q[8] = {ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, eb.z, eb.w};
-		uint32_t st[8];
-#pragma unroll
-		for (int k = 0; k < 8; k++) st[k] = q[k] == kEntNone ? 0u : state[q[k] & 0x7ffffffu];
-		uint32_t out[2] = {0, 0};
-#pragma unroll
-		for (int k = 0; k < 8; k++) {
-			const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
-			out[k >> 2] |= v << (8 * (k & 3));
-		}
-		sp32[w] = out[0];
-		if (two) sp32[w + kCollectRows] = out[1];
-	}
-	__syncthreads();
+	// the row's own words, needed after the barrier, fly with phase 1
 	const size_t s = r0 + tid;
 	const bool act = s < r1;
-	uint32_t mask = 0, l[kList];
+	const uint32_t rb = act ? ptr[s] : 0u, re = act ? ptr[s + 1] : 0u, pc = act ? l0c[s] : 0u;
+	// phase 1: kWords index words (4 kWords state gathers) in flight per thread
+	constexpr int kWords = DCCRGX_COLLECT_WORDS;
+	for (uint32_t w = tid; w < nw; w += kWords * kCollectRows) {
+		uint32_t q[4 * kWords];
 #pragma unroll
-	for (int i = 0; i < kList; i++) l[i] = 13;
-	int n = 0;
+		for (int c = 0; c < kWords; c++) {
+			const uint32_t wc = w + uint32_t(c) * kCollectRows;
+			const uint4 e4 = wc < nw ? ent4[wc] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
+			q[4 * c] = e4.x;
+			q[4 * c + 1] = e4.y;
+			q[4 * c + 2] = e4.z;
+			q[4 * c + 3] = e4.w;
+		}
+		uint32_t st[4 * kWords];
+#pragma unroll
+		for (int k = 0; k < 4 * kWords; k++) st[k] = q[k] == kEntNone ? 0u : state[q[k] & 0x7ffffffu];
+#pragma unroll
+		for (int c = 0; c < kWords; c++) {
+			uint32_t out = 0;
+#pragma unroll
+			for (int k = 4 * c; k < 4 * c + 4; k++) {
+				const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
+				out |= v << (8 * (k & 3));
+			}
+			const uint32_t wc = w + uint32_t(c) * kCollectRows;
+			if (wc < nw) sp32[wc] = out;
+		}
+	}
+	__syncthreads();
+	// the walk, branch-free: `mask` the bits of the live parents seen so far,
+	// `codes` the list (5 bits per entry, first-seen order), `ebits` the
+	// reference's aborts (1: a ninth live parent, 2: a dead neighbor whose
+	// parent was already recorded alive); entries without a slot (31) and of
+	// the own parent (13) change nothing
+	uint32_t mask = 0, n = 0, ebits = 0;
+	uint64_t codes = 0;
 	auto visit = [&](uint32_t v) {
 		const uint32_t c = v & 31u;
-		if (c == 31u || c == 13u) return;  // no slot / the own level-0 parent
-		const uint32_t bit = 1u << c;
-		if (v & 32u) {
-			if (!(mask & bit)) {
-				mask |= bit;
-				if (n == kList) {
-					atomicOr(err, 1);
-				} else {
-#pragma unroll
-					for (int i = 0; i < kList; i++)
-						if (i == n) l[i] = c;
-					n++;
-				}
-			}
-		} else if (mask & bit) {
-			atomicOr(err, 2);
-		}
+		const uint32_t bit = (c != 31u && c != 13u) ? (1u << c) : 0u;
+		const uint32_t alive = (v >> 5) & 1u;
+		const uint32_t seen = (mask & bit) != 0u ? 1u : 0u;
+		const uint32_t fresh = alive & (bit != 0u ? 1u : 0u) & (seen ^ 1u);
+		ebits |= ((alive ^ 1u) & seen) << 1;
+		ebits |= fresh & (n >= uint32_t(kList) ? 1u : 0u);
+		const uint32_t app = fresh & (n < uint32_t(kList) ? 1u : 0u);
+		codes |= uint64_t(app ? c : 0u) << (5u * n);
+		n += app;
+		mask |= alive ? bit : 0u;
 	};
-	// the row's entry bytes a 4-byte word at a time (E0 is word aligned)
-	for (uint32_t j = act ? ptr[s] : 0, e = act ? ptr[s + 1] : 0; j < e;) {
-		const uint32_t b0 = j & 3u, b1 = e - j < 4u - b0 ? b0 + (e - j) : 4u;
+	// the row's entry bytes a 4-byte word at a time (E0 is word aligned);
+	// bytes of the word outside the row count as "no slot"
+	for (uint32_t j = rb & ~3u; j < re; j += 4) {
+		uint32_t word;
 		if (j - E0 < nB) {
-			const uint32_t word = sp32[(j - E0) >> 2];
-			for (uint32_t b = b0; b < b1; b++) visit((word >> (8 * b)) & 0xffu);
+			word = sp32[(j - E0) >> 2];
 		} else {
-			for (uint32_t b = b0; b < b1; b++) visit(mask_entry_byte(ent[(j & ~3u) + b], state));
+			word = 0;
+#pragma unroll
+			for (uint32_t b = 0; b < 4; b++)
+				word |= (j + b < re ? mask_entry_byte(ent[j + b], state) : 31u) << (8 * b);
 		}
-		j += b1 - b0;
+#pragma unroll
+		for (uint32_t b = 0; b < 4; b++) {
+			const bool in = j + b >= rb && j + b < re;
+			visit(in ? (word >> (8 * b)) & 0xffu : 31u);
+		}
 	}
+	if (ebits) atomicOr(err, int(ebits));
+	uint32_t l[kList];
+#pragma unroll
+	for (int i = 0; i < kList; i++) l[i] = uint32_t(codes >> (5 * i)) & 31u;
 	// level-0 ids of the listed positions: the row's three wrapped x, y, z
 	// coordinates once, then per entry 1 + x + y lx + z lx ly
 	int px, py, pz;
-	l0_unpack(act ? l0c[s] : 0u, G, px, py, pz);
+	l0_unpack(pc, G, px, py, pz);
 	auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
 	const uint64_t lxy = uint64_t(G.lx) * G.ly;
 	const uint64_t X[3] = {uint64_t(wrap(px - 1, int(G.lx))) + 1, uint64_t(px) + 1, uint64_t(wrap(px + 1, int(G.lx))) + 1};
@@ -393,7 +415,7 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 #pragma unroll
 	for (int i = 0; i < kList; i++) {
 		const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
-		out[i] = i < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
+		out[i] = uint32_t(i) < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
 	}
 	// the lists through LDS: each row's 64 B at its place, then the block's
 	// rows stored as one contiguous run, 16 B per lane and instruction,

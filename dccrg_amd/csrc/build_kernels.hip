@@ -379,10 +379,34 @@ __global__ void iterator_fill_kernel(const uint32_t* nof_ptr, const uint64_t* no
 	}
 }
 
-// face lists (get_face_neighbors_of semantics), one thread per local slot
-__global__ void face_lists_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                                  const uint32_t* ptr, int32_t* ent, int32_t* err, int pass) {
-	const DevExists ex{M};
+// face lists (get_face_neighbors_of semantics), one thread per local slot,
+// in two passes.  Pass 0 counts the entries of each row and keeps, per
+// direction, what the probes found: the slot of a single (same-size or
+// coarser) neighbor, -1 none, -2 four finer ones, -3 a single neighbor
+// without a slot.  Pass 1 writes the rows from those hints and probes again
+// only in the directions with finer neighbors.
+struct SlotExists {
+	DevMesh M;
+	mutable int32_t slot = -1;
+	// DevExists's answer, and the slot of the cell it found
+	__device__ __forceinline__ bool operator()(uint64_t id) const {
+		slot = -1;
+		if (id == 0 || id > M.last) return false;
+		if (M.implicit) {
+			if (id > M.bp.n0) return false;
+			slot = dm_slot(M, id);
+			return true;
+		}
+		int32_t o, sl;
+		if (!dm_lookup(M, id, o, sl)) return false;
+		slot = sl;
+		return o >= 0;
+	}
+};
+
+__global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
+                                  int32_t* hint) {
+	const SlotExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		uint64_t c[3];
 		int lvl;
@@ -391,16 +415,38 @@ __global__ void face_lists_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 		for (int dir = 0; dir < 6; dir++) {
 			uint64_t out[4];
 			const int nf = face_dir(m, c, lvl, dir, ex, out);
+			// a single neighbor was the last cell found (face_dir returns on it)
+			hint[6 * r + dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -3));
+			k += uint32_t(nf);
+		}
+		cnt[r] = k;
+	}
+}
+
+__global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, const int32_t* hint,
+                                 const uint32_t* ptr, int32_t* ent, int32_t* err) {
+	const DevExists ex{M};
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
+		uint32_t k = ptr[r];
+		for (int dir = 0; dir < 6; dir++) {
+			const int32_t h = hint[6 * r + dir];
+			if (h == -1) continue;
+			if (h != -2) {
+				if (h == -3) atomicExch(err, 1);
+				ent[k++] = (h == -3 ? -1 : h) * 8 + dir;
+				continue;
+			}
+			uint64_t c[3];
+			int lvl;
+			cell_coords(m, slot_ids[r], c, lvl);
+			uint64_t out[4];
+			const int nf = face_dir(m, c, lvl, dir, ex, out);
 			for (int i = 0; i < nf; i++) {
-				if (pass == 1) {
-					const int32_t s = dm_slot(M, out[i]);
-					if (s < 0) atomicExch(err, 1);
-					ent[ptr[r] + k] = s * 8 + dir;
-				}
-				k++;
+				const int32_t sl = dm_slot(M, out[i]);
+				if (sl < 0) atomicExch(err, 1);
+				ent[k++] = sl * 8 + dir;
 			}
 		}
-		if (pass == 0) cnt[r] = k;
 	}
 }
 
@@ -901,9 +947,12 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 }
 
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                  const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s) {
+                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s) {
 	if (!nrows) return;
-	face_lists_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, cnt, ptr, ent, err_flag, pass);
+	if (pass == 0)
+		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, cnt, hint);
+	else
+		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, ptr, ent, err_flag);
 	HIP_CHECK(hipGetLastError());
 }
 

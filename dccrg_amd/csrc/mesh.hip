@@ -455,10 +455,12 @@ void ensure_face(Grid& g) {
 	DBuf<int32_t> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, nullptr, nullptr, err.p, 0, s);
+	DBuf<int32_t> hint;  // per row and direction what pass 0 found (build_kernels.hip)
+	hint.alloc(6 * nl + 6);
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, err.p, 0, s);
 	const size_t t = scan_exclusive_u32(cnt.p, g.face_ptr.p, nl, s);
 	g.face_ent.alloc(t + 1);
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, g.face_ptr.p, g.face_ent.p, err.p, 1, s);
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, g.face_ptr.p, g.face_ent.p, err.p, 1, s);
 	int32_t herr = 0;
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));

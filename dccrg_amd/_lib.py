@@ -108,6 +108,9 @@ _SIGS = {
     "dccrgx_get_user_update_list": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, sz, P(sz)]),
     "dccrgx_update_copies_of_remote_neighbors_hood": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_cell_process": (C.c_int, [vp, vp, vp, sz, P(sz)]),
+    "dccrgx_find_neighbors_of": (C.c_int, [vp, u64, vp, sz, vp, vp, sz, P(sz)]),
+    "dccrgx_get_face_cache": (C.c_int, [vp, vp, vp, sz, P(sz)]),
+    "dccrgx_unpin_all_cells": (C.c_int, [vp]),
     "dccrgx_add_field": (C.c_int, [vp, C.c_char_p, sz, C.c_int, P(C.c_int)]),
     "dccrgx_set_field_transfer": (C.c_int, [vp, C.c_int, C.c_int]),
     "dccrgx_add_variable_field": (C.c_int, [vp, C.c_char_p, C.c_int, P(C.c_int)]),

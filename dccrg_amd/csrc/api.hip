@@ -407,6 +407,14 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 	}
 	if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
 	if (mine) pwrite_all(fd, data.data(), data.size(), data0);
+	// the file ends where the last record ends: bytes of an older, longer
+	// file at this path must not extend the last record (a loader bounds it
+	// by the end of the file)
+	if (g.rank == 0) {
+		uint64_t all = 0;
+		for (int p = 0; p < g.size; p++) all += cnt[size_t(p)][1];
+		DX_REQUIRE(::ftruncate(fd, off_t(list0 + 16 * total + all)) == 0, "grid file truncate failed");
+	}
 }
 
 // start_loading_grid_data (1795-2083): the grid block and the cell list; every
@@ -487,6 +495,15 @@ static void start_load_impl(Grid& g, const char* path, uint64_t offset, size_t h
 			if (nx != starts.end()) e = *nx;
 		}
 		cells[i] = {list[2 * i], p, e};
+	}
+	if (!monotone) {
+		// records sharing a start: only the last of them in list order holds
+		// bytes, the others are empty (as a writer lays out an empty record
+		// followed by a full one at the same position)
+		std::unordered_map<uint64_t, size_t> last;
+		for (size_t i = 0; i < total; i++) last[list[2 * i + 1]] = i;
+		for (size_t i = 0; i < total; i++)
+			if (last[list[2 * i + 1]] != i) cells[i].end = cells[i].pos;
 	}
 	std::sort(cells.begin(), cells.end());
 	// owners as load_cells (3647) produces them: the level-0 block
@@ -1077,8 +1094,47 @@ int dccrgx_get_neighbors_to(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, size_
 int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32_t* dirs, size_t cap, size_t* n) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
+		static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
 		const int64_t s = lookup_slot(g, cell);
-		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
+		if (s < 0 || size_t(s) >= g.n_local) {
+			// a remote cell this process knows (e.g. a copy in all_cells()): its
+			// faces from the known leaves, probed at every level at each face's
+			// probe point (the leaf there must be known, else the face lies
+			// beyond the ghost region and the cell is not answered)
+			if (lookup_owner(g, cell) < 0) return DCCRGX_ENOTFOUND;
+			const MapCtx& m = g.m;
+			uint64_t c[3], p[3];
+			const int lvl = map_indices(m, cell, c[0], c[1], c[2]);
+			std::vector<uint64_t> cand;
+			for (int dir = 0; dir < 6; dir++)
+				if (face_probe(m, c, lvl, dir, p))
+					for (int l = 0; l <= m.R; l++) cand.push_back(map_from_indices(m, p[0], p[1], p[2], l));
+			std::sort(cand.begin(), cand.end());
+			cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+			std::vector<int32_t> own(cand.size());
+			lookup_batch(g, cand.data(), cand.size(), own.data(), nullptr);
+			const auto exists = [&](uint64_t id) {
+				const auto it = std::lower_bound(cand.begin(), cand.end(), id);
+				return it != cand.end() && *it == id && own[size_t(it - cand.begin())] >= 0;
+			};
+			std::vector<std::pair<uint64_t, int>> out;
+			for (int dir = 0; dir < 6; dir++) {
+				if (!face_probe(m, c, lvl, dir, p)) continue;
+				bool any = false;
+				for (int l = 0; l <= m.R && !any; l++) any = exists(map_from_indices(m, p[0], p[1], p[2], l));
+				if (!any) throw Error(DCCRGX_ENOTFOUND, "a face of this remote cell lies beyond the ghost region");
+				uint64_t f[4];
+				const int k = face_dir(m, c, lvl, dir, exists, f);
+				for (int i = 0; i < k; i++) out.push_back({f[i], dmap[dir]});
+			}
+			if (n) *n = out.size();
+			if (out.size() > cap) return DCCRGX_ERANGE;
+			for (size_t i = 0; i < out.size(); i++) {
+				ids[i] = out[i].first;
+				if (dirs) dirs[i] = out[i].second;
+			}
+			return 0;
+		}
 		ensure_face(g);
 		uint32_t be[2];
 		HIP_CHECK(hipMemcpy(be, g.face_ptr.p + s, 8, hipMemcpyDeviceToHost));
@@ -1088,7 +1144,6 @@ int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, 
 		std::vector<int32_t> ent(k);
 		if (k) HIP_CHECK(hipMemcpy(ent.data(), g.face_ent.p + be[0], k * 4, hipMemcpyDeviceToHost));
 		const auto& sid = slot_ids_host(g);
-		static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
 		for (size_t i = 0; i < k; i++) {
 			ids[i] = sid[size_t(ent[i] >> 3)];
 			if (dirs) dirs[i] = dmap[ent[i] & 7];
@@ -1209,6 +1264,118 @@ int dccrgx_get_cell_process(dccrgx_grid* gp, uint64_t* ids, int32_t* owners, siz
 		if (cap < k.size()) return int(DCCRGX_ERANGE);
 		std::copy(k.begin(), k.end(), ids);
 		if (owners) std::copy(o.begin(), o.end(), owners);
+		return 0;
+	});
+}
+
+static int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+int dccrgx_find_neighbors_of(dccrgx_grid* gp, uint64_t cell, const int32_t* items, size_t n_items, uint64_t* ids,
+                             int32_t* offs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		DX_REQUIRE(items || !n_items, "null neighborhood");
+		const MapCtx& m = g.m;
+		if (lookup_owner(g, cell) < 0) return DCCRGX_ENOTFOUND;  // 4354-4362: unknown cell
+		uint64_t c[3];
+		const int lvl = map_indices(m, cell, c[0], c[1], c[2]);
+		const bool local = is_local_cell(g, cell);
+		const int64_t len = int64_t(1) << (m.R - lvl), l0 = int64_t(1) << m.R;
+		const int64_t r = std::max(1, int(g.hood_len));
+		// the three cells an item's box can resolve to (nof_item): finer,
+		// same size and coarser, all probed in one device lookup
+		std::vector<uint64_t> cand;
+		for (size_t i = 0; i < n_items; i++) {
+			const int32_t* h = items + 3 * i;
+			uint64_t w[3];
+			bool inside = true;
+			for (int d = 0; d < 3; d++) {
+				const int64_t lo = int64_t(c[d]) + int64_t(h[d]) * len;
+				// a local cell's box must lie in the level-0 cells this rank
+				// knows (its ghost region); a remote cell's list may be
+				// incomplete, as the reference documents (4327-4328)
+				if (local) {
+					const int64_t own = int64_t(c[d]) / l0;
+					if (std::abs(floor_div(lo, l0) - own) > r || std::abs(floor_div(lo + len - 1, l0) - own) > r)
+						throw Error(DCCRGX_EINVAL, "neighborhood item beyond the ghost region of this process");
+				}
+				inside = inside && map_wrap(m, d, lo, w[d]);
+			}
+			if (!inside) continue;
+			for (int l = std::max(0, lvl - 1); l <= std::min(m.R, lvl + 1); l++)
+				cand.push_back(map_from_indices(m, w[0], w[1], w[2], l));
+		}
+		std::sort(cand.begin(), cand.end());
+		cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+		std::vector<int32_t> own(cand.size());
+		lookup_batch(g, cand.data(), cand.size(), own.data(), nullptr);
+		const auto exists = [&](uint64_t id) {
+			const auto it = std::lower_bound(cand.begin(), cand.end(), id);
+			return it != cand.end() && *it == id && own[size_t(it - cand.begin())] >= 0;
+		};
+		std::vector<uint64_t> oi;
+		std::vector<int32_t> oo;
+		ItemOut o;
+		for (size_t i = 0; i < n_items; i++) {
+			nof_item(m, c, lvl, items + 3 * i, exists, o);
+			for (int k = 0; k < o.n; k++) {
+				oi.push_back(o.id[k]);
+				oo.insert(oo.end(), o.off[k], o.off[k] + 3);
+			}
+		}
+		if (n) *n = oi.size();
+		if (oi.size() > cap || (!ids && !oi.empty())) return DCCRGX_ERANGE;
+		std::copy(oi.begin(), oi.end(), ids);
+		if (offs) std::copy(oo.begin(), oo.end(), offs);
+		return 0;
+	});
+}
+
+int dccrgx_get_face_cache(dccrgx_grid* gp, uint64_t* ids, uint64_t* nbrs, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.initialized, "not initialized");
+		const MapCtx& m = g.m;
+		std::vector<uint64_t> k;
+		std::vector<int32_t> o;
+		known_leaves(g, k, o);
+		// every leaf under a known level-0 cell is known (own + ghost region)
+		std::vector<uint64_t> l0;
+		for (uint64_t id : k) l0.push_back(map_level0_parent(m, id));
+		std::sort(l0.begin(), l0.end());
+		l0.erase(std::unique(l0.begin(), l0.end()), l0.end());
+		const auto exists = [&](uint64_t id) { return std::binary_search(k.begin(), k.end(), id); };
+		std::vector<uint64_t> oi, on;
+		for (uint64_t id : k) {
+			uint64_t c[3];
+			const int lvl = map_indices(m, id, c[0], c[1], c[2]);
+			std::array<uint64_t, 6> e;
+			bool known = true;
+			for (int dir = 0; dir < 6 && known; dir++) {
+				uint64_t p[3], f[4];
+				e[size_t(dir)] = error_cell;
+				if (!face_probe(m, c, lvl, dir, p)) continue;
+				// the probe's level-0 cell must be known for the entry to be exact
+				known = std::binary_search(l0.begin(), l0.end(), map_from_indices(m, p[0], p[1], p[2], 0));
+				if (known && face_dir(m, c, lvl, dir, exists, f) > 0) e[size_t(dir)] = f[0];
+			}
+			if (!known) continue;
+			oi.push_back(id);
+			on.insert(on.end(), e.begin(), e.end());
+		}
+		if (n) *n = oi.size();
+		if (oi.size() > cap || (!ids && !oi.empty())) return DCCRGX_ERANGE;
+		std::copy(oi.begin(), oi.end(), ids);
+		if (nbrs) std::copy(on.begin(), on.end(), nbrs);
+		return 0;
+	});
+}
+
+int dccrgx_unpin_all_cells(dccrgx_grid* gp) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		g.pins.clear();
 		return 0;
 	});
 }

@@ -558,6 +558,10 @@ void ensure_tiles(Grid& g);
 const std::vector<uint64_t>& slot_ids_host(Grid& g);
 // batch lookups of known leaves: owner (-1 unknown) and slot (-1 none)
 void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot);
+void lists_on_host(Grid& g, const std::vector<uint64_t>& of_id, const std::vector<uint64_t>& to_id,
+                   const std::vector<uint32_t>& to_ptr, const std::vector<uint64_t>& self,
+                   std::map<int, std::vector<uint64_t>>& recv_ids, std::map<int, std::vector<uint64_t>>& send_ids,
+                   std::vector<uint64_t>* extra_remote);
 int32_t lookup_owner(Grid& g, uint64_t id);
 bool is_local_cell(Grid& g, uint64_t id);
 int64_t lookup_slot(Grid& g, uint64_t id);

@@ -128,27 +128,40 @@ DX_HD uint64_t nto_candidate(const MapCtx& m, const uint64_t c[3], int lvl, cons
 // with the face cache update_neighbors_ 9324-9458 inlined): dir 0..5 =
 // -x,+x,-y,+y,-z,+z.  Returns the count (0, 1 or 4) and their ids in the
 // reference order: n0, n0+a, n0+b, n0+b+a with (a,b) the two in-face dims.
-template <class Exists>
-DX_HD int face_dir(const MapCtx& m, const uint64_t c[3], int lvl, int dir, const Exists& exists, uint64_t out[4]) {
+// The probe point of face direction `dir` (update_neighbors_ 9324-9381): the
+// index just outside the cell's min corner across that face, wrapped; false
+// outside a non-periodic boundary.
+DX_HD bool face_probe(const MapCtx& m, const uint64_t c[3], int lvl, int dir, uint64_t p[3]) {
 	const uint64_t len = uint64_t(1) << (m.R - lvl);
 	const int d = dir >> 1;
-	uint64_t p[3] = {c[0], c[1], c[2]};
+	p[0] = c[0];
+	p[1] = c[1];
+	p[2] = c[2];
 	const uint64_t maxi = m.glen[d] - 1;
 	if ((dir & 1) == 0) {
 		if (p[d] == 0) {
-			if (!m.periodic[d]) return 0;
+			if (!m.periodic[d]) return false;
 			p[d] = maxi;
 		} else {
 			p[d]--;
 		}
 	} else {
 		if (maxi < len || p[d] > maxi - len) {
-			if (!m.periodic[d]) return 0;
+			if (!m.periodic[d]) return false;
 			p[d] = 0;
 		} else {
 			p[d] += len;
 		}
 	}
+	return true;
+}
+
+template <class Exists>
+DX_HD int face_dir(const MapCtx& m, const uint64_t c[3], int lvl, int dir, const Exists& exists, uint64_t out[4]) {
+	const uint64_t len = uint64_t(1) << (m.R - lvl);
+	const int d = dir >> 1;
+	uint64_t p[3];
+	if (!face_probe(m, c, lvl, dir, p)) return 0;
 	// get_existing_cell over levels [lvl-1, lvl+1], finest first (11275-11308)
 	const int lo = lvl == 0 ? 0 : lvl - 1;
 	const int hi = lvl == m.R ? m.R : lvl + 1;

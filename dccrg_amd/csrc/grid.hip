@@ -289,7 +289,11 @@ UserHood& ensure_uhood(Grid& g, int id) {
 	HaloPlan& P = h.plan;
 	P.send_ids.clear();
 	P.recv_ids.clear();
-	if (g.size > 1) {
+	if (g.size > 1 && uint64_t(g.size) > ~uint64_t(0) / (g.m.last + 1)) {
+		// ids too large for owner * (last + 1) + id keys (mesh.hip rebuild)
+		lists_on_host(g, download(h.nof_id.p, t_of, s), download(h.nto_id.p, t_to, s), download(h.nto_ptr.p, nl + 1, s),
+		              download(g.slot_ids.p, nl, s), P.recv_ids, P.send_ids, nullptr);
+	} else if (g.size > 1) {
 		const uint64_t stride = g.m.last + 1;
 		DBuf<uint64_t> keys;
 		keys.alloc(std::max(t_of, t_to) + 1);

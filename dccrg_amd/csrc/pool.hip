@@ -8,6 +8,7 @@
 // `pending`; it becomes reusable only after a device synchronisation, done on
 // demand when a request finds no ready block but a pending one - the same
 // guarantee hipFree gave, paid once for every block pending at that moment.
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -17,7 +18,16 @@ namespace dccrgx {
 
 namespace {
 
-constexpr size_t kMaxHeld = size_t(16) << 30;  // cached bytes kept at most (the rest is hipFree'd)
+// cached bytes kept at most (the rest is hipFree'd): 16 GiB, or
+// DCCRGX_POOL_MAX_MB (processes sharing one GPU - the host transport - each
+// take their share; the facade sets it from the ranks per device)
+size_t max_held() {
+	static const size_t v = [] {
+		const char* e = std::getenv("DCCRGX_POOL_MAX_MB");
+		return e && *e ? size_t(std::strtoull(e, nullptr, 10)) << 20 : size_t(16) << 30;
+	}();
+	return v;
+}
 constexpr size_t kBig = size_t(1) << 20;
 
 struct Pool {
@@ -118,7 +128,7 @@ void pool_free(void* raw, size_t cap) {
 	if (!raw) return;
 	Pool& P = pool();
 	std::lock_guard<std::mutex> lock(P.mu);
-	if (P.held + cap > kMaxHeld) {
+	if (P.held + cap > max_held()) {
 		(void)hipFree(raw);
 		return;
 	}

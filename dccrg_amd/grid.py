@@ -441,6 +441,40 @@ class Dccrg:
         check(rc)
         return [(int(ids[i]), int(dirs[i])) for i in range(n.value)]
 
+    def find_neighbors_of(self, cell, neighborhood):
+        """find_neighbors_of(cell, neighborhood) (dccrg.hpp:4339): [(id, (x, y,
+        z)), ...] for any list of offsets; raises for a cell this process
+        does not know (the reference throws)."""
+        o = np.ascontiguousarray(np.asarray(neighborhood, np.int32).reshape(-1, 3))
+        n = C.c_size_t()
+        rc = lib().dccrgx_find_neighbors_of(self.h, int(cell), _ptr(o), o.shape[0], None, None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        k = n.value
+        ids = np.empty(max(k, 1), np.uint64)
+        offs = np.empty(3 * max(k, 1), np.int32)
+        check(lib().dccrgx_find_neighbors_of(self.h, int(cell), _ptr(o), o.shape[0], _ptr(ids), _ptr(offs), k,
+                                             C.byref(n)))
+        return [(int(ids[i]), tuple(int(v) for v in offs[3 * i: 3 * i + 3])) for i in range(k)]
+
+    def get_neighbors_(self):
+        """The face-neighbor cache (get_neighbors_, dccrg.hpp:7107): {leaf:
+        (-x, +x, -y, +y, -z, +z)} over the leaves whose faces this process
+        can resolve (every local leaf)."""
+        n = C.c_size_t()
+        rc = lib().dccrgx_get_face_cache(self.h, None, None, 0, C.byref(n))
+        if rc not in (0, ERANGE):
+            check(rc)
+        k = n.value
+        ids = np.empty(max(k, 1), np.uint64)
+        nb = np.empty(6 * max(k, 1), np.uint64)
+        check(lib().dccrgx_get_face_cache(self.h, _ptr(ids), _ptr(nb), k, C.byref(n)))
+        return {int(ids[i]): tuple(int(v) for v in nb[6 * i: 6 * i + 6]) for i in range(k)}
+
+    def unpin_all_cells(self):
+        check(lib().dccrgx_unpin_all_cells(self.h))
+        return self
+
     def neighbor_entries(self, kind="of"):
         """Number of entries of a local CSR (no download of the entries)."""
         n = C.c_size_t()

@@ -225,7 +225,17 @@ inline int mpi_exchange(void* ctx, const void* const* send, const size_t* sb, vo
 }
 }  // namespace detail
 
-// ---- value types (dccrg_length.hpp, dccrg_topology.hpp, dccrg_mapping.hpp) --
+// ---- value types (dccrg_types.hpp:34-86, dccrg_length.hpp, dccrg_topology.hpp,
+// dccrg_mapping.hpp) --------------------------------------------------------
+template <unsigned int Dimensions>
+class Types {
+public:
+	// a cell's indices in units of the finest cells, x first
+	typedef std::array<uint64_t, Dimensions> indices_t;
+	// one neighborhood item: an offset in units of the cell's own size
+	typedef std::array<int, Dimensions> neighborhood_item_t;
+};
+
 class Grid_Length {
 public:
 	std::array<uint64_t, 3> get() const { return l_; }
@@ -515,6 +525,21 @@ public:
 		return cell_exists ? cell : error_cell;
 	}
 
+	// 11275-11308: the smallest cell known to exist at the indices between the
+	// two refinement levels (finest first); error_cell outside the grid
+	uint64_t get_existing_cell(const Types<3>::indices_t& indices, const int minimum_refinement_level,
+	                           const int maximum_refinement_level) const {
+		const auto L = mapping_rw.length.get();
+		const int R = mapping_rw.get_maximum_refinement_level();
+		for (size_t d = 0; d < 3; d++)
+			if (indices[d] >= L[d] * (uint64_t(1) << R)) return error_cell;
+		for (int l = maximum_refinement_level; l >= minimum_refinement_level; l--) {
+			const uint64_t c = mapping_rw.get_cell_from_indices(indices, l);
+			if (c != error_cell && dccrgx_get_process(g_, c) >= 0) return c;
+		}
+		return error_cell;
+	}
+
 	// ---- queries ----------------------------------------------------------------
 	// get_cells (651-739) with is_neighbor_type_match (2946-3053)
 	std::vector<uint64_t> get_cells(const std::vector<int>& criteria = std::vector<int>(), const bool exact_match = false,
@@ -661,16 +686,83 @@ public:
 		       wait_remote_neighbor_copy_update_sends(neighborhood_id);
 	}
 
+	// the default neighborhood and its opposite (6738 / 6748, initialize_neighborhoods
+	// 7895-7954): length 0 = the six face offsets, otherwise the cube without
+	// (0, 0, 0), z outermost, x innermost
+	const std::vector<Types<3>::neighborhood_item_t>& get_neighborhood_of() const {
+		default_hoods();
+		return hood_of_;
+	}
+	const std::vector<Types<3>::neighborhood_item_t>& get_neighborhood_to() const {
+		default_hoods();
+		return hood_to_;
+	}
+	// the user neighborhoods (6755-6775)
+	const std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>>& get_user_hood_of() const {
+		return user_hood_of_;
+	}
+	const std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>>& get_user_hood_to() const {
+		return user_hood_to_;
+	}
+	// 4339-4680: the neighbors of a cell for any neighborhood, in item order
+	// (a finer box as its eight cells); throws for a cell this process does
+	// not know.  For a local cell the items must stay within the process's
+	// ghost region (max(neighborhood length, 1) level-0 cells); for a remote
+	// cell the list may be incomplete, as the reference documents (4327).
+	neighbor_list_t find_neighbors_of(const uint64_t cell,
+	                                  const std::vector<Types<3>::neighborhood_item_t>& neighborhood) const {
+		std::vector<int32_t> items;
+		for (const auto& it : neighborhood) items.insert(items.end(), it.begin(), it.end());
+		size_t n = 0;
+		int rc = dccrgx_find_neighbors_of(g_, cell, items.data(), neighborhood.size(), nullptr, nullptr, 0, &n);
+		if (rc == DCCRGX_ENOTFOUND) throw std::runtime_error("dccrg: invalid cell: " + std::to_string(cell));
+		if (rc != DCCRGX_ERANGE) detail::check(rc);
+		std::vector<uint64_t> ids(n);
+		std::vector<int32_t> off(3 * n);
+		detail::check(dccrgx_find_neighbors_of(g_, cell, items.data(), neighborhood.size(), ids.data(), off.data(), n, &n));
+		neighbor_list_t r;
+		r.reserve(n);
+		for (size_t i = 0; i < n; i++) r.push_back({ids[i], {{off[3 * i], off[3 * i + 1], off[3 * i + 2]}}});
+		return r;
+	}
+	// 7107: the face-neighbor cache, per leaf the cell just across each face
+	// at the min corner (-x, +x, -y, +y, -z, +z; error_cell where none).  The
+	// reference holds every leaf of the grid; here the leaves this process can
+	// resolve: all local ones and the ghosts within its ghost region.  Valid
+	// until the next structural change.
+	const std::map<uint64_t, std::array<uint64_t, 6>>& get_neighbors_() const {
+		if (!face_cache_valid_) {
+			size_t n = 0;
+			int rc = dccrgx_get_face_cache(g_, nullptr, nullptr, 0, &n);
+			if (rc != DCCRGX_ERANGE) detail::check(rc);
+			std::vector<uint64_t> ids(n), nb(6 * n);
+			detail::check(dccrgx_get_face_cache(g_, ids.data(), nb.data(), n, &n));
+			face_cache_.clear();
+			for (size_t i = 0; i < n; i++)
+				face_cache_[ids[i]] = {{nb[6 * i], nb[6 * i + 1], nb[6 * i + 2], nb[6 * i + 3], nb[6 * i + 4], nb[6 * i + 5]}};
+			face_cache_valid_ = true;
+		}
+		return face_cache_;
+	}
+
 	// ---- user neighborhoods (6383-6603) -----------------------------------------------
 	bool add_neighborhood(const int neighborhood_id, const std::vector<std::array<int, 3>>& items) {
 		std::vector<int32_t> o;
 		for (const auto& it : items) o.insert(o.end(), it.begin(), it.end());
 		const bool ok = dccrgx_add_neighborhood(g_, neighborhood_id, o.data(), items.size()) == DCCRGX_OK;
-		if (ok) refresh_items();
+		if (ok) {
+			user_hood_of_[neighborhood_id] = items;
+			auto& to = user_hood_to_[neighborhood_id];
+			to.clear();
+			for (const auto& it : items) to.push_back({{-it[0], -it[1], -it[2]}});
+			refresh_items();
+		}
 		return ok;
 	}
 	void remove_neighborhood(const int neighborhood_id) {
 		detail::check(dccrgx_remove_neighborhood(g_, neighborhood_id));
+		user_hood_of_.erase(neighborhood_id);
+		user_hood_to_.erase(neighborhood_id);
 		refresh_items();
 	}
 
@@ -684,11 +776,17 @@ public:
 		size_t n = 0;
 		detail::check(dccrgx_stop_refining(g_, nullptr, 0, &n));
 		std::unordered_map<uint64_t, Cell_Data> gone;
-		// the local cells before the change, for the refined parents' data
+		// the refined local parents' data before the change (the parents of
+		// the new cells), for refined_cell_data below
 		std::unordered_map<uint64_t, Cell_Data> before;
-		if constexpr (!serialized_)
-			for (size_t s = 0; s < n_local_ && s < slot_ids_.size() && s < host_.size(); s++)
-				before.emplace(slot_ids_[s], host_[s]);
+		if constexpr (!serialized_) {
+			const auto created =
+			    detail::fetch_u64([&](uint64_t* o, size_t c, size_t* k) { return dccrgx_get_new_cells(g_, o, c, k); });
+			std::unordered_set<uint64_t> parents;
+			for (const uint64_t c : created) parents.insert(mapping_rw.get_parent(c));
+			for (size_t s = 0; s < n_local_ && s < slot_ids_.size() && s < host_.size() && !parents.empty(); s++)
+				if (parents.count(slot_ids_[s])) before.emplace(slot_ids_[s], host_[s]);
+		}
 		refresh(&gone);
 		if constexpr (serialized_) before = gone;
 		// removed cells' payloads on the parent's process (unrefined_cell_data 7250)
@@ -735,6 +833,11 @@ public:
 	bool pin(const uint64_t cell) { return pin(cell, rank_); }
 	bool pin(const uint64_t cell, const int process) { return dccrgx_pin(g_, cell, process) == DCCRGX_OK; }
 	bool unpin(const uint64_t cell) { return dccrgx_unpin(g_, cell) == DCCRGX_OK; }
+	// 6017: every pin is dropped (call on every process)
+	Dccrg& unpin_all_cells() {
+		detail::check(dccrgx_unpin_all_cells(g_));
+		return *this;
+	}
 	// 5952: unpin every local cell
 	bool unpin_local_cells() {
 		bool ok = true;
@@ -786,6 +889,7 @@ public:
 	// raw-byte header form
 	bool save_grid_data(const std::string& name, const uint64_t offset, const void* header = nullptr,
 	                    const size_t header_bytes = 0) {
+		sync_window();  // the bytes get_mpi_datatype describes now
 		upload_local();
 		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
 	}
@@ -951,6 +1055,11 @@ private:
 		detail::check(dccrgx_device_count(&ndev));
 		if (ndev < 1) throw std::runtime_error("dccrg: no GPU visible");
 		const int device = lrank % ndev;
+		// processes sharing a GPU split the library's device-memory cache
+		if (lsize > ndev && !std::getenv("DCCRGX_POOL_MAX_MB")) {
+			const int per_dev = (lsize + ndev - 1) / ndev;
+			setenv("DCCRGX_POOL_MAX_MB", std::to_string(16384 / per_dev).c_str(), 0);
+		}
 		const char* env = std::getenv("DCCRGX_TRANSPORT");
 		const bool host = env && std::string(env) == "host";
 		if (size_ == 1) {
@@ -1151,8 +1260,26 @@ private:
 		if constexpr (!serialized_) detail::check(dccrgx_removed_field_download(g_, payload_, out, bytes));
 	}
 
+	void default_hoods() const {
+		if (hood_set_ == hood_) return;
+		hood_of_.clear();
+		hood_to_.clear();
+		const int L = int(hood_);
+		if (L == 0) {
+			hood_of_ = {{{0, 0, -1}}, {{0, -1, 0}}, {{-1, 0, 0}}, {{1, 0, 0}}, {{0, 1, 0}}, {{0, 0, 1}}};
+		} else {
+			for (int z = -L; z <= L; z++)
+				for (int y = -L; y <= L; y++)
+					for (int x = -L; x <= L; x++)
+						if (x || y || z) hood_of_.push_back({{x, y, z}});
+		}
+		for (const auto& it : hood_of_) hood_to_.push_back({{-it[0], -it[1], -it[2]}});
+		hood_set_ = hood_;
+	}
+
 	void refresh_items() {
 		if (!g_) return;
+		face_cache_valid_ = false;
 		lists_.clear();
 		send_maps_.clear();
 		recv_maps_.clear();
@@ -1412,6 +1539,11 @@ private:
 	std::map<int, std::array<Iterator_Storage<Cells_Item>, 5>> user_ranges_;
 	mutable std::map<std::tuple<uint64_t, int, int>, neighbor_list_t> lists_;
 	mutable std::map<int, list_map> send_maps_, recv_maps_;
+	mutable std::vector<Types<3>::neighborhood_item_t> hood_of_, hood_to_;
+	mutable unsigned hood_set_ = ~0u;
+	std::unordered_map<int, std::vector<Types<3>::neighborhood_item_t>> user_hood_of_, user_hood_to_;
+	mutable std::map<uint64_t, std::array<uint64_t, 6>> face_cache_;
+	mutable bool face_cache_valid_ = false;
 };
 
 }  // namespace dccrg

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 6 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 7 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -147,7 +147,10 @@ int dccrgx_download_user_csr(dccrgx_grid* g, int hood_id, int kind, uint32_t* pt
                              size_t cap, size_t* n);
 /* get_neighbors_to 883 (ascending id, offsets 0) */
 int dccrgx_get_neighbors_to(dccrgx_grid* g, uint64_t cell, uint64_t* ids, size_t cap, size_t* n);
-/* get_face_neighbors_of 2806 (dirs -1,+1,-2,+2,-3,+3) */
+/* get_face_neighbors_of 2806 (dirs -1,+1,-2,+2,-3,+3): a local cell from the
+ * device face lists; a remote cell this process knows (e.g. a copy in
+ * all_cells()) from its known leaves, DCCRGX_ENOTFOUND if one of its faces
+ * lies beyond the ghost region */
 int dccrgx_get_face_neighbors_of(dccrgx_grid* g, uint64_t cell, uint64_t* ids, int32_t* dirs, size_t cap, size_t* n);
 /* is_local 3270, get_process 5807 (-1 for unknown cells) */
 int dccrgx_is_local(dccrgx_grid* g, uint64_t cell);
@@ -163,6 +166,29 @@ int dccrgx_get_cells_to_receive(dccrgx_grid* g, int peer, uint64_t* ids, size_t 
  * and its ghost leaves (the reference's get_cell_process 6848 returns every
  * leaf of the grid); ids == NULL: *n = count only */
 int dccrgx_get_cell_process(dccrgx_grid* g, uint64_t* ids, int32_t* owners, size_t cap, size_t* n);
+
+/* find_neighbors_of(cell, neighborhood) 4339-4680 for any list of n_items
+ * offsets (3 x int32 each, cell-sized units): the (id, x/y/z offset) pairs in
+ * item order, a finer box as its 8 cells in z-order, error cells dropped -
+ * the sequence the reference's walk over the face cache produces.
+ * DCCRGX_ENOTFOUND for a cell this process does not know (the reference
+ * throws, 4354-4362).  For a local cell every item's box must lie within the
+ * process's ghost region (max(neighborhood length, 1) level-0 cells around
+ * the cell's level-0 parent; DCCRGX_EINVAL otherwise); for a remote cell the
+ * list may be incomplete, as the reference documents (4327-4328). */
+int dccrgx_find_neighbors_of(dccrgx_grid* g, uint64_t cell, const int32_t* items, size_t n_items, uint64_t* ids,
+                             int32_t* offsets, size_t cap, size_t* n);
+/* get_neighbors_ 7098-7109 (the face-neighbor cache of update_neighbors_
+ * 9313-9458): per leaf the cell at the min corner just across each face,
+ * directions -x,+x,-y,+y,-z,+z, error_cell (0) where none.  The reference
+ * holds an entry for every leaf of the grid; here every known leaf whose six
+ * probes land in level-0 cells this process knows (all own leaves and the
+ * inner ghosts): n leaves ascending in ids, 6 x n entries in nbrs.  Costs
+ * O(known leaves) on the host (a query for tests, not a sweep). */
+int dccrgx_get_face_cache(dccrgx_grid* g, uint64_t* ids, uint64_t* nbrs, size_t cap, size_t* n);
+/* unpin_all_cells 6017: drop every pin of this process (collective in the
+ * reference; pins here are held by the process owning the cell) */
+int dccrgx_unpin_all_cells(dccrgx_grid* g);
 
 /* get_number_of_update_send_cells / _receive_cells 5382-5490 */
 int dccrgx_get_number_of_update_cells(dccrgx_grid* g, uint64_t* n_send, uint64_t* n_receive);

@@ -209,3 +209,30 @@ def test_variable_payload_file_empty_records(gpu, tmp_path):
     g.close()
     h.close()
     h2.close()
+
+
+def test_save_over_longer_file(gpu, tmp_path):
+    """save_grid_data over an older, longer file at the same path:
+    the file ends where the last record ends, so the last cell of a
+    variable-size field gets exactly its own bytes back."""
+    path = tmp_path / "reuse.dc"
+    big, _ = make_pair((9, 2, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    d = big.add_variable_field("data", np.int32)
+    d.set([np.full(40, 3, np.int32) for _ in range(big.n_local)])
+    big.save_grid_data(path)
+    long_size = os.path.getsize(path)
+    g, _ = make_pair((6, 1, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    data = g.add_variable_field("data", np.int32)
+    ids = g.slot_ids()[: g.n_local]
+    cnt = _counts(ids)
+    data.set([np.arange(int(k), dtype=np.int32) + 7 for k in cnt])
+    g.save_grid_data(path)
+    assert os.path.getsize(path) < long_size
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    e = h.add_variable_field("data", np.int32)
+    h.load_grid_data(path)
+    hid = h.slot_ids()[: h.n_local]
+    got = e.get(0, h.n_local)
+    assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, _counts(hid)))
+    for x in (big, g, h):
+        x.close()

@@ -1,0 +1,42 @@
+"""The reference's own known-answer test programs for the hot path, run
+through the drop-in facade on the GPU.
+
+Each program is compiled from /root/reference by __graft_entry__.build_examples()
+with only its include line rewritten (examples/bin/ref_kat_*); its checks are
+its own: it abort()s or returns non-zero on a wrong answer.  They pin, against
+reference-held assertions rather than the oracle:
+  get_cells/test1.cpp            get_cells criteria with user neighborhoods,
+                                 pins + balance_load(false), unpin_all_cells (a8, f4)
+  proc_bdy_cells/test1.cpp       local / remote cells on process boundaries (a8)
+  iterators/test1-5.cpp          inner / outer / remote ranges, cell.neighbors_of
+                                 / _to, refinement, find_neighbors_of (a9, a10)
+  get_face_neighbors/test1.cpp   face neighbor counts, periodicity, pins (a11)
+  get_neighbors_/test1.cpp       the face-neighbor cache, refined grids (a4)
+  user_neighborhood/neighbor_list_length.cpp   user-hood list lengths (f4)
+The reference's makefiles run every test at 1 process and under mpiexec
+(makefiles/homedir: -n 3); so does this file (get_cells needs >= 2).  Ranks
+share the one GPU through the library's host exchange over MPI."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "examples", "bin")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+KATS = ["get_cells", "proc_bdy_cells", "iterators1", "iterators2", "iterators3", "iterators4", "iterators5",
+        "get_face_neighbors", "get_neighbors_", "neighbor_list_length"]
+CASES = [(k, p) for k in KATS for p in ((2, 3) if k == "get_cells" else (1, 3))]
+
+
+@pytest.mark.parametrize("kat,P", CASES, ids=[f"{k}-n{p}" for k, p in CASES])
+def test_reference_kat(gpu, kat, P):
+    exe = os.path.join(BIN, "ref_kat_" + kat)
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} missing: run __graft_entry__.build() first")
+    r = subprocess.run([MPIEXEC, "-n", str(P), exe], capture_output=True, text=True, timeout=110)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "FAILED" not in out, out[-4000:]

@@ -92,14 +92,10 @@ def cpu_baseline(workload, seconds):
     return dict(value=total, unit="cell-updates/s", cores=cores, kind="port",
                 sample=f"oracle restatement ({outs[0]['sample']}, {outs[0]['cells']} cells) x {cores} processes, "
                        f"~{seconds:.0f} s each; per core {min(per_core):.3g}-{max(per_core):.3g} cell-updates/s",
-                cores_note=f"{cores} = this GPU's share of the host (the GPU box allots {CPU_SHARE} cores per GPU; "
-                           f"its worker pools are capped there), not all {nproc} cores: each process is one MPI "
-                           "rank on a per-rank subdomain (the advection sample is config 3 / 256 ranks in size)",
-                per_core_mean=total / cores,
-                extrapolated_all_cores={"value": total / cores * nproc, "cores": nproc,
-                                        "how": "per-core mean x all host cores (assumes linear scaling; "
-                                               "not measured)"},
-                nproc=nproc, affinity=avail, cpu_model=cpu_model())
+                cores_note=f"measured on {cores} cores, running at once: this GPU's share of the host (the GPU box "
+                           f"allots {CPU_SHARE} cores per GPU and caps worker pools there; {nproc} are visible); "
+                           "each process is one MPI rank of the reference's layout on its own subdomain",
+                per_core_mean=total / cores, nproc=nproc, affinity=avail, cpu_model=cpu_model())
 
 
 def measured_traffic(workload, cells, alg_bytes, world):

@@ -757,7 +757,7 @@ int dccrgx_create(int rank, int size, int device, const void* nccl_id, dccrgx_gr
 	return guard([&] {
 		DX_REQUIRE(out, "null output");
 		dccrgx_grid* h = new_grid(rank, size, device);
-		if (size > 1 && nccl_id) {  // without an id: a detached view of one rank (no transport)
+		if (nccl_id) {  // without an id: a detached view of one rank (no transport)
 			ncclUniqueId id;
 			std::memcpy(&id, nccl_id, sizeof(id));
 			const ncclResult_t r = ncclCommInitRank(&h->g.nccl, size, id, rank);
@@ -2491,6 +2491,21 @@ int dccrgx_barrier(dccrgx_grid* gp) {
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		double z = 0;
 		comm_allreduce_f64(g, &z, 1, 0);
+		return 0;
+	});
+}
+
+int dccrgx_comm_loopback(dccrgx_grid* gp, int field_id, size_t slot0, size_t n, size_t dst_slot0) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(g.nccl && !g.xfn, "loopback needs the RCCL transport");
+		Field& f = field(g, field_id);
+		DX_REQUIRE(!f.var, "loopback of a variable-size field");
+		DX_REQUIRE(slot0 + n <= g.n_slots && dst_slot0 + n <= g.n_slots, "slot range beyond the field");
+		DX_REQUIRE(slot0 + n <= dst_slot0 || dst_slot0 + n <= slot0, "overlapping slot ranges");
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));  // the field's producers
+		comm_loopback(g, f.data.p + slot0 * f.elem, f.data.p + dst_slot0 * f.elem, n * f.elem, g.s_comm);
+		HIP_CHECK(hipStreamSynchronize(g.s_comm));
 		return 0;
 	});
 }

@@ -85,6 +85,13 @@ void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t 
 	move_bytes(g, msgs, s);
 }
 
+// one message to this rank itself through the RCCL branch of the byte mover
+// (a grouped ncclSend / ncclRecv pair; a host exchange has no self peer)
+void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, hipStream_t s) {
+	DX_REQUIRE(g.nccl && !g.xfn, "loopback needs the RCCL transport");
+	move_bytes(g, {DevMsg{g.rank, static_cast<const uint8_t*>(send), bytes, static_cast<uint8_t*>(recv), bytes}}, s);
+}
+
 // every rank's `bytes` bytes at `mine` into all[p * bytes] (device), own
 // slot included; queued on s
 void comm_allgather_dev(Grid& g, const void* mine, size_t bytes, uint8_t* all, hipStream_t s) {

@@ -536,6 +536,7 @@ struct DevMsg {
 // one grouped point-to-point round of device messages (the same message list
 // for every transport; see comm.hip)
 void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s);
+void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, hipStream_t s);
 // every rank's `bytes` at `mine` into all[p * bytes] on the device (own slot included)
 void comm_allgather_dev(Grid& g, const void* mine, size_t bytes, uint8_t* all, hipStream_t s);
 // P x count values, rank-major, combined in rank order (op 0 sum, 1 min, 2 max)

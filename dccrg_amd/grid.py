@@ -187,9 +187,10 @@ class Dccrg:
             check(L.dccrgx_create_with_exchange(rank, size, device, exchange.fn, None, C.byref(h)))
         else:
             uid = None
-            if size > 1 and unique_id is not None:
+            if unique_id is not None:
                 # without a unique id the grid is a detached view of rank `rank`
-                # (structures only, no halo transport / collectives)
+                # (structures only, no halo transport / collectives); with one,
+                # an RCCL communicator (also of one rank)
                 uid = C.create_string_buffer(bytes(unique_id), 128)
             check(L.dccrgx_create(rank, size, device, uid, C.byref(h)))
         self.h = h
@@ -470,6 +471,11 @@ class Dccrg:
         nb = np.empty(6 * max(k, 1), np.uint64)
         check(lib().dccrgx_get_face_cache(self.h, _ptr(ids), _ptr(nb), k, C.byref(n)))
         return {int(ids[i]): tuple(int(v) for v in nb[6 * i: 6 * i + 6]) for i in range(k)}
+
+    def comm_loopback(self, field, slot0, n, dst_slot0):
+        """Field slots [slot0, slot0 + n) sent to this process itself through
+        the RCCL byte mover, received into [dst_slot0, ...) (transport check)."""
+        check(lib().dccrgx_comm_loopback(self.h, field.id, slot0, n, dst_slot0))
 
     def unpin_all_cells(self):
         check(lib().dccrgx_unpin_all_cells(self.h))

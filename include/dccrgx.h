@@ -462,6 +462,14 @@ int dccrgx_poisson_field(dccrgx_grid* g, const char* name, int* field_id);
 int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 sum, 1 min, 2 max */);
 int dccrgx_barrier(dccrgx_grid* g);
 
+/* Transport check (no reference counterpart): the bytes of a fixed-size
+ * field's slots [slot0, slot0 + n) sent by this process to itself and
+ * received straight into slots [dst_slot0, dst_slot0 + n) of the same field,
+ * through the grid's RCCL byte mover (one grouped ncclSend / ncclRecv, the
+ * path of every halo and migration message; a grid created with an RCCL id,
+ * also at size 1).  DCCRGX_EINVAL on a host-exchange or detached grid. */
+int dccrgx_comm_loopback(dccrgx_grid* g, int field_id, size_t slot0, size_t n, size_t dst_slot0);
+
 /* ---- stream / timing ----------------------------------------------------- */
 int dccrgx_synchronize(dccrgx_grid* g);
 void* dccrgx_compute_stream(dccrgx_grid* g);

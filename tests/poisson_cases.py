@@ -50,3 +50,72 @@ def boundary1d_classes(ix, nx):
     skip = (ix == 0) | (ix == nx - 1)
     bdy = (ix == 1) | (ix == nx - 2)
     return ~(skip | bdy), bdy, skip
+
+
+# ---- poisson1d.cpp / poisson2d.cpp / poisson1d_amr.cpp ----------------------
+GOLDEN = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "poisson1d_ref.npz")
+POISSON1D_SIZES = [8 << k for k in range(13)]  # 8 ... 32768 (poisson1d.cpp:149-154)
+POISSON1D_SOLVER = (10, 0, 1e-7, 2, 10)        # Poisson_Solve solver(10, 0, 1e-7, 2, 10, false), :164
+POISSON1D_THRESHOLD = 3e-7                     # norm_threshold, :283
+
+
+def poisson1d_reference(n):
+    """(solution, rhs) of the reference's serial solver for n cells
+    (tests/golden/poisson1d_ref.npz, made by tests/golden/make_poisson_ref.py
+    from tests/poisson/reference_poisson_solve.hpp compiled unmodified)."""
+    with np.load(GOLDEN) as z:
+        return z[f"n{n}"].copy(), z[f"rhs{n}"].copy()
+
+
+def offset_last(sol_by_index):
+    """offset_solution (poisson1d.cpp:90-121): zero in the last cell."""
+    return sol_by_index - sol_by_index[-1]
+
+
+def p_norm(a, b, p=2.0):
+    return float(np.sum(np.abs(a - b) ** p) ** (1.0 / p))
+
+
+def poisson2d_solution(x, y):
+    """poisson2d.cpp:37-45"""
+    return np.sin(x) * np.cos(2 * y)
+
+
+def poisson2d_rhs(x, y):
+    return -5 * poisson2d_solution(x, y)
+
+
+def poisson2d_cases(max_cells=128):
+    """The (cells_x, cells_y) sequence of poisson2d.cpp:150-165, whose loop
+    bounds move inside the loops: 4x4, 8x4, 4x8, 8x8, 16x8, 8x16, ...,
+    128x128 (the C loops executed as written)."""
+    out = []
+    lo, hi = 4, 8
+    cy = lo
+    while cy <= hi:
+        cx = lo
+        while cx <= hi:
+            if cy == 2 * cx:
+                lo = hi
+                if hi < max_cells:
+                    hi *= 2
+            out.append((cx, cy))
+            cx *= 2
+        cy *= 2
+    return out
+
+
+def amr1d_solution(x):
+    """poisson1d_amr.cpp:37-45"""
+    return np.sin(x / 2) ** 2
+
+
+def amr1d_rhs(x):
+    return 0.5 * (np.cos(x / 2) ** 2 - np.sin(x / 2) ** 2)
+
+
+def amr1d_normalize(sol, lvl, exact):
+    """normalize_solution (poisson1d_amr.cpp:47-105): offset so that the
+    8^-level weighted averages of solution and analytic agree."""
+    w = 1.0 / 8.0 ** lvl
+    return sol - (np.sum(w * sol) / np.sum(w) - np.sum(w * exact) / np.sum(w))

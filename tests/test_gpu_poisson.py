@@ -225,3 +225,129 @@ def test_failsafe_matches_oracle(gpu):
     assert it == oit
     assert abs(norm - onorm) <= 1e-12 * abs(onorm)
     compare_state(g, o, slots, 1e-13, ("solution",))
+
+
+# ---- the reference's own Poisson test programs through the product ----------
+def _grid_1d(n, d, h, R=0):
+    length = [1, 1, 1]
+    length[d] = n
+    L0 = [1.0, 1.0, 1.0]
+    L0[d] = h
+    g = dccrg_amd.Dccrg(0, 1, 0).set_initial_length(tuple(length)).set_neighborhood_length(0)
+    g.set_maximum_refinement_level(R).set_periodic(True, True, True).initialize()
+    g.set_geometry((0, 0, 0), tuple(L0))
+    return g
+
+
+def _solve_sorted(g, rhs_of_ids, solver):
+    """rhs / solution fields set from sorted local ids, solved, the solution
+    returned in sorted id order."""
+    ids = g.local_cells()
+    slots = g.slot_ids()[: g.n_local]
+    rhs = g.add_field("rhs", np.float64, False)
+    sol = g.add_field("solution", np.float64, False)
+    order = np.searchsorted(ids, slots)
+    rhs.set(rhs_of_ids(ids)[order])
+    sol.set(np.zeros(slots.size))
+    it, _ = solver.solve(ids, g)
+    out = np.empty(ids.size)
+    out[order] = sol.get(0, slots.size)
+    return ids, out, it
+
+
+def test_poisson1d_reference_through_product(gpu):
+    """tests/poisson/poisson1d.cpp:147-350 with the product's BiCG: n = 8 ...
+    32768 cells along x, y and z (periodic), Poisson_Solve(10, 0, 1e-7, 2,
+    10), offset to zero in the last cell; every solution within the 2-norm
+    3e-7 (norm_threshold, :283) of the reference's serial solution
+    (reference_poisson_solve.hpp compiled unmodified: tests/golden/
+    poisson1d_ref.npz) and of the other orientations."""
+    from poisson_cases import (POISSON1D_SIZES, POISSON1D_SOLVER, POISSON1D_THRESHOLD, offset_last, p_norm,
+                               poisson1d_reference)
+
+    for n in POISSON1D_SIZES:
+        ref, rhs = poisson1d_reference(n)
+        h = 2 * math.pi / n
+        sols = []
+        for d in range(3):
+            g = _grid_1d(n, d, h)
+            ids, sol, _ = _solve_sorted(g, lambda i: rhs[i.astype(np.int64) - 1],
+                                        dccrg_amd.Poisson_Solve(*POISSON1D_SOLVER))
+            assert np.array_equal(ids, np.arange(1, n + 1, dtype=np.uint64))
+            sol = offset_last(sol)
+            assert p_norm(sol, ref) <= POISSON1D_THRESHOLD, (n, d, p_norm(sol, ref))
+            sols.append(sol)
+            g.close()
+        for a in range(3):
+            for b in range(a + 1, 3):
+                assert p_norm(sols[a], sols[b]) <= POISSON1D_THRESHOLD, (n, a, b)
+
+
+def test_poisson2d_kat_through_product(gpu):
+    """tests/poisson/poisson2d.cpp:120-448: 2-D periodic grids in the yz, xz
+    and xy planes, 4x4 ... 128x128 cells, default solver; for each shape
+    class (n x n, 2n x n, n x 2n) the 2-norm error against sin(x) cos(2y)
+    must not grow with resolution (the program's PASSED criterion)."""
+    from poisson_cases import poisson2d_cases, poisson2d_rhs, poisson2d_solution
+
+    old = {}
+    for cx, cy in poisson2d_cases():
+        hx, hy = 2 * math.pi / cx, math.pi / cy
+        kind = "nn" if cx == cy else ("n2n" if cx == 2 * cy else ("2nn" if cy == 2 * cx else None))
+        for plane, (da, db) in enumerate(((1, 2), (0, 2), (0, 1))):
+            length = [1, 1, 1]
+            length[da], length[db] = cx, cy
+            L0 = [1.0, 1.0, 1.0]
+            L0[da], L0[db] = hx, hy
+            g = dccrg_amd.Dccrg(0, 1, 0).set_initial_length(tuple(length)).set_neighborhood_length(0)
+            g.set_maximum_refinement_level(0).set_periodic(True, True, True).initialize()
+            g.set_geometry((0, 0, 0), tuple(L0))
+            ids = g.local_cells()
+            c, _ = g.geometry(ids)
+            cmap = dict(zip(ids.tolist(), range(ids.size)))
+            _, sol, _ = _solve_sorted(g, lambda i: poisson2d_rhs(c[[cmap[int(k)] for k in i], da],
+                                                               c[[cmap[int(k)] for k in i], db]),
+                                      dccrg_amd.Poisson_Solve())
+            norm = math.sqrt(float(np.sum((sol - poisson2d_solution(c[:, da], c[:, db])) ** 2)))
+            if kind is not None:
+                key = (kind, plane)
+                assert norm <= old.get(key, float("inf")), (cx, cy, plane, norm, old.get(key))
+                old[key] = norm
+            g.close()
+    assert len(old) == 9
+
+
+def test_poisson1d_amr_kat_through_product(gpu):
+    """tests/poisson/poisson1d_amr.cpp:133-440: 1-D periodic grids of 32 ...
+    4096 level-0 cells along x, y and z at the deepest refinement level
+    (set_maximum_refinement_level(-1)), every even cell refined once, default
+    solver, solutions normalized to the analytic average (normalize_solution
+    :47-105); the 2-norm error must not grow with resolution and must stay
+    below the unrefined grid's (the program's PASSED criteria)."""
+    from poisson_cases import amr1d_normalize, amr1d_rhs, amr1d_solution
+
+    old = float("inf")
+    n = 32
+    while n <= 4096:
+        h = 2 * math.pi / n
+        norms = []
+        for d in range(4):  # x, y, z refined; 3 = the unrefined reference grid along x
+            g = _grid_1d(n, d % 3, h, R=-1 if d < 3 else 0)
+            if d < 3:
+                for cell in g.local_cells():
+                    if cell % 2 == 0:
+                        g.refine_completely(int(cell))
+                g.stop_refining()
+            ids = g.local_cells()
+            c, _ = g.geometry(ids)
+            x = c[:, d % 3]
+            _, sol, _ = _solve_sorted(g, lambda i: amr1d_rhs(x[np.searchsorted(ids, i)]), dccrg_amd.Poisson_Solve())
+            lvl = np.array([g.get_refinement_level(int(i)) for i in ids])
+            sol = amr1d_normalize(sol, lvl, amr1d_solution(x))
+            norms.append(math.sqrt(float(np.sum((sol - amr1d_solution(x)) ** 2))))
+            g.close()
+        for d in range(3):
+            assert norms[d] <= old, (n, d, norms[d], old)
+            assert norms[d] <= norms[3], (n, d, norms[d], norms[3])
+        old = norms[0]
+        n *= 2

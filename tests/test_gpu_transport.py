@@ -927,10 +927,59 @@ def sc_poisson(rank, world):
     return res
 
 
+def sc_poisson1d(rank, world):
+    """tests/poisson/poisson1d.cpp:147-350 across real processes: 1-D
+    periodic grids of n cells along x, y and z, every cell pinned to rank
+    id % size (its emulated RANDOM balance, 205-217), balance_load(false),
+    unpin_all_cells, Poisson_Solve(10, 0, 1e-7, 2, 10) on every local cell,
+    offset to zero in the last cell; the gathered solution within the 2-norm
+    3e-7 of the reference's serial solver (tests/golden/poisson1d_ref.npz)
+    and of the other orientations."""
+    import math
+
+    import dccrg_amd
+    from poisson_cases import (POISSON1D_SIZES, POISSON1D_SOLVER, POISSON1D_THRESHOLD, offset_last, p_norm,
+                               poisson1d_reference)
+
+    res = {"spans_ranks": False}
+    for n in POISSON1D_SIZES[::3]:  # 8, 64, 512, 4096, 32768
+        ref, rhs = poisson1d_reference(n)
+        h = 2 * math.pi / n
+        sols = []
+        for d in range(3):
+            length, L0 = [1, 1, 1], [1.0, 1.0, 1.0]
+            length[d], L0[d] = n, h
+            g = _grid(tuple(length), 0, (True, True, True), 0)
+            g.set_geometry((0, 0, 0), tuple(L0))
+            for c in g.local_cells():
+                g.pin(int(c), int(c) % world)
+            g.balance_load(False)
+            g.unpin_all_cells()
+            slots = g.slot_ids()[: g.n_local]
+            res["spans_ranks"] = res["spans_ranks"] or len(g.remote_cells()) > 0
+            rf = g.add_field("rhs", np.float64, False)
+            sf = g.add_field("solution", np.float64, False)
+            rf.set(rhs[slots.astype(np.int64) - 1])
+            sf.set(np.zeros(slots.size))
+            dccrg_amd.Poisson_Solve(*POISSON1D_SOLVER).solve(slots, g)
+            parts = _gather(dict(zip(slots.tolist(), sf.get(0, slots.size).tolist())))
+            d_all = {}
+            for part in parts:
+                d_all.update(part)
+            sols.append(offset_last(np.array([d_all[i] for i in range(1, n + 1)])))
+            res[f"owners_{n}_{d}"] = bool(np.all(slots % world == rank))
+            g.close()
+        res[f"n{n}"] = bool(all(p_norm(s_, ref) <= POISSON1D_THRESHOLD for s_ in sols) and
+                            all(p_norm(sols[a], sols[b]) <= POISSON1D_THRESHOLD for a in range(3)
+                                for b in range(a + 1, 3)))
+    return res
+
+
 SCENARIOS = {
-    2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson", "sc_gol_halfshift"],
+    2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson", "sc_gol_halfshift", "sc_poisson1d"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
-        "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable", "sc_poisson", "sc_gol_halfshift"],
+        "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable", "sc_poisson", "sc_gol_halfshift",
+        "sc_poisson1d"],
 }
 
 
@@ -1061,6 +1110,15 @@ def test_advection_adapt_across_ranks(transport_results):
 def test_poisson_distributed(transport_results):
     """Config 4 across 2 and 3 real processes (sc_poisson runs at both)."""
     _check(transport_results, "sc_poisson", ["mesh", "spans_ranks", "iters_1", "iters_5", "iters_20", "kat"])
+
+
+def test_poisson1d_reference_distributed(transport_results):
+    """poisson1d.cpp's grids at 2 and 3 processes against the reference's
+    serial solver (sc_poisson1d)."""
+    keys = ["spans_ranks"] + [f"n{n}" for n in (8, 64, 512, 4096, 32768)]
+    _check(transport_results, "sc_poisson1d", keys)
+    for _, out in transport_results["sc_poisson1d"].values():
+        assert all(v for k, v in out.items() if k.startswith("owners_"))
 
 
 def test_save_grid_data_three_ranks(transport_results):

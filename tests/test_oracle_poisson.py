@@ -96,3 +96,35 @@ def test_failsafe_converges():
     o, ids, c, L, L0 = oracle_poisson3d(n=4, rounds=1)
     it, norm = o.po_solve(max_iterations=20000, stop_residual=1e-9, failsafe=True)
     assert norm <= 1e-9 and it < 20000
+
+
+def test_poisson1d_reference_fixture_and_oracle():
+    """tests/poisson/poisson1d.cpp:147-350 on the oracle: 1-D periodic grids
+    of n cells (x, y and z orientation) solved by BiCG (10, 0, 1e-7, 2, 10),
+    offset to zero in the last cell, must lie within the 2-norm 3e-7 of the
+    reference's own serial solution (tests/golden/poisson1d_ref.npz, from
+    reference_poisson_solve.hpp compiled unmodified) and of each other."""
+    from poisson_cases import (POISSON1D_SOLVER, POISSON1D_THRESHOLD, offset_last, p_norm,
+                               poisson1d_reference)
+
+    for n in (8, 16, 64, 256, 1024):
+        ref, rhs = poisson1d_reference(n)
+        assert abs(float(np.sum(rhs))) < 1e-12 and abs(ref[-1]) < 1e-9  # the recurrence ends near 0
+        h = 2 * math.pi / n
+        sols = []
+        for d in range(3):
+            length = [1, 1, 1]
+            length[d] = n
+            L0 = [1.0, 1.0, 1.0]
+            L0[d] = h
+            o = O.Grid(tuple(length), 0, (True, True, True), 0, 1)
+            o.set_geometry((0, 0, 0), tuple(L0))
+            ids, _ = o.cells()
+            o.po_set(ids, rhs[ids.astype(np.int64) - 1], np.zeros(ids.size), np.zeros(ids.size, np.int32))
+            o.po_solve(*POISSON1D_SOLVER)
+            sol = offset_last(o.po_get(ids)[:, 0])
+            assert p_norm(sol, ref) <= POISSON1D_THRESHOLD, (n, d, p_norm(sol, ref))
+            sols.append(sol)
+        for a in range(3):
+            for b in range(a + 1, 3):
+                assert p_norm(sols[a], sols[b]) <= POISSON1D_THRESHOLD

@@ -134,6 +134,7 @@ _SIGS = {
     "dccrgx_gol_step": (C.c_int, [vp, C.c_int, C.c_int]),
     "dccrgx_gol_commit": (C.c_int, [vp, C.c_int]),
     "dccrgx_gol_amr": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "dccrgx_get_live_neighbors": (C.c_int, [vp, C.c_int, C.c_int]),
     "dccrgx_advection_step": (C.c_int, [vp, P(C.c_int), C.c_double, C.c_int]),
     "dccrgx_advection_commit": (C.c_int, [vp, C.c_int]),
     "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),

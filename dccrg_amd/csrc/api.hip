@@ -1805,6 +1805,7 @@ int dccrgx_migration_pack(dccrgx_grid* gp, int peer, void* buf, size_t cap) {
 int dccrgx_migration_place(dccrgx_grid* gp, int peer, const void* buf, size_t bytes) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
+		for (auto& f : g.fields) f.local_zero = false;
 		migration_place_peer(g, peer, static_cast<const uint8_t*>(buf), bytes);
 		return 0;
 	});
@@ -1838,6 +1839,7 @@ int dccrgx_start_loading_grid_data(dccrgx_grid* gp, const char* path, uint64_t o
 int dccrgx_continue_loading_grid_data(dccrgx_grid* gp, int field_id, const uint64_t* sizes) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
+		for (auto& f : g.fields) f.local_zero = false;
 		continue_load_impl(g, field_id, sizes);
 		return 0;
 	});
@@ -2050,6 +2052,7 @@ int dccrgx_set_field_window(dccrgx_grid* gp, int fid, size_t offset, size_t byte
 int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
+		field(g, fid).local_zero = false;
 		*ptr = fixed_field(g, fid).data.p;
 		return 0;
 	});
@@ -2058,6 +2061,7 @@ int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const void* host) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
+		field(g, fid).local_zero = false;
 		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
@@ -2162,11 +2166,78 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 		k_gol_amr(phase, g.gola, g.n_slots, g.n_local, (uint32_t*)st.data.p, (uint64_t*)ls.data.p, g.nof_ptr.p, g.nof_slot.p, s0,
 		          s1, err.p, g.s_comp);
 		k_time_end(g);
+		if (phase == 0) ls.local_zero = false;
 		int h = 0;
 		HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
 		DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+		return 0;
+	});
+}
+
+// One turn of get_live_neighbors (tests/game_of_life/solve.hpp:37-170):
+// collect, the halo, spread + rule, and every local list error_cell-cleared
+// at the end as the reference's rule loop leaves it (163).  Collected lists
+// stay in the kernels' per-cell masks; only the cells other processes read
+// (the outer run) write theirs into list_field for the halo, then clear them.
+static void check_gol_err(Grid& g, DBuf<int>& err) {
+	int h = 0;
+	HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+	DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+}
+
+int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		Field& st = field(g, sf);
+		Field& ls = field(g, lf);
+		DX_REQUIRE(st.elem == 4, "game of life state must be a 4-byte field");
+		DX_REQUIRE(ls.elem == 64, "live level-0 neighbor list must be a 64-byte field (8 x uint64)");
+		const size_t nl = g.n_local;
+		if (!nl && g.size == 1) return 0;
+		ensure_csr(g);
+		DBuf<int> err;
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		if (!g.gola.valid)
+			k_gol_amr_tables(g.m, g.slot_ids.p, g.n_slots, g.n_local, g.hood_len, g.nof_ptr.p, g.nof_slot.p, g.gola,
+			                 g.s_comp);
+		uint64_t* L = reinterpret_cast<uint64_t*>(ls.data.p);
+		uint32_t* S = reinterpret_cast<uint32_t*>(st.data.p);
+		// the inner cells' lists are never written by the turn: clear them once
+		const bool lean = g.gola.mask_path;
+		if (lean && !ls.local_zero && g.n_inner) HIP_CHECK(hipMemsetAsync(L, 0, g.n_inner * 64, g.s_comp));
+		k_time_begin(g);
+		bool exact = true;
+		if (lean && g.gola.geo) {
+			// the geometric collect; the exact per-entry one when a family's
+			// leaves disagree or a reached level-0 cell is unknown (the
+			// reference's abort conditions then depend on the entry order)
+			k_gol_amr_geo(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, nl, nl + g.n_recv, L, g.n_inner, err.p,
+			              g.s_comp);
+			int h = 0;
+			HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+			exact = (h & (4 | 8)) != 0;
+			if (exact) HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		}
+		if (exact)
+			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp,
+			          lean ? g.n_inner : 0);
+		k_time_end(g);
+		check_gol_err(g, err);
+		halo_start(g);  // update_copies_of_remote_neighbors (solve.hpp:111)
+		halo_wait(g);
+		k_time_begin(g);
+		k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp);
+		k_time_end(g);
+		const size_t c0 = lean ? g.n_inner : 0;
+		if (nl > c0) HIP_CHECK(hipMemsetAsync(L + c0 * 8, 0, (nl - c0) * 64, g.s_comp));
+		check_gol_err(g, err);
+		ls.local_zero = true;
 		return 0;
 	});
 }

@@ -237,6 +237,10 @@ struct Field {
 	// (rm_off, one entry per removed cell + 1)
 	bool var = false;
 	DBuf<uint64_t> voff, rm_off;
+	// every local element known to be all-zero bytes (set by the refined game
+	// of life turn, which leaves each local list error_cell-cleared as the
+	// reference does; dropped by anything that may write local payloads)
+	bool local_zero = false;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
@@ -380,6 +384,14 @@ struct GolAmrTables {
 	DBuf<uint32_t> l0c, ent, mask;
 	size_t n_ent = 0;
 	uint32_t bx = 0, by = 0, lx = 0, ly = 0, lz = 0;
+	// geometric collect (maximum refinement level <= 1, mask path): per local
+	// slot its child octant (bit 7: a level-0 leaf); per level-0 cell of the
+	// known region's bounding box a byte (bit 0: a known leaf there alive,
+	// bit 1: one dead)
+	bool geo = false;
+	DBuf<uint8_t> corner, l0tab;
+	uint32_t box0[3] = {0, 0, 0}, boxn[3] = {0, 0, 0};
+	int per[3] = {0, 0, 0};
 };
 
 struct GolBox {
@@ -731,8 +743,15 @@ void var_remap(Field& f, const uint64_t* old_ids, size_t n_old_local, const DevM
 // refined game of life (gol_amr.hip): per-mesh tables, then one phase
 void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots, size_t n_local, unsigned hood_len,
                       const uint32_t* ptr, const int32_t* nslot, GolAmrTables& T, hipStream_t s);
+// the geometric collect of one turn (gol_amr.hip): level-0 cell states from
+// the known leaves, then every local row's live level-0 parents as a mask
+// (lists written for rows >= list_from); err bits 1 (over 8), 4 (a family's
+// leaves disagree) and 8 (a reached level-0 cell unknown): with 4 or 8 the
+// caller runs the exact collect instead
+void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t* state, size_t n_local, size_t n_state,
+                   uint64_t* lst, size_t list_from, int* err, hipStream_t s);
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
-               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s);
+               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots

@@ -29,6 +29,7 @@
 // (a dependent gather per neighbor entry).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "dccrgx_internal.hpp"
@@ -309,7 +310,7 @@ __device__ __forceinline__ uint32_t mask_entry_byte(uint32_t q, const uint32_t* 
 __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
     const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ ptr,
     const uint32_t* __restrict__ l0c, L0Geom G, uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0,
-    size_t s1, int* __restrict__ err) {
+    size_t s1, size_t w0, int* __restrict__ err) {
 	// entry bytes staged per block; after the walks the same 16 KB hold the
 	// block's lists (256 rows x 64 B) for a coalesced store
 	// (the lists at a row stride of 80 B: five 16-B slots, conflict-free
@@ -417,22 +418,28 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 		const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
 		out[i] = uint32_t(i) < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
 	}
-	// the lists through LDS: each row's 64 B at its place, then the block's
-	// rows stored as one contiguous run, 16 B per lane and instruction,
-	// non-temporal (paired A/B: 0.713 -> 0.693 ms per step)
-	__syncthreads();  // every walk done: the staged entry bytes are free
-	ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
-	if (act)
+	// the lists of rows [w0, s1) through LDS: each row's 64 B at its place,
+	// then the block's rows stored as one contiguous run, 16 B per lane and
+	// instruction, non-temporal (paired A/B: 0.713 -> 0.693 ms per step).
+	// Rows below w0 keep their lists in the mask only (the turn's inner
+	// cells: no other process reads them, block-uniform skip)
+	if (r1 > w0) {
+		const size_t rs = r0 > w0 ? r0 : w0;
+		__syncthreads();  // every walk done: the staged entry bytes are free
+		ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
+		if (act)
 #pragma unroll
-		for (int i = 0; i < kList / 2; i++) so[tid * kRowSlots + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
-	__syncthreads();
-	ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + r0 * kList);
-	const uint32_t n16 = uint32_t(r1 - r0) * (kList / 2);
-	for (uint32_t k = tid; k < n16; k += kCollectRows) {
-		typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
-		const ulonglong2 v = so[(k / (kList / 2)) * kRowSlots + k % (kList / 2)];
-		const u2v w = {v.x, v.y};
-		__builtin_nontemporal_store(w, reinterpret_cast<u2v*>(dst + k));
+			for (int i = 0; i < kList / 2; i++) so[tid * kRowSlots + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+		__syncthreads();
+		ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + rs * kList);
+		const uint32_t skip = uint32_t(rs - r0);
+		const uint32_t n16 = uint32_t(r1 - rs) * (kList / 2);
+		for (uint32_t k = tid; k < n16; k += kCollectRows) {
+			typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+			const ulonglong2 v = so[(skip + k / (kList / 2)) * kRowSlots + k % (kList / 2)];
+			const u2v w = {v.x, v.y};
+			__builtin_nontemporal_store(w, reinterpret_cast<u2v*>(dst + k));
+		}
 	}
 	if (act) mask_out[s] = mask;
 }
@@ -497,6 +504,241 @@ __global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ g
 	if (n > kList && m == 0) atomicOr(err, 1);
 	for (uint32_t j = b + m; j < e; j += 8)
 		if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
+}
+
+// ---- geometric collect ------------------------------------------------------
+// With at most one refinement level, the level-0 cells a leaf's stencil
+// reaches are fixed by geometry: a level-0 leaf's item h reaches the level-0
+// cell at offset h; a level-1 leaf (child octant c) reaches, per axis,
+// floor((c + h) / 2) (-1, 0 or +1).  Every neighbor leaf the reference's
+// walk (find_neighbors_of, dccrg.hpp:4339-4680) lists for that item lies in
+// that level-0 cell, and every level-0 cell reached holds at least one of
+// them.  When the known leaves of every level-0 cell agree on their state
+// (siblings always do in the emulated game; the reference aborts otherwise,
+// solve.hpp:81-90), the live level-0 parents of a row are the reached cells
+// whose leaves are alive: the collect needs one byte per level-0 cell instead
+// of the row's neighbor entries.  Disagreeing families, or a reached cell
+// without a known leaf, set an error bit and the caller runs the exact
+// per-entry collect instead.
+struct GeoBox {
+	uint32_t x0, y0, z0, nx, ny, nz;
+	int px, py, pz;
+	__device__ __forceinline__ bool index(const L0Geom& G, int x, int y, int z, uint32_t& out) const {
+		if (x < 0 || x >= int(G.lx)) {
+			if (!px) return false;
+			x = x < 0 ? x + int(G.lx) : x - int(G.lx);
+		}
+		if (y < 0 || y >= int(G.ly)) {
+			if (!py) return false;
+			y = y < 0 ? y + int(G.ly) : y - int(G.ly);
+		}
+		if (z < 0 || z >= int(G.lz)) {
+			if (!pz) return false;
+			z = z < 0 ? z + int(G.lz) : z - int(G.lz);
+		}
+		const uint32_t ix = uint32_t(x) - x0, iy = uint32_t(y) - y0, iz = uint32_t(z) - z0;
+		out = ix < nx && iy < ny && iz < nz ? ix + nx * (iy + ny * iz) : 0xffffffffu;
+		return true;
+	}
+};
+
+// level-0 leaves: their own state (one writer per cell)
+__global__ void geo_l0_leaves_kernel(const uint32_t* __restrict__ l0, const uint32_t* __restrict__ l0c,
+                                     const uint32_t* __restrict__ state, size_t n, L0Geom G, GeoBox B,
+                                     uint8_t* __restrict__ tab) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		if (!(l0[s] & kLevel0)) continue;
+		int x, y, z;
+		l0_unpack(l0c[s], G, x, y, z);
+		uint32_t k;
+		if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = state[s] ? 1u : 2u;
+	}
+}
+
+// refined level-0 cells: the OR of their known leaves' states (a group is
+// one level-0 parent's leaves), eight lanes per group side by side, OR-ed by
+// shuffles; both bits set = the leaves disagree
+__global__ void geo_l0_groups_kernel(const uint32_t* __restrict__ gptr, size_t ng, const uint32_t* __restrict__ gslot,
+                                     const uint32_t* __restrict__ l0c, const uint32_t* __restrict__ state, size_t n_state,
+                                     L0Geom G, GeoBox B, uint8_t* __restrict__ tab, int* __restrict__ err) {
+	const size_t t = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	const size_t gi = t >> 3;
+	const uint32_t m = uint32_t(t & 7u);
+	const bool live = gi < ng;  // the eight lanes of a group share a wave: no early exit
+	const uint32_t b = live ? gptr[gi] : 0u, e = live ? gptr[gi + 1] : 0u;
+	uint32_t v = 0, any = 0;
+	for (uint32_t j = b + m; j < e; j += 8) {
+		const uint32_t gs = gslot[j];
+		if (gs >= n_state) continue;  // a remote cell whose state is never received
+		v |= state[gs] ? 1u : 2u;
+		any = gs + 1;
+	}
+#pragma unroll
+	for (int o = 1; o < 8; o <<= 1) {
+		v |= __shfl_xor(v, o, 8);
+		any = max(any, uint32_t(__shfl_xor(int(any), o, 8)));
+	}
+	if (!live || !any || m != 0) return;
+	if (v == 3u) atomicOr(err, 4);
+	int x, y, z;
+	l0_unpack(l0c[any - 1], G, x, y, z);
+	uint32_t k;
+	if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = uint8_t(v);
+}
+
+// one axis of a row's reach: for offsets -1, 0, +1 whether the row's stencil
+// reaches that level-0 layer (a level-1 leaf only its own and the one on its
+// octant's side; nothing beyond a non-periodic boundary), whether that layer
+// lies in the table's box, and its offset into the table
+__device__ __forceinline__ void geo_axis(int p, uint32_t L, uint32_t b0, uint32_t bn, int per, bool lvl0, int side,
+                                         uint32_t stride, bool (&reach)[3], bool (&in)[3], uint32_t (&off)[3]) {
+#pragma unroll
+	for (int i = 0; i < 3; i++) {
+		const int d = i - 1;
+		int q = p + d;
+		bool r = lvl0 || d == 0 || d == side;
+		if (q < 0 || q >= int(L)) {
+			r = r && per;
+			q = q < 0 ? q + int(L) : q - int(L);
+		}
+		const uint32_t k = uint32_t(q) - b0;
+		reach[i] = r;
+		in[i] = k < bn;
+		off[i] = k * stride;
+	}
+}
+
+// CUBE: neighborhood length 1 (the 26 offsets around the cell: a level-0
+// leaf reaches the 26 level-0 cells around it, a level-1 leaf the 7 of its
+// octant's 2 x 2 x 2 corner); else length 0 (the 6 faces: a level-0 leaf its
+// 6 face neighbors' level-0 cells, a level-1 leaf the 3 on its octant's sides)
+template <bool CUBE>
+__global__ __launch_bounds__(256) void geo_collect_kernel(const uint32_t* __restrict__ l0c,
+                                                          const uint8_t* __restrict__ corner,
+                                                          const uint8_t* __restrict__ tab, L0Geom G, GeoBox B,
+                                                          size_t n, uint32_t* __restrict__ mask_out,
+                                                          uint64_t* __restrict__ lst, size_t w0, int* __restrict__ err) {
+	const size_t s = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	if (s >= n) return;
+	int px, py, pz;
+	l0_unpack(l0c[s], G, px, py, pz);
+	const uint32_t c = corner[s];
+	const bool lvl0 = c & 0x80u;
+	bool rx[3], ry[3], rz[3], ix[3], iy[3], iz[3];
+	uint32_t ox[3], oy[3], oz[3];
+	geo_axis(px, G.lx, B.x0, B.nx, B.px, lvl0, (c & 1u) ? 1 : -1, 1u, rx, ix, ox);
+	geo_axis(py, G.ly, B.y0, B.ny, B.py, lvl0, (c & 2u) ? 1 : -1, B.nx, ry, iy, oy);
+	geo_axis(pz, G.lz, B.z0, B.nz, B.pz, lvl0, (c & 4u) ? 1 : -1, B.nx * B.ny, rz, iz, oz);
+	// every reached cell's byte in flight at once, then the bits; the own
+	// level-0 parent (solve.hpp:72-74) is never read
+	constexpr int K = CUBE ? 27 : 7;
+	uint32_t v[K];
+	bool r[K];
+#pragma unroll
+	for (int t = 0; t < K; t++) {
+		int a, b, d;
+		if (CUBE) {
+			a = t % 3;
+			b = (t / 3) % 3;
+			d = t / 9;
+		} else {  // the centre, then -x, +x, -y, +y, -z, +z
+			a = t == 1 ? 0 : (t == 2 ? 2 : 1);
+			b = t == 3 ? 0 : (t == 4 ? 2 : 1);
+			d = t == 5 ? 0 : (t == 6 ? 2 : 1);
+		}
+		const bool centre = a == 1 && b == 1 && d == 1;
+		r[t] = !centre && rx[a] && ry[b] && rz[d];
+		const bool inb = ix[a] && iy[b] && iz[d];
+		v[t] = r[t] ? (inb ? uint32_t(tab[ox[a] + oy[b] + oz[d]]) : 0u) : 0u;
+	}
+	uint32_t mask = 0, e = 0;
+#pragma unroll
+	for (int t = 0; t < K; t++) {
+		int a, b, d;
+		if (CUBE) {
+			a = t % 3;
+			b = (t / 3) % 3;
+			d = t / 9;
+		} else {
+			a = t == 1 ? 0 : (t == 2 ? 2 : 1);
+			b = t == 3 ? 0 : (t == 4 ? 2 : 1);
+			d = t == 5 ? 0 : (t == 6 ? 2 : 1);
+		}
+		e |= (r[t] && v[t] == 0u) ? 8u : 0u;  // a reached cell without a known leaf
+		mask |= (r[t] && v[t] == 1u) ? (1u << (9 * d + 3 * b + a)) : 0u;
+	}
+	const uint32_t cnt = __popc(mask);
+	if (cnt > uint32_t(kList)) e |= 1u;
+	if (e) atomicOr(err, int(e));
+	mask_out[s] = mask;
+	if (s < w0) return;
+	// the row's list for the processes that receive it: the live parents in
+	// position order (a set to the receiver's spread), error_cell padded
+	auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
+	const uint64_t lxy = uint64_t(G.lx) * G.ly;
+	uint64_t out[kList];
+	uint32_t m = mask;
+#pragma unroll
+	for (int i = 0; i < kList; i++) {
+		out[i] = error_cell;
+		if (!m) continue;
+		const int b = __ffs(m) - 1;
+		m &= m - 1u;
+		const int bz = b / 9, by = (b / 3) % 3, bx = b % 3;
+		out[i] = 1 + uint64_t(wrap(px + bx - 1, int(G.lx))) + uint64_t(wrap(py + by - 1, int(G.ly))) * G.lx +
+		         uint64_t(wrap(pz + bz - 1, int(G.lz))) * lxy;
+	}
+	ulonglong2* o = reinterpret_cast<ulonglong2*>(lst + s * kList);
+#pragma unroll
+	for (int i = 0; i < kList / 2; i++) o[i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+}
+
+// per local slot: the child octant of a level-1 leaf, bit 7 for a level-0 leaf
+__global__ void geo_corner_kernel(MapCtx m, const uint64_t* __restrict__ ids, size_t n, uint8_t* __restrict__ corner) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		uint64_t x, y, z;
+		const int l = map_indices(m, ids[s], x, y, z);
+		corner[s] = l <= 0 ? 0x80u : uint8_t((x & 1u) | ((y & 1u) << 1) | ((z & 1u) << 2));
+	}
+}
+
+// bounding box of the known level-0 coordinates (min / max per axis)
+__global__ void geo_bbox_kernel(const uint32_t* __restrict__ l0c, size_t n, L0Geom G, int* __restrict__ mm) {
+	int lo[3] = {1 << 30, 1 << 30, 1 << 30}, hi[3] = {-1, -1, -1};
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		int v[3];
+		l0_unpack(l0c[s], G, v[0], v[1], v[2]);
+		for (int d = 0; d < 3; d++) {
+			lo[d] = min(lo[d], v[d]);
+			hi[d] = max(hi[d], v[d]);
+		}
+	}
+	for (int d = 0; d < 3; d++) {
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			lo[d] = min(lo[d], __shfl_xor(lo[d], o, 64));
+			hi[d] = max(hi[d], __shfl_xor(hi[d], o, 64));
+		}
+	}
+	// one atomic per block and bound (same-address atomics serialise)
+	__shared__ int sl[3][4], shh[3][4];
+	const unsigned w = threadIdx.x >> 6;
+	if ((threadIdx.x & 63u) == 0)
+		for (int d = 0; d < 3; d++) {
+			sl[d][w] = lo[d];
+			shh[d][w] = hi[d];
+		}
+	__syncthreads();
+	if (threadIdx.x < 3) {
+		const int d = int(threadIdx.x);
+		int a = sl[d][0], b = shh[d][0];
+		for (unsigned k = 1; k < (blockDim.x >> 6); k++) {
+			a = min(a, sl[d][k]);
+			b = max(b, shh[d][k]);
+		}
+		atomicMin(mm + d, a);
+		atomicMax(mm + 3 + d, b);
+	}
 }
 
 }  // namespace
@@ -592,17 +834,82 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		HIP_CHECK(hipStreamSynchronize(s));
 		T.mask_path = hb == 0;
 	}
+	// geometric collect: maximum refinement level <= 1 on the mask path, the
+	// level-0 cells of the known region's bounding box in one table
+	T.geo = false;
+	T.corner.release();
+	T.l0tab.release();
+	if (T.mask_path && m.R <= 1 && n_slots) {
+		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
+		DBuf<int> mm;
+		mm.alloc(6);
+		const int init[6] = {1 << 30, 1 << 30, 1 << 30, -1, -1, -1};
+		HIP_CHECK(hipMemcpyAsync(mm.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+		geo_bbox_kernel<<<std::min<unsigned>(grid_for(n_slots, 256), 1024), 256, 0, s>>>(T.l0c.p, n_slots, G, mm.p);
+		HIP_CHECK(hipGetLastError());
+		int h[6];
+		HIP_CHECK(hipMemcpyAsync(h, mm.p, sizeof(h), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		const uint32_t L[3] = {T.lx, T.ly, T.lz};
+		uint64_t vol = 1;
+		for (int d = 0; d < 3; d++) {
+			T.per[d] = m.periodic[d];
+			// a periodic axis whose known coordinates touch both ends wraps:
+			// the whole axis
+			const bool whole = m.periodic[d] && h[d] == 0 && h[3 + d] == int(L[d]) - 1;
+			T.box0[d] = whole ? 0u : uint32_t(h[d]);
+			T.boxn[d] = whole ? L[d] : uint32_t(h[3 + d] - h[d] + 1);
+			vol *= T.boxn[d];
+		}
+		if (vol < (uint64_t(1) << 31)) {
+			T.l0tab.alloc(size_t(vol));
+			HIP_CHECK(hipMemsetAsync(T.l0tab.p, 0, size_t(vol), s));
+			T.corner.alloc(n_local + 1);
+			if (n_local) {
+				geo_corner_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(m, slot_ids, n_local, T.corner.p);
+				HIP_CHECK(hipGetLastError());
+			}
+			HIP_CHECK(hipStreamSynchronize(s));
+			T.geo = true;
+		}
+	}
 	T.valid = true;
 }
 
+void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t* state, size_t n_local, size_t n_state,
+                   uint64_t* lst, size_t list_from, int* err, hipStream_t s) {
+	DX_REQUIRE(T.geo && (nh == 26 || nh == 6), "geometric collect not available");
+	const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
+	const GeoBox B{T.box0[0], T.box0[1], T.box0[2], T.boxn[0], T.boxn[1], T.boxn[2], T.per[0], T.per[1], T.per[2]};
+	if (n_state) {
+		geo_l0_leaves_kernel<<<grid_for(n_state, 256), 256, 0, s>>>(T.l0.p, T.l0c.p, state, n_state, G, B, T.l0tab.p);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (T.ng) {
+		geo_l0_groups_kernel<<<xcd_grid((8 * T.ng + 255) / 256), 256, 0, s>>>(T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state,
+		                                                                      n_state, G, B, T.l0tab.p, err);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (n_local) {
+		const unsigned nb = xcd_grid((n_local + 255) / 256);
+		if (nh == 26)
+			geo_collect_kernel<true><<<nb, 256, 0, s>>>(T.l0c.p, T.corner.p, T.l0tab.p, G, B, n_local, T.mask.p, lst,
+			                                            list_from, err);
+		else
+			geo_collect_kernel<false><<<nb, 256, 0, s>>>(T.l0c.p, T.corner.p, T.l0tab.p, G, B, n_local, T.mask.p, lst,
+			                                             list_from, err);
+		HIP_CHECK(hipGetLastError());
+	}
+}
+
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
-               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s) {
+               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from) {
 	if (s1 <= s0) return;
 	if (T.mask_path) {
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
 			gol_amr_collect_mask_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
-			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, err);
+			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, list_from < s0 ? s0 : list_from, err);
 		} else {
 			if (T.n_lvl0)
 				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,

@@ -434,6 +434,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_carry_src(g.slot_ids.p, g.n_slots, nl, m, odm, old_n_local, src.p, s);
 	}
 	for (auto& f : g.fields) {
+		f.local_zero = false;
 		if (f.var) {  // children and new copies start empty (the reference default-constructs them)
 			var_remap(f, old_slot_ids.p, old_slot_ids.p ? old_n_local : 0, dm, g.n_slots, s);
 			continue;

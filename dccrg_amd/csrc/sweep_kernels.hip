@@ -490,6 +490,51 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		}
 		st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
 	};
+#if DCCRGX_REG_DEPTH2
+	// two tiles in flight per block: register sets ra / rb alternate; a set
+	// is refilled with the tile after next as soon as it has been staged.
+	// A tile's record is read before the loads of the tile before it, so the
+	// in-order vector counter never makes a record wait for field loads
+	// younger than the ones being staged.
+	RegSet ra, rb;
+	uint32_t tA = t;
+	RM mA = unpack(tile_record_word(meta, tA, lane));
+	uint32_t tB = tk.next(tA);
+	uint32_t recB = tB < t1 ? tile_record_word(meta, tB, lane) : 0u;
+	load(mA, ra);
+	RM mB = mA;
+	uint32_t tL = t1, recL = 0u;
+	if (tB < t1) {
+		mB = unpack(recB);
+		tL = tk.next(tB);
+		recL = tL < t1 ? tile_record_word(meta, tL, lane) : 0u;
+		load(mB, rb);
+	}
+	// the tile held by S (meta mS, index tS < t1): staged, S refilled with
+	// tile tL, then computed; tS becomes the refilled tile (t1: none)
+	auto body = [&](RegSet& S, RM& mS, uint32_t& tS) {
+		__syncthreads();  // the previous tile's faces have been read from LDS
+		stage(S);
+		__syncthreads();
+		const RM mc = mS;
+		if (tL < t1) {
+			mS = unpack(recL);
+			tS = tL;
+			tL = tk.next(tL);
+			recL = tL < t1 ? tile_record_word(meta, tL, lane) : 0u;
+			load(mS, S);
+		} else {
+			tS = t1;
+		}
+		compute(mc);
+	};
+	for (;;) {
+		body(ra, mA, tA);
+		if (tB >= t1) break;
+		body(rb, mB, tB);
+		if (tA >= t1) break;
+	}
+#else
 	RegSet ra;
 	RM cur = unpack(tile_record_word(meta, t, lane));
 	uint32_t tn = tk.next(t);
@@ -514,6 +559,7 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		cur = nxt;
 		tn = tk.next(tn);
 	}
+#endif
 }
 
 // Persistent, software-pipelined form of advection_tiles_kernel for any tile

@@ -817,11 +817,10 @@ class Dccrg:
 
     def get_live_neighbors(self, state: Field, lst: Field):
         """One turn of the refined game emulating the unrefined one, as
-        tests/game_of_life/solve.hpp:37-170 (collect, halo of both fields,
-        spread + rule).  `lst` is a 64-byte field (8 x uint64)."""
-        self.gol_amr_collect(state, lst)
-        self.update_copies_of_remote_neighbors()
-        self.gol_amr_spread(state, lst)
+        tests/game_of_life/solve.hpp:37-170 (collect, halo of the transferred
+        fields, spread + rule; every local list error_cell at the end, as the
+        reference leaves it).  `lst` is a 64-byte field (8 x uint64)."""
+        check(lib().dccrgx_get_live_neighbors(self.h, state.id, lst.id))
 
     @staticmethod
     def _fids(fields):

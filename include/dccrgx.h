@@ -401,6 +401,14 @@ int dccrgx_gol_commit(dccrgx_grid* g, int state_field);
  * DCCRGX_EINVAL where the reference aborts (list overflow, siblings
  * disagreeing on their state). */
 int dccrgx_gol_amr(dccrgx_grid* g, int phase, int state_field, int list_field, int region);
+/* One whole turn of get_live_neighbors (solve.hpp:37-170): collect, the halo
+ * (update_copies_of_remote_neighbors, every transferred field), spread + rule,
+ * and every local list left error_cell-cleared as the reference's rule loop
+ * leaves it (163).  Inside the turn the collected lists live in the kernels'
+ * per-cell bit masks; list_field receives only the lists other processes
+ * read (the outer cells'), for the halo, and those are cleared at the end.
+ * Same states as phase 0 + halo + phase 1; same errors. */
+int dccrgx_get_live_neighbors(dccrgx_grid* g, int state_field, int list_field);
 /* first-order upwind advection over face neighbors, flux + apply fused
  * (tests/advection/solve.hpp:44-279).  fields: density, vx, vy, vz, lx, ly, lz
  * (all fp64).  Writes the new density into a scratch buffer; commit swaps. */

@@ -186,3 +186,59 @@ def test_three_rank_emulation_equals_one_rank(gpu):
         assert np.array_equal(g.fields["is_alive"].get(0, g.n_local), np.array([final[int(c)] for c in sl]))
     for g in gs + [ref]:
         g.close()
+
+
+def test_turn_equals_split_phases_and_clears_lists(gpu):
+    """dccrgx_get_live_neighbors (the whole turn, lists kept in masks and
+    every local list error_cell at the end, solve.hpp:163) gives the states
+    of the split form (collect, halo, spread) at every step, on a list field
+    holding garbage before the first turn and after the mesh changes."""
+    length = (24, 20, 1)
+    o = refined_oracle(length, (True, True, False), 0.5, 9)
+    g, st, ls = product_on(o, length, (True, True, False))
+    h, hst, hls = product_on(o, length, (True, True, False))
+    rng = np.random.default_rng(59)
+    live0 = {int(c) for c in np.nonzero(rng.random(480) < 0.35)[0] + 1}
+    slots = g.slot_ids()[: g.n_local]
+    a0, _ = states_by_parent(o, slots, live0)
+    st.set(a0)
+    hst.set(a0)
+    ls.set(np.full((g.n_slots, 8), 5, np.uint64))
+    for step in range(12):
+        g.get_live_neighbors(st, ls)
+        h.gol_amr_collect(hst, hls)
+        h.update_copies_of_remote_neighbors()
+        h.gol_amr_spread(hst, hls)
+        assert np.array_equal(st.get(0, g.n_local), hst.get(0, h.n_local)), f"step {step}"
+        assert not np.any(ls.get(0, g.n_local)), f"step {step}: lists not cleared"
+    g.close()
+    h.close()
+
+
+def test_turn_with_disagreeing_families_follows_the_reference(gpu):
+    """One refined level-0 cell with a single live child: the family
+    disagrees, so the geometric collect gives way to the exact per-entry
+    walk, and the turn does what the reference's loop does - abort when some
+    row meets a dead child after the live one (solve.hpp:81-90; children 0-6
+    here), else (child 7, always met last) the oracle's states."""
+    length = (6, 6, 1)
+    for k in (0, 3, 7):
+        o = O.Grid(length, 1, (False, False, False), 1, 1)
+        o.refine_completely(15)
+        o.stop_refining()
+        g, st, ls = product_on(o, length, (False, False, False))
+        slots = g.slot_ids()[: g.n_local]
+        kids = np.sort(slots[slots > np.uint64(36)])
+        a = (slots == kids[k]).astype(np.uint32)
+        st.set(a)
+        o.gola_set(slots, a)
+        if k == 7:
+            o.gola_steps(1)
+            g.get_live_neighbors(st, ls)
+            assert np.array_equal(st.get(0, g.n_local), o.gola_get(slots))
+        else:
+            with pytest.raises(RuntimeError, match="should not be alive"):
+                o.gola_steps(1)
+            with pytest.raises(dccrg_amd.DccrgError, match="recorded alive"):
+                g.get_live_neighbors(st, ls)
+        g.close()

@@ -975,11 +975,65 @@ def sc_poisson1d(rank, world):
     return res
 
 
+def sc_gol_amr_turn(rank, world):
+    """The refined game's whole turn (dccrgx_get_live_neighbors: collect,
+    halo, spread + rule, lists cleared; solve.hpp:37-170) across real
+    processes, with families split across ranks (children exported one by
+    one), so a leaf's siblings are partly remote copies whose lists arrive
+    through the halo: every state equals the oracle's one-rank game after
+    each of 8 turns, and every local list is error_cell at the end of a turn
+    (as the reference's rule loop leaves it)."""
+    from oracle import oracle as O
+
+    length, per = (14, 12, 1), (True, False, False)
+    g = _grid(length, 1, per, 1)
+    rng = np.random.default_rng(70 + rank)
+    loc = g.local_cells()
+    for c in rng.choice(loc, size=max(1, loc.size // 3), replace=False):
+        g.refine_completely(int(c))
+    g.stop_refining()
+    kids = g.local_cells()
+    kids = kids[kids > np.uint64(length[0] * length[1])]
+    move = kids[(kids % np.uint64(3)) == np.uint64(0)]
+    g.balance_load_to(move, np.full(move.size, (rank + 1) % world, np.int32))
+    leaves = np.sort(np.concatenate(_gather(g.local_cells())))
+    o = O.Grid(length, 1, per, 1, 1)
+    o.set_cells(leaves, np.zeros(leaves.size, np.int32))
+    par = o.mapping.batch(leaves)["level0_parent"].astype(np.int64)
+    live0 = np.random.default_rng(5).random(length[0] * length[1]) < 0.35
+    a0 = live0[par - 1].astype(np.uint32)
+    o.gola_set(leaves, a0)
+    st = g.add_field("is_alive", np.uint32)
+    ls = g.add_field("gol_list", np.dtype((np.uint64, 8)))
+    sl = g.slot_ids()[: g.n_local]
+    st.set(a0[np.searchsorted(leaves, sl)])
+    ls.set(np.full((g.n_local, 8), 7, np.uint64))  # garbage the turn must clear
+    res = {"split": False, "equal": True, "cleared": True}
+    for _ in range(8):
+        # the copies of remote neighbors hold the states of this turn, as
+        # unrefined2d.cpp:186-218 refreshes them before get_live_neighbors
+        g.update_copies_of_remote_neighbors()
+        g.get_live_neighbors(st, ls)
+        o.gola_steps(1)
+        exp = o.gola_get(sl)
+        res["equal"] = res["equal"] and bool(np.array_equal(st.get(0, g.n_local), exp))
+        res["cleared"] = res["cleared"] and bool(not np.any(ls.get(0, g.n_local)))
+    # a family really spans ranks: some local child has a sibling held remotely
+    rem = set(g.remote_cells().tolist())
+    mb = o.mapping.batch(sl)
+    for c, sib in zip(sl.tolist(), mb["siblings"]):
+        if int(c) > length[0] * length[1] and any(int(k) in rem for k in sib):
+            res["split"] = True
+            break
+    g.close()
+    return res
+
+
 SCENARIOS = {
     2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson", "sc_gol_halfshift", "sc_poisson1d"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
         "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable", "sc_poisson", "sc_gol_halfshift",
-        "sc_poisson1d"],
+        "sc_poisson1d", "sc_gol_amr_turn"],
 }
 
 
@@ -1119,6 +1173,12 @@ def test_poisson1d_reference_distributed(transport_results):
     _check(transport_results, "sc_poisson1d", keys)
     for _, out in transport_results["sc_poisson1d"].values():
         assert all(v for k, v in out.items() if k.startswith("owners_"))
+
+
+def test_gol_amr_turn_split_families(transport_results):
+    """dccrgx_get_live_neighbors at 3 processes with families split across
+    ranks (sc_gol_amr_turn)."""
+    _check(transport_results, "sc_gol_amr_turn", ["equal", "cleared", "split"])
 
 
 def test_save_grid_data_three_ranks(transport_results):

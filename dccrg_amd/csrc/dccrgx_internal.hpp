@@ -708,7 +708,8 @@ struct AdvRequests {
 	std::vector<uint64_t> part_ids;
 	std::vector<uint8_t> part_bands;
 };
-AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint8_t* band, size_t n, hipStream_t s);
+AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
+                           hipStream_t s);
 void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
                  const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
                  double unrefine_sensitivity, uint8_t* band, hipStream_t s);

@@ -795,9 +795,10 @@ __global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const
 // run goes to the host, which merges the runs of a parent (families split
 // between runs or processes).  Lists are appended through counters
 // cnt[0] refines, cnt[1] unrefines, cnt[2] kept families, cnt[3] partial runs.
-__global__ void adv_requests_kernel(MapCtx m, const uint64_t* __restrict__ ids, const uint8_t* __restrict__ band,
-                                    size_t n, uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
-                                    uint32_t* __restrict__ part, unsigned long long* __restrict__ cnt) {
+__global__ void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restrict__ ids,
+                                    const uint8_t* __restrict__ band, size_t n, uint64_t* __restrict__ ref,
+                                    uint64_t* __restrict__ unref, uint32_t* __restrict__ part,
+                                    unsigned long long* __restrict__ cnt) {
 	// each lane a run of kRun slots: classify them, reserve its positions in
 	// the three lists with one atomic per wave and list, then write
 	constexpr int kRun = 8;
@@ -830,7 +831,19 @@ __global__ void adv_requests_kernel(MapCtx m, const uint64_t* __restrict__ ids, 
 			k++;
 		}
 		runk[j] = uint8_t(k);
+		bool whole = true;  // every child of p is a leaf (some of them held elsewhere)
 		if (k < 8) {
+			uint64_t ch[8];
+			map_all_children(m, p, ch);
+			for (int i = 0; i < 8; i++) whole = whole && dm_owner(M, ch[i]) >= 0;
+		}
+		if (k < 8 && !whole) {
+			// a sibling has children: the family cannot be unrefined in this
+			// round (unrefine_completely refuses, a dont_unrefine mark changes
+			// nothing), so the host never sees it; counted as the host's
+			// decide() would count it
+			if (keep) ck++;
+		} else if (k < 8) {
 			what[j] |= 2;
 			cp++;
 		} else if (keep) {
@@ -1092,7 +1105,8 @@ static void k_gather_ids_bands(const uint64_t* ids, const uint8_t* band, const u
 	HIP_CHECK(hipGetLastError());
 }
 
-AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint8_t* band, size_t n, hipStream_t s) {
+AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
+                           hipStream_t s) {
 	AdvRequests out;
 	if (!n) return out;
 	DX_REQUIRE(n < (size_t(1) << 28), "too many local cells for the request runs");
@@ -1104,8 +1118,8 @@ AdvRequests k_adv_requests(const MapCtx& m, const uint64_t* slot_ids, const uint
 	part.alloc(n);
 	cnt.alloc(4);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
-	adv_requests_kernel<<<unsigned((n + 256 * 8 - 1) / (256 * 8)), 256, 0, s>>>(m, slot_ids, band, n, ref.p, unref.p,
-	                                                                        part.p, cnt.p);
+	adv_requests_kernel<<<unsigned((n + 256 * 8 - 1) / (256 * 8)), 256, 0, s>>>(m, dm, slot_ids, band, n, ref.p,
+	                                                                        unref.p, part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	HIP_CHECK(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -502,6 +502,11 @@ struct Grid {
 	// the pipelined kernel's capacities (> 1024 ext cells or > 512 finer
 	// faces): the run is then swept by the untiled face-CSR kernel
 	DBuf<uint32_t> tmeta;
+	// both kinds in tile order per run (advection_fused_kernel), 8 x u32 per
+	// tile, word 7 = 1 for a regular tile (then RegTileMeta's words), 0 for
+	// another (then tmeta's); empty with tmeta
+	DBuf<uint32_t> tfused;
+	size_t tfused_n[2] = {0, 0};
 	std::map<int, UserHood> uhoods;  // add_neighborhood ids
 	GolAmrTables gola;  // refined game of life: per-mesh tables (gol_amr.hip)
 	// uniform game of life: the regions as plane boxes (gol_slab_plan), built lazily

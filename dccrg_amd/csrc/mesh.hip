@@ -569,6 +569,35 @@ void ensure_tiles(Grid& g) {
 	}
 	g.tmeta.release();
 	if (fits && ni) upload(g.tmeta, rec, g.s_comp);
+	// the same records merged with the regular tiles' in tile order
+	g.tfused.release();
+	g.tfused_n[0] = g.tfused_n[1] = 0;
+	if (fits && nt) {
+		const size_t nr = g.tcount[0] + g.tcount[1];
+		const auto lr = download(g.tlists.p, nr, g.s_comp);
+		std::vector<RegTileMeta> rm(nr);
+		if (nr) HIP_CHECK(hipMemcpyAsync(rm.data(), g.tregmeta.p, nr * sizeof(RegTileMeta), hipMemcpyDeviceToHost, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		std::vector<int64_t> where(nt, -1);  // tile -> regular list index (>= 0) or -(irregular index) - 2
+		for (size_t i = 0; i < nr; i++) where[lr[i]] = int64_t(i);
+		for (size_t i = 0; i < ni; i++) where[li[i]] = -int64_t(i) - 2;
+		std::vector<uint32_t> fu(8 * nt, 0u);
+		for (size_t t = 0; t < nt; t++) {
+			uint32_t* r = &fu[8 * t];
+			if (where[t] >= 0) {
+				const RegTileMeta& m = rm[size_t(where[t])];
+				r[0] = m.ts;
+				for (int d = 0; d < 6; d++) r[1 + d] = uint32_t(m.nst[d]);
+				r[7] = 1u;
+			} else {
+				const uint32_t* q = &rec[8 * size_t(-where[t] - 2)];
+				for (int k = 0; k < 8; k++) r[k] = q[k];
+			}
+		}
+		upload(g.tfused, fu, g.s_comp);
+		g.tfused_n[0] = g.n_tiles_inner;
+		g.tfused_n[1] = g.n_tiles_outer;
+	}
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	DX_LAP("tiles.3_meta");
 	g.tiles_valid = true;

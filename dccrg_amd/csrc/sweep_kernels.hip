@@ -701,6 +701,237 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		tn = tk.next(tn);
 	}
 }
+// Both kinds of tile in ONE persistent sweep, in tile order (the Morton
+// order of the slots): the same XCD-contiguous static schedule, so the tiles
+// an XCD has in flight are neighbors of both kinds and read each other's face
+// lines from its L2, and one launch has one tail.  Per tile one 32-B record,
+// word 7 its kind (1: a regular box, advection_regular_pp_kernel's record;
+// 0: any other tile, advection_tiles_pp_kernel's); the LDS holds either
+// layout, the registers of the tile in flight either register set (the
+// regular one in c[] and xa[0..3]).  Each kind's face fluxes are its own
+// kernel's expressions in its own order, so every density is bitwise that of
+// the two-kernel sweep.
+#if DCCRGX_FUSED_SWEEP
+template <int MINW>
+__global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
+    AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, uint32_t tplane,
+    const uint32_t* __restrict__ ext, const uint32_t* __restrict__ tfine, const uint32_t* __restrict__ meta,
+    uint32_t ntiles, uint32_t ecap, double dt) {
+#pragma clang fp contract(off)
+	constexpr uint32_t T = 512;
+	constexpr uint32_t WR = 512 + 6 * 64;  // regular layout: [7][WR] then [3][512] + [3][64] face fluxes
+	extern __shared__ double shd[];
+	const uint32_t W = T + ecap;  // general layout: [7][W] then 2 x T u32 finer-face pairs
+	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
+	double* shg = shd + 7 * WR;
+	double* shm = shg + 3 * 512;
+	const StaticTiles tk(ntiles);
+	const uint32_t t1 = tk.t1;
+	uint32_t t = tk.first();
+	if (t >= t1) return;  // block-uniform
+	const uint32_t tid = threadIdx.x;
+	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+	const double* const rho = P.p[0];
+	const double* const lx = P.p[1];
+	const double* const ly = P.p[2];
+	const double* const lz = P.p[3];
+	const double* const vx = P.p[4];
+	const double* const vy = P.p[5];
+	const double* const vz = P.p[6];
+	// the tile in flight: own fields (both kinds), regular out-of-tile rows
+	// in xa[0..3] or general ext cells in xa / xb, face codes, finer pairs
+	double c[7], xa[7], xb[7];
+	uint32_t row[3], fq[2];
+	auto load7 = [&](uint32_t slot, double (&v)[7]) {
+		const uint32_t o = slot << 3;
+		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
+		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+	};
+	auto is_reg = [](uint32_t v) { return word_of(v, 7) != 0u; };
+	// ---- regular tiles (advection_regular_pp_kernel) ----
+	auto reg_l = [&](int a) -> uint32_t {
+		return a == 0 ? ((tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u))
+		              : (a == 1 ? (((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u))
+		                        : (((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)));
+	};
+	auto vrow = [](uint32_t val, uint32_t a) -> uint32_t { return val == 0 ? 0u : (val == 4 ? 1u + a : val + 3u); };
+	auto reg_load = [&](uint32_t v) {
+		const uint32_t ts = word_of(v, 0);
+		load7(ts + tid, c);
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint32_t rw = w + 8u * uint32_t(i);  // wave-uniform
+			xa[i] = 0;
+			if (rw >= 30u) continue;
+			const uint32_t d = rw / 5u, val = rw - 5u * d, a = d >> 1;
+			const int32_t st = int32_t(word_of(v, int(1 + d)));
+			if (st < 0) continue;
+			const uint32_t u = lane & 7u, vv = lane >> 3, side = (d & 1u) ? 0u : 7u;
+			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : vv), q2 = a == 2 ? side : vv;
+			xa[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+		}
+	};
+	auto reg_stage = [&]() {
+		// own fields in the order rho vx vy vz lx ly lz (= the regular rows 0..6)
+#pragma unroll
+		for (int k = 0; k < 7; k++) shd[k * WR + tid] = c[k];
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint32_t rw = w + 8u * uint32_t(i);
+			if (rw < 30u) {
+				const uint32_t d = rw / 5u, val = rw - 5u * d;
+				shd[vrow(val, d >> 1) * WR + 512u + 64u * d + lane] = xa[i];
+			}
+		}
+	};
+	auto reg_compute = [&](uint32_t v) {
+		const uint32_t ts = word_of(v, 0);
+		const uint32_t l[3] = {reg_l(0), reg_l(1), reg_l(2)};
+		const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
+		auto nst = [&](uint32_t d) { return int32_t(word_of(v, int(1 + d))); };
+		const double cd = shd[tid], clx = shd[4 * WR + tid], cly = shd[5 * WR + tid], clz = shd[6 * WR + tid];
+		const double cva[3] = {shd[WR + tid], shd[2 * WR + tid], shd[3 * WR + tid]};
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] += 1;
+			const uint32_t li = l[a] < 7 ? m9(q[0], q[1], q[2]) : 512u + 64u * uint32_t(2 * a + 1) + fi[a];
+			const double gg = adv_face_g(a, cd, clx, cly, clz, cva[a],
+			                             AdvNb{shd[li], shd[4 * WR + li], shd[5 * WR + li], shd[6 * WR + li],
+			                                   shd[(1 + a) * WR + li]},
+			                             dt);
+			const bool has = l[a] < 7 || nst(2 * a + 1) >= 0;
+			shg[a * 512 + tid] = has ? gg : 0.0;
+		}
+		if (w < 3 && nst(2 * w) >= 0) {
+			const uint32_t bu = lane & 7u, bv = lane >> 3;
+			const uint32_t bcell = w == 0 ? m9(0, bu, bv) : (w == 1 ? m9(bu, 0, bv) : m9(bu, bv, 0));
+			const uint32_t k = 512u + 64u * (2u * w) + lane;
+			const AdvNb self{shd[bcell], shd[4 * WR + bcell], shd[5 * WR + bcell], shd[6 * WR + bcell],
+			                 shd[(1 + w) * WR + bcell]};
+			double gmv;
+			if (w == 0) gmv = adv_face_g(0, shd[k], shd[4 * WR + k], shd[5 * WR + k], shd[6 * WR + k], shd[WR + k], self, dt);
+			else if (w == 1)
+				gmv = adv_face_g(1, shd[k], shd[4 * WR + k], shd[5 * WR + k], shd[6 * WR + k], shd[2 * WR + k], self, dt);
+			else gmv = adv_face_g(2, shd[k], shd[4 * WR + k], shd[5 * WR + k], shd[6 * WR + k], shd[3 * WR + k], self, dt);
+			shm[w * 64 + lane] = gmv;
+		}
+		__syncthreads();
+		double acc = 0;
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] -= 1;
+			double gm = 0;
+			if (l[a] > 0) gm = shg[a * 512 + m9(q[0] & 7u, q[1] & 7u, q[2] & 7u)];
+			else if (nst(2 * a) >= 0) gm = shm[a * 64 + fi[a]];
+			acc += gm;
+			acc += -shg[a * 512 + tid];
+		}
+		st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
+	};
+	// ---- other tiles (advection_tiles_pp_kernel) ----
+	auto gen_load = [&](uint32_t v) {
+		const uint32_t ts = word_of(v, 0), n = word_of(v, 1), e0 = word_of(v, 2), ne = word_of(v, 3),
+		               fb = word_of(v, 4), nf = word_of(v, 5);
+		if (tid < n) {
+			load7(ts + tid, c);
+			row[0] = __builtin_nontemporal_load(tell + (ts + tid));
+			row[1] = __builtin_nontemporal_load(tell + tplane + (ts + tid));
+			row[2] = __builtin_nontemporal_load(tell + 2 * tplane + (ts + tid));
+		}
+		auto load5 = [&](uint32_t q, double (&vv)[7]) {
+			const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
+			vv[0] = ldo(rho, o); vv[4] = ldo(lx, o); vv[5] = ldo(ly, o); vv[6] = ldo(lz, o);
+			vv[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
+			vv[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
+			vv[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
+		};
+		if (tid < ne) load5(__builtin_nontemporal_load(ext + e0 + tid), xa);
+		if (tid + T < ne) load5(__builtin_nontemporal_load(ext + e0 + tid + T), xb);
+		if (tid < nf) {
+			typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+			const u2v q = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(tfine) + (fb + tid));
+			fq[0] = q.x;
+			fq[1] = q.y;
+		}
+	};
+	uint32_t rr[3] = {0, 0, 0};
+	auto gen_stage = [&](uint32_t v) {
+		const uint32_t n = word_of(v, 1), ne = word_of(v, 3), nf = word_of(v, 5);
+		if (tid < n)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + tid] = c[k];
+		if (tid < ne)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + T + tid] = xa[k];
+		if (tid + T < ne)
+#pragma unroll
+			for (int k = 0; k < 7; k++) shd[k * W + 2 * T + tid] = xb[k];
+		if (tid < nf) {
+			shf[2 * tid] = fq[0];
+			shf[2 * tid + 1] = fq[1];
+		}
+		rr[0] = row[0];
+		rr[1] = row[1];
+		rr[2] = row[2];
+	};
+	auto gen_compute = [&](uint32_t v) {
+		const uint32_t ts = word_of(v, 0), n = word_of(v, 1);
+		if (tid >= n) return;
+		const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
+		             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
+		auto fetch = [&](uint32_t li, int d) -> AdvNb {
+			return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
+		};
+		double acc = 0;
+#pragma unroll
+		for (int d = 0; d < 6; d++) {
+			const uint32_t code = (rr[d >> 1] >> (16 * (d & 1))) & 0xffffu;
+			if (code == 0xffffu) continue;
+			if (code & 0x8000u) {
+				const uint32_t fk = code & 0x7fffu;
+				const uint32_t q0 = shf[2 * fk], q1 = shf[2 * fk + 1];
+				const uint32_t li[4] = {q0 & 0xffffu, q0 >> 16, q1 & 0xffffu, q1 >> 16};
+#pragma unroll
+				for (int k = 0; k < 4; k++) acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(li[k], d), dt);
+			} else {
+				acc += adv_face_flux_d(d, cd, clx, cly, clz, cvx, cvy, cvz, fetch(code, d), dt);
+			}
+		}
+		st_nt(rho_out, ts + tid, cd + acc / (clx * cly * clz));
+	};
+	uint32_t cur = tile_record_word(meta, t, lane);
+	if (is_reg(cur)) reg_load(cur);
+	else gen_load(cur);
+	uint32_t tn = tk.next(t);
+	uint32_t rec = tn < t1 ? tile_record_word(meta, tn, lane) : 0u;  // tile tn's record
+	for (;;) {
+		__syncthreads();  // the previous tile's faces have been read from LDS
+		const bool creg = is_reg(cur);
+		if (creg) reg_stage();
+		else gen_stage(cur);
+		__syncthreads();
+		const bool more = tn < t1;
+		const uint32_t nxt = rec;
+		if (more) {
+			// the next tile's loads fly while this one is computed, then the
+			// record of the tile after it
+			if (is_reg(nxt)) reg_load(nxt);
+			else gen_load(nxt);
+			const uint32_t tnn = tk.next(tn);
+			rec = tnn < t1 ? tile_record_word(meta, tnn, lane) : 0u;
+		}
+		if (creg) reg_compute(cur);
+		else gen_compute(cur);
+		if (!more) break;
+		cur = nxt;
+		tn = tk.next(tn);
+	}
+}
+
+#endif
+
 // max_time_step local part (solve.hpp:289-333): block minima
 __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __restrict__ vy,
                               const double* __restrict__ vz, const double* __restrict__ lx,
@@ -1027,6 +1258,20 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 		k_advection(f, rho_out, g.face_ptr.p, g.face_ent.p, s0, s1, dt, s);
 		return;
 	}
+#if DCCRGX_FUSED_SWEEP
+	if (g.tfused.n && g.tfused_n[run]) {
+		const uint32_t* meta = g.tfused.p + 8 * (run == 0 ? 0 : g.tfused_n[0]);
+		const size_t nt = g.tfused_n[run];
+		const uint32_t ecap = uint32_t(g.max_ext);
+		const size_t lgen = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t);
+		const size_t lreg = (size_t(7) * (512 + 6 * 64) + 3 * 512 + 3 * 64) * sizeof(double);
+		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (nt + 7) / 8 * 8));
+		advection_fused_kernel<4><<<nblk, 512, std::max(lgen, lreg), s>>>(
+		    P, rho_out, g.tell.p, uint32_t(g.n_local + 1), g.ext_pk.p, g.tfine.p, meta, uint32_t(nt), ecap, dt);
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
+#endif
 	if (n_reg) {
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_reg + 7) / 8 * 8));

@@ -404,15 +404,55 @@ struct SlotExists {
 	}
 };
 
-__global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                                  int32_t* hint) {
+__device__ __forceinline__ uint64_t spread3(uint64_t v) {
+	v &= 0x1FFFFFull;
+	v = (v | (v << 32)) & 0x1F00000000FFFFull;
+	v = (v | (v << 16)) & 0x1F0000FF0000FFull;
+	v = (v | (v << 8)) & 0x100F00F00F00F00Full;
+	v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
+	v = (v | (v << 2)) & 0x1249249249249249ull;
+	return v;
+}
+
+__device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
+	return spread3(c[0]) | (spread3(c[1]) << 1) | (spread3(c[2]) << 2);
+}
+
+// morton: the rows [0, nrows) are Morton-ordered runs [0, run1) and [run1,
+// nrows) (k_morton_sort of rebuild step 2).  Then a same-size face neighbor
+// is predicted at the row its Morton distance away - exact whenever every
+// leaf between the two has that size - and taken when the row holds its id:
+// a same-size leaf is the one face neighbor in that direction (no finer or
+// coarser probe needed).  Otherwise, and for the misses, the probes of
+// face_dir.  The hints are the same either way.
+__global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1, bool morton,
+                                  uint32_t* cnt, int32_t* hint) {
 	const SlotExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		uint64_t c[3];
 		int lvl;
-		cell_coords(m, slot_ids[r], c, lvl);
+		const uint64_t id = slot_ids[r];
+		cell_coords(m, id, c, lvl);
+		const int sh = 3 * (m.R - lvl);
+		const uint64_t len = uint64_t(1) << (m.R - lvl);
+		const int64_t key = int64_t(morton3(c) >> sh);
+		const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
 		uint32_t k = 0;
 		for (int dir = 0; dir < 6; dir++) {
+			if (morton) {
+				uint64_t p[3];
+				if (!face_probe(m, c, lvl, dir, p)) {
+					hint[6 * r + dir] = -1;
+					continue;
+				}
+				for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
+				const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
+				if (q >= lo && q < hi && slot_ids[q] == map_from_indices(m, p[0], p[1], p[2], lvl)) {
+					hint[6 * r + dir] = int32_t(q);
+					k += 1;
+					continue;
+				}
+			}
 			uint64_t out[4];
 			const int nf = face_dir(m, c, lvl, dir, ex, out);
 			// a single neighbor was the last cell found (face_dir returns on it)
@@ -484,16 +524,6 @@ __global__ void gather_bytes_kernel(const uint8_t* __restrict__ old, const int32
 	}
 }
 
-__device__ __forceinline__ uint64_t spread3(uint64_t v) {
-	v &= 0x1FFFFFull;
-	v = (v | (v << 32)) & 0x1F00000000FFFFull;
-	v = (v | (v << 16)) & 0x1F0000FF0000FFull;
-	v = (v | (v << 8)) & 0x100F00F00F00F00Full;
-	v = (v | (v << 4)) & 0x10C30C30C30C30C3ull;
-	v = (v | (v << 2)) & 0x1249249249249249ull;
-	return v;
-}
-
 __global__ void morton_keys_kernel(MapCtx m, const uint64_t* ids, size_t n, uint64_t* keys) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		uint64_t x, y, z;
@@ -507,22 +537,42 @@ __global__ void morton_keys_kernel(MapCtx m, const uint64_t* ids, size_t n, uint
 // finer face whose 4 slots are fine[4k..4k+3] (reference order)
 __global__ void face_ell_kernel(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine,
                                 unsigned int* nfine) {
-	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
+	// whole waves per iteration (the counter below is shared by the wave)
+	const size_t stride = size_t(gridDim.x) * blockDim.x;
+	for (size_t r0 = blockIdx.x * size_t(blockDim.x) + (threadIdx.x & ~(WAVE - 1)); r0 < nrows; r0 += stride) {
+		const size_t r = r0 + lane_id();
+		const bool act = r < nrows;
 		int32_t row[6] = {-1, -1, -1, -1, -1, -1};
-		uint32_t e = ptr[r];
-		const uint32_t e1 = ptr[r + 1];
+		uint32_t e = act ? ptr[r] : 0u;
+		const uint32_t e1 = act ? ptr[r + 1] : 0u;
 		while (e < e1) {
 			const int d = ent[e] & 7;
 			uint32_t k = e + 1;
 			while (k < e1 && (ent[k] & 7) == d) k++;
-			if (k - e == 1) {
-				row[d] = ent[e] >> 3;
-			} else {
-				const unsigned int f = atomicAdd(nfine, 1u);
+			row[d] = k - e == 1 ? ent[e] >> 3 : -2;  // finer: numbered below
+			e = k;
+		}
+		// finer faces numbered through one counter atomic per wave
+		uint32_t nf = 0;
+		for (int d = 0; d < 6; d++) nf += row[d] == -2 ? 1u : 0u;
+		uint32_t incl = nf;
+		for (int o = 1; o < WAVE; o <<= 1) {
+			const uint32_t v = __shfl_up(incl, o);
+			if (lane_id() >= o) incl += v;
+		}
+		const uint32_t total = __shfl(incl, WAVE - 1);
+		unsigned int base = 0;
+		if (lane_id() == 0 && total) base = atomicAdd(nfine, total);
+		unsigned int f = __shfl(base, 0) + (incl - nf);
+		if (!act) continue;
+		e = ptr[r];
+		for (int d = 0; d < 6; d++) {
+			if (row[d] == -2) {
+				while ((ent[e] & 7) != d) e++;
 				for (int i = 0; i < 4; i++) fine[4 * size_t(f) + i] = ent[e + i] >> 3;
 				row[d] = -2 - int32_t(f);
+				f++;
 			}
-			e = k;
 		}
 		for (int d = 0; d < 6; d++) ell[6 * r + d] = row[d];
 	}
@@ -947,10 +997,12 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 }
 
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s) {
+                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s,
+                  bool morton, size_t run1) {
 	if (!nrows) return;
 	if (pass == 0)
-		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, cnt, hint);
+		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, cnt,
+		                                                       hint);
 	else
 		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, ptr, ent, err_flag);
 	HIP_CHECK(hipGetLastError());

@@ -634,7 +634,8 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
                       uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
                       int pass, hipStream_t s);
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s);
+                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s,
+                  bool morton = false, size_t run1 = 0);
 void k_carry_src(const uint64_t* slot_ids, size_t n_slots, size_t nl, const MapCtx& m, const DevMesh& oldM,
                  size_t old_n_local, int32_t* src, hipStream_t s);
 void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t elem, uint8_t* out, hipStream_t s);

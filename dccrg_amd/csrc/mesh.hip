@@ -515,7 +515,7 @@ void ensure_face(Grid& g) {
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
 	DBuf<int32_t> hint;  // per row and direction what pass 0 found (build_kernels.hip)
 	hint.alloc(6 * nl + 6);
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, err.p, 0, s);
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, err.p, 0, s, g.morton_slots, g.n_inner);
 	const size_t t = scan_exclusive_u32(cnt.p, g.face_ptr.p, nl, s);
 	g.face_ent.alloc(t + 1);
 	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, g.face_ptr.p, g.face_ent.p, err.p, 1, s);
@@ -569,9 +569,11 @@ void ensure_tiles(Grid& g) {
 	}
 	g.tmeta.release();
 	if (fits && ni) upload(g.tmeta, rec, g.s_comp);
-	// the same records merged with the regular tiles' in tile order
+	// the same records merged with the regular tiles' in tile order (only for
+	// the fused-sweep experiment, sweep_kernels.hip)
 	g.tfused.release();
 	g.tfused_n[0] = g.tfused_n[1] = 0;
+#if DCCRGX_FUSED_SWEEP
 	if (fits && nt) {
 		const size_t nr = g.tcount[0] + g.tcount[1];
 		const auto lr = download(g.tlists.p, nr, g.s_comp);
@@ -598,6 +600,7 @@ void ensure_tiles(Grid& g) {
 		g.tfused_n[0] = g.n_tiles_inner;
 		g.tfused_n[1] = g.n_tiles_outer;
 	}
+#endif
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	DX_LAP("tiles.3_meta");
 	g.tiles_valid = true;

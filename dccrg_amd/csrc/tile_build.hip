@@ -172,6 +172,177 @@ __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restr
 
 
 // ---------------------------------------------------------------------------
+// Per-tile build (tiles of at most kXT slots): one 512-thread block per tile
+// gathers its out-of-tile face entries in LDS, sorts them (bitonic) and drops
+// repeats - the tile's ascending ext list - then, in the second pass, writes
+// that list at the tile's ext offset and its cells' tile-local rows (steps
+// 1-5 above without the global sort).  Pass 0 only counts (distinct ext
+// cells, finer faces) per tile; the offsets are their scans.  A tile with
+// more than kXCap out-of-tile entries sets err bit 2 (then the global build).
+constexpr uint32_t kXT = 512;
+constexpr uint32_t kXCap = 8192;
+
+// exclusive scan over a 512-thread block; sh: 8 words of LDS
+__device__ __forceinline__ uint32_t block_scan512(uint32_t v, uint32_t* sh, uint32_t& total) {
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	uint32_t incl = v;
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t x = __shfl_up(incl, o);
+		if (lane >= uint32_t(o)) incl += x;
+	}
+	if (lane == 63) sh[w] = incl;
+	__syncthreads();
+	uint32_t base = 0;
+	total = 0;
+	for (uint32_t k = 0; k < 8; k++) {
+		const uint32_t x = sh[k];
+		base += k < w ? x : 0u;
+		total += x;
+	}
+	__syncthreads();
+	return base + incl - v;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restrict__ tstart, uint32_t T,
+                                                        const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
+                                                        uint32_t* __restrict__ ext_cnt, uint32_t* __restrict__ fine_cnt,
+                                                        const uint32_t* __restrict__ ext_ptr,
+                                                        const uint32_t* __restrict__ fine_base, uint32_t* __restrict__ ext,
+                                                        uint32_t* __restrict__ ext_pk, uint32_t* __restrict__ tell,
+                                                        size_t pl, uint32_t* __restrict__ tfine, int* __restrict__ err) {
+	__shared__ uint32_t key[kXCap];
+	__shared__ uint32_t sh[8];
+	__shared__ uint32_t n_raw;
+	const uint32_t t = blockIdx.x, tid = threadIdx.x;
+	const uint32_t ts = tstart[t], te = tstart[t + 1];
+	if (tid == 0) n_raw = 0;
+	__syncthreads();
+	const uint32_t r = ts + tid;
+	const bool row = r < te;  // tiles hold at most kXT = blockDim.x slots
+	const uint32_t e0 = row ? ptr[r] : 0u, e1 = row ? ptr[r + 1] : 0u;
+	for (uint32_t e = e0; e < e1; e++) {
+		const uint32_t n = uint32_t(ent[e] >> 3);
+		if (n >= ts && n < te) continue;
+		const uint32_t i = atomicAdd(&n_raw, 1u);
+		if (i < kXCap) key[i] = n;
+	}
+	__syncthreads();
+	const uint32_t N = n_raw;
+	if (N > kXCap) {  // block-uniform
+		if (tid == 0) atomicOr(err, 2);
+		return;
+	}
+	uint32_t P = 64;
+	while (P < N) P <<= 1;
+	for (uint32_t i = N + tid; i < P; i += 512) key[i] = 0xffffffffu;
+	// bitonic sort of key[0, P)
+	for (uint32_t k = 2; k <= P; k <<= 1)
+		for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+			__syncthreads();
+			for (uint32_t i = tid; i < P; i += 512) {
+				const uint32_t q = i ^ j;
+				if (q > i) {
+					const uint32_t x = key[i], y = key[q];
+					const bool up = (i & k) == 0;
+					if ((x > y) == up) {
+						key[i] = y;
+						key[q] = x;
+					}
+				}
+			}
+		}
+	__syncthreads();
+	// distinct values, compacted in place: each thread a contiguous chunk
+	const uint32_t chunk = (P + 511) / 512;  // <= kXCap / 512 = 16
+	uint32_t v[16];
+	uint32_t nu = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < 16; j++) {
+		const uint32_t i = tid * chunk + j;
+		v[j] = 0xffffffffu;
+		if (j < chunk && i < N && (i == 0 || key[i] != key[i - 1])) v[j] = key[i];
+		nu += v[j] != 0xffffffffu;
+	}
+	uint32_t U;
+	const uint32_t ub = block_scan512(nu, sh, U);  // (its barriers also end the reads above)
+	uint32_t o = ub;
+#pragma unroll
+	for (uint32_t j = 0; j < 16; j++)
+		if (v[j] != 0xffffffffu) key[o++] = v[j];
+	// finer faces of this thread's row
+	uint32_t nf = 0;
+	for (uint32_t e = e0; e < e1;) {
+		const int d = ent[e] & 7;
+		uint32_t k = e + 1;
+		while (k < e1 && (ent[k] & 7) == d) k++;
+		nf += (k - e) > 1;
+		e = k;
+	}
+	uint32_t F;
+	const uint32_t fb = block_scan512(nf, sh, F);
+	if (PASS == 0) {
+		if (tid == 0) {
+			ext_cnt[t] = U;
+			fine_cnt[t] = F;
+		}
+		return;
+	}
+	// pass 1: tile-local rows (tile_ell_kernel's codes), axis bits ORed into
+	// the ext entries' top bits (slots < 2^29)
+	auto local = [&](uint32_t n) -> uint32_t {
+		if (n >= ts && n < te) return n - ts;
+		uint32_t lo = 0, hi = U;
+		while (lo < hi) {
+			const uint32_t mid = (lo + hi) >> 1;
+			if ((key[mid] & 0x1fffffffu) < n) lo = mid + 1;
+			else hi = mid;
+		}
+		if (lo >= U || (key[lo] & 0x1fffffffu) != n) {
+			atomicOr(err, 1);
+			return 0;
+		}
+		return T + lo;
+	};
+	if (row) {
+		const uint32_t fbase = fine_base[t];
+		uint32_t fk = fbase + fb;
+		uint32_t code[6] = {0xffffu, 0xffffu, 0xffffu, 0xffffu, 0xffffu, 0xffffu};
+		for (uint32_t e = e0; e < e1;) {
+			const int d = ent[e] & 7;
+			uint32_t k = e + 1;
+			while (k < e1 && (ent[k] & 7) == d) k++;
+			const uint32_t axbit = 1u << (29 + (d >> 1));
+			if (k - e == 1) {
+				code[d] = local(uint32_t(ent[e] >> 3));
+				if (code[d] >= T) atomicOr(&key[code[d] - T], axbit);
+			} else {
+				uint32_t li[4];
+				for (int i = 0; i < 4; i++) {
+					li[i] = local(uint32_t(ent[e + i] >> 3));
+					if (li[i] >= T) atomicOr(&key[li[i] - T], axbit);
+				}
+				tfine[2 * size_t(fk)] = li[0] | (li[1] << 16);
+				tfine[2 * size_t(fk) + 1] = li[2] | (li[3] << 16);
+				code[d] = 0x8000u | (fk - fbase);
+				fk++;
+			}
+			e = k;
+		}
+		tell[size_t(r)] = code[0] | (code[1] << 16);
+		tell[pl + size_t(r)] = code[2] | (code[3] << 16);
+		tell[2 * pl + size_t(r)] = code[4] | (code[5] << 16);
+	}
+	__syncthreads();
+	const uint32_t eb = ext_ptr[t];
+	for (uint32_t i = tid; i < U; i += 512) {
+		const uint32_t x = key[i];
+		ext_pk[eb + i] = x;
+		ext[eb + i] = x & 0x1fffffffu;
+	}
+}
+
+// ---------------------------------------------------------------------------
 // Regular tiles: a tile of exactly 512 slots that is an aligned 8x8x8 box of
 // cells of one level whose face neighbors on each of its six sides are,
 // all of them, either absent (non-periodic boundary) or the same-level
@@ -334,11 +505,28 @@ constexpr uint32_t kCutMaxT = 4096;
 
 __global__ __launch_bounds__(kCutBlock) void cut_next_kernel(const uint8_t* __restrict__ al, uint32_t r0, uint32_t r1,
                                                               uint32_t T, uint32_t lo, uint32_t* __restrict__ next) {
-	__shared__ uint8_t w[kCutBlock + kCutMaxT + 1];
+	// window maxima by doubling (a sparse table level by level): key of LDS
+	// position p = alignment << 16 | p, so the max is the best alignment at
+	// its latest position, and the window [lo, T] of every slot is the max of
+	// two overlapping power-of-two spans
+	__shared__ uint32_t kb[2][kCutBlock + kCutMaxT + 1];
 	const uint32_t a0 = r0 + blockIdx.x * kCutBlock;
 	if (a0 >= r1) return;  // block-uniform
 	const uint32_t span = kCutBlock + T + 1;
-	for (uint32_t i = threadIdx.x; i < span; i += kCutBlock) w[i] = a0 + i < r1 ? al[a0 + i] : 0;
+	for (uint32_t i = threadIdx.x; i < span; i += kCutBlock) kb[0][i] = ((a0 + i < r1 ? uint32_t(al[a0 + i]) : 0u) << 16) | i;
+	const uint32_t len = T - lo + 1;  // window length
+	int lv = 0;
+	while ((2u << lv) <= len) lv++;  // 2^lv <= len < 2^(lv+1)
+	int cur = 0;
+	for (int k = 0; k < lv; k++) {
+		__syncthreads();
+		const uint32_t h = 1u << k;
+		for (uint32_t i = threadIdx.x; i < span; i += kCutBlock) {
+			const uint32_t x = kb[cur][i];
+			kb[cur ^ 1][i] = i + h < span ? max(x, kb[cur][i + h]) : x;
+		}
+		cur ^= 1;
+	}
 	__syncthreads();
 	const uint32_t a = a0 + threadIdx.x;
 	if (a >= r1) return;
@@ -346,13 +534,8 @@ __global__ __launch_bounds__(kCutBlock) void cut_next_kernel(const uint8_t* __re
 		next[a] = r1;
 		return;
 	}
-	// key = alignment * 8192 + offset: the max is the best alignment, latest
-	uint32_t best = 0;
-	for (uint32_t o = lo; o <= T; o++) {
-		const uint32_t k = (uint32_t(w[threadIdx.x + o]) << 13) | o;
-		best = k > best ? k : best;
-	}
-	next[a] = a + (best & 8191u);
+	const uint32_t best = max(kb[cur][threadIdx.x + lo], kb[cur][threadIdx.x + T + 1 - (1u << lv)]);
+	next[a] = a0 + (best & 0xffffu);
 }
 
 __global__ void jump_double_kernel(const uint32_t* __restrict__ in, size_t n, uint32_t* __restrict__ out) {
@@ -494,6 +677,42 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		ext_pk.alloc(1);
 		tfine.alloc(2);
 		return out;
+	}
+	if (T <= kXT && ntiles) {
+		// per-tile build (tile_ext_kernel)
+		DBuf<uint32_t> ecnt, fcnt;
+		DBuf<int> err;
+		ecnt.alloc(ntiles + 1);
+		fcnt.alloc(ntiles + 1);
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+		tile_ext_kernel<0><<<unsigned(ntiles), 512, 0, s>>>(tstart.p, T, face_ptr, face_ent, ecnt.p, fcnt.p, nullptr,
+		                                                    nullptr, nullptr, nullptr, nullptr, 0, nullptr, err.p);
+		HIP_CHECK(hipGetLastError());
+		const size_t m = scan_exclusive_u32(ecnt.p, ext_ptr.p, ntiles, s);
+		out.n_fine = scan_exclusive_u32(fcnt.p, fine_base.p, ntiles, s);
+		int herr = 0;
+		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+		std::vector<uint32_t> hptr = download(ext_ptr.p, ntiles + 1, s);
+		if (herr == 0) {
+			out.total_ext = m;
+			for (size_t t = 0; t < ntiles; t++) out.max_ext = std::max<size_t>(out.max_ext, hptr[t + 1] - hptr[t]);
+			DX_REQUIRE(size_t(T) + out.max_ext < 0x8000u, "tile too large for 16-bit local indices");
+			DX_LAP("tb.3_ext_count");
+			ext.alloc(m + 1);
+			ext_pk.alloc(m + 1);
+			tfine.alloc(2 * out.n_fine + 2);
+			tile_ext_kernel<1><<<unsigned(ntiles), 512, 0, s>>>(tstart.p, T, face_ptr, face_ent, nullptr, nullptr,
+			                                                    ext_ptr.p, fine_base.p, ext.p, ext_pk.p, tell.p,
+			                                                    n_local + 1, tfine.p, err.p);
+			HIP_CHECK(hipGetLastError());
+			HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipStreamSynchronize(s));
+			DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
+			DX_LAP("tb.4_ext_rows");
+			return out;
+		}
+		out.n_fine = 0;  // a tile beyond kXCap out-of-tile entries: the global build
 	}
 	uint32_t n_ent = 0;
 	HIP_CHECK(hipMemcpyAsync(&n_ent, face_ptr + n_local, 4, hipMemcpyDeviceToHost, s));

@@ -490,7 +490,8 @@ __global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, 
 	}
 }
 
-// where each slot of a rebuilt mesh takes its payload from (rebuild step 6):
+// where each slot of a rebuilt mesh takes its payload from (rebuild step 6;
+// the gathers below write zeros where there is no source):
 // the old local slot of the same cell, else (a new local cell absent from the
 // old mesh: a refined cell's child) the old slot of its parent, else nothing
 __global__ void carry_src_kernel(const uint64_t* __restrict__ slot_ids, size_t n_slots, size_t nl, MapCtx m,
@@ -513,14 +514,14 @@ template <class T>
 __global__ void gather_rows_kernel(const T* __restrict__ old, const int32_t* __restrict__ src, size_t n,
                                    T* __restrict__ out) {
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x)
-		if (src[s] >= 0) out[s] = old[src[s]];
+		out[s] = src[s] >= 0 ? old[src[s]] : T{};
 }
 
 __global__ void gather_bytes_kernel(const uint8_t* __restrict__ old, const int32_t* __restrict__ src, size_t n,
                                     size_t elem, uint8_t* __restrict__ out) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n * elem; i += size_t(gridDim.x) * blockDim.x) {
 		const size_t s = i / elem;
-		if (src[s] >= 0) out[i] = old[size_t(src[s]) * elem + (i - s * elem)];
+		out[i] = src[s] >= 0 ? old[size_t(src[s]) * elem + (i - s * elem)] : uint8_t(0);
 	}
 }
 
@@ -1177,7 +1178,7 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
-                     hipStream_t s) {
+                     hipStream_t s, const size_t* at, size_t* pos_at, int n_at) {
 	DBuf<uint64_t> dS, dF;
 	upload(dS, S, s);
 	upload(dF, F, s);
@@ -1190,6 +1191,13 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 		HIP_CHECK(hipGetLastError());
 	}
 	n_out = scan_exclusive_u32(cnt.p, pos.p, n, s);
+	// where input positions at[k] land (the expanded list's run boundaries)
+	for (int k = 0; k < n_at; k++) {
+		uint32_t v = 0;
+		HIP_CHECK(hipMemcpyAsync(&v, pos.p + at[k], 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		pos_at[k] = v;
+	}
 	out_id.alloc(n_out + 1);
 	out_own.alloc(n_out + 1);
 	if (n) {

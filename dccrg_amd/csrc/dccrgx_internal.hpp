@@ -324,6 +324,10 @@ struct Mesh {
 	DBuf<uint64_t> kid;   // explicit: known leaves, any order
 	DBuf<int32_t> kown;   // their owners
 	size_t n_known = 0;
+	// when > 0 (explicit meshes on Morton slots): kid[0, n_prefix) are the own
+	// leaves, kid[0, prefix_run1) and kid[prefix_run1, n_prefix) each in Morton
+	// order (set by rebuild, carried through refinement by k_apply_refines)
+	size_t n_prefix = 0, prefix_run1 = 0;
 	DBuf<HashEntry> tab;
 	uint64_t mask = 0;
 	uint32_t shift = 63;
@@ -663,7 +667,7 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 // first child)
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
-                     hipStream_t s);
+                     hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0);
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {

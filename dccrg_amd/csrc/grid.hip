@@ -496,6 +496,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
 	for (uint64_t c : g.unrefine_bulk) req_par.push_back(map_parent(g.m, c));
 	req_par = sorted_unique(g, req_par);
+	DX_LAP("sr.3a_parents");
 	g.unrefine_requests.clear();
 	g.unrefine_bulk.clear();
 	const std::vector<uint64_t> DU = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_unrefine_cells))));
@@ -510,6 +511,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	blocked = sorted_unique(g, std::move(blocked));
 	std::vector<uint64_t> cand;
 	std::set_difference(req_par.begin(), req_par.end(), blocked.begin(), blocked.end(), std::back_inserter(cand));
+	DX_LAP("sr.3b_candidates");
 	const std::vector<uint8_t> ok = k_unrefine_check(g.m, g.d_hood.p, nh, g.dm(), cand, S, s);
 	std::vector<uint64_t> fmine;
 	for (size_t i = 0; i < cand.size(); i++)
@@ -521,12 +523,14 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	// local refined cells -> the new local cells; weights follow (6199-6200)
 	std::vector<int32_t> own(S.size());
 	lookup_batch(g, S.data(), S.size(), own.data(), nullptr);
+	DX_LAP("sr.4a_lookup");
 	std::vector<uint64_t> created;
 	for (size_t i = 0; i < S.size(); i++) {
 		if (own[i] != g.rank) continue;
 		uint64_t ch[8];
 		map_all_children(g.m, S[i], ch);
 		created.insert(created.end(), ch, ch + 8);
+		if (g.weights.empty() && g.pins.empty()) continue;
 		auto w = g.weights.find(S[i]);
 		if (w != g.weights.end()) {
 			const double wv = w->second;
@@ -552,12 +556,14 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		for (size_t i = 0; i < F.size(); i++) map_all_children(g.m, F[i], ch_all.data() + 8 * i);
 		std::vector<int32_t> ch_own(ch_all.size());
 		lookup_batch(g, ch_all.data(), ch_all.size(), ch_own.data(), nullptr);
+		DX_LAP("sr.5a_lookup");
+		const bool attrs = !g.weights.empty() || !g.pins.empty();
 		for (size_t i = 0; i < F.size(); i++) {
 			const int parent_owner = ch_own[8 * i];
 			for (int k = 0; k < 8; k++) {
 				const uint64_t c = ch_all[8 * i + k];
 				const int o = ch_own[8 * i + k];
-				if (o == g.rank) {
+				if (o == g.rank && attrs) {
 					g.weights.erase(c);
 					g.pins.erase(c);
 				}
@@ -568,7 +574,9 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		}
 		for (auto* mp : {&send_ids, &recv_ids})
 			for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
+		DX_LAP("sr.5b_loop");
 		host_sort_u64(keep_ids, false, s);
+		DX_LAP("sr.5c_sort");
 	}
 	size_t bpc = 0;
 	for (auto& f : g.fields) bpc += f.elem;
@@ -690,7 +698,17 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	mesh_materialize(g, known);
 	nm.implicit = false;
 	nm.bp = known.bp;
-	k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s);
+	{
+		// the own leaves stay kid's prefix: refined ones expand in place into
+		// their children (Morton order), a merged family's first child becomes
+		// its parent, the other children drop out
+		const size_t at[2] = {known.prefix_run1, known.n_prefix};
+		size_t pos_at[2] = {0, 0};
+		k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s, at, pos_at,
+		                known.n_prefix ? 2 : 0);
+		nm.prefix_run1 = pos_at[0];
+		nm.n_prefix = pos_at[1];
+	}
 	DX_LAP("sr.6_apply");
 	rebuild(g, nm);
 	DX_LAP("sr.7_rebuild");

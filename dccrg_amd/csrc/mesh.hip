@@ -30,6 +30,22 @@ __global__ void select_owner_kernel(const uint64_t* ids, const int32_t* own, siz
 		}
 }
 
+// the entries NOT owned by `rank`, with their owners (same launch)
+__global__ void select_other_kernel(const uint64_t* ids, const int32_t* own, size_t n, int rank, uint64_t* out,
+                                    int32_t* out_own, unsigned long long* counter) {
+	const size_t i0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kAppendRun;
+	unsigned c = 0;
+	for (int k = 0; k < kAppendRun; k++)
+		if (i0 + k < n && own[i0 + k] != rank) c++;
+	unsigned long long at = wave_reserve(counter, c);
+	for (int k = 0; k < kAppendRun && c; k++)
+		if (i0 + k < n && own[i0 + k] != rank) {
+			out[at] = ids[i0 + k];
+			out_own[at++] = own[i0 + k];
+			c--;
+		}
+}
+
 unsigned select_owner_grid(size_t n) { return unsigned((n + size_t(256) * kAppendRun - 1) / (size_t(256) * kAppendRun)); }
 
 __global__ void fill_owner_kernel(int32_t* own, size_t n, int32_t v) {
@@ -123,6 +139,8 @@ void mesh_materialize(Grid& g, Mesh& out) {
 		out.kid.alloc(g.mesh.n_known + 1);
 		out.kown.alloc(g.mesh.n_known + 1);
 		out.n_known = g.mesh.n_known;
+		out.n_prefix = g.mesh.n_prefix;
+		out.prefix_run1 = g.mesh.prefix_run1;
 		if (out.n_known) {
 			HIP_CHECK(hipMemcpyAsync(out.kid.p, g.mesh.kid.p, out.n_known * 8, hipMemcpyDeviceToDevice, s));
 			HIP_CHECK(hipMemcpyAsync(out.kown.p, g.mesh.kown.p, out.n_known * 4, hipMemcpyDeviceToDevice, s));
@@ -274,6 +292,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	// 1. own leaves, ascending (in any order when the Morton sort of step 2
 	// decides the slot order)
 	DBuf<uint64_t> d_local;
+	bool prefix_sorted = false;  // d_local already in Morton order
 	if (M.implicit) {
 		uint64_t f, c;
 		M.bp.range(uint64_t(g.rank), f, c);
@@ -282,20 +301,29 @@ void rebuild(Grid& g, Mesh& nm) {
 		g.n_local = c;
 	} else {
 		mesh_build_hash(M, M.kid.p, M.kown.p, M.n_known, s);
-		d_local.alloc(M.n_known + 1);
-		DBuf<unsigned long long> ctr;
-		ctr.alloc(1);
-		HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
-		if (M.n_known) {
-			select_owner_kernel<<<select_owner_grid(M.n_known), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank, d_local.p,
-			                                                              ctr.p);
-			HIP_CHECK(hipGetLastError());
+		DX_LAP("rb.1a_hash");
+		if (M.n_prefix && g.morton_slots) {
+			// the own leaves are kid's prefix, in (at most two runs of) Morton order
+			g.n_local = M.n_prefix;
+			d_local.alloc(g.n_local + 1);
+			HIP_CHECK(hipMemcpyAsync(d_local.p, M.kid.p, g.n_local * 8, hipMemcpyDeviceToDevice, s));
+			prefix_sorted = M.prefix_run1 == M.n_prefix;
+		} else {
+			d_local.alloc(M.n_known + 1);
+			DBuf<unsigned long long> ctr;
+			ctr.alloc(1);
+			HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
+			if (M.n_known) {
+				select_owner_kernel<<<select_owner_grid(M.n_known), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank,
+				                                                              d_local.p, ctr.p);
+				HIP_CHECK(hipGetLastError());
+			}
+			unsigned long long hn = 0;
+			HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipStreamSynchronize(s));
+			g.n_local = size_t(hn);
+			if (!g.morton_slots) sort_u64(d_local.p, g.n_local, s);
 		}
-		unsigned long long hn = 0;
-		HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
-		g.n_local = size_t(hn);
-		if (!g.morton_slots) sort_u64(d_local.p, g.n_local, s);
 	}
 	const size_t nl = g.n_local;
 	DevMesh dm = g.dm();  // implicit: no table yet (owners by formula)
@@ -313,7 +341,8 @@ void rebuild(Grid& g, Mesh& nm) {
 	local_slots.alloc(nl + 1);
 	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
 	d_local.release();
-	if (g.morton_slots) {
+	if (g.morton_slots && !prefix_sorted) {
+		// (a Morton-ordered d_local stays so in both runs: the split is stable)
 		k_morton_sort(m, local_slots.p, g.n_inner, s);
 		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
 	}
@@ -441,13 +470,44 @@ void rebuild(Grid& g, Mesh& nm) {
 		}
 		DBuf<uint8_t> nd;
 		nd.alloc(g.n_slots * f.elem);
-		if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
-		if (f.data.p && old_slot_ids.p) k_gather_rows(f.data.p, src.p, g.n_slots, f.elem, nd.p, s);
+		if (f.data.p && old_slot_ids.p) k_gather_rows(f.data.p, src.p, g.n_slots, f.elem, nd.p, s);  // zeros where no source
+		else if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
 		f.data.swap(nd);
 		f.scratch.release();
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_LAP("rb.6_carry_fields");
+	// the known list as [own leaves in slot order | the others] for the next
+	// refinement (Mesh::n_prefix)
+	M.n_prefix = M.prefix_run1 = 0;
+	if (!M.implicit && g.morton_slots && nl) {
+		DBuf<uint64_t> kid;
+		DBuf<int32_t> kown;
+		kid.alloc(M.n_known + 1);
+		kown.alloc(M.n_known + 1);
+		HIP_CHECK(hipMemcpyAsync(kid.p, g.slot_ids.p, nl * 8, hipMemcpyDeviceToDevice, s));
+		k_fill_i32(kown.p, nl, g.rank, s);
+		size_t ng = 0;
+		if (M.n_known > nl) {
+			DBuf<unsigned long long> ctr;
+			ctr.alloc(1);
+			HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
+			select_other_kernel<<<select_owner_grid(M.n_known), 256, 0, s>>>(M.kid.p, M.kown.p, M.n_known, g.rank, kid.p + nl,
+			                                                          kown.p + nl, ctr.p);
+			HIP_CHECK(hipGetLastError());
+			unsigned long long hn = 0;
+			HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipStreamSynchronize(s));
+			ng = size_t(hn);
+		}
+		DX_REQUIRE(nl + ng == M.n_known, "internal error: known leaves are not own + others");
+		M.kid.swap(kid);
+		M.kown.swap(kown);
+		M.n_prefix = nl;
+		M.prefix_run1 = g.n_inner;
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+	DX_LAP("rb.7_known_order");
 	g.csr_valid = false;
 	g.face_valid = false;
 	g.tiles_valid = false;

@@ -62,7 +62,7 @@ __global__ void iota_u64_kernel(uint64_t* out, uint64_t first, size_t n) {
 
 // insert (id, owner, slot = -1); keys are unique
 __global__ void hash_insert_kernel(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids,
-                                   const int32_t* owners, int32_t owner_const, size_t n) {
+                                   const int32_t* owners, int32_t owner_const, size_t n, size_t slot_upto) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = ids[i];
 		uint64_t h = hash_home(id, shift);
@@ -71,7 +71,7 @@ __global__ void hash_insert_kernel(HashEntry* tab, uint64_t mask, uint32_t shift
 			const unsigned long long prev = atomicCAS(kp, 0ull, (unsigned long long)id);
 			if (prev == 0ull || prev == id) {
 				tab[h].owner = owners ? owners[i] : owner_const;
-				tab[h].slot = -1;
+				tab[h].slot = i < slot_upto ? int32_t(i) : -1;
 				break;
 			}
 			h = (h + 1) & mask;
@@ -778,6 +778,58 @@ __global__ void refine_fill_kernel(MapCtx m, const uint64_t* kid, const int32_t*
 	}
 }
 
+// The own-leaf prefix of the known list (Mesh::n_prefix: kid index = slot)
+// classified by lookups of the refined cells and the merged families'
+// children instead of a search per entry: cls 1 refined, 2 a family's first
+// child (becomes the parent), 3 another child (drops out), 0 unchanged.
+__global__ void mark_refined_kernel(DevMesh M, const uint64_t* S, size_t nS, size_t n_prefix, uint8_t* cls) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < nS; i += size_t(gridDim.x) * blockDim.x) {
+		const int32_t sl = dm_slot(M, S[i]);
+		if (sl >= 0 && size_t(sl) < n_prefix) cls[sl] = 1;
+	}
+}
+
+__global__ void mark_families_kernel(MapCtx m, DevMesh M, const uint64_t* F, size_t nF, size_t n_prefix, uint8_t* cls) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < 8 * nF; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t ch[8];
+		map_all_children(m, F[i >> 3], ch);
+		const int k = int(i & 7);
+		const int32_t sl = dm_slot(M, ch[k]);
+		if (sl >= 0 && size_t(sl) < n_prefix) cls[sl] = k == 0 ? 2 : 3;
+	}
+}
+
+__global__ void prefix_count_kernel(const uint8_t* cls, size_t n, uint32_t* cnt) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint8_t c = cls[i];
+		cnt[i] = c == 1 ? 8u : (c == 3 ? 0u : 1u);
+	}
+}
+
+// src (optional): per output entry the input index its payload comes from
+// (-1: a merged parent, which starts zeroed)
+__global__ void prefix_fill_kernel(MapCtx m, const uint64_t* kid, const int32_t* kown, const uint8_t* cls, size_t n,
+                                   const uint32_t* pos, uint64_t* oid, int32_t* oown, int32_t* src) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint8_t c = cls[i];
+		const size_t p = pos[i];
+		if (c == 3) continue;
+		if (c == 1) {
+			uint64_t ch[8];
+			map_all_children(m, kid[i], ch);
+			for (int k = 0; k < 8; k++) {
+				oid[p + k] = ch[k];
+				oown[p + k] = kown[i];
+				if (src) src[p + k] = int32_t(i);
+			}
+		} else {
+			oid[p] = c == 2 ? map_parent(m, kid[i]) : kid[i];
+			oown[p] = kown[i];
+			if (src) src[p] = c == 2 ? -1 : int32_t(i);
+		}
+	}
+}
+
 }  // namespace
 
 // ============================================================================
@@ -802,9 +854,9 @@ void k_iota_u64(uint64_t* out, uint64_t first, size_t n, hipStream_t s) {
 }
 
 void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids, const int32_t* owners,
-                   int32_t owner_const, size_t n, hipStream_t s) {
+                   int32_t owner_const, size_t n, hipStream_t s, size_t slot_upto) {
 	if (!n) return;
-	hash_insert_kernel<<<grid_for(n, 256), 256, 0, s>>>(tab, mask, shift, ids, owners, owner_const, n);
+	hash_insert_kernel<<<grid_for(n, 256), 256, 0, s>>>(tab, mask, shift, ids, owners, owner_const, n, slot_upto);
 	HIP_CHECK(hipGetLastError());
 }
 
@@ -1178,7 +1230,8 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
-                     hipStream_t s, const size_t* at, size_t* pos_at, int n_at) {
+                     hipStream_t s, const size_t* at, size_t* pos_at, int n_at, size_t n_prefix, const DevMesh* dm,
+                     DBuf<int32_t>* src) {
 	DBuf<uint64_t> dS, dF;
 	upload(dS, S, s);
 	upload(dF, F, s);
@@ -1186,8 +1239,21 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 	cnt.alloc(n + 1);
 	pos.alloc(n + 1);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, (n + 1) * 4, s));
-	if (n) {
-		refine_count_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, n, dS.p, S.size(), dF.p, F.size(), cnt.p);
+	// [0, np): the own-leaf prefix classified by lookups; the rest searched
+	const size_t np = dm ? std::min(n_prefix, n) : 0;
+	DBuf<uint8_t> cls;
+	if (np) {
+		cls.alloc(np);
+		HIP_CHECK(hipMemsetAsync(cls.p, 0, np, s));
+		if (!S.empty()) mark_refined_kernel<<<grid_for(S.size(), 256), 256, 0, s>>>(*dm, dS.p, S.size(), np, cls.p);
+		if (!F.empty())
+			mark_families_kernel<<<grid_for(8 * F.size(), 256), 256, 0, s>>>(m, *dm, dF.p, F.size(), np, cls.p);
+		prefix_count_kernel<<<grid_for(np, 256), 256, 0, s>>>(cls.p, np, cnt.p);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (n > np) {
+		refine_count_kernel<<<grid_for(n - np, 256), 256, 0, s>>>(m, kid + np, n - np, dS.p, S.size(), dF.p, F.size(),
+		                                                          cnt.p + np);
 		HIP_CHECK(hipGetLastError());
 	}
 	n_out = scan_exclusive_u32(cnt.p, pos.p, n, s);
@@ -1200,9 +1266,18 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 	}
 	out_id.alloc(n_out + 1);
 	out_own.alloc(n_out + 1);
-	if (n) {
-		refine_fill_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, kid, kown, n, pos.p, cnt.p, dF.p, F.size(), out_id.p,
-		                                                    out_own.p);
+	if (src) {
+		src->alloc(n_out + 1);
+		HIP_CHECK(hipMemsetAsync(src->p, 0xff, (n_out + 1) * 4, s));
+	}
+	if (np) {
+		prefix_fill_kernel<<<grid_for(np, 256), 256, 0, s>>>(m, kid, kown, cls.p, np, pos.p, out_id.p, out_own.p,
+		                                                     src ? src->p : nullptr);
+		HIP_CHECK(hipGetLastError());
+	}
+	if (n > np) {
+		refine_fill_kernel<<<grid_for(n - np, 256), 256, 0, s>>>(m, kid + np, kown + np, n - np, pos.p + np, cnt.p + np,
+		                                                         dF.p, F.size(), out_id.p, out_own.p);
 		HIP_CHECK(hipGetLastError());
 	}
 	HIP_CHECK(hipStreamSynchronize(s));

@@ -328,6 +328,10 @@ struct Mesh {
 	// leaves, kid[0, prefix_run1) and kid[prefix_run1, n_prefix) each in Morton
 	// order (set by rebuild, carried through refinement by k_apply_refines)
 	size_t n_prefix = 0, prefix_run1 = 0;
+	// per own leaf of the prefix, the old slot its payload comes from (-1
+	// none), when k_apply_refines made this mesh from one whose prefix was
+	// the old slot order; used (and released) by rebuild's carry step
+	DBuf<int32_t> carry;
 	DBuf<HashEntry> tab;
 	uint64_t mask = 0;
 	uint32_t shift = 63;
@@ -572,7 +576,9 @@ void mesh_from_global(Grid& g, Mesh& out, const std::vector<uint64_t>& ids, cons
 void mesh_materialize(Grid& g, Mesh& out);
 // after a repartition: own leaves known, ghosts fetched from their owners
 void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n_local);
-void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s);
+// (entries i < slot_upto get slot i, the others -1)
+void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
+                     size_t slot_upto = 0);
 void rebuild(Grid& g, Mesh& new_mesh);  // new_mesh is moved into g.mesh
 void ensure_csr(Grid& g);
 void ensure_face(Grid& g);
@@ -596,7 +602,7 @@ inline const uint64_t* local_ids_dev(const Grid& g) { return g.slot_ids.p; }
 void k_fill_i32(int32_t* p, size_t n, int32_t v, hipStream_t s);
 void k_iota_u64(uint64_t* out, uint64_t first, size_t n, hipStream_t s);
 void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t* ids, const int32_t* owners,
-                   int32_t owner_const, size_t n, hipStream_t s);
+                   int32_t owner_const, size_t n, hipStream_t s, size_t slot_upto = 0);
 void k_hash_set_slots(const DevMesh& M, const uint64_t* slot_ids, size_t n, int32_t* err, hipStream_t s);
 void k_lookup(const DevMesh& M, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot, hipStream_t s);
 // flag local cells that have a remote neighbors_of / neighbors_to entry
@@ -667,7 +673,8 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 // first child)
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
-                     hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0);
+                     hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0,
+                     size_t n_prefix = 0, const DevMesh* dm = nullptr, DBuf<int32_t>* src = nullptr);
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {

@@ -591,13 +591,11 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (!F.empty()) {
 		// removed store order: the kept children ascending, then per source
 		// process (ascending rank) its children ascending
+		const DBuf<int32_t> ksl = keep_ids.empty() ? DBuf<int32_t>() : slots_of(g, keep_ids);
 		for (auto& f : g.fields) {
 			if (f.var) continue;
 			f.removed.alloc(n_rm * f.elem + 1);
-			if (!keep_ids.empty()) {
-				const DBuf<int32_t> sl = slots_of(g, keep_ids);
-				k_pack(f.data.p, f.elem, 0, f.elem, sl.p, keep_ids.size(), f.removed.p, s);
-			}
+			if (!keep_ids.empty()) k_pack(f.data.p, f.elem, 0, f.elem, ksl.p, keep_ids.size(), f.removed.p, s);
 		}
 		g.removed_ids_h = keep_ids;
 		std::vector<size_t> soff, roff;
@@ -704,8 +702,9 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		// its parent, the other children drop out
 		const size_t at[2] = {known.prefix_run1, known.n_prefix};
 		size_t pos_at[2] = {0, 0};
+		const DevMesh dm = g.dm();
 		k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s, at, pos_at,
-		                known.n_prefix ? 2 : 0);
+		                known.n_prefix ? 2 : 0, known.n_prefix, &dm, g.size == 1 && known.n_prefix ? &nm.carry : nullptr);
 		nm.prefix_run1 = pos_at[0];
 		nm.n_prefix = pos_at[1];
 	}

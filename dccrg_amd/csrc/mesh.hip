@@ -65,14 +65,14 @@ std::vector<int> HaloPlan::peers() const {
 
 static int ghost_radius(const Grid& g) { return std::max(1, int(g.hood_len)); }
 
-void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s) {
+void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s, size_t slot_upto) {
 	uint32_t bits = 4;
 	while ((uint64_t(1) << bits) < 2 * uint64_t(n)) bits++;
 	M.tab.alloc(size_t(1) << bits);
 	HIP_CHECK(hipMemsetAsync(M.tab.p, 0, M.tab.n * sizeof(HashEntry), s));
 	M.mask = (uint64_t(1) << bits) - 1;
 	M.shift = 64u - bits;
-	k_hash_insert(M.tab.p, M.mask, M.shift, ids, owners, -2, n, s);
+	k_hash_insert(M.tab.p, M.mask, M.shift, ids, owners, -2, n, s, slot_upto);
 }
 
 void mesh_init_implicit(Grid& g) {
@@ -293,6 +293,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	// decides the slot order)
 	DBuf<uint64_t> d_local;
 	bool prefix_sorted = false;  // d_local already in Morton order
+	bool direct = false;         // ... and slot i = d_local[i] (table slots set on insert)
 	if (M.implicit) {
 		uint64_t f, c;
 		M.bp.range(uint64_t(g.rank), f, c);
@@ -300,7 +301,10 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_iota_u64(d_local.p, f, c, s);
 		g.n_local = c;
 	} else {
-		mesh_build_hash(M, M.kid.p, M.kown.p, M.n_known, s);
+		// one process, own leaves already in Morton order: the prefix is the
+		// slot order, so the table gets its slots as it is built
+		direct = g.size == 1 && M.n_prefix && g.morton_slots && M.prefix_run1 == M.n_prefix && M.n_known == M.n_prefix;
+		mesh_build_hash(M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
 		DX_LAP("rb.1a_hash");
 		if (M.n_prefix && g.morton_slots) {
 			// the own leaves are kid's prefix, in (at most two runs of) Morton order
@@ -426,7 +430,8 @@ void rebuild(Grid& g, Mesh& nm) {
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
 	if (M.implicit) mesh_build_hash(M, g.slot_ids.p, nullptr, g.n_slots, s);
 	dm = g.dm();
-	k_hash_set_slots(dm, g.slot_ids.p, g.n_slots, err.p, s);
+	DX_REQUIRE(!direct || (g.n_slots == nl && g.n_inner == nl), "internal error: direct slots with halo or outer cells");
+	if (!direct) k_hash_set_slots(dm, g.slot_ids.p, g.n_slots, err.p, s);
 	{
 		std::vector<int32_t> rs(H.n_recv);
 		std::iota(rs.begin(), rs.end(), int32_t(nl));
@@ -459,9 +464,14 @@ void rebuild(Grid& g, Mesh& nm) {
 	const DevMesh odm = old.dev(m.last);
 	DBuf<int32_t> src;
 	if (old_slot_ids.p && std::any_of(g.fields.begin(), g.fields.end(), [](const Field& f) { return !f.var; })) {
-		src.alloc(g.n_slots + 1);
-		k_carry_src(g.slot_ids.p, g.n_slots, nl, m, odm, old_n_local, src.p, s);
+		if (direct && M.carry.n >= g.n_slots) {
+			src.swap(M.carry);  // from k_apply_refines: new prefix index = new slot
+		} else {
+			src.alloc(g.n_slots + 1);
+			k_carry_src(g.slot_ids.p, g.n_slots, nl, m, odm, old_n_local, src.p, s);
+		}
 	}
+	M.carry.release();
 	for (auto& f : g.fields) {
 		f.local_zero = false;
 		if (f.var) {  // children and new copies start empty (the reference default-constructs them)

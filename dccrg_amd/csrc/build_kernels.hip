@@ -426,7 +426,7 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // coarser probe needed).  Otherwise, and for the misses, the probes of
 // face_dir.  The hints are the same either way.
 __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1, bool morton,
-                                  uint32_t* cnt, int32_t* hint) {
+                                  uint64_t* cnt, int32_t* hint) {
 	const SlotExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		uint64_t c[3];
@@ -437,7 +437,7 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 		const uint64_t len = uint64_t(1) << (m.R - lvl);
 		const int64_t key = int64_t(morton3(c) >> sh);
 		const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
-		uint32_t k = 0;
+		uint32_t k = 0, kf = 0;  // entries, finer faces
 		for (int dir = 0; dir < 6; dir++) {
 			if (morton) {
 				uint64_t p[3];
@@ -458,22 +458,36 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 			// a single neighbor was the last cell found (face_dir returns on it)
 			hint[6 * r + dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -3));
 			k += uint32_t(nf);
+			kf += nf == 4 ? 1u : 0u;
 		}
-		cnt[r] = k;
+		cnt[r] = (uint64_t(kf) << 32) | k;
 	}
 }
 
+// pass 1: the rows from the hints (finer directions probed again), with the
+// fixed-width table: ell[6 r + d] = the neighbor's slot (same size or
+// coarser), -1 none, or -2 - f for the finer face f whose 4 slots are
+// fine[4 f ..] (reference order); pos = the scan of pass 0's counts (finer
+// faces numbered in row order)
 __global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, const int32_t* hint,
-                                 const uint32_t* ptr, int32_t* ent, int32_t* err) {
+                                 const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
+                                 int32_t* err) {
 	const DevExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
-		uint32_t k = ptr[r];
+		const uint64_t pr = pos[r];
+		uint32_t k = uint32_t(pr), f = uint32_t(pr >> 32);
+		ptr[r] = k;
+		if (r + 1 == nrows) ptr[nrows] = uint32_t(pos[nrows]);
 		for (int dir = 0; dir < 6; dir++) {
 			const int32_t h = hint[6 * r + dir];
-			if (h == -1) continue;
+			if (h == -1) {
+				ell[6 * r + dir] = -1;
+				continue;
+			}
 			if (h != -2) {
 				if (h == -3) atomicExch(err, 1);
 				ent[k++] = (h == -3 ? -1 : h) * 8 + dir;
+				ell[6 * r + dir] = h == -3 ? -1 : h;
 				continue;
 			}
 			uint64_t c[3];
@@ -485,7 +499,10 @@ __global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, 
 				const int32_t sl = dm_slot(M, out[i]);
 				if (sl < 0) atomicExch(err, 1);
 				ent[k++] = sl * 8 + dir;
+				fine[4 * size_t(f) + i] = sl;
 			}
+			ell[6 * r + dir] = -2 - int32_t(f);
+			f++;
 		}
 	}
 }
@@ -530,52 +547,6 @@ __global__ void morton_keys_kernel(MapCtx m, const uint64_t* ids, size_t n, uint
 		uint64_t x, y, z;
 		map_indices(m, ids[i], x, y, z);
 		keys[i] = spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
-	}
-}
-
-// fixed-width face table: per local slot and direction one int32 = the
-// neighbor's slot (same size or coarser), -1 (no neighbor), or -2 - k for a
-// finer face whose 4 slots are fine[4k..4k+3] (reference order)
-__global__ void face_ell_kernel(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine,
-                                unsigned int* nfine) {
-	// whole waves per iteration (the counter below is shared by the wave)
-	const size_t stride = size_t(gridDim.x) * blockDim.x;
-	for (size_t r0 = blockIdx.x * size_t(blockDim.x) + (threadIdx.x & ~(WAVE - 1)); r0 < nrows; r0 += stride) {
-		const size_t r = r0 + lane_id();
-		const bool act = r < nrows;
-		int32_t row[6] = {-1, -1, -1, -1, -1, -1};
-		uint32_t e = act ? ptr[r] : 0u;
-		const uint32_t e1 = act ? ptr[r + 1] : 0u;
-		while (e < e1) {
-			const int d = ent[e] & 7;
-			uint32_t k = e + 1;
-			while (k < e1 && (ent[k] & 7) == d) k++;
-			row[d] = k - e == 1 ? ent[e] >> 3 : -2;  // finer: numbered below
-			e = k;
-		}
-		// finer faces numbered through one counter atomic per wave
-		uint32_t nf = 0;
-		for (int d = 0; d < 6; d++) nf += row[d] == -2 ? 1u : 0u;
-		uint32_t incl = nf;
-		for (int o = 1; o < WAVE; o <<= 1) {
-			const uint32_t v = __shfl_up(incl, o);
-			if (lane_id() >= o) incl += v;
-		}
-		const uint32_t total = __shfl(incl, WAVE - 1);
-		unsigned int base = 0;
-		if (lane_id() == 0 && total) base = atomicAdd(nfine, total);
-		unsigned int f = __shfl(base, 0) + (incl - nf);
-		if (!act) continue;
-		e = ptr[r];
-		for (int d = 0; d < 6; d++) {
-			if (row[d] == -2) {
-				while ((ent[e] & 7) != d) e++;
-				for (int i = 0; i < 4; i++) fine[4 * size_t(f) + i] = ent[e + i] >> 3;
-				row[d] = -2 - int32_t(f);
-				f++;
-			}
-		}
-		for (int d = 0; d < 6; d++) ell[6 * r + d] = row[d];
 	}
 }
 
@@ -677,11 +648,15 @@ __global__ void cells_under_kernel(MapCtx m, const uint64_t* ids, size_t n, cons
 __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M, int rank,
                                const uint64_t* req, size_t n, uint64_t* out, unsigned long long* counter,
                                unsigned long long cap, int finer) {
+	// one thread per (request, candidate): the nh neighbors_of items, then
+	// the 10 nh neighbors_to candidates
 	const DevExists ex{M};
-	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
-	for (size_t w = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; w < n; w += waves) {
+	const size_t per = size_t(11) * size_t(nh);
+	for (size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x; t < n * per; t += size_t(gridDim.x) * blockDim.x) {
+		const size_t w = t / per;
+		const int k = int(t - w * per);
 		const uint64_t r = req[w];
-		if (dm_owner(M, r) != rank) continue;  // wave-uniform
+		if (dm_owner(M, r) != rank) continue;
 		uint64_t c[3];
 		int lvl;
 		cell_coords(m, r, c, lvl);
@@ -692,12 +667,13 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 			const unsigned long long pos = atomicAdd(counter, 1ull);
 			if (pos < cap) out[pos] = q;
 		};
-		for (int k = lane_id(); k < nh; k += WAVE) {
+		if (k < nh) {
 			ItemOut o;
 			nof_item(m, c, lvl, hood + 3 * k, ex, o);
 			for (int i = 0; i < o.n; i++) emit(o.id[i]);
+		} else {
+			emit(nto_candidate(m, c, lvl, hood_to, nh, k - nh, ex));
 		}
-		for (int k = lane_id(); k < 10 * nh; k += WAVE) emit(nto_candidate(m, c, lvl, hood_to, nh, k, ex));
 	}
 }
 
@@ -709,30 +685,32 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 // box: a box covered by one leaf of p's level or coarser passes, otherwise
 // each of its eight level-L cells must be a leaf that is not being refined.
 __global__ void unrefine_check_kernel(MapCtx m, const int32_t* hood, int nh, DevMesh M, const uint64_t* parents,
-                                      size_t n, const uint64_t* S, size_t nS, uint8_t* ok) {
+                                      size_t n, const uint64_t* S, size_t nS, uint32_t* ok) {
+	// one thread per (parent, neighborhood box); ok starts 1, a failing box
+	// clears it
 	const DevExists ex{M};
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+	for (size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x; t < n * size_t(nh); t += size_t(gridDim.x) * blockDim.x) {
+		const size_t i = t / size_t(nh);
+		const int k = int(t - i * size_t(nh));
 		uint64_t c[3];
 		int pl;
 		cell_coords(m, parents[i], c, pl);
 		const int64_t len = int64_t(1) << (m.R - pl);
+		uint64_t w[3];
+		bool inside = true;
+		for (int d = 0; d < 3; d++) inside = inside && map_wrap(m, d, int64_t(c[d]) + int64_t(hood[3 * k + d]) * len, w[d]);
+		if (!inside) continue;
+		bool covered = false;
+		for (int l = pl; l >= 0 && !covered; l--) covered = ex(map_from_indices(m, w[0], w[1], w[2], l));
+		if (covered) continue;
+		const uint64_t hl = uint64_t(len / 2);
 		bool good = true;
-		for (int k = 0; k < nh && good; k++) {
-			uint64_t w[3];
-			bool inside = true;
-			for (int d = 0; d < 3; d++) inside = inside && map_wrap(m, d, int64_t(c[d]) + int64_t(hood[3 * k + d]) * len, w[d]);
-			if (!inside) continue;
-			bool covered = false;
-			for (int l = pl; l >= 0 && !covered; l--) covered = ex(map_from_indices(m, w[0], w[1], w[2], l));
-			if (covered) continue;
-			const uint64_t hl = uint64_t(len / 2);
-			for (int q = 0; q < 8 && good; q++) {
-				const uint64_t id = map_from_indices(m, w[0] + (q & 1) * hl, w[1] + ((q >> 1) & 1) * hl,
-				                                     w[2] + ((q >> 2) & 1) * hl, pl + 1);
-				if (!ex(id) || sorted_has(S, nS, id)) good = false;
-			}
+		for (int q = 0; q < 8 && good; q++) {
+			const uint64_t id = map_from_indices(m, w[0] + (q & 1) * hl, w[1] + ((q >> 1) & 1) * hl,
+			                                     w[2] + ((q >> 2) & 1) * hl, pl + 1);
+			if (!ex(id) || sorted_has(S, nS, id)) good = false;
 		}
-		ok[i] = good ? 1 : 0;
+		if (!good) ok[i] = 0;
 	}
 }
 
@@ -828,6 +806,40 @@ __global__ void prefix_fill_kernel(MapCtx m, const uint64_t* kid, const int32_t*
 			if (src) src[p] = c == 2 ? -1 : int32_t(i);
 		}
 	}
+}
+
+// the children of the refined cells owned by `rank` (stop_refining's
+// created cells); one thread per refined cell, full waves (wave_reserve)
+__global__ void created_children_kernel(MapCtx m, DevMesh M, int rank, const uint64_t* S, size_t nS, uint64_t* out,
+                                        unsigned long long* ctr) {
+	const size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+	const bool mine = i < nS && dm_owner(M, S[i]) == rank;
+	const unsigned long long at = wave_reserve(ctr, mine ? 8u : 0u);
+	if (!mine) return;
+	uint64_t ch[8];
+	map_all_children(m, S[i], ch);
+	for (int k = 0; k < 8; k++) out[at + k] = ch[k];
+}
+
+// the children of merged families that stay on `rank` (owned here, as is the
+// family's first child, which becomes the parent's owner), with their slots
+__global__ void kept_children_kernel(MapCtx m, DevMesh M, int rank, const uint64_t* F, size_t nF, uint64_t* out,
+                                     int32_t* out_slot, unsigned long long* ctr) {
+	const size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+	bool keep = false;
+	uint64_t c = 0;
+	int32_t sl = -1;
+	if (t < 8 * nF) {
+		uint64_t ch[8];
+		map_all_children(m, F[t >> 3], ch);
+		c = ch[t & 7];
+		keep = dm_owner(M, c) == rank && dm_owner(M, ch[0]) == rank;
+		if (keep) sl = dm_slot(M, c);
+	}
+	const unsigned long long at = wave_reserve(ctr, keep ? 1u : 0u);
+	if (!keep) return;
+	out[at] = c;
+	out_slot[at] = sl;
 }
 
 }  // namespace
@@ -1049,15 +1061,16 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s,
-                  bool morton, size_t run1) {
+void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint64_t* cnt,
+                  int32_t* hint, const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
+                  int32_t* err_flag, int pass, hipStream_t s, bool morton, size_t run1) {
 	if (!nrows) return;
 	if (pass == 0)
 		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, cnt,
 		                                                       hint);
 	else
-		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, ptr, ent, err_flag);
+		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, pos, ptr, ent, ell, fine,
+		                                                      err_flag);
 	HIP_CHECK(hipGetLastError());
 }
 
@@ -1082,18 +1095,6 @@ void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t
 }
 
 
-size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s) {
-	if (!nrows) return 0;
-	DBuf<unsigned int> ctr;
-	ctr.alloc(1);
-	HIP_CHECK(hipMemsetAsync(ctr.p, 0, 4, s));
-	face_ell_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(ptr, ent, nrows, ell, fine, ctr.p);
-	HIP_CHECK(hipGetLastError());
-	unsigned int h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
-	return h;
-}
 
 // Reorder a run of cell ids along the Morton (z-order) curve of their min
 // corners at finest-level resolution (leaves have distinct min corners).
@@ -1200,8 +1201,8 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 		out.alloc(size_t(cap));
 		DBuf<unsigned long long> ctr;
 		zero_counter(ctr, s);
-		induced_kernel<<<grid_for(req.size(), 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p,
-		                                                       ctr.p, cap, finer ? 1 : 0);
+		induced_kernel<<<grid_for(req.size() * size_t(11) * size_t(nh), 256), 256, 0, s>>>(
+		    m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p, ctr.p, cap, finer ? 1 : 0);
 		HIP_CHECK(hipGetLastError());
 		const size_t k = read_counter(ctr, s);
 		if (k > cap) {
@@ -1220,12 +1221,16 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 	DBuf<uint64_t> dp, dS;
 	upload(dp, parents, s);
 	upload(dS, S, s);
-	DBuf<uint8_t> ok;
+	DBuf<uint32_t> ok;
 	ok.alloc(parents.size());
-	unrefine_check_kernel<<<grid_for(parents.size(), 256), 256, 0, s>>>(m, hood, nh, M, dp.p, parents.size(), dS.p,
-	                                                                   S.size(), ok.p);
+	k_fill_i32(reinterpret_cast<int32_t*>(ok.p), parents.size(), 1, s);
+	if (nh > 0)
+		unrefine_check_kernel<<<grid_for(parents.size() * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, dp.p,
+		                                                                                 parents.size(), dS.p, S.size(),
+		                                                                                 ok.p);
 	HIP_CHECK(hipGetLastError());
-	return download(ok.p, parents.size(), s);
+	const std::vector<uint32_t> h = download(ok.p, parents.size(), s);
+	return std::vector<uint8_t>(h.begin(), h.end());
 }
 
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
@@ -1281,6 +1286,51 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 		HIP_CHECK(hipGetLastError());
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
+                                         hipStream_t s) {
+	if (S.empty()) return {};
+	DBuf<uint64_t> dS, out;
+	upload(dS, S, s);
+	out.alloc(8 * S.size() + 1);
+	DBuf<unsigned long long> ctr;
+	ctr.alloc(1);
+	HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
+	created_children_kernel<<<unsigned((S.size() + 255) / 256), 256, 0, s>>>(m, M, rank, dS.p, S.size(), out.p, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t n = read_counter(ctr, s);
+	sort_u64(out.p, n, s);
+	return download(out.p, n, s);
+}
+
+void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
+                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s) {
+	ids.clear();
+	slots.release();
+	if (F.empty()) return;
+	DBuf<uint64_t> dF, k1, k2;
+	DBuf<int32_t> v1;
+	upload(dF, F, s);
+	const size_t cap = 8 * F.size();
+	k1.alloc(cap + 1);
+	k2.alloc(cap + 1);
+	v1.alloc(cap + 1);
+	slots.alloc(cap + 1);
+	DBuf<unsigned long long> ctr;
+	ctr.alloc(1);
+	HIP_CHECK(hipMemsetAsync(ctr.p, 0, 8, s));
+	kept_children_kernel<<<unsigned((cap + 255) / 256), 256, 0, s>>>(m, M, rank, dF.p, F.size(), k1.p, v1.p, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t n = read_counter(ctr, s);
+	if (n) {
+		size_t bytes = 0;
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
+		DBuf<uint8_t> temp;
+		temp.alloc(bytes + 1);
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
+		ids = download(k2.p, n, s);
+	}
 }
 
 }  // namespace dccrgx

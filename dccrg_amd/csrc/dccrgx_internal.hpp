@@ -633,7 +633,6 @@ void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s);  // ho
 void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
                          hipStream_t s);
 void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
-size_t k_face_ell(const uint32_t* ptr, const int32_t* ent, size_t nrows, int32_t* ell, int32_t* fine, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
 void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s);
 // iterator ranges cell.neighbors_of (update_cell_pointers 11451-11500): pass
@@ -643,9 +642,9 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
                       const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
                       uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
                       int pass, hipStream_t s);
-void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint32_t* cnt,
-                  int32_t* hint, const uint32_t* ptr, int32_t* ent, int32_t* err_flag, int pass, hipStream_t s,
-                  bool morton = false, size_t run1 = 0);
+void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint64_t* cnt,
+                  int32_t* hint, const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
+                  int32_t* err_flag, int pass, hipStream_t s, bool morton = false, size_t run1 = 0);
 void k_carry_src(const uint64_t* slot_ids, size_t n_slots, size_t nl, const MapCtx& m, const DevMesh& oldM,
                  size_t old_n_local, int32_t* src, hipStream_t s);
 void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t elem, uint8_t* out, hipStream_t s);
@@ -671,6 +670,13 @@ std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int 
 // the sorted parents F: every known leaf in S is replaced by its 8 children
 // (same owner), the children of a parent in F by the parent (owner of the
 // first child)
+// stop_refining on the device: the children of the refined cells owned by
+// `rank`, ascending; the children of merged families staying on `rank`
+// (owned here, like the family's first child), ascending, and their slots
+std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
+                                         hipStream_t s);
+void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
+                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s);
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
                      hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0,
@@ -678,7 +684,10 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {
-	size_t n_tiles_inner, n_tiles_outer, max_ext, total_ext, n_fine;
+	size_t n_tiles_inner = 0, n_tiles_outer = 0, max_ext = 0, total_ext = 0, n_fine = 0;
+	// per tile: first ext entry (of ext_pk) and count, first finer face (of
+	// tfine, 2 words each) and count
+	std::vector<uint32_t> ext_off, ext_n, fine_off, fine_n;
 };
 TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const uint64_t* slot_ids, const MapCtx& m,
                         bool morton, size_t n_inner, size_t n_local, int tile, DBuf<uint32_t>& tstart,

@@ -520,63 +520,65 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	DX_LAP("sr.3_override_unrefines");
 	if (S.empty() && F.empty()) return {};
 
-	// local refined cells -> the new local cells; weights follow (6199-6200)
-	std::vector<int32_t> own(S.size());
-	lookup_batch(g, S.data(), S.size(), own.data(), nullptr);
-	DX_LAP("sr.4a_lookup");
-	std::vector<uint64_t> created;
-	for (size_t i = 0; i < S.size(); i++) {
-		if (own[i] != g.rank) continue;
-		uint64_t ch[8];
-		map_all_children(g.m, S[i], ch);
-		created.insert(created.end(), ch, ch + 8);
-		if (g.weights.empty() && g.pins.empty()) continue;
-		auto w = g.weights.find(S[i]);
-		if (w != g.weights.end()) {
-			const double wv = w->second;
-			g.weights.erase(w);
-			for (uint64_t c : ch) g.weights[c] = wv;
-		}
-		// children inherit their parent's pin (10239-10251)
-		auto pn = g.pins.find(S[i]);
-		if (pn != g.pins.end()) {
-			const int pv = pn->second;
-			g.pins.erase(pn);
-			for (uint64_t c : ch) g.pins[c] = pv;
+	// local refined cells -> the new local cells (on the device); weights and
+	// pins follow (6199-6200, 10239-10251)
+	std::vector<uint64_t> created = k_created_children(g.m, g.dm(), g.rank, S, s);
+	if (!g.weights.empty() || !g.pins.empty()) {
+		std::vector<int32_t> own(S.size());
+		lookup_batch(g, S.data(), S.size(), own.data(), nullptr);
+		for (size_t i = 0; i < S.size(); i++) {
+			if (own[i] != g.rank) continue;
+			uint64_t ch[8];
+			map_all_children(g.m, S[i], ch);
+			auto w = g.weights.find(S[i]);
+			if (w != g.weights.end()) {
+				const double wv = w->second;
+				g.weights.erase(w);
+				for (uint64_t c : ch) g.weights[c] = wv;
+			}
+			// children inherit their parent's pin (10239-10251)
+			auto pn = g.pins.find(S[i]);
+			if (pn != g.pins.end()) {
+				const int pv = pn->second;
+				g.pins.erase(pn);
+				for (uint64_t c : ch) g.pins[c] = pv;
+			}
 		}
 	}
-	host_sort_u64(created, false, s);
 	DX_LAP("sr.4_created");
 
 	// merged families: the children's payloads to the parent's new process
 	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
 	std::vector<uint64_t> keep_ids;  // removed children staying on this rank
+	DBuf<int32_t> ksl;               // and their slots (device)
 	if (!F.empty()) {
-		std::vector<uint64_t> ch_all(8 * F.size());
-		for (size_t i = 0; i < F.size(); i++) map_all_children(g.m, F[i], ch_all.data() + 8 * i);
-		std::vector<int32_t> ch_own(ch_all.size());
-		lookup_batch(g, ch_all.data(), ch_all.size(), ch_own.data(), nullptr);
-		DX_LAP("sr.5a_lookup");
+		k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s);
+		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
-		for (size_t i = 0; i < F.size(); i++) {
-			const int parent_owner = ch_own[8 * i];
-			for (int k = 0; k < 8; k++) {
-				const uint64_t c = ch_all[8 * i + k];
-				const int o = ch_own[8 * i + k];
-				if (o == g.rank && attrs) {
-					g.weights.erase(c);
-					g.pins.erase(c);
+		if (g.size > 1 || attrs) {
+			// the children leaving / arriving, and the weights / pins of the
+			// removed local ones
+			std::vector<uint64_t> ch_all(8 * F.size());
+			for (size_t i = 0; i < F.size(); i++) map_all_children(g.m, F[i], ch_all.data() + 8 * i);
+			std::vector<int32_t> ch_own(ch_all.size());
+			lookup_batch(g, ch_all.data(), ch_all.size(), ch_own.data(), nullptr);
+			for (size_t i = 0; i < F.size(); i++) {
+				const int parent_owner = ch_own[8 * i];
+				for (int k = 0; k < 8; k++) {
+					const uint64_t c = ch_all[8 * i + k];
+					const int o = ch_own[8 * i + k];
+					if (o == g.rank && attrs) {
+						g.weights.erase(c);
+						g.pins.erase(c);
+					}
+					if (o == g.rank && parent_owner != g.rank) send_ids[parent_owner].push_back(c);
+					else if (o != g.rank && parent_owner == g.rank && o >= 0) recv_ids[o].push_back(c);
 				}
-				if (o == g.rank && parent_owner == g.rank) keep_ids.push_back(c);
-				else if (o == g.rank) send_ids[parent_owner].push_back(c);
-				else if (parent_owner == g.rank && o >= 0) recv_ids[o].push_back(c);
 			}
+			for (auto* mp : {&send_ids, &recv_ids})
+				for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
 		}
-		for (auto* mp : {&send_ids, &recv_ids})
-			for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
-		DX_LAP("sr.5b_loop");
-		host_sort_u64(keep_ids, false, s);
-		DX_LAP("sr.5c_sort");
+		DX_LAP("sr.5b_moving");
 	}
 	size_t bpc = 0;
 	for (auto& f : g.fields) bpc += f.elem;
@@ -591,7 +593,6 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (!F.empty()) {
 		// removed store order: the kept children ascending, then per source
 		// process (ascending rank) its children ascending
-		const DBuf<int32_t> ksl = keep_ids.empty() ? DBuf<int32_t>() : slots_of(g, keep_ids);
 		for (auto& f : g.fields) {
 			if (f.var) continue;
 			f.removed.alloc(n_rm * f.elem + 1);
@@ -668,7 +669,6 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 				ro2 += nr;
 			}
 			const DBuf<int32_t> osl = slots_of(g, out_all);
-			const DBuf<int32_t> ksl = slots_of(g, keep_ids);
 			for (auto& f : g.fields) {
 				if (!f.var) continue;
 				VarMsg K, X;

@@ -577,25 +577,32 @@ void ensure_face(Grid& g) {
 	DX_PHASE("face.build", s);
 	const size_t nl = g.n_local;
 	const DevMesh dm = g.dm();
-	DBuf<uint32_t> cnt;
+	// pass 0: per row (finer faces << 32 | entries) and per direction a hint;
+	// pass 1: CSR rows and the fixed-width table from the scan
+	DBuf<uint64_t> cnt, pos;
 	cnt.alloc(nl + 1);
+	pos.alloc(nl + 1);
 	g.face_ptr.alloc(nl + 1);
 	DBuf<int32_t> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
 	DBuf<int32_t> hint;  // per row and direction what pass 0 found (build_kernels.hip)
 	hint.alloc(6 * nl + 6);
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, err.p, 0, s, g.morton_slots, g.n_inner);
-	const size_t t = scan_exclusive_u32(cnt.p, g.face_ptr.p, nl, s);
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, nullptr, nullptr, nullptr, err.p, 0, s,
+	             g.morton_slots, g.n_inner);
+	const uint64_t tot = nl ? scan_exclusive_u64(cnt.p, pos.p, nl, s) : 0;
+	const size_t t = size_t(tot & 0xffffffffu);
+	g.n_fine_faces = size_t(tot >> 32);
 	g.face_ent.alloc(t + 1);
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, g.face_ptr.p, g.face_ent.p, err.p, 1, s);
+	g.face_ell.alloc(6 * nl + 6);
+	g.face_fine.alloc(4 * g.n_fine_faces + 4);
+	if (!nl) HIP_CHECK(hipMemsetAsync(g.face_ptr.p, 0, 4, s));
+	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, pos.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p,
+	             g.face_fine.p, err.p, 1, s);
 	int32_t herr = 0;
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
-	g.face_ell.alloc(6 * nl + 6);
-	g.face_fine.alloc(t / 4 + 4);
-	g.n_fine_faces = k_face_ell(g.face_ptr.p, g.face_ent.p, nl, g.face_ell.p, g.face_fine.p, s);
 	g.face_valid = true;
 }
 
@@ -618,23 +625,18 @@ void ensure_tiles(Grid& g) {
 	// records of the irregular tiles for the pipelined tile kernel
 	const size_t nt = g.n_tiles_inner + g.n_tiles_outer, ni = g.tcount[2] + g.tcount[3];
 	const auto ts = download(g.tstart.p, nt + 1, g.s_comp);
-	const auto ep = download(g.ext_ptr.p, nt + 1, g.s_comp);
-	const auto fb = download(g.fine_base.p, nt + 1, g.s_comp);
 	const auto li = download(g.tlists.p + g.tcount[0] + g.tcount[1], ni, g.s_comp);
 	std::vector<uint32_t> rec(8 * ni, 0u);
 	bool fits = true;
 	for (size_t i = 0; i < ni; i++) {
 		const uint32_t t = li[i];
-		// finer faces of tile t: up to the next tile's first one (fine_base is
-		// the exclusive scan at each tile's first slot)
-		const uint32_t fend = t + 1 < nt ? fb[t + 1] : uint32_t(g.n_fine_faces);
 		uint32_t* r = &rec[8 * i];
 		r[0] = ts[t];
 		r[1] = ts[t + 1] - ts[t];
-		r[2] = ep[t];
-		r[3] = ep[t + 1] - ep[t];
-		r[4] = fb[t];
-		r[5] = fend - fb[t];
+		r[2] = tb.ext_off[t];
+		r[3] = tb.ext_n[t];
+		r[4] = tb.fine_off[t];
+		r[5] = tb.fine_n[t];
 		if (r[3] > 1024u || r[5] > 512u || r[1] > 512u) fits = false;
 	}
 	g.tmeta.release();

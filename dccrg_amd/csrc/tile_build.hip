@@ -172,13 +172,14 @@ __global__ void tile_ell_kernel(TileGeom tg, uint32_t T, const uint32_t* __restr
 
 
 // ---------------------------------------------------------------------------
-// Per-tile build (tiles of at most kXT slots): one 512-thread block per tile
-// gathers its out-of-tile face entries in LDS, sorts them (bitonic) and drops
-// repeats - the tile's ascending ext list - then, in the second pass, writes
-// that list at the tile's ext offset and its cells' tile-local rows (steps
-// 1-5 above without the global sort).  Pass 0 only counts (distinct ext
-// cells, finer faces) per tile; the offsets are their scans.  A tile with
-// more than kXCap out-of-tile entries sets err bit 2 (then the global build).
+// Per-tile build (tiles of at most kXT slots), steps 1-5 without a global
+// sort: one 512-thread block per tile gathers its out-of-tile face entries in
+// LDS, sorts them (bitonic) and drops repeats - the tile's ascending ext list
+// - and writes its cells' tile-local rows.  A tile's ext list and finer faces
+// go to fixed places that need no scan: the ext list at the tile's first face
+// entry (it has at most as many cells as the tile has face entries), the
+// finer faces at a quarter of that (each has four entries).  A tile with more
+// than kXCap out-of-tile entries sets err bit 2 (then the global build).
 constexpr uint32_t kXT = 512;
 constexpr uint32_t kXCap = 8192;
 
@@ -203,12 +204,10 @@ __device__ __forceinline__ uint32_t block_scan512(uint32_t v, uint32_t* sh, uint
 	return base + incl - v;
 }
 
-template <int PASS>
 __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restrict__ tstart, uint32_t T,
                                                         const uint32_t* __restrict__ ptr, const int32_t* __restrict__ ent,
-                                                        uint32_t* __restrict__ ext_cnt, uint32_t* __restrict__ fine_cnt,
-                                                        const uint32_t* __restrict__ ext_ptr,
-                                                        const uint32_t* __restrict__ fine_base, uint32_t* __restrict__ ext,
+                                                        uint32_t* __restrict__ ext_n, uint32_t* __restrict__ fine_n,
+                                                        uint32_t* __restrict__ scr_off,
                                                         uint32_t* __restrict__ ext_pk, uint32_t* __restrict__ tell,
                                                         size_t pl, uint32_t* __restrict__ tfine, int* __restrict__ err) {
 	__shared__ uint32_t key[kXCap];
@@ -270,7 +269,7 @@ __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restric
 #pragma unroll
 	for (uint32_t j = 0; j < 16; j++)
 		if (v[j] != 0xffffffffu) key[o++] = v[j];
-	// finer faces of this thread's row
+	// finer faces of this thread's row, numbered in row order
 	uint32_t nf = 0;
 	for (uint32_t e = e0; e < e1;) {
 		const int d = ent[e] & 7;
@@ -281,14 +280,13 @@ __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restric
 	}
 	uint32_t F;
 	const uint32_t fb = block_scan512(nf, sh, F);
-	if (PASS == 0) {
-		if (tid == 0) {
-			ext_cnt[t] = U;
-			fine_cnt[t] = F;
-		}
-		return;
+	const uint32_t eoff = ptr[ts], foff = eoff / 4;
+	if (tid == 0) {
+		ext_n[t] = U;
+		fine_n[t] = F;
+		scr_off[t] = eoff;
 	}
-	// pass 1: tile-local rows (tile_ell_kernel's codes), axis bits ORed into
+	// tile-local rows (tile_ell_kernel's codes); the axis bits are ORed into
 	// the ext entries' top bits (slots < 2^29)
 	auto local = [&](uint32_t n) -> uint32_t {
 		if (n >= ts && n < te) return n - ts;
@@ -305,8 +303,7 @@ __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restric
 		return T + lo;
 	};
 	if (row) {
-		const uint32_t fbase = fine_base[t];
-		uint32_t fk = fbase + fb;
+		uint32_t fk = fb;
 		uint32_t code[6] = {0xffffu, 0xffffu, 0xffffu, 0xffffu, 0xffffu, 0xffffu};
 		for (uint32_t e = e0; e < e1;) {
 			const int d = ent[e] & 7;
@@ -322,9 +319,9 @@ __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restric
 					li[i] = local(uint32_t(ent[e + i] >> 3));
 					if (li[i] >= T) atomicOr(&key[li[i] - T], axbit);
 				}
-				tfine[2 * size_t(fk)] = li[0] | (li[1] << 16);
-				tfine[2 * size_t(fk) + 1] = li[2] | (li[3] << 16);
-				code[d] = 0x8000u | (fk - fbase);
+				tfine[2 * size_t(foff + fk)] = li[0] | (li[1] << 16);
+				tfine[2 * size_t(foff + fk) + 1] = li[2] | (li[3] << 16);
+				code[d] = 0x8000u | fk;
 				fk++;
 			}
 			e = k;
@@ -334,12 +331,20 @@ __global__ __launch_bounds__(512) void tile_ext_kernel(const uint32_t* __restric
 		tell[2 * pl + size_t(r)] = code[4] | (code[5] << 16);
 	}
 	__syncthreads();
-	const uint32_t eb = ext_ptr[t];
-	for (uint32_t i = tid; i < U; i += 512) {
-		const uint32_t x = key[i];
-		ext_pk[eb + i] = x;
-		ext[eb + i] = x & 0x1fffffffu;
-	}
+	for (uint32_t i = tid; i < U; i += 512) ext_pk[eoff + i] = key[i];
+}
+
+// the per-tile lists from their scratch places to dense arrays (off: per tile
+// the dense ext offset, then per tile the dense finer-face offset)
+__global__ void tile_compact_kernel(const uint32_t* __restrict__ ext_n, const uint32_t* __restrict__ fine_n,
+                                    const uint32_t* __restrict__ scr_off, const uint32_t* __restrict__ off,
+                                    uint32_t ntiles, const uint32_t* __restrict__ scr_ext,
+                                    const uint32_t* __restrict__ scr_fine, uint32_t* __restrict__ ext_pk,
+                                    uint32_t* __restrict__ tfine) {
+	const uint32_t t = blockIdx.x;
+	const uint32_t so = scr_off[t], eo = off[t], fo = off[ntiles + t], ne = ext_n[t], nf = 2 * fine_n[t];
+	for (uint32_t i = threadIdx.x; i < ne; i += blockDim.x) ext_pk[eo + i] = scr_ext[so + i];
+	for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) tfine[2 * size_t(fo) + i] = scr_fine[2 * size_t(so / 4) + i];
 }
 
 // ---------------------------------------------------------------------------
@@ -678,46 +683,54 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		tfine.alloc(2);
 		return out;
 	}
-	if (T <= kXT && ntiles) {
-		// per-tile build (tile_ext_kernel)
-		DBuf<uint32_t> ecnt, fcnt;
-		DBuf<int> err;
-		ecnt.alloc(ntiles + 1);
-		fcnt.alloc(ntiles + 1);
-		err.alloc(1);
-		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
-		tile_ext_kernel<0><<<unsigned(ntiles), 512, 0, s>>>(tstart.p, T, face_ptr, face_ent, ecnt.p, fcnt.p, nullptr,
-		                                                    nullptr, nullptr, nullptr, nullptr, 0, nullptr, err.p);
-		HIP_CHECK(hipGetLastError());
-		const size_t m = scan_exclusive_u32(ecnt.p, ext_ptr.p, ntiles, s);
-		out.n_fine = scan_exclusive_u32(fcnt.p, fine_base.p, ntiles, s);
-		int herr = 0;
-		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-		std::vector<uint32_t> hptr = download(ext_ptr.p, ntiles + 1, s);
-		if (herr == 0) {
-			out.total_ext = m;
-			for (size_t t = 0; t < ntiles; t++) out.max_ext = std::max<size_t>(out.max_ext, hptr[t + 1] - hptr[t]);
-			DX_REQUIRE(size_t(T) + out.max_ext < 0x8000u, "tile too large for 16-bit local indices");
-			DX_LAP("tb.3_ext_count");
-			ext.alloc(m + 1);
-			ext_pk.alloc(m + 1);
-			tfine.alloc(2 * out.n_fine + 2);
-			tile_ext_kernel<1><<<unsigned(ntiles), 512, 0, s>>>(tstart.p, T, face_ptr, face_ent, nullptr, nullptr,
-			                                                    ext_ptr.p, fine_base.p, ext.p, ext_pk.p, tell.p,
-			                                                    n_local + 1, tfine.p, err.p);
-			HIP_CHECK(hipGetLastError());
-			HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipStreamSynchronize(s));
-			DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
-			DX_LAP("tb.4_ext_rows");
-			return out;
-		}
-		out.n_fine = 0;  // a tile beyond kXCap out-of-tile entries: the global build
-	}
 	uint32_t n_ent = 0;
 	HIP_CHECK(hipMemcpyAsync(&n_ent, face_ptr + n_local, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
-
+	if (T <= kXT && ntiles) {
+		// per-tile build (tile_ext_kernel): each tile's lists at scratch places
+		// first, then packed densely
+		DBuf<uint32_t> en, fn, so, off, sext, sfine;
+		DBuf<int> err;
+		en.alloc(ntiles + 1);
+		fn.alloc(ntiles + 1);
+		so.alloc(ntiles + 1);
+		err.alloc(1);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
+		sext.alloc(size_t(n_ent) + 1);
+		sfine.alloc(2 * (size_t(n_ent) / 4 + 2));
+		tile_ext_kernel<<<unsigned(ntiles), 512, 0, s>>>(tstart.p, T, face_ptr, face_ent, en.p, fn.p, so.p, sext.p, tell.p,
+		                                                 n_local + 1, sfine.p, err.p);
+		HIP_CHECK(hipGetLastError());
+		int herr = 0;
+		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
+		out.ext_n = download(en.p, ntiles, s);
+		out.fine_n = download(fn.p, ntiles, s);
+		if (herr == 0) {
+			std::vector<uint32_t> ho(2 * ntiles);
+			out.ext_off.resize(ntiles);
+			out.fine_off.resize(ntiles);
+			for (size_t t = 0; t < ntiles; t++) {
+				out.ext_off[t] = ho[t] = uint32_t(out.total_ext);
+				out.fine_off[t] = ho[ntiles + t] = uint32_t(out.n_fine);
+				out.total_ext += out.ext_n[t];
+				out.n_fine += out.fine_n[t];
+				out.max_ext = std::max<size_t>(out.max_ext, out.ext_n[t]);
+			}
+			DX_REQUIRE(size_t(T) + out.max_ext < 0x8000u, "tile too large for 16-bit local indices");
+			upload(off, ho, s);
+			ext_pk.alloc(out.total_ext + 1);
+			tfine.alloc(2 * out.n_fine + 2);
+			tile_compact_kernel<<<unsigned(ntiles), 256, 0, s>>>(en.p, fn.p, so.p, off.p, uint32_t(ntiles), sext.p, sfine.p,
+			                                                    ext_pk.p, tfine.p);
+			HIP_CHECK(hipGetLastError());
+			HIP_CHECK(hipStreamSynchronize(s));
+			ext.alloc(1);
+			DX_LAP("tb.3_ext_rows");
+			return out;
+		}
+		DX_REQUIRE((herr & 2) != 0, "internal error: face neighbor missing from its tile's external list");
+		// a tile beyond kXCap out-of-tile entries: the global build
+	}
 	// 1-3: per-tile distinct external neighbors: the out-of-tile entries'
 	// keys compacted first (about an eighth of the face entries on config 3),
 	// then sorted on the bits a (tile, slot) key uses
@@ -785,6 +798,17 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
+	{
+		const std::vector<uint32_t> fbh = download(fine_base.p, ntiles, s);
+		out.ext_off.assign(hptr.begin(), hptr.begin() + ntiles);
+		out.ext_n.resize(ntiles);
+		out.fine_off = fbh;
+		out.fine_n.resize(ntiles);
+		for (size_t t = 0; t < ntiles; t++) {
+			out.ext_n[t] = hptr[t + 1] - hptr[t];
+			out.fine_n[t] = uint32_t((t + 1 < ntiles ? fbh[t + 1] : out.n_fine) - fbh[t]);
+		}
+	}
 	DX_LAP("tb.6_tile_rows");
 	return out;
 }

@@ -2181,12 +2181,16 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 // at the end as the reference's rule loop leaves it (163).  Collected lists
 // stay in the kernels' per-cell masks; only the cells other processes read
 // (the outer run) write theirs into list_field for the halo, then clear them.
-static void check_gol_err(Grid& g, DBuf<int>& err) {
-	int h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
+// the whole turn's error words: err[0] the collect, err[2] the spread (in
+// the order the reference would have aborted)
+static void check_gol_turn_err(Grid& g, DBuf<int>& err) {
+	int h[3] = {0, 0, 0};
+	HIP_CHECK(hipMemcpyAsync(h, err.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
-	DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
-	DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+	for (int k : {0, 2}) {
+		DX_REQUIRE(!(h[k] & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+		DX_REQUIRE(!(h[k] & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+	}
 }
 
 int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
@@ -2199,9 +2203,11 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		const size_t nl = g.n_local;
 		if (!nl && g.size == 1) return 0;
 		ensure_csr(g);
+		// err[0] the collect, err[1] the gate of the exact collect, err[2] the
+		// spread: one host read per turn, at its end
 		DBuf<int> err;
-		err.alloc(1);
-		HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
+		err.alloc(3);
+		HIP_CHECK(hipMemsetAsync(err.p, 0, 3 * sizeof(int), g.s_comp));
 		if (!g.gola.valid)
 			k_gol_amr_tables(g.m, g.slot_ids.p, g.n_slots, g.n_local, g.hood_len, g.nof_ptr.p, g.nof_slot.p, g.gola,
 			                 g.s_comp);
@@ -2211,32 +2217,29 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		const bool lean = g.gola.mask_path;
 		if (lean && !ls.local_zero && g.n_inner) HIP_CHECK(hipMemsetAsync(L, 0, g.n_inner * 64, g.s_comp));
 		k_time_begin(g);
-		bool exact = true;
 		if (lean && g.gola.geo) {
-			// the geometric collect; the exact per-entry one when a family's
-			// leaves disagree or a reached level-0 cell is unknown (the
-			// reference's abort conditions then depend on the entry order)
+			// the geometric collect; the exact per-entry one (gated on the
+			// device) when a family's leaves disagree or a reached level-0 cell
+			// is unknown - the reference's abort conditions then depend on the
+			// entry order
 			k_gol_amr_geo(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, nl, nl + g.n_recv, L, g.n_inner, err.p,
 			              g.s_comp);
-			int h = 0;
-			HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
-			HIP_CHECK(hipStreamSynchronize(g.s_comp));
-			exact = (h & (4 | 8)) != 0;
-			if (exact) HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), g.s_comp));
-		}
-		if (exact)
+			k_gol_gate(err.p, g.s_comp);
+			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp, g.n_inner,
+			          err.p + 1);
+		} else {
 			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp,
 			          lean ? g.n_inner : 0);
+		}
 		k_time_end(g);
-		check_gol_err(g, err);
 		halo_start(g);  // update_copies_of_remote_neighbors (solve.hpp:111)
 		halo_wait(g);
 		k_time_begin(g);
-		k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp);
+		k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp);
 		k_time_end(g);
 		const size_t c0 = lean ? g.n_inner : 0;
 		if (nl > c0) HIP_CHECK(hipMemsetAsync(L + c0 * 8, 0, (nl - c0) * 64, g.s_comp));
-		check_gol_err(g, err);
+		check_gol_turn_err(g, err);
 		ls.local_zero = true;
 		return 0;
 	});

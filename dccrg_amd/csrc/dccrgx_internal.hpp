@@ -778,7 +778,9 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t* state, size_t n_local, size_t n_state,
                    uint64_t* lst, size_t list_from, int* err, hipStream_t s);
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
-               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0);
+               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0,
+               const int* gate = nullptr);
+void k_gol_gate(int* err, hipStream_t s);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots

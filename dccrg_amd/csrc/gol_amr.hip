@@ -310,7 +310,7 @@ __device__ __forceinline__ uint32_t mask_entry_byte(uint32_t q, const uint32_t* 
 __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
     const uint32_t* __restrict__ state, const uint32_t* __restrict__ ent, const uint32_t* __restrict__ ptr,
     const uint32_t* __restrict__ l0c, L0Geom G, uint64_t* __restrict__ lst, uint32_t* __restrict__ mask_out, size_t s0,
-    size_t s1, size_t w0, int* __restrict__ err) {
+    size_t s1, size_t w0, int* __restrict__ err, const int* __restrict__ gate) {
 	// entry bytes staged per block; after the walks the same 16 KB hold the
 	// block's lists (256 rows x 64 B) for a coalesced store
 	// (the lists at a row stride of 80 B: five 16-B slots, conflict-free
@@ -322,6 +322,7 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	const uint32_t tid = threadIdx.x;
 	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
 	if (r0 >= s1) return;  // block-uniform
+	if (gate && (*gate & (4 | 8)) == 0) return;  // the geometric collect held (gol_gate_kernel)
 	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
 	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
 	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
@@ -902,14 +903,29 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
 	}
 }
 
+// err[1] = err[0]; when the geometric collect met a disagreeing family or an
+// unknown reached cell (bits 4 | 8) err[0] is cleared for the exact collect,
+// which runs only then (its blocks read err[1])
+__global__ void gol_gate_kernel(int* err) {
+	const int v = err[0];
+	err[1] = v;
+	if (v & (4 | 8)) err[0] = 0;
+}
+
+void k_gol_gate(int* err, hipStream_t s) {
+	gol_gate_kernel<<<1, 1, 0, s>>>(err);
+	HIP_CHECK(hipGetLastError());
+}
+
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
-               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from) {
+               const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from, const int* gate) {
 	if (s1 <= s0) return;
+	DX_REQUIRE(!gate || (T.mask_path && phase == 0), "internal error: gated refined-game launch off the mask path");
 	if (T.mask_path) {
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
 			gol_amr_collect_mask_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
-			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, list_from < s0 ? s0 : list_from, err);
+			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, list_from < s0 ? s0 : list_from, err, gate);
 		} else {
 			if (T.n_lvl0)
 				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,

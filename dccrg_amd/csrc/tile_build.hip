@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 
@@ -829,6 +830,11 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 	classify_tiles_kernel<<<unsigned(nt), 512, 0, s>>>(m, tstart, slot_ids, face_ell, treg.p, tnb.p);
 	HIP_CHECK(hipGetLastError());
 	const std::vector<uint32_t> h = download(treg.p, nt, s);
+	if (std::getenv("DCCRGX_TILE_REASONS")) {  // diagnostics: why tiles are not regular
+		std::map<uint32_t, size_t> hist;
+		for (uint32_t v : h) hist[v]++;
+		for (auto& kv : hist) std::fprintf(stderr, "[tiles] reason 0x%x: %zu tiles\n", kv.first, kv.second);
+	}
 	// layout: [regular inner | regular outer | irregular inner | irregular outer]
 	std::vector<uint32_t> reg[2], irr[2];
 	for (size_t t = 0; t < nt; t++) {

@@ -602,6 +602,15 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
 		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
 	};
+	// ext = slot | axis mask << 29: density and lengths, and only the
+	// velocity components along the axes its faces cross
+	auto load5 = [&](uint32_t q, double (&v)[7]) {
+		const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
+		v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+		v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
+		v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
+		v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
+	};
 	const uint32_t lane = tid & 63u;
 	struct GM {
 		uint32_t ts, n, e0, ne, fb, nf;
@@ -621,15 +630,6 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			row[1] = __builtin_nontemporal_load(tell + tplane + (ts + tid));
 			row[2] = __builtin_nontemporal_load(tell + 2 * tplane + (ts + tid));
 		}
-		// ext = slot | axis mask << 29: density and lengths, and only the
-		// velocity components along the axes its faces cross
-		auto load5 = [&](uint32_t q, double (&v)[7]) {
-			const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
-			v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
-			v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
-			v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
-			v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
-		};
 		if (tid < ne) load5(__builtin_nontemporal_load(ext + e0 + tid), xa);
 		if (tid + T < ne) load5(__builtin_nontemporal_load(ext + e0 + tid + T), xb);
 		if (tid < nf) {
@@ -739,9 +739,17 @@ __global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
 	const double* const vy = P.p[5];
 	const double* const vz = P.p[6];
 	// the tile in flight: own fields (both kinds), regular out-of-tile rows
-	// in xa[0..3] or general ext cells in xa / xb, face codes, finer pairs
-	double c[7], xa[7], xb[7];
+	// in xa[0..3] or general ext cells in xa (the rare ones beyond 512 are
+	// loaded at staging), face codes, finer pairs
+	double c[7], xa[7];
 	uint32_t row[3], fq[2];
+	auto load5 = [&](uint32_t q, double (&vv)[7]) {
+		const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
+		vv[0] = ldo(rho, o); vv[4] = ldo(lx, o); vv[5] = ldo(ly, o); vv[6] = ldo(lz, o);
+		vv[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
+		vv[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
+		vv[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
+	};
 	auto load7 = [&](uint32_t slot, double (&v)[7]) {
 		const uint32_t o = slot << 3;
 		v[0] = ldo(rho, o); v[1] = ldo(vx, o); v[2] = ldo(vy, o); v[3] = ldo(vz, o);
@@ -840,15 +848,7 @@ __global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
 			row[1] = __builtin_nontemporal_load(tell + tplane + (ts + tid));
 			row[2] = __builtin_nontemporal_load(tell + 2 * tplane + (ts + tid));
 		}
-		auto load5 = [&](uint32_t q, double (&vv)[7]) {
-			const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
-			vv[0] = ldo(rho, o); vv[4] = ldo(lx, o); vv[5] = ldo(ly, o); vv[6] = ldo(lz, o);
-			vv[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
-			vv[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
-			vv[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
-		};
 		if (tid < ne) load5(__builtin_nontemporal_load(ext + e0 + tid), xa);
-		if (tid + T < ne) load5(__builtin_nontemporal_load(ext + e0 + tid + T), xb);
 		if (tid < nf) {
 			typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 			const u2v q = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(tfine) + (fb + tid));
@@ -865,9 +865,12 @@ __global__ __launch_bounds__(512, MINW) void advection_fused_kernel(
 		if (tid < ne)
 #pragma unroll
 			for (int k = 0; k < 7; k++) shd[k * W + T + tid] = xa[k];
-		if (tid + T < ne)
+		if (tid + T < ne) {  // ext cells beyond the first T: loaded here (rare)
+			double xb[7];
+			load5(__builtin_nontemporal_load(ext + word_of(v, 2) + tid + T), xb);
 #pragma unroll
 			for (int k = 0; k < 7; k++) shd[k * W + 2 * T + tid] = xb[k];
+		}
 		if (tid < nf) {
 			shf[2 * tid] = fq[0];
 			shf[2 * tid + 1] = fq[1];

@@ -433,22 +433,42 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 		int lvl;
 		const uint64_t id = slot_ids[r];
 		cell_coords(m, id, c, lvl);
-		const int sh = 3 * (m.R - lvl);
-		const uint64_t len = uint64_t(1) << (m.R - lvl);
-		const int64_t key = int64_t(morton3(c) >> sh);
-		const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
 		uint32_t k = 0, kf = 0;  // entries, finer faces
+		// the six predictions first, their six row loads in flight together
+		int32_t h[6];
+		uint64_t want[6], got[6];
+		bool probe[6];
+		if (morton) {
+			const int sh = 3 * (m.R - lvl);
+			const uint64_t len = uint64_t(1) << (m.R - lvl);
+			const int64_t key = int64_t(morton3(c) >> sh);
+			const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
+#pragma unroll
+			for (int dir = 0; dir < 6; dir++) {
+				uint64_t p[3];
+				h[dir] = -1;
+				want[dir] = ~uint64_t(0);
+				probe[dir] = face_probe(m, c, lvl, dir, p);
+				if (!probe[dir]) continue;
+				for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
+				const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
+				if (q >= lo && q < hi) {
+					h[dir] = int32_t(q);
+					want[dir] = map_from_indices(m, p[0], p[1], p[2], lvl);
+				}
+			}
+#pragma unroll
+			for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
+		}
+#pragma unroll
 		for (int dir = 0; dir < 6; dir++) {
 			if (morton) {
-				uint64_t p[3];
-				if (!face_probe(m, c, lvl, dir, p)) {
+				if (!probe[dir]) {
 					hint[6 * r + dir] = -1;
 					continue;
 				}
-				for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
-				const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
-				if (q >= lo && q < hi && slot_ids[q] == map_from_indices(m, p[0], p[1], p[2], lvl)) {
-					hint[6 * r + dir] = int32_t(q);
+				if (h[dir] >= 0 && got[dir] == want[dir]) {
+					hint[6 * r + dir] = h[dir];
 					k += 1;
 					continue;
 				}
@@ -648,15 +668,11 @@ __global__ void cells_under_kernel(MapCtx m, const uint64_t* ids, size_t n, cons
 __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hood_to, int nh, DevMesh M, int rank,
                                const uint64_t* req, size_t n, uint64_t* out, unsigned long long* counter,
                                unsigned long long cap, int finer) {
-	// one thread per (request, candidate): the nh neighbors_of items, then
-	// the 10 nh neighbors_to candidates
 	const DevExists ex{M};
-	const size_t per = size_t(11) * size_t(nh);
-	for (size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x; t < n * per; t += size_t(gridDim.x) * blockDim.x) {
-		const size_t w = t / per;
-		const int k = int(t - w * per);
+	const size_t waves = size_t(gridDim.x) * (blockDim.x / WAVE);
+	for (size_t w = blockIdx.x * size_t(blockDim.x / WAVE) + threadIdx.x / WAVE; w < n; w += waves) {
 		const uint64_t r = req[w];
-		if (dm_owner(M, r) != rank) continue;
+		if (dm_owner(M, r) != rank) continue;  // wave-uniform
 		uint64_t c[3];
 		int lvl;
 		cell_coords(m, r, c, lvl);
@@ -667,13 +683,12 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 			const unsigned long long pos = atomicAdd(counter, 1ull);
 			if (pos < cap) out[pos] = q;
 		};
-		if (k < nh) {
+		for (int k = lane_id(); k < nh; k += WAVE) {
 			ItemOut o;
 			nof_item(m, c, lvl, hood + 3 * k, ex, o);
 			for (int i = 0; i < o.n; i++) emit(o.id[i]);
-		} else {
-			emit(nto_candidate(m, c, lvl, hood_to, nh, k - nh, ex));
 		}
+		for (int k = lane_id(); k < 10 * nh; k += WAVE) emit(nto_candidate(m, c, lvl, hood_to, nh, k, ex));
 	}
 }
 
@@ -1201,8 +1216,8 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 		out.alloc(size_t(cap));
 		DBuf<unsigned long long> ctr;
 		zero_counter(ctr, s);
-		induced_kernel<<<grid_for(req.size() * size_t(11) * size_t(nh), 256), 256, 0, s>>>(
-		    m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p, ctr.p, cap, finer ? 1 : 0);
+		induced_kernel<<<grid_for(req.size(), 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, dreq.p, req.size(), out.p,
+		                                                       ctr.p, cap, finer ? 1 : 0);
 		HIP_CHECK(hipGetLastError());
 		const size_t k = read_counter(ctr, s);
 		if (k > cap) {

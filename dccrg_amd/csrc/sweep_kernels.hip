@@ -1034,19 +1034,33 @@ __global__ void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restr
                                     uint64_t* __restrict__ unref, uint32_t* __restrict__ part,
                                     unsigned long long* __restrict__ cnt) {
 	// each lane a run of kRun slots: classify them, reserve its positions in
-	// the three lists with one atomic per wave and list, then write
+	// the three lists with one atomic per wave and list, then write.  The
+	// parents of slots s0 - 1 .. s0 + kRun + 6 (a family run starting at the
+	// lane's last slot reaches 7 further) are computed once each.
 	constexpr int kRun = 8;
+	constexpr int kWin = kRun + 8;  // window index w <-> slot s0 - 1 + w
 	const size_t s0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kRun;
+	uint64_t par[kWin];  // parent id, or ~0 for a level-0 cell / outside [0, n)
+#pragma unroll
+	for (int w = 0; w < kWin; w++) {
+		const size_t s = s0 + size_t(w) - 1;  // wraps to a huge value for s0 = 0, w = 0
+		par[w] = ~uint64_t(0);
+		if (s < n && (w > 0 || s0 > 0)) {
+			const uint64_t id = ids[s];
+			if (map_level(m, id) > 0) par[w] = map_parent(m, id);
+		}
+	}
 	uint8_t what[kRun];  // bit 0 refine, 1 partial run head, 2 kept family head, 3 unrefine family head
 	uint8_t runk[kRun];
 	unsigned cr = 0, cp = 0, ck = 0, cu = 0;
+#pragma unroll
 	for (int j = 0; j < kRun; j++) {
 		what[j] = 0;
 		runk[j] = 0;
 		const size_t s = s0 + j;
 		if (s >= n) continue;
-		const uint64_t id = ids[s];
-		const int lvl = map_level(m, id);
+		const uint64_t p = par[j + 1];
+		const int lvl = p == ~uint64_t(0) ? 0 : map_level(m, p) + 1;
 		if (band[s] == 2 && lvl < int(m.R)) {
 			what[j] |= 1;
 			cr++;
@@ -1054,14 +1068,14 @@ __global__ void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restr
 		if (lvl == 0) continue;
 		// run head of a family: the first slot of a run of consecutive slots
 		// with one parent
-		const uint64_t p = map_parent(m, id);
-		if (s > 0 && map_level(m, ids[s - 1]) > 0 && map_parent(m, ids[s - 1]) == p) continue;
+		if (par[j] == p) continue;
 		uint32_t k = 1;
 		bool keep = band[s] >= 1;
-		while (k < 8 && s + k < n) {
-			const uint64_t c = ids[s + k];
-			if (map_level(m, c) == 0 || map_parent(m, c) != p) break;
-			keep = keep || band[s + k] >= 1;
+#pragma unroll
+		for (int q = 1; q < 8; q++) {
+			if (k != uint32_t(q)) break;
+			if (par[j + 1 + q] != p) break;
+			keep = keep || band[s + q] >= 1;
 			k++;
 		}
 		runk[j] = uint8_t(k);

@@ -729,6 +729,28 @@ __global__ void unrefine_check_kernel(MapCtx m, const int32_t* hood, int nh, Dev
 	}
 }
 
+// override_unrefines' candidates (9796-9898): the parents of the requested
+// cells (level-0 cells have none: ~0, dropped by the sort)
+__global__ void request_parents_kernel(MapCtx m, const uint64_t* req, size_t n, uint64_t* par) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t c = req[i];
+		par[i] = map_level(m, c) > 0 ? map_parent(m, c) : ~uint64_t(0);
+	}
+}
+
+// a family is blocked when one of its children is being refined or is
+// marked dont_unrefine
+__global__ void family_blocked_kernel(MapCtx m, const uint64_t* cand, size_t n, const uint64_t* S, size_t nS,
+                                      const uint64_t* DU, size_t nDU, uint32_t* ok) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t ch[8];
+		map_all_children(m, cand[i], ch);
+		bool blocked = false;
+		for (int k = 0; k < 8; k++) blocked = blocked || sorted_has(S, nS, ch[k]) || sorted_has(DU, nDU, ch[k]);
+		if (blocked) ok[i] = 0;
+	}
+}
+
 // execute_refines (10104-10554): children replace refined leaves and inherit
 // the owner (10228-10237); the children of an unrefined parent are replaced
 // by the parent, owned by the owner of its first child (10298)
@@ -1229,23 +1251,40 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 	}
 }
 
-std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
-                                      const std::vector<uint64_t>& parents, const std::vector<uint64_t>& S,
-                                      hipStream_t s) {
-	if (parents.empty()) return {};
-	DBuf<uint64_t> dp, dS;
-	upload(dp, parents, s);
+std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
+                                          const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
+                                          const std::vector<uint64_t>& DU, hipStream_t s) {
+	if (req.empty()) return {};
+	DBuf<uint64_t> dr, par, dS, dDU;
+	upload(dr, req, s);
 	upload(dS, S, s);
-	DBuf<uint32_t> ok;
-	ok.alloc(parents.size());
-	k_fill_i32(reinterpret_cast<int32_t*>(ok.p), parents.size(), 1, s);
-	if (nh > 0)
-		unrefine_check_kernel<<<grid_for(parents.size() * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, dp.p,
-		                                                                                 parents.size(), dS.p, S.size(),
-		                                                                                 ok.p);
+	upload(dDU, DU, s);
+	par.alloc(req.size() + 1);
+	request_parents_kernel<<<grid_for(req.size(), 256), 256, 0, s>>>(m, dr.p, req.size(), par.p);
 	HIP_CHECK(hipGetLastError());
-	const std::vector<uint32_t> h = download(ok.p, parents.size(), s);
-	return std::vector<uint8_t>(h.begin(), h.end());
+	size_t n = sort_unique_u64(par.p, req.size(), s);
+	{
+		// the level-0 requests' marker sorts last
+		uint64_t last = 0;
+		if (n) HIP_CHECK(hipMemcpyAsync(&last, par.p + n - 1, 8, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		if (n && last == ~uint64_t(0)) n--;
+	}
+	if (!n) return {};
+	DBuf<uint32_t> ok;
+	ok.alloc(n);
+	k_fill_i32(reinterpret_cast<int32_t*>(ok.p), n, 1, s);
+	family_blocked_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, par.p, n, dS.p, S.size(), dDU.p, DU.size(), ok.p);
+	if (nh > 0)
+		unrefine_check_kernel<<<grid_for(n * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, par.p, n, dS.p, S.size(),
+		                                                                    ok.p);
+	HIP_CHECK(hipGetLastError());
+	const std::vector<uint64_t> cand = download(par.p, n, s);
+	const std::vector<uint32_t> h = download(ok.p, n, s);
+	std::vector<uint64_t> out;
+	for (size_t i = 0; i < n; i++)
+		if (h[i]) out.push_back(cand[i]);
+	return out;
 }
 
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,

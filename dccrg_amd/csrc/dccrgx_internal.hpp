@@ -661,11 +661,14 @@ std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size
 std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
                                         const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s,
                                         bool finer = false);
-// override_unrefines (9796-9898) for the families under `parents`: 1 where
-// the family may merge given the final refine set S (sorted)
-std::vector<uint8_t> k_unrefine_check(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
-                                      const std::vector<uint64_t>& parents, const std::vector<uint64_t>& S,
-                                      hipStream_t s);
+// override_unrefines (9796-9898) on the device: the requested cells'
+// parents (sorted, unique) whose families may merge given the final refine
+// set S (sorted): none of the children refined or marked dont_unrefine (DU,
+// sorted), and no finer leaf or refined same-level leaf in the parent's
+// neighborhood (unrefine_check_kernel)
+std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
+                                          const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
+                                          const std::vector<uint64_t>& DU, hipStream_t s);
 // known list after refining the sorted set S and merging the families under
 // the sorted parents F: every known leaf in S is replaced by its 8 children
 // (same owner), the children of a parent in F by the parent (owner of the

@@ -491,31 +491,17 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	if (!S.empty()) close_set(g, S, false);
 	DX_LAP("sr.2_induce_refines");
 
-	// unrefines: one family per requested parent
-	std::vector<uint64_t> req_par;
-	for (uint64_t c : g.unrefine_requests) req_par.push_back(map_parent(g.m, c));
-	for (uint64_t c : g.unrefine_bulk) req_par.push_back(map_parent(g.m, c));
-	req_par = sorted_unique(g, req_par);
-	DX_LAP("sr.3a_parents");
+	// unrefines: one family per requested parent, unless one of its children
+	// is refined or marked dont_unrefine, or its neighborhood forbids it (on
+	// the device)
+	std::vector<uint64_t> req(g.unrefine_requests.begin(), g.unrefine_requests.end());
+	req.insert(req.end(), g.unrefine_bulk.begin(), g.unrefine_bulk.end());
 	g.unrefine_requests.clear();
 	g.unrefine_bulk.clear();
 	const std::vector<uint64_t> DU = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_unrefine_cells))));
 	g.dont_unrefine_cells.clear();
-	// a family is a candidate unless one of its children is refined or marked
-	// dont_unrefine: the requested parents minus the parents of S and of DU
-	std::vector<uint64_t> blocked;
-	blocked.reserve(S.size() + DU.size());
-	for (const std::vector<uint64_t>* v : {static_cast<const std::vector<uint64_t>*>(&S), &DU})
-		for (uint64_t c : *v)
-			if (map_level(g.m, c) > 0) blocked.push_back(map_parent(g.m, c));
-	blocked = sorted_unique(g, std::move(blocked));
-	std::vector<uint64_t> cand;
-	std::set_difference(req_par.begin(), req_par.end(), blocked.begin(), blocked.end(), std::back_inserter(cand));
-	DX_LAP("sr.3b_candidates");
-	const std::vector<uint8_t> ok = k_unrefine_check(g.m, g.d_hood.p, nh, g.dm(), cand, S, s);
-	std::vector<uint64_t> fmine;
-	for (size_t i = 0; i < cand.size(); i++)
-		if (ok[i]) fmine.push_back(cand[i]);
+	DX_LAP("sr.3a_requests");
+	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s);
 	const std::vector<uint64_t> F = union_sorted(g, comm_allgather_u64(g, fmine));
 	DX_LAP("sr.3_override_unrefines");
 	if (S.empty() && F.empty()) return {};

@@ -460,15 +460,16 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 #pragma unroll
 			for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
 		}
+		int32_t o6[6];
 #pragma unroll
 		for (int dir = 0; dir < 6; dir++) {
 			if (morton) {
 				if (!probe[dir]) {
-					hint[6 * r + dir] = -1;
+					o6[dir] = -1;
 					continue;
 				}
 				if (h[dir] >= 0 && got[dir] == want[dir]) {
-					hint[6 * r + dir] = h[dir];
+					o6[dir] = h[dir];
 					k += 1;
 					continue;
 				}
@@ -476,10 +477,14 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 			uint64_t out[4];
 			const int nf = face_dir(m, c, lvl, dir, ex, out);
 			// a single neighbor was the last cell found (face_dir returns on it)
-			hint[6 * r + dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -3));
+			o6[dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -3));
 			k += uint32_t(nf);
 			kf += nf == 4 ? 1u : 0u;
 		}
+		typedef int i2v __attribute__((ext_vector_type(2)));
+		i2v* hv = reinterpret_cast<i2v*>(hint + 6 * r);
+#pragma unroll
+		for (int j = 0; j < 3; j++) hv[j] = i2v{o6[2 * j], o6[2 * j + 1]};
 		cnt[r] = (uint64_t(kf) << 32) | k;
 	}
 }
@@ -493,21 +498,32 @@ __global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, 
                                  const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
                                  int32_t* err) {
 	const DevExists ex{M};
+	typedef int i2v __attribute__((ext_vector_type(2)));
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t pr = pos[r];
 		uint32_t k = uint32_t(pr), f = uint32_t(pr >> 32);
 		ptr[r] = k;
 		if (r + 1 == nrows) ptr[nrows] = uint32_t(pos[nrows]);
+		// the row's hints and table entries as three 8-B words
+		int32_t h6[6], e6[6];
+		const i2v* hv = reinterpret_cast<const i2v*>(hint + 6 * r);
+#pragma unroll
+		for (int j = 0; j < 3; j++) {
+			const i2v v = hv[j];
+			h6[2 * j] = v.x;
+			h6[2 * j + 1] = v.y;
+		}
+#pragma unroll
 		for (int dir = 0; dir < 6; dir++) {
-			const int32_t h = hint[6 * r + dir];
+			const int32_t h = h6[dir];
 			if (h == -1) {
-				ell[6 * r + dir] = -1;
+				e6[dir] = -1;
 				continue;
 			}
 			if (h != -2) {
 				if (h == -3) atomicExch(err, 1);
 				ent[k++] = (h == -3 ? -1 : h) * 8 + dir;
-				ell[6 * r + dir] = h == -3 ? -1 : h;
+				e6[dir] = h == -3 ? -1 : h;
 				continue;
 			}
 			uint64_t c[3];
@@ -521,9 +537,12 @@ __global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, 
 				ent[k++] = sl * 8 + dir;
 				fine[4 * size_t(f) + i] = sl;
 			}
-			ell[6 * r + dir] = -2 - int32_t(f);
+			e6[dir] = -2 - int32_t(f);
 			f++;
 		}
+		i2v* ev = reinterpret_cast<i2v*>(ell + 6 * r);
+#pragma unroll
+		for (int j = 0; j < 3; j++) ev[j] = i2v{e6[2 * j], e6[2 * j + 1]};
 	}
 }
 

@@ -2181,15 +2181,17 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 // at the end as the reference's rule loop leaves it (163).  Collected lists
 // stay in the kernels' per-cell masks; only the cells other processes read
 // (the outer run) write theirs into list_field for the halo, then clear them.
-// the whole turn's error words: err[0] the collect, err[2] the spread (in
-// the order the reference would have aborted)
+// the whole turn's error words: err[0] the collect (the geometric one's,
+// replaced by err[1], the exact one's, when that had to run: err[0] bits 4 |
+// 8), err[2] the spread - in the order the reference would have aborted
 static void check_gol_turn_err(Grid& g, DBuf<int>& err) {
 	int h[3] = {0, 0, 0};
 	HIP_CHECK(hipMemcpyAsync(h, err.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
-	for (int k : {0, 2}) {
-		DX_REQUIRE(!(h[k] & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
-		DX_REQUIRE(!(h[k] & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+	const int collect = (h[0] & (4 | 8)) ? h[1] : h[0];
+	for (int e : {collect, h[2]}) {
+		DX_REQUIRE(!(e & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+		DX_REQUIRE(!(e & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
 	}
 }
 
@@ -2203,8 +2205,8 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		const size_t nl = g.n_local;
 		if (!nl && g.size == 1) return 0;
 		ensure_csr(g);
-		// err[0] the collect, err[1] the gate of the exact collect, err[2] the
-		// spread: one host read per turn, at its end
+		// err[0] the (geometric) collect, err[1] the exact collect, err[2]
+		// the spread: one host read per turn, at its end
 		DBuf<int> err;
 		err.alloc(3);
 		HIP_CHECK(hipMemsetAsync(err.p, 0, 3 * sizeof(int), g.s_comp));
@@ -2224,9 +2226,8 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 			// entry order
 			k_gol_amr_geo(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, nl, nl + g.n_recv, L, g.n_inner, err.p,
 			              g.s_comp);
-			k_gol_gate(err.p, g.s_comp);
-			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp, g.n_inner,
-			          err.p + 1);
+			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 1, g.s_comp, g.n_inner,
+			          err.p);
 		} else {
 			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p, g.s_comp,
 			          lean ? g.n_inner : 0);

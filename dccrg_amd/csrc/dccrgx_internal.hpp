@@ -399,6 +399,7 @@ struct GolAmrTables {
 	bool geo = false;
 	DBuf<uint8_t> corner, l0tab;
 	uint32_t box0[3] = {0, 0, 0}, boxn[3] = {0, 0, 0};
+	uint32_t geo_lb[3] = {0, 0, 0}, geo_bstride[3] = {1, 1, 1}, geo_istride[3] = {1, 1, 1};  // table blocks
 	int per[3] = {0, 0, 0};
 };
 
@@ -783,7 +784,6 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0,
                const int* gate = nullptr);
-void k_gol_gate(int* err, hipStream_t s);
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots

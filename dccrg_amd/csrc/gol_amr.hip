@@ -320,129 +320,136 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 	static_assert(cap >= 8192, "LDS too small for the entry bytes");
 	__shared__ uint32_t sp32[cap / 4];
 	const uint32_t tid = threadIdx.x;
-	const size_t r0 = s0 + size_t(xcd_block()) * kCollectRows;
-	if (r0 >= s1) return;  // block-uniform
-	if (gate && (*gate & (4 | 8)) == 0) return;  // the geometric collect held (gol_gate_kernel)
-	const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
-	const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
-	const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
-	const uint32_t nw = (nB + 3) / 4;
-	const uint4* ent4 = reinterpret_cast<const uint4*>(ent) + (E0 >> 2);
-	// the row's own words, needed after the barrier, fly with phase 1
-	const size_t s = r0 + tid;
-	const bool act = s < r1;
-	const uint32_t rb = act ? ptr[s] : 0u, re = act ? ptr[s + 1] : 0u, pc = act ? l0c[s] : 0u;
-	// phase 1: kWords index words (4 kWords state gathers) in flight per thread
-	constexpr int kWords = DCCRGX_COLLECT_WORDS;
-	for (uint32_t w = tid; w < nw; w += kWords * kCollectRows) {
-		uint32_t q[4 * kWords];
-#pragma unroll
-		for (int c = 0; c < kWords; c++) {
-			const uint32_t wc = w + uint32_t(c) * kCollectRows;
-			const uint4 e4 = wc < nw ? ent4[wc] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
-			q[4 * c] = e4.x;
-			q[4 * c + 1] = e4.y;
-			q[4 * c + 2] = e4.z;
-			q[4 * c + 3] = e4.w;
-		}
-		uint32_t st[4 * kWords];
-#pragma unroll
-		for (int k = 0; k < 4 * kWords; k++) st[k] = q[k] == kEntNone ? 0u : state[q[k] & 0x7ffffffu];
-#pragma unroll
-		for (int c = 0; c < kWords; c++) {
-			uint32_t out = 0;
-#pragma unroll
-			for (int k = 4 * c; k < 4 * c + 4; k++) {
-				const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
-				out |= v << (8 * (k & 3));
+	// gated (the exact collect behind the geometric one): nothing to do
+	// unless that one met a disagreeing family or an unknown reached cell
+	// (err[0] bits 4 | 8); a gated launch has a capped grid whose blocks walk
+	// the chunks, an ungated one a block per chunk
+	if (gate && (*gate & (4 | 8)) == 0) return;  // block-uniform
+	const size_t nchunk = (s1 - s0 + kCollectRows - 1) / kCollectRows;
+	for (size_t ch = gate ? blockIdx.x : xcd_block(); ch < nchunk; ch += gate ? gridDim.x : nchunk) {
+		const size_t r0 = s0 + ch * kCollectRows;
+		const size_t r1 = r0 + kCollectRows < s1 ? r0 + kCollectRows : s1;
+		const uint32_t E0 = ptr[r0] & ~3u, E1 = ptr[r1];
+		const uint32_t nB = E1 - E0 < cap ? E1 - E0 : cap;
+		const uint32_t nw = (nB + 3) / 4;
+		const uint4* ent4 = reinterpret_cast<const uint4*>(ent) + (E0 >> 2);
+		// the row's own words, needed after the barrier, fly with phase 1
+		const size_t s = r0 + tid;
+		const bool act = s < r1;
+		const uint32_t rb = act ? ptr[s] : 0u, re = act ? ptr[s + 1] : 0u, pc = act ? l0c[s] : 0u;
+		// phase 1: kWords index words (4 kWords state gathers) in flight per thread
+		constexpr int kWords = DCCRGX_COLLECT_WORDS;
+		for (uint32_t w = tid; w < nw; w += kWords * kCollectRows) {
+			uint32_t q[4 * kWords];
+	#pragma unroll
+			for (int c = 0; c < kWords; c++) {
+				const uint32_t wc = w + uint32_t(c) * kCollectRows;
+				const uint4 e4 = wc < nw ? ent4[wc] : make_uint4(kEntNone, kEntNone, kEntNone, kEntNone);
+				q[4 * c] = e4.x;
+				q[4 * c + 1] = e4.y;
+				q[4 * c + 2] = e4.z;
+				q[4 * c + 3] = e4.w;
 			}
-			const uint32_t wc = w + uint32_t(c) * kCollectRows;
-			if (wc < nw) sp32[wc] = out;
+			uint32_t st[4 * kWords];
+	#pragma unroll
+			for (int k = 0; k < 4 * kWords; k++) st[k] = q[k] == kEntNone ? 0u : state[q[k] & 0x7ffffffu];
+	#pragma unroll
+			for (int c = 0; c < kWords; c++) {
+				uint32_t out = 0;
+	#pragma unroll
+				for (int k = 4 * c; k < 4 * c + 4; k++) {
+					const uint32_t v = q[k] == kEntNone ? 31u : ((q[k] >> 27) | (st[k] ? 32u : 0u));
+					out |= v << (8 * (k & 3));
+				}
+				const uint32_t wc = w + uint32_t(c) * kCollectRows;
+				if (wc < nw) sp32[wc] = out;
+			}
 		}
-	}
-	__syncthreads();
-	// the walk, branch-free: `mask` the bits of the live parents seen so far,
-	// `codes` the list (5 bits per entry, first-seen order), `ebits` the
-	// reference's aborts (1: a ninth live parent, 2: a dead neighbor whose
-	// parent was already recorded alive); entries without a slot (31) and of
-	// the own parent (13) change nothing
-	uint32_t mask = 0, n = 0, ebits = 0;
-	uint64_t codes = 0;
-	auto visit = [&](uint32_t v) {
-		const uint32_t c = v & 31u;
-		const uint32_t bit = (c != 31u && c != 13u) ? (1u << c) : 0u;
-		const uint32_t alive = (v >> 5) & 1u;
-		const uint32_t seen = (mask & bit) != 0u ? 1u : 0u;
-		const uint32_t fresh = alive & (bit != 0u ? 1u : 0u) & (seen ^ 1u);
-		ebits |= ((alive ^ 1u) & seen) << 1;
-		ebits |= fresh & (n >= uint32_t(kList) ? 1u : 0u);
-		const uint32_t app = fresh & (n < uint32_t(kList) ? 1u : 0u);
-		codes |= uint64_t(app ? c : 0u) << (5u * n);
-		n += app;
-		mask |= alive ? bit : 0u;
-	};
-	// the row's entry bytes a 4-byte word at a time (E0 is word aligned);
-	// bytes of the word outside the row count as "no slot"
-	for (uint32_t j = rb & ~3u; j < re; j += 4) {
-		uint32_t word;
-		if (j - E0 < nB) {
-			word = sp32[(j - E0) >> 2];
-		} else {
-			word = 0;
-#pragma unroll
-			for (uint32_t b = 0; b < 4; b++)
-				word |= (j + b < re ? mask_entry_byte(ent[j + b], state) : 31u) << (8 * b);
-		}
-#pragma unroll
-		for (uint32_t b = 0; b < 4; b++) {
-			const bool in = j + b >= rb && j + b < re;
-			visit(in ? (word >> (8 * b)) & 0xffu : 31u);
-		}
-	}
-	if (ebits) atomicOr(err, int(ebits));
-	uint32_t l[kList];
-#pragma unroll
-	for (int i = 0; i < kList; i++) l[i] = uint32_t(codes >> (5 * i)) & 31u;
-	// level-0 ids of the listed positions: the row's three wrapped x, y, z
-	// coordinates once, then per entry 1 + x + y lx + z lx ly
-	int px, py, pz;
-	l0_unpack(pc, G, px, py, pz);
-	auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
-	const uint64_t lxy = uint64_t(G.lx) * G.ly;
-	const uint64_t X[3] = {uint64_t(wrap(px - 1, int(G.lx))) + 1, uint64_t(px) + 1, uint64_t(wrap(px + 1, int(G.lx))) + 1};
-	const uint64_t Y[3] = {uint64_t(wrap(py - 1, int(G.ly))) * G.lx, uint64_t(py) * G.lx,
-	                       uint64_t(wrap(py + 1, int(G.ly))) * G.lx};
-	const uint64_t Z[3] = {uint64_t(wrap(pz - 1, int(G.lz))) * lxy, uint64_t(pz) * lxy, uint64_t(wrap(pz + 1, int(G.lz))) * lxy};
-	uint64_t out[kList];
-#pragma unroll
-	for (int i = 0; i < kList; i++) {
-		const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
-		out[i] = uint32_t(i) < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
-	}
-	// the lists of rows [w0, s1) through LDS: each row's 64 B at its place,
-	// then the block's rows stored as one contiguous run, 16 B per lane and
-	// instruction, non-temporal (paired A/B: 0.713 -> 0.693 ms per step).
-	// Rows below w0 keep their lists in the mask only (the turn's inner
-	// cells: no other process reads them, block-uniform skip)
-	if (r1 > w0) {
-		const size_t rs = r0 > w0 ? r0 : w0;
-		__syncthreads();  // every walk done: the staged entry bytes are free
-		ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
-		if (act)
-#pragma unroll
-			for (int i = 0; i < kList / 2; i++) so[tid * kRowSlots + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
 		__syncthreads();
-		ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + rs * kList);
-		const uint32_t skip = uint32_t(rs - r0);
-		const uint32_t n16 = uint32_t(r1 - rs) * (kList / 2);
-		for (uint32_t k = tid; k < n16; k += kCollectRows) {
-			typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
-			const ulonglong2 v = so[(skip + k / (kList / 2)) * kRowSlots + k % (kList / 2)];
-			const u2v w = {v.x, v.y};
-			__builtin_nontemporal_store(w, reinterpret_cast<u2v*>(dst + k));
+		// the walk, branch-free: `mask` the bits of the live parents seen so far,
+		// `codes` the list (5 bits per entry, first-seen order), `ebits` the
+		// reference's aborts (1: a ninth live parent, 2: a dead neighbor whose
+		// parent was already recorded alive); entries without a slot (31) and of
+		// the own parent (13) change nothing
+		uint32_t mask = 0, n = 0, ebits = 0;
+		uint64_t codes = 0;
+		auto visit = [&](uint32_t v) {
+			const uint32_t c = v & 31u;
+			const uint32_t bit = (c != 31u && c != 13u) ? (1u << c) : 0u;
+			const uint32_t alive = (v >> 5) & 1u;
+			const uint32_t seen = (mask & bit) != 0u ? 1u : 0u;
+			const uint32_t fresh = alive & (bit != 0u ? 1u : 0u) & (seen ^ 1u);
+			ebits |= ((alive ^ 1u) & seen) << 1;
+			ebits |= fresh & (n >= uint32_t(kList) ? 1u : 0u);
+			const uint32_t app = fresh & (n < uint32_t(kList) ? 1u : 0u);
+			codes |= uint64_t(app ? c : 0u) << (5u * n);
+			n += app;
+			mask |= alive ? bit : 0u;
+		};
+		// the row's entry bytes a 4-byte word at a time (E0 is word aligned);
+		// bytes of the word outside the row count as "no slot"
+		for (uint32_t j = rb & ~3u; j < re; j += 4) {
+			uint32_t word;
+			if (j - E0 < nB) {
+				word = sp32[(j - E0) >> 2];
+			} else {
+				word = 0;
+	#pragma unroll
+				for (uint32_t b = 0; b < 4; b++)
+					word |= (j + b < re ? mask_entry_byte(ent[j + b], state) : 31u) << (8 * b);
+			}
+	#pragma unroll
+			for (uint32_t b = 0; b < 4; b++) {
+				const bool in = j + b >= rb && j + b < re;
+				visit(in ? (word >> (8 * b)) & 0xffu : 31u);
+			}
 		}
+		if (ebits) atomicOr(err, int(ebits));
+		uint32_t l[kList];
+	#pragma unroll
+		for (int i = 0; i < kList; i++) l[i] = uint32_t(codes >> (5 * i)) & 31u;
+		// level-0 ids of the listed positions: the row's three wrapped x, y, z
+		// coordinates once, then per entry 1 + x + y lx + z lx ly
+		int px, py, pz;
+		l0_unpack(pc, G, px, py, pz);
+		auto wrap = [](int v, int L) { return v < 0 ? v + L : (v >= L ? v - L : v); };
+		const uint64_t lxy = uint64_t(G.lx) * G.ly;
+		const uint64_t X[3] = {uint64_t(wrap(px - 1, int(G.lx))) + 1, uint64_t(px) + 1, uint64_t(wrap(px + 1, int(G.lx))) + 1};
+		const uint64_t Y[3] = {uint64_t(wrap(py - 1, int(G.ly))) * G.lx, uint64_t(py) * G.lx,
+		                       uint64_t(wrap(py + 1, int(G.ly))) * G.lx};
+		const uint64_t Z[3] = {uint64_t(wrap(pz - 1, int(G.lz))) * lxy, uint64_t(pz) * lxy, uint64_t(wrap(pz + 1, int(G.lz))) * lxy};
+		uint64_t out[kList];
+	#pragma unroll
+		for (int i = 0; i < kList; i++) {
+			const uint32_t c = l[i], cz = (c * 57u) >> 9, cy = ((c * 11u) >> 5) - 3u * cz, cx = c - 3u * ((c * 11u) >> 5);
+			out[i] = uint32_t(i) < n ? X[cx] + Y[cy] + Z[cz] : error_cell;
+		}
+		// the lists of rows [w0, s1) through LDS: each row's 64 B at its place,
+		// then the block's rows stored as one contiguous run, 16 B per lane and
+		// instruction, non-temporal (paired A/B: 0.713 -> 0.693 ms per step).
+		// Rows below w0 keep their lists in the mask only (the turn's inner
+		// cells: no other process reads them, block-uniform skip)
+		if (r1 > w0) {
+			const size_t rs = r0 > w0 ? r0 : w0;
+			__syncthreads();  // every walk done: the staged entry bytes are free
+			ulonglong2* so = reinterpret_cast<ulonglong2*>(sp32);
+			if (act)
+	#pragma unroll
+				for (int i = 0; i < kList / 2; i++) so[tid * kRowSlots + i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+			__syncthreads();
+			ulonglong2* dst = reinterpret_cast<ulonglong2*>(lst + rs * kList);
+			const uint32_t skip = uint32_t(rs - r0);
+			const uint32_t n16 = uint32_t(r1 - rs) * (kList / 2);
+			for (uint32_t k = tid; k < n16; k += kCollectRows) {
+				typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+				const ulonglong2 v = so[(skip + k / (kList / 2)) * kRowSlots + k % (kList / 2)];
+				const u2v w = {v.x, v.y};
+				__builtin_nontemporal_store(w, reinterpret_cast<u2v*>(dst + k));
+			}
+		}
+		if (act) mask_out[s] = mask;
+		__syncthreads();  // a next chunk reuses the LDS
 	}
-	if (act) mask_out[s] = mask;
 }
 
 __global__ void gol_amr_spread0_mask_kernel(const uint32_t* __restrict__ lvl0, size_t n0, uint32_t* __restrict__ state,
@@ -521,9 +528,18 @@ __global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ g
 // of the row's neighbor entries.  Disagreeing families, or a reached cell
 // without a known leaf, set an error bit and the caller runs the exact
 // per-entry collect instead.
+// The table is laid out in blocks of 2^lb[0] x 2^lb[1] x 2^lb[2] cells (128
+// B: 16 x 8 x 1 on a one-layer grid, else 8 x 4 x 4), so the few cells a
+// stencil reaches share lines; an axis' part of a cell's index is
+// (k >> lb) * bstride + (k & (2^lb - 1)) * istride, the three parts summed
+// (lb = 0 everywhere is the plain raster order)
 struct GeoBox {
 	uint32_t x0, y0, z0, nx, ny, nz;
 	int px, py, pz;
+	uint32_t lb[3], bstride[3], istride[3];
+	__device__ __forceinline__ uint32_t part(int a, uint32_t k) const {
+		return (k >> lb[a]) * bstride[a] + (k & ((1u << lb[a]) - 1u)) * istride[a];
+	}
 	__device__ __forceinline__ bool index(const L0Geom& G, int x, int y, int z, uint32_t& out) const {
 		if (x < 0 || x >= int(G.lx)) {
 			if (!px) return false;
@@ -538,7 +554,7 @@ struct GeoBox {
 			z = z < 0 ? z + int(G.lz) : z - int(G.lz);
 		}
 		const uint32_t ix = uint32_t(x) - x0, iy = uint32_t(y) - y0, iz = uint32_t(z) - z0;
-		out = ix < nx && iy < ny && iz < nz ? ix + nx * (iy + ny * iz) : 0xffffffffu;
+		out = ix < nx && iy < ny && iz < nz ? part(0, ix) + part(1, iy) + part(2, iz) : 0xffffffffu;
 		return true;
 	}
 };
@@ -592,7 +608,8 @@ __global__ void geo_l0_groups_kernel(const uint32_t* __restrict__ gptr, size_t n
 // octant's side; nothing beyond a non-periodic boundary), whether that layer
 // lies in the table's box, and its offset into the table
 __device__ __forceinline__ void geo_axis(int p, uint32_t L, uint32_t b0, uint32_t bn, int per, bool lvl0, int side,
-                                         uint32_t stride, bool (&reach)[3], bool (&in)[3], uint32_t (&off)[3]) {
+                                         const GeoBox& B, int axis, bool (&reach)[3], bool (&in)[3],
+                                         uint32_t (&off)[3]) {
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
 		const int d = i - 1;
@@ -605,7 +622,7 @@ __device__ __forceinline__ void geo_axis(int p, uint32_t L, uint32_t b0, uint32_
 		const uint32_t k = uint32_t(q) - b0;
 		reach[i] = r;
 		in[i] = k < bn;
-		off[i] = k * stride;
+		off[i] = B.part(axis, k);
 	}
 }
 
@@ -627,9 +644,9 @@ __global__ __launch_bounds__(256) void geo_collect_kernel(const uint32_t* __rest
 	const bool lvl0 = c & 0x80u;
 	bool rx[3], ry[3], rz[3], ix[3], iy[3], iz[3];
 	uint32_t ox[3], oy[3], oz[3];
-	geo_axis(px, G.lx, B.x0, B.nx, B.px, lvl0, (c & 1u) ? 1 : -1, 1u, rx, ix, ox);
-	geo_axis(py, G.ly, B.y0, B.ny, B.py, lvl0, (c & 2u) ? 1 : -1, B.nx, ry, iy, oy);
-	geo_axis(pz, G.lz, B.z0, B.nz, B.pz, lvl0, (c & 4u) ? 1 : -1, B.nx * B.ny, rz, iz, oz);
+	geo_axis(px, G.lx, B.x0, B.nx, B.px, lvl0, (c & 1u) ? 1 : -1, B, 0, rx, ix, ox);
+	geo_axis(py, G.ly, B.y0, B.ny, B.py, lvl0, (c & 2u) ? 1 : -1, B, 1, ry, iy, oy);
+	geo_axis(pz, G.lz, B.z0, B.nz, B.pz, lvl0, (c & 4u) ? 1 : -1, B, 2, rz, iz, oz);
 	// every reached cell's byte in flight at once, then the bits; the own
 	// level-0 parent (solve.hpp:72-74) is never read
 	constexpr int K = CUBE ? 27 : 7;
@@ -852,7 +869,6 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		HIP_CHECK(hipMemcpyAsync(h, mm.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		const uint32_t L[3] = {T.lx, T.ly, T.lz};
-		uint64_t vol = 1;
 		for (int d = 0; d < 3; d++) {
 			T.per[d] = m.periodic[d];
 			// a periodic axis whose known coordinates touch both ends wraps:
@@ -860,8 +876,26 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 			const bool whole = m.periodic[d] && h[d] == 0 && h[3 + d] == int(L[d]) - 1;
 			T.box0[d] = whole ? 0u : uint32_t(h[d]);
 			T.boxn[d] = whole ? L[d] : uint32_t(h[3 + d] - h[d] + 1);
-			vol *= T.boxn[d];
 		}
+		// 128-cell blocks (GeoBox), the box rounded up to whole blocks
+#if DCCRGX_GEO_RASTER
+		const uint32_t lb[3] = {0, 0, 0};
+#else
+		const uint32_t lb[3] = {T.boxn[2] == 1 ? 4u : 3u, T.boxn[2] == 1 ? 3u : 2u, T.boxn[2] == 1 ? 0u : 2u};
+#endif
+		uint64_t nb[3], vol = uint64_t(1) << (lb[0] + lb[1] + lb[2]);
+		for (int d = 0; d < 3; d++) {
+			nb[d] = (uint64_t(T.boxn[d]) + (uint64_t(1) << lb[d]) - 1) >> lb[d];
+			vol *= nb[d];
+		}
+		const uint64_t bv = uint64_t(1) << (lb[0] + lb[1] + lb[2]);
+		for (int d = 0; d < 3; d++) T.geo_lb[d] = lb[d];
+		T.geo_bstride[0] = uint32_t(bv);
+		T.geo_bstride[1] = uint32_t(std::min<uint64_t>(nb[0] * bv, 0xffffffffu));
+		T.geo_bstride[2] = uint32_t(std::min<uint64_t>(nb[0] * nb[1] * bv, 0xffffffffu));
+		T.geo_istride[0] = 1u;
+		T.geo_istride[1] = 1u << lb[0];
+		T.geo_istride[2] = 1u << (lb[0] + lb[1]);
 		if (vol < (uint64_t(1) << 31)) {
 			T.l0tab.alloc(size_t(vol));
 			HIP_CHECK(hipMemsetAsync(T.l0tab.p, 0, size_t(vol), s));
@@ -881,7 +915,18 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
                    uint64_t* lst, size_t list_from, int* err, hipStream_t s) {
 	DX_REQUIRE(T.geo && (nh == 26 || nh == 6), "geometric collect not available");
 	const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
-	const GeoBox B{T.box0[0], T.box0[1], T.box0[2], T.boxn[0], T.boxn[1], T.boxn[2], T.per[0], T.per[1], T.per[2]};
+	const GeoBox B{T.box0[0],
+	               T.box0[1],
+	               T.box0[2],
+	               T.boxn[0],
+	               T.boxn[1],
+	               T.boxn[2],
+	               T.per[0],
+	               T.per[1],
+	               T.per[2],
+	               {T.geo_lb[0], T.geo_lb[1], T.geo_lb[2]},
+	               {T.geo_bstride[0], T.geo_bstride[1], T.geo_bstride[2]},
+	               {T.geo_istride[0], T.geo_istride[1], T.geo_istride[2]}};
 	if (n_state) {
 		geo_l0_leaves_kernel<<<grid_for(n_state, 256), 256, 0, s>>>(T.l0.p, T.l0c.p, state, n_state, G, B, T.l0tab.p);
 		HIP_CHECK(hipGetLastError());
@@ -903,20 +948,6 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
 	}
 }
 
-// err[1] = err[0]; when the geometric collect met a disagreeing family or an
-// unknown reached cell (bits 4 | 8) err[0] is cleared for the exact collect,
-// which runs only then (its blocks read err[1])
-__global__ void gol_gate_kernel(int* err) {
-	const int v = err[0];
-	err[1] = v;
-	if (v & (4 | 8)) err[0] = 0;
-}
-
-void k_gol_gate(int* err, hipStream_t s) {
-	gol_gate_kernel<<<1, 1, 0, s>>>(err);
-	HIP_CHECK(hipGetLastError());
-}
-
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from, const int* gate) {
 	if (s1 <= s0) return;
@@ -924,7 +955,9 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 	if (T.mask_path) {
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
-			gol_amr_collect_mask_kernel<<<xcd_grid((s1 - s0 + kCollectRows - 1) / kCollectRows), kCollectRows, 0, s>>>(
+			const size_t nchunk = (s1 - s0 + kCollectRows - 1) / kCollectRows;
+			gol_amr_collect_mask_kernel<<<gate ? unsigned(std::min<size_t>(nchunk, 1024)) : xcd_grid(nchunk), kCollectRows, 0,
+			                              s>>>(
 			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, list_from < s0 ? s0 : list_from, err, gate);
 		} else {
 			if (T.n_lvl0)

@@ -2366,8 +2366,9 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_incr
 		Field& F = field(g, df);
 		DBuf<uint64_t> d;
 		d.alloc(g.n_local + 1);
-		const size_t k = k_adv_candidates(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p,
-		                                  g.n_local, diff_increase, diff_threshold, d.p, g.s_comp);
+		const FaceView fv{g.face_ell.p, g.face_fine.p, g.slot_ids.p, g.n_local};
+		const size_t k = k_adv_candidates(g.m, (const double*)F.data.p, fv, g.slot_lvl.p, g.n_local, diff_increase,
+		                                  diff_threshold, d.p, g.s_comp);
 		auto v = download(d.p, k, g.s_comp);
 		std::sort(v.begin(), v.end());
 		return copy_out_u64(v, out, cap, n);
@@ -2399,8 +2400,9 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		const size_t n = g.n_local;
 		DBuf<uint8_t> band;
 		band.alloc(n + 1);
-		k_adv_bands(g.m, (const double*)F.data.p, g.face_ptr.p, g.face_ent.p, g.slot_ids.p, n, diff_increase,
-		            diff_threshold, unrefine_sensitivity, band.p, g.s_comp);
+		const FaceView fv{g.face_ell.p, g.face_fine.p, g.slot_ids.p, g.n_local};
+		k_adv_bands(g.m, (const double*)F.data.p, fv, g.slot_lvl.p, n, diff_increase, diff_threshold,
+		            unrefine_sensitivity, band.p, g.s_comp);
 		DX_LAP("chk.1_bands");
 		uint64_t nref = 0, nkeep = 0, nunref = 0;
 		// decide one family from its local members (bands bb, ids ii, k of

@@ -898,6 +898,11 @@ __global__ void kept_children_kernel(MapCtx m, DevMesh M, int rank, const uint64
 	out_slot[at] = sl;
 }
 
+__global__ void slot_levels_kernel(MapCtx m, const uint64_t* slot_ids, size_t n, uint8_t* lvl) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		lvl[i] = uint8_t(map_level(m, slot_ids[i]));
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1404,6 +1409,12 @@ void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vec
 		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
 		ids = download(k2.p, n, s);
 	}
+}
+
+void k_slot_levels(const MapCtx& m, const uint64_t* slot_ids, size_t n, uint8_t* lvl, hipStream_t s) {
+	if (!n) return;
+	slot_levels_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, slot_ids, n, lvl);
+	HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dccrgx

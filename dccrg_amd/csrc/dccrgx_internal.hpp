@@ -480,6 +480,7 @@ struct Grid {
 	DBuf<uint32_t> face_ptr;
 	DBuf<int32_t> face_ent;
 	DBuf<int32_t> face_ell, face_fine;  // fixed-width form used by the advection sweep
+	DBuf<uint8_t> slot_lvl;             // refinement level of every slot (with the face table)
 	size_t n_fine_faces = 0;
 	// face tiles (built lazily from the face CSR): the inner and the outer run
 	// of slots are cut into tiles of at most `tile` consecutive slots
@@ -599,6 +600,16 @@ void known_leaves(Grid& g, std::vector<uint64_t>& ids, std::vector<int32_t>& own
 // local leaf ids on the device (slot order)
 inline const uint64_t* local_ids_dev(const Grid& g) { return g.slot_ids.p; }
 
+// the face table of the local rows (ensure_face): per row and direction the
+// neighbor's slot (same size or coarser), -1, or -2 - k for the finer face k
+// (its 4 slots at fine[4 k ..]), in reference order
+struct FaceView {
+	const int32_t* ell;
+	const int32_t* fine;
+	const uint64_t* slot_ids;
+	size_t n_local;
+};
+
 // --- launchers implemented in build_kernels.hip -----------------------------
 void k_fill_i32(int32_t* p, size_t n, int32_t v, hipStream_t s);
 void k_iota_u64(uint64_t* out, uint64_t first, size_t n, hipStream_t s);
@@ -643,6 +654,7 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
                       const int32_t* nof_slot, const uint32_t* nto_ptr, const uint64_t* nto_id, size_t nrows,
                       uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
                       int pass, hipStream_t s);
+void k_slot_levels(const MapCtx& m, const uint64_t* slot_ids, size_t n, uint8_t* lvl, hipStream_t s);
 void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint64_t* cnt,
                   int32_t* hint, const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
                   int32_t* err_flag, int pass, hipStream_t s, bool morton = false, size_t run1 = 0);
@@ -721,9 +733,8 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 // (run 0 inner, 1 outer: tiles never straddle the two)
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
-size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
-                        const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
-                        uint64_t* out, hipStream_t s);
+size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
+                        double diff_increase, double diff_threshold, uint64_t* out, hipStream_t s);
 // adaptation of tests/advection/adapter.hpp: per local cell band (2 refine,
 // 1 keep, 0 unrefine), merged parents' densities, velocity + length reset
 // check_for_adaptation's requests computed on the device (sweep_kernels.hip
@@ -740,9 +751,9 @@ struct AdvRequests {
 };
 AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
                            hipStream_t s);
-void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
-                 const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
-                 double unrefine_sensitivity, uint8_t* band, hipStream_t s);
+void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
+                 double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
+                 hipStream_t s);
 void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
                          double* rho, const double* removed_rho, hipStream_t s);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,

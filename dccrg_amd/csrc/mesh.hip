@@ -599,6 +599,8 @@ void ensure_face(Grid& g) {
 	if (!nl) HIP_CHECK(hipMemsetAsync(g.face_ptr.p, 0, 4, s));
 	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, pos.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p,
 	             g.face_fine.p, err.p, 1, s);
+	g.slot_lvl.alloc(g.n_slots + 1);
+	k_slot_levels(g.m, g.slot_ids.p, g.n_slots, g.slot_lvl.p, s);
 	int32_t herr = 0;
 	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));

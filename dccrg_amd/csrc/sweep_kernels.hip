@@ -965,57 +965,79 @@ __global__ void adv_dt_kernel(const double* __restrict__ vx, const double* __res
 // neighbors, counting a finer neighbor only at the cell's corner and a
 // coarser one only when the cell sits at its corner (the x, y, z offset
 // test of 84-102, the same from either side of a face)
-__device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
-                               const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t s,
-                               double diff_threshold, int& lvl) {
-	uint64_t c[3];
-	lvl = map_indices(m, slot_ids[s], c[0], c[1], c[2]);
-	const uint64_t len = uint64_t(1) << (m.R - lvl);
+// max_diff of one local cell (adapter.hpp:47-123) over the fixed-width face
+// table: a same-size neighbor always counts, a coarser one only when the
+// cell sits at the corner of the coarser cell's face, of four finer ones only
+// the first (the one at the cell's corner); lvl8: the level of every slot
+__device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const int32_t* __restrict__ ell,
+                               const int32_t* __restrict__ fine, const uint8_t* __restrict__ lvl8,
+                               const uint64_t* __restrict__ slot_ids, size_t s, double diff_threshold, int& lvl) {
+	typedef int i2v __attribute__((ext_vector_type(2)));
+	lvl = lvl8[s];
+	int32_t e6[6];
+	const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
+#pragma unroll
+	for (int j = 0; j < 3; j++) {
+		const i2v v = ev[j];
+		e6[2 * j] = v.x;
+		e6[2 * j + 1] = v.y;
+	}
+	const double a = rho[s];
 	double md = 0;
-	const uint32_t e0 = ptr[s], e1 = ptr[s + 1];
-	for (uint32_t e = e0; e < e1; e++) {
-		const int32_t en = ent[e];
-		const int32_t nsl = en >> 3;
-		const int d = (en & 7) >> 1;
-		const int nl = map_level(m, slot_ids[nsl]);
-		bool zero = true;
-		if (nl > lvl) {
-			// finer: only the first of the four face cells sits at the cell's corner
-			zero = (e == e0 || ((ent[e - 1] & 7) != (en & 7)));
-		} else if (nl < lvl) {
-			const uint64_t pl = len * 2;
-			for (int k = 0; k < 3; k++)
-				if (k != d && (c[k] & (pl - 1)) != 0) zero = false;
+	bool have_c = false;
+	uint64_t c[3] = {0, 0, 0};
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) {
+		const int32_t e = e6[dir];
+		if (e == -1) continue;
+		int32_t nsl;
+		if (e >= 0) {
+			nsl = e;
+			if (int(lvl8[e]) < lvl) {
+				if (!have_c) {
+					map_indices(m, slot_ids[s], c[0], c[1], c[2]);
+					have_c = true;
+				}
+				const uint64_t pl = (uint64_t(1) << (m.R - lvl)) * 2;
+				const int d = dir >> 1;
+				bool zero = true;
+				for (int k = 0; k < 3; k++)
+					if (k != d && (c[k] & (pl - 1)) != 0) zero = false;
+				if (!zero) continue;
+			}
+		} else {
+			nsl = fine[4 * size_t(-2 - e)];
 		}
-		if (!zero) continue;
-		const double a = rho[s], b = rho[nsl];
+		const double b = rho[nsl];
 		const double diff = fabs(a - b) / (fmin(a, b) + diff_threshold);
 		md = fmax(diff, md);
 	}
 	return md;
 }
 
-__global__ void adv_candidates_kernel(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
-                                      const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t n,
+__global__ void adv_candidates_kernel(MapCtx m, const double* __restrict__ rho, const int32_t* __restrict__ ell,
+                                      const int32_t* __restrict__ fine, const uint8_t* __restrict__ lvl8,
+                                      const uint64_t* __restrict__ slot_ids, size_t n,
                                       double diff_increase, double diff_threshold, uint64_t* out,
                                       unsigned long long* counter) {
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
 		int lvl;
-		const double md = adv_max_diff(m, rho, ptr, ent, slot_ids, s, diff_threshold, lvl);
+		const double md = adv_max_diff(m, rho, ell, fine, lvl8, slot_ids, s, diff_threshold, lvl);
 		if (md > (lvl + 1) * diff_increase) out[atomicAdd(counter, 1ull)] = slot_ids[s];
 	}
 }
 
 // the band of each local cell (adapter.hpp:124-176): 2 refine, 1 keep (no
 // unrefine), 0 unrefine
-__global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const uint32_t* __restrict__ ptr,
-                                 const int32_t* __restrict__ ent, const uint64_t* __restrict__ slot_ids, size_t n,
+__global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const int32_t* __restrict__ ell,
+                                 const int32_t* __restrict__ fine, const uint8_t* __restrict__ lvl8,
+                                 const uint64_t* __restrict__ slot_ids, size_t n,
                                  double diff_increase, double diff_threshold, double unrefine_sensitivity,
                                  uint8_t* __restrict__ band) {
 #pragma clang fp contract(off)
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
 		int lvl;
-		const double md = adv_max_diff(m, rho, ptr, ent, slot_ids, s, diff_threshold, lvl);
+		const double md = adv_max_diff(m, rho, ell, fine, lvl8, slot_ids, s, diff_threshold, lvl);
 		const double refine_diff = (lvl + 1) * diff_increase, unrefine_diff = unrefine_sensitivity * refine_diff;
 		band[s] = md > refine_diff ? 2 : (md >= unrefine_diff ? 1 : 0);
 	}
@@ -1312,11 +1334,11 @@ void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblock
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_adv_bands(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
-                 const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
-                 double unrefine_sensitivity, uint8_t* band, hipStream_t s) {
+void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
+                 double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
+                 hipStream_t s) {
 	if (!n) return;
-	adv_bands_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, face_ptr, face_ent, slot_ids, n, diff_increase,
+	adv_bands_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, F.ell, F.fine, lvl8, F.slot_ids, n, diff_increase,
 	                                                  diff_threshold, unrefine_sensitivity, band);
 	HIP_CHECK(hipGetLastError());
 }
@@ -1421,14 +1443,13 @@ void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const doub
 	HIP_CHECK(hipGetLastError());
 }
 
-size_t k_adv_candidates(const MapCtx& m, const double* rho, const uint32_t* face_ptr, const int32_t* face_ent,
-                        const uint64_t* slot_ids, size_t n, double diff_increase, double diff_threshold,
-                        uint64_t* out, hipStream_t s) {
+size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
+                        double diff_increase, double diff_threshold, uint64_t* out, hipStream_t s) {
 	if (!n) return 0;
 	DBuf<unsigned long long> ctr;
 	ctr.alloc(1);
 	HIP_CHECK(hipMemsetAsync(ctr.p, 0, sizeof(unsigned long long), s));
-	adv_candidates_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, face_ptr, face_ent, slot_ids, n, diff_increase,
+	adv_candidates_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rho, F.ell, F.fine, lvl8, F.slot_ids, n, diff_increase,
 	                                                       diff_threshold, out, ctr.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h = 0;

@@ -1383,7 +1383,7 @@ std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int 
 }
 
 void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s) {
+                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, DBuf<uint64_t>* ids_dev) {
 	ids.clear();
 	slots.release();
 	if (F.empty()) return;
@@ -1408,6 +1408,7 @@ void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vec
 		temp.alloc(bytes + 1);
 		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
 		ids = download(k2.p, n, s);
+		if (ids_dev) ids_dev->swap(k2);
 	}
 }
 

@@ -452,6 +452,7 @@ struct Grid {
 	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
 	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
 	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)
+	DBuf<uint64_t> removed_ids_d;               // the same on the device when n > 0, else empty
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;
 
@@ -692,7 +693,8 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
                                          hipStream_t s);
 void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s);
+                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s,
+                     DBuf<uint64_t>* ids_dev = nullptr);
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
                      hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0,
@@ -755,7 +757,7 @@ void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const ui
                  double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
                  hipStream_t s);
 void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
-                         double* rho, const double* removed_rho, hipStream_t s);
+                         double* rho, const double* removed_rho, hipStream_t s, const uint64_t* rm_dev = nullptr);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
                           size_t np, hipStream_t s);
 void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],

@@ -471,6 +471,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		f.rm_off.release();
 	}
 	g.removed_ids_h.clear();
+	g.removed_ids_d.release();
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
 	std::vector<uint64_t> D = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_refine_cells))));
@@ -538,7 +539,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	std::vector<uint64_t> keep_ids;  // removed children staying on this rank
 	DBuf<int32_t> ksl;               // and their slots (device)
 	if (!F.empty()) {
-		k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s);
+		k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, &g.removed_ids_d);
 		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
 		if (g.size > 1 || attrs) {
@@ -595,6 +596,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			roff.push_back(ro);
 			ro += kv.second.size() * bpc;
 			g.removed_ids_h.insert(g.removed_ids_h.end(), kv.second.begin(), kv.second.end());
+			g.removed_ids_d.release();  // the device copy holds the kept ones only
 		}
 		DBuf<uint8_t> sbuf, rbuf;
 		sbuf.alloc(so + 1);
@@ -760,6 +762,7 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 	}
 	g.weights.clear();
 	g.removed_ids_h.clear();  // unrefined_cell_data (3811)
+	g.removed_ids_d.release();
 	for (auto& f : g.fields) {
 		f.removed.release();
 		f.rm_off.release();

@@ -1347,13 +1347,16 @@ void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const ui
 // ids `rm` (store order): parents grouped, their eight children in ascending
 // id, the parents' local slots, then the mean density
 void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
-                         double* rho, const double* removed_rho, hipStream_t s) {
+                         double* rho, const double* removed_rho, hipStream_t s, const uint64_t* rm_dev) {
 	if (rm.empty()) return;
 	const size_t n = rm.size();
-	DBuf<uint64_t> d_rm, par;
-	upload(d_rm, rm, s);
+	DBuf<uint64_t> up, par;
+	if (!rm_dev) {
+		upload(up, rm, s);
+		rm_dev = up.p;
+	}
 	par.alloc(n);
-	removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, d_rm.p, n, par.p);
+	removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p);
 	HIP_CHECK(hipGetLastError());
 	const size_t np = sort_unique_u64(par.p, n, s);
 	DX_REQUIRE(np * 8 == n, "a merged family's removed children are incomplete");
@@ -1364,7 +1367,7 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, con
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(cidx.p, 0xff, 8 * np * sizeof(int32_t), s));
 	HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), s));
-	removed_rows_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, d_rm.p, n, par.p, np, cidx.p, err.p);
+	removed_rows_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p, np, cidx.p, err.p);
 	HIP_CHECK(hipGetLastError());
 	k_lookup_slots(par.p, np, dm, pslot.p, err.p, s);  // a missing parent sets err too
 	check_rows_kernel<<<grid_for(np, 256), 256, 0, s>>>(cidx.p, pslot.p, np, n_local, err.p);

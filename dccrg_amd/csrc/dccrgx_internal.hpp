@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -530,7 +531,7 @@ struct Grid {
 	bool timing = false;
 	double timed_ms = 0;
 	int64_t timed_count = 0;
-	std::vector<std::pair<hipEvent_t, hipEvent_t>> pending_events;
+	std::deque<std::pair<hipEvent_t, hipEvent_t>> pending_events;
 
 	// slot order inside the inner and outer runs: 0 = ascending id (raster,
 	// needed by the structured uniform kernels), 1 = Morton order of the min

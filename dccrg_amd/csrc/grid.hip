@@ -123,8 +123,21 @@ void region_range(const Grid& g, int region, size_t& s0, size_t& s1) {
 void k_time_begin(Grid& g) {
 	if (!g.timing) return;
 	hipEvent_t a, b;
-	HIP_CHECK(hipEventCreate(&a));
-	HIP_CHECK(hipEventCreate(&b));
+	if (!g.pending_events.empty() && hipEventQuery(g.pending_events.front().second) == hipSuccess) {
+		// the oldest pair has completed: its time is taken now and its events
+		// are reused (no event creation per timed launch)
+		const auto ab = g.pending_events.front();
+		g.pending_events.pop_front();
+		float ms = 0;
+		HIP_CHECK(hipEventElapsedTime(&ms, ab.first, ab.second));
+		g.timed_ms += ms;
+		g.timed_count++;
+		a = ab.first;
+		b = ab.second;
+	} else {
+		HIP_CHECK(hipEventCreate(&a));
+		HIP_CHECK(hipEventCreate(&b));
+	}
 	HIP_CHECK(hipEventRecord(a, g.s_comp));
 	g.pending_events.push_back({a, b});
 }

@@ -687,7 +687,9 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	uint32_t n_ent = 0;
 	HIP_CHECK(hipMemcpyAsync(&n_ent, face_ptr + n_local, 4, hipMemcpyDeviceToHost, s));
 	HIP_CHECK(hipStreamSynchronize(s));
-	if (T <= kXT && ntiles) {
+	// (DCCRGX_TILE_GLOBAL=1: always the global build below, the fallback,
+	// so that tests compare the two)
+	if (T <= kXT && ntiles && !std::getenv("DCCRGX_TILE_GLOBAL")) {
 		// per-tile build (tile_ext_kernel): each tile's lists at scratch places
 		// first, then packed densely
 		DBuf<uint32_t> en, fn, so, off, sext, sfine;

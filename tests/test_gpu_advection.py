@@ -155,6 +155,26 @@ def test_parity_grid_exercises_both_tile_kernels(gpu):
     g.close()
 
 
+def test_tile_build_paths_bitwise(gpu, monkeypatch):
+    """The tile ext lists are built per tile in LDS (tile_build.hip
+    tile_ext_kernel) unless a tile has more distinct out-of-tile neighbors
+    than its LDS holds; then by one global sort (the fallback).  Forced to the
+    fallback (DCCRGX_TILE_GLOBAL=1), the parity grid must give the same layout
+    and the same densities bit for bit after 20 steps."""
+    base, R, steps = (32, 32, 8), 2, 20
+    g1, f1, lay1, _, ids1 = _run_parity_grid(base, R, steps)
+    rho1 = f1[0].get(0, ids1.size)
+    g1.close()
+    monkeypatch.setenv("DCCRGX_TILE_GLOBAL", "1")
+    g2, f2, lay2, _, ids2 = _run_parity_grid(base, R, steps)
+    rho2 = f2[0].get(0, ids2.size)
+    g2.close()
+    assert np.array_equal(ids1, ids2)
+    for k in ("tiles", "ext_total", "ext_max", "finer_faces", "regular_tiles"):
+        assert lay1[k] == lay2[k], k
+    assert np.array_equal(rho1, rho2)
+
+
 def test_parity_grid_four_rank_slabs_bitwise(gpu):
     """The parity grid, 16 level-0 cells deep, split into 4 z-slabs (block
     partition of the level-0 cells, children inherit, execute_refines

@@ -15,8 +15,6 @@
 // the block-partition formula on the initial level-0 grid).
 #include <hipcub/hipcub.hpp>
 
-#include <cstdio>
-
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -427,17 +425,8 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // a same-size leaf is the one face neighbor in that direction (no finer or
 // coarser probe needed).  Otherwise, and for the misses, the probes of
 // face_dir.  The hints are the same either way.
-// per level-0 cell the first row (of [0, nrows), Morton-ordered runs) whose
-// leaf lies in it: the second predictor of face_hints_kernel
-__global__ void l0_first_kernel(MapCtx m, const uint64_t* slot_ids, size_t nrows, size_t run1, uint32_t* l0_first) {
-	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
-		const uint64_t p = map_level0_parent(m, slot_ids[r]);
-		if (r == 0 || r == run1 || map_level0_parent(m, slot_ids[r - 1]) != p) l0_first[p - 1] = uint32_t(r);
-	}
-}
-
 __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1, bool morton,
-                                  const uint32_t* l0_first, uint64_t* cnt, int32_t* hint, unsigned long long* stats) {
+                                  uint64_t* cnt, int32_t* hint) {
 	const SlotExists ex{M};
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		uint64_t c[3];
@@ -470,30 +459,6 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 			}
 #pragma unroll
 			for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
-			// second prediction for the misses: the neighbor's level-0 cell's
-			// first row + its Morton rank inside that cell (right whenever the
-			// level-0 cell is uniformly refined to the neighbor's level)
-			if (l0_first) {
-				const uint64_t l0m = (uint64_t(1) << m.R) - 1;
-#pragma unroll
-				for (int dir = 0; dir < 6; dir++) {
-					if (!probe[dir] || (h[dir] >= 0 && got[dir] == want[dir])) continue;
-					uint64_t p[3];
-					face_probe(m, c, lvl, dir, p);
-					for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
-					const uint64_t l0 = (p[0] >> m.R) + (p[1] >> m.R) * m.len[0] + (p[2] >> m.R) * m.len[0] * m.len[1];
-					const uint32_t f = l0_first[l0];
-					h[dir] = -1;
-					if (f == 0xffffffffu) continue;
-					const uint64_t lp[3] = {p[0] & l0m, p[1] & l0m, p[2] & l0m};
-					const int64_t q = int64_t(f) + int64_t(morton3(lp) >> sh);
-					if (q >= lo && q < hi) {
-						h[dir] = int32_t(q);
-						want[dir] = map_from_indices(m, p[0], p[1], p[2], lvl);
-						got[dir] = slot_ids[q];
-					}
-				}
-			}
 		}
 		int32_t o6[6];
 #pragma unroll
@@ -509,7 +474,6 @@ __global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 					continue;
 				}
 			}
-			if (stats) atomicAdd(stats, 1ull);  // (diagnostics: directions probed)
 			uint64_t out[4];
 			const int nf = face_dir(m, c, lvl, dir, ex, out);
 			// a single neighbor was the last cell found (face_dir returns on it)
@@ -1163,33 +1127,8 @@ void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, s
                   int32_t* err_flag, int pass, hipStream_t s, bool morton, size_t run1) {
 	if (!nrows) return;
 	if (pass == 0)
-	{
-		// DCCRGX_FACE_STATS=1 (diagnostics): how many of the 6 n directions
-		// missed the Morton prediction and were probed
-		DBuf<unsigned long long> st;
-		const bool diag = std::getenv("DCCRGX_FACE_STATS") != nullptr;
-		if (diag) {
-			st.alloc(1);
-			HIP_CHECK(hipMemsetAsync(st.p, 0, 8, s));
-		}
-		// the level-0 first rows (the second prediction)
-		DBuf<uint32_t> l0f;
-		const bool pred = morton && !M.implicit;
-		const uint64_t n0 = m.len[0] * m.len[1] * m.len[2];
-		if (pred && n0 < (uint64_t(1) << 31)) {
-			l0f.alloc(n0);
-			HIP_CHECK(hipMemsetAsync(l0f.p, 0xff, n0 * 4, s));
-			l0_first_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, slot_ids, nrows, run1, l0f.p);
-		}
-		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, pred, l0f.p, cnt, hint,
-		                                                       diag ? st.p : nullptr);
-		if (diag) {
-			unsigned long long h = 0;
-			HIP_CHECK(hipMemcpyAsync(&h, st.p, 8, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipStreamSynchronize(s));
-			std::fprintf(stderr, "[face] %zu rows, %llu of %zu directions probed\n", nrows, h, 6 * nrows);
-		}
-	}
+		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, cnt,
+		                                                       hint);
 	else
 		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, pos, ptr, ent, ell, fine,
 		                                                      err_flag);

@@ -819,6 +819,40 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 // Regular / irregular split of the tiles of one layout (see
 // classify_tiles_kernel): per-run lists of tile indices, and for regular
 // tiles the six neighbor-box start slots.
+__global__ void tile_first_ids_kernel(const uint32_t* __restrict__ tstart, const uint64_t* __restrict__ slot_ids,
+                                      uint64_t* __restrict__ out, size_t nt) {
+	const size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x;
+	if (t < nt) out[t] = slot_ids[tstart[t]];
+}
+
+// 3-D Hilbert index of (x, y, z), b bits per axis (Skilling's transpose
+// form, "Programming the Hilbert curve", AIP Conf. Proc. 707, 2004)
+static uint64_t hilbert3(uint32_t x, uint32_t y, uint32_t z, int b) {
+	uint32_t X[3] = {x, y, z};
+	const uint32_t M = 1u << (b - 1);
+	for (uint32_t Q = M; Q > 1; Q >>= 1) {
+		const uint32_t P = Q - 1;
+		for (int i = 0; i < 3; i++) {
+			if (X[i] & Q) {
+				X[0] ^= P;
+			} else {
+				const uint32_t t = (X[0] ^ X[i]) & P;
+				X[0] ^= t;
+				X[i] ^= t;
+			}
+		}
+	}
+	for (int i = 1; i < 3; i++) X[i] ^= X[i - 1];
+	uint32_t t = 0;
+	for (uint32_t Q = M; Q > 1; Q >>= 1)
+		if (X[2] & Q) t ^= Q - 1;
+	for (int i = 0; i < 3; i++) X[i] ^= t;
+	uint64_t h = 0;
+	for (int j = b - 1; j >= 0; j--)
+		for (int i = 0; i < 3; i++) h = (h << 1) | ((X[i] >> j) & 1u);
+	return h;
+}
+
 void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_inner, size_t n_tiles_outer,
                       const uint64_t* slot_ids, const int32_t* face_ell, DBuf<uint32_t>& lists, DBuf<int32_t>& tnb,
                       DBuf<RegTileMeta>& regmeta, size_t counts[4], hipStream_t s) {
@@ -842,6 +876,34 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 	for (size_t t = 0; t < nt; t++) {
 		const int run = t < n_tiles_inner ? 0 : 1;
 		(h[t] == 1u ? reg[run] : irr[run]).push_back(uint32_t(t));
+	}
+	// experiment (DCCRGX_TILE_HILBERT=1): the regular tiles of each run in the
+	// Hilbert order of their boxes' corners instead of Morton (slot) order;
+	// the sweep is independent of the order (bitwise the same densities)
+	// (=2: the irregular tiles too)
+	const int hilbert = std::getenv("DCCRGX_TILE_HILBERT") ? std::atoi(std::getenv("DCCRGX_TILE_HILBERT")) : 0;
+	if (hilbert > 0) {
+		DBuf<uint64_t> fid;
+		fid.alloc(nt);
+		tile_first_ids_kernel<<<unsigned((nt + 255) / 256), 256, 0, s>>>(tstart, slot_ids, fid.p, nt);
+		HIP_CHECK(hipGetLastError());
+		const std::vector<uint64_t> ids = download(fid.p, nt, s);
+		uint64_t gmax = std::max(m.glen[0], std::max(m.glen[1], m.glen[2])) >> 3;
+		int b = 1;
+		while (b < 21 && (uint64_t(1) << b) < gmax) b++;
+		for (int k = 0; k < (hilbert > 1 ? 4 : 2); k++) {
+			std::vector<uint32_t>& L = k < 2 ? reg[k] : irr[k - 2];
+			std::vector<std::pair<uint64_t, uint32_t>> key;
+			key.reserve(L.size());
+			for (uint32_t t : L) {
+				uint64_t x, y, z;
+				map_indices(m, ids[t], x, y, z);
+				key.push_back({hilbert3(uint32_t(x >> 3), uint32_t(y >> 3), uint32_t(z >> 3), b), t});
+			}
+			std::stable_sort(key.begin(), key.end(),
+			                 [](const auto& a, const auto& c) { return a.first < c.first; });
+			for (size_t i = 0; i < key.size(); i++) L[i] = key[i].second;
+		}
 	}
 	std::vector<uint32_t> all;
 	for (auto* v : {&reg[0], &reg[1], &irr[0], &irr[1]}) all.insert(all.end(), v->begin(), v->end());

@@ -65,9 +65,15 @@ std::vector<int> HaloPlan::peers() const {
 
 static int ghost_radius(const Grid& g) { return std::max(1, int(g.hood_len)); }
 
+// table entries per known leaf, x4: 8 = at least two entries per leaf (load
+// factor 0.25..0.5)
+#ifndef DCCRGX_HASH_ROOM4
+#define DCCRGX_HASH_ROOM4 8
+#endif
+
 void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s, size_t slot_upto) {
 	uint32_t bits = 4;
-	while ((uint64_t(1) << bits) < 2 * uint64_t(n)) bits++;
+	while ((uint64_t(4) << bits) < uint64_t(DCCRGX_HASH_ROOM4) * uint64_t(n)) bits++;
 	M.tab.alloc(size_t(1) << bits);
 	HIP_CHECK(hipMemsetAsync(M.tab.p, 0, M.tab.n * sizeof(HashEntry), s));
 	M.mask = (uint64_t(1) << bits) - 1;

@@ -480,7 +480,14 @@ public:
 		return *this;
 	}
 	const std::string& get_load_balancing_method() const { return lb_method_; }  // 8228
-	Dccrg& set_send_single_cells(bool) { return *this; }  // one message per peer (the reference default)
+	// set / get_send_single_cells (6658-6681): the flag is kept and reported;
+	// the wire stays one message per peer (the same bytes in the same order)
+	Dccrg& set_send_single_cells(const bool given) {
+		send_single_cells_ = given;
+		if (g_) detail::check(dccrgx_set_send_single_cells(g_, given ? 1 : 0));
+		return *this;
+	}
+	bool get_send_single_cells() const { return send_single_cells_; }
 
 	// initialize (472-552)
 	Dccrg& initialize(const MPI_Comm& comm, const uint64_t /*sfc_caching_batches*/ = 1) {
@@ -1073,6 +1080,7 @@ private:
 			detail::check(dccrgx_create_with_exchange(rank_, size_, device, &detail::mpi_exchange, &comm_, &g_));
 		}
 		mapping_rw.attach(g_);
+		if (send_single_cells_) detail::check(dccrgx_set_send_single_cells(g_, 1));
 		geometry_rw.attach(g_);
 		geometry_rw.set(geometry_rw.get_params_or_default());
 	}
@@ -1514,6 +1522,7 @@ private:
 	int max_ref_ = 0;
 	unsigned hood_ = 1;
 	std::string lb_method_ = "RCB";
+	bool send_single_cells_ = false;
 	std::pair<size_t, size_t> window_{0, sizeof(Cell_Data)};
 	Grid_Topology topology_rw;
 	Mapping mapping_rw;

@@ -100,7 +100,13 @@ __global__ __launch_bounds__(kGolRows) void gol_csr_kernel(const uint32_t* __res
 // and the segment-edge columns are re-reads served by L2).  Blocks are
 // dealt to XCDs in contiguous runs of the (x segment, y, z chunk) order, so
 // the rows shared by vertically adjacent blocks stay in one XCD's L2.
-constexpr int G3_ROWS = 4;
+#ifndef DCCRGX_G3_ROWS
+#define DCCRGX_G3_ROWS 4
+#endif
+#ifndef DCCRGX_G3_DEPTH
+#define DCCRGX_G3_DEPTH 3
+#endif
+constexpr int G3_ROWS = DCCRGX_G3_ROWS;
 
 struct G3Plane {
 	uint4 m, c, p;  // rows y-1, y, y+1 at this lane's 4 x
@@ -1267,7 +1273,7 @@ bool k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 	               nbz = unsigned((n[2] + zc - 1) / zc);
 	const size_t nb = size_t(nbx) * nby * nbz;
 	const unsigned grid = unsigned((nb + 7) / 8 * 8);
-	gol_structured_v3<3><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1],
+	gol_structured_v3<DCCRGX_G3_DEPTH><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1],
 	                                                    per[2], zc, nbx, nby, unsigned(nb), lo, hi);
 	HIP_CHECK(hipGetLastError());
 	return true;

@@ -251,16 +251,18 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     nl = g.n_local
     kbar = g.neighbor_entries("of") / nl
     f1 = float(np.mean(lvl == 1))
-    # roofline bytes per leaf and step: SURVEY §8(d)'s fixed figure for the
-    # game of life on the CSR / AMR path, 8 B + 4 B per neighbor entry + 4 B
-    # row pointer.  The turn's geometric collect (gol_amr.hip) reads no
-    # neighbor entries: it moves far fewer bytes than that model (the PMC
-    # traffic beside it), so on this workload `frac` is the SURVEY-model
-    # bytes over the turn's kernel time, a throughput figure, not the share
-    # of HBM bandwidth the kernels draw.
+    # roofline: the bytes the turn's kernels must move per leaf (the geometric
+    # collect, gol_amr.hip: level-0 coordinates 4 B, octant 1 B, state read 4 B
+    # and written 4 B, mask written 4 B and read back 4 B) over the turn's
+    # kernel time: `achieved` / `frac` are a share of HBM bandwidth.  SURVEY
+    # §8(d)'s fixed CSR/AMR figure (8 B + 4 B per neighbor entry + 4 B row
+    # pointer) counts neighbor-entry reads this path does not make; it is
+    # reported beside it as model_throughput_GBs / frac_model, a throughput
+    # figure, not bandwidth.
     per_cell = 8 + 4 * kbar + 4
-    moved = 4 + 1 + 4 + 4 + 4 + 4  # l0 coords, octant, state (read, conditional write), mask (write, read)
-    ach = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
+    moved = 4 + 1 + 4 + 4 + 4 + 4
+    ach = moved * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
+    model = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
                      nl * a.steps / el, 1, a, el / a.steps * 1e3, "u32",
                      "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
@@ -268,14 +270,13 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                       "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
     line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS if ach else None,
-                        "traffic": measured_traffic("gol_amr", nl, per_cell * nl, 1),
+                        "traffic": measured_traffic("gol_amr", nl, moved * nl, 1),
                         "kernel": "geo_l0_leaves + geo_l0_groups + geo_collect + gol_amr_spread0_mask + "
                                   "gol_amr_spread_groups_mask",
-                        "alg_bytes_per_leaf": per_cell, "alg_bytes_model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
-                        "alg_bytes_per_step": per_cell * nl,
-                        "moved_bytes_per_leaf_min": moved,
-                        "frac_of_moved_bytes": (moved * nl * a.steps / (kms / 1e3) / 1e9 / PEAK_HBM_GBS
-                                                if kms > 0 else None),
+                        "alg_bytes_per_leaf": moved, "alg_bytes_per_step": moved * nl,
+                        "alg_bytes_model": "bytes the geometric collect moves per leaf",
+                        "model_bytes_per_leaf": per_cell, "model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
+                        "model_throughput_GBs": model, "frac_model": model / PEAK_HBM_GBS if model else None,
                         "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}
     line["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline("gol_amr", a.cpu_seconds)
     print(json.dumps(line), flush=True)

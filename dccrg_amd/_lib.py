@@ -43,6 +43,10 @@ _SIGS = {
     "dccrgx_set_initial_length": (C.c_int, [vp, P(u64)]),
     "dccrgx_set_maximum_refinement_level": (C.c_int, [vp, C.c_int]),
     "dccrgx_get_maximum_refinement_level": (C.c_int, [vp, P(C.c_int)]),
+    "dccrgx_get_neighborhood_length": (C.c_int, [vp, P(C.c_uint)]),
+    "dccrgx_get_initial_length": (C.c_int, [vp, vp]),
+    "dccrgx_get_periodic": (C.c_int, [vp, vp]),
+    "dccrgx_get_geometry": (C.c_int, [vp, vp, vp]),
     "dccrgx_set_periodic": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
     "dccrgx_set_neighborhood_length": (C.c_int, [vp, C.c_uint]),
     "dccrgx_initialize": (C.c_int, [vp]),
@@ -139,6 +143,7 @@ _SIGS = {
     "dccrgx_advection_commit": (C.c_int, [vp, C.c_int]),
     "dccrgx_advection_initialize": (C.c_int, [vp, P(C.c_int)]),
     "dccrgx_advection_max_time_step": (C.c_int, [vp, P(C.c_int), P(C.c_double)]),
+    "dccrgx_advection_max_time_step_device": (C.c_int, [vp, P(C.c_int), vp]),
     "dccrgx_advection_check_adaptation": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, C.c_double, vp]),
     "dccrgx_advection_adapt": (C.c_int, [vp, vp, vp]),
     "dccrgx_advection_refine_candidates": (C.c_int, [vp, C.c_int, C.c_double, C.c_double, vp, sz, P(sz)]),
@@ -148,6 +153,7 @@ _SIGS = {
                                        P(C.c_uint), P(C.c_double)]),
     "dccrgx_poisson_field": (C.c_int, [vp, C.c_char_p, P(C.c_int)]),
     "dccrgx_allreduce_f64": (C.c_int, [vp, P(C.c_double), C.c_int, C.c_int]),
+    "dccrgx_allreduce_f64_device": (C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
     "dccrgx_barrier": (C.c_int, [vp]),
     "dccrgx_comm_loopback": (C.c_int, [vp, C.c_int, sz, sz, sz]),
     "dccrgx_synchronize": (C.c_int, [vp]),

@@ -407,14 +407,9 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 	}
 	if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
 	if (mine) pwrite_all(fd, data.data(), data.size(), data0);
-	// the file ends where the last record ends: bytes of an older, longer
-	// file at this path must not extend the last record (a loader bounds it
-	// by the end of the file)
-	if (g.rank == 0) {
-		uint64_t all = 0;
-		for (int p = 0; p < g.size; p++) all += cnt[size_t(p)][1];
-		DX_REQUIRE(::ftruncate(fd, off_t(list0 + 16 * total + all)) == 0, "grid file truncate failed");
-	}
+	// no truncation: like the reference (MPI_MODE_CREATE | MPI_MODE_WRONLY,
+	// dccrg.hpp:1131), bytes already in the file past the grid data stay
+	// (ADVICE r04); a loader bounds the last record by the end of the file
 }
 
 // start_loading_grid_data (1795-2083): the grid block and the cell list; every
@@ -856,6 +851,22 @@ int dccrgx_set_initial_length(dccrgx_grid* gp, const uint64_t length[3]) {
 	});
 }
 
+int dccrgx_get_initial_length(dccrgx_grid* gp, uint64_t length[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		for (int d = 0; d < 3; d++) length[d] = g.len[d];
+		return 0;
+	});
+}
+
+int dccrgx_get_periodic(dccrgx_grid* gp, int periodic[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		for (int d = 0; d < 3; d++) periodic[d] = g.per[d] ? 1 : 0;
+		return 0;
+	});
+}
+
 int dccrgx_set_maximum_refinement_level(dccrgx_grid* gp, int level) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
@@ -872,6 +883,15 @@ int dccrgx_get_maximum_refinement_level(dccrgx_grid* gp, int* level) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		*level = g.R;
+		return 0;
+	});
+}
+
+int dccrgx_get_neighborhood_length(dccrgx_grid* gp, unsigned* length) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(length != nullptr, "null output");
+		*length = g.hood_len;
 		return 0;
 	});
 }
@@ -913,6 +933,17 @@ int dccrgx_set_geometry(dccrgx_grid* gp, const double start[3], const double l0[
 		for (int d = 0; d < 3; d++) {
 			g.start[d] = start[d];
 			g.l0[d] = l0[d];
+		}
+		return 0;
+	});
+}
+
+int dccrgx_get_geometry(dccrgx_grid* gp, double start[3], double l0[3]) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		for (int d = 0; d < 3; d++) {
+			if (start) start[d] = g.start[d];
+			if (l0) l0[d] = g.l0[d];
 		}
 		return 0;
 	});
@@ -1396,13 +1427,55 @@ static void flush_bulk_requests(Grid& g) {
 	g.unrefine_bulk.clear();
 }
 
+// whether the leaf `d` is one of neighbors_of(cell) in the default
+// neighborhood, for a `d` at least as large as the cell: it overlaps one of
+// the cell-sized boxes at the neighborhood's offsets (find_neighbors_of
+// 4339-4680 lists exactly the leaves overlapping those boxes)
+static bool in_neighbors_of(const Grid& g, uint64_t cell, uint64_t d) {
+	uint64_t c[3], o[3];
+	if (map_indices(g.m, cell, c[0], c[1], c[2]) < 0 || map_indices(g.m, d, o[0], o[1], o[2]) < 0) return false;
+	const uint64_t cl = map_cell_len(g.m, cell), dl = map_cell_len(g.m, d);
+	for (size_t k = 0; k + 2 < g.hood.size(); k += 3) {
+		bool hit = true;
+		for (int a = 0; a < 3 && hit; a++) {
+			uint64_t w = 0;
+			if (!map_wrap(g.m, a, int64_t(c[a]) + int64_t(g.hood[k + size_t(a)]) * int64_t(cl), w)) hit = false;
+			else hit = w < o[a] + dl && o[a] < w + cl;
+		}
+		if (hit) return true;
+	}
+	return false;
+}
+
+// refine_completely (2434-2530): only local leaves; at the maximum level it
+// is dont_unrefine (2472-2475); refused (false) when the cell, or a coarser
+// neighbor of it, is in the dont_refine set that persists from the last
+// stop_refining (2477-2491)
 int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
 		flush_bulk_requests(g);
 		if (!is_local_cell(g, cell)) return DCCRGX_ENOTFOUND;  // 2449-2459: only local cells
-		if (map_level(g.m, cell) >= g.R) return 0;                      // 2474-2477: no-op at max level
+		const int lvl = map_level(g.m, cell);
+		if (lvl >= g.R) {
+			// 2472-2475: dont_unrefine (2679-2733) and true
+			if (lvl == 0) return 0;
+			uint64_t sib[8];
+			map_siblings(g.m, cell, sib);
+			for (uint64_t s : sib)
+				if (g.dont_unrefine_cells.count(s)) return 0;
+			for (uint64_t s : sib) g.unrefine_requests.erase(s);
+			g.dont_unrefine_cells.insert(cell);
+			return 0;
+		}
+		if (!g.dont_refine_cells.empty()) {
+			if (g.dont_refine_cells.count(cell)) return DCCRGX_ENOTFOUND;
+			for (uint64_t d : g.dont_refine_cells)
+				if (map_level(g.m, d) >= 0 && map_level(g.m, d) < lvl && in_neighbors_of(g, cell, d) &&
+				    lookup_owner(g, d) >= 0)
+					return DCCRGX_ENOTFOUND;
+		}
 		g.refine_requests.insert(cell);
 		return 0;
 	});
@@ -1453,7 +1526,8 @@ int dccrgx_dont_unrefine(dccrgx_grid* gp, uint64_t cell) {
 }
 
 // dont_refine (2744-2784): the local leaf and, in stop_refining, its finer
-// neighbors (override_refines) are not refined by request
+// neighbors (override_refines) are not refined by request; the spread set
+// persists after stop_refining (10039) until balance_load clears it (3812)
 int dccrgx_dont_refine(dccrgx_grid* gp, uint64_t cell) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
@@ -2358,6 +2432,21 @@ int dccrgx_advection_max_time_step(dccrgx_grid* gp, const int fids[7], double* o
 	});
 }
 
+int dccrgx_advection_max_time_step_device(dccrgx_grid* gp, const int fids[7], double* d_out) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(d_out != nullptr, "null device pointer");
+		const double* f[7];
+		adv_fields(g, fids, f);
+		const size_t nb = 512;
+		g.dt_part.reserve(nb);
+		k_adv_dt(f, g.n_local, g.dt_part.p, nb, g.s_comp);
+		k_min_partials(g.dt_part.p, nb, d_out, g.s_comp);
+		comm_allreduce_f64_dev(g, d_out, d_out, 1, 1, g.s_comp);
+		return 0;
+	});
+}
+
 int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_increase, double diff_threshold,
                                        uint64_t* out, size_t cap, size_t* n) {
 	return guard([&] {
@@ -2563,6 +2652,15 @@ int dccrgx_allreduce_f64(dccrgx_grid* gp, double* v, int count, int op) {
 	});
 }
 
+int dccrgx_allreduce_f64_device(dccrgx_grid* gp, const double* d_in, double* d_out, int count, int op) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(count >= 0 && (count == 0 || (d_in && d_out)), "allreduce: null device buffer");
+		comm_allreduce_f64_dev(g, d_in, d_out, count, op, g.s_comp);
+		return 0;
+	});
+}
+
 int dccrgx_barrier(dccrgx_grid* gp) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
@@ -2581,6 +2679,7 @@ int dccrgx_comm_loopback(dccrgx_grid* gp, int field_id, size_t slot0, size_t n, 
 		DX_REQUIRE(!f.var, "loopback of a variable-size field");
 		DX_REQUIRE(slot0 + n <= g.n_slots && dst_slot0 + n <= g.n_slots, "slot range beyond the field");
 		DX_REQUIRE(slot0 + n <= dst_slot0 || dst_slot0 + n <= slot0, "overlapping slot ranges");
+		f.local_zero = false;  // the receive may land in local slots
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));  // the field's producers
 		comm_loopback(g, f.data.p + slot0 * f.elem, f.data.p + dst_slot0 * f.elem, n * f.elem, g.s_comm);
 		HIP_CHECK(hipStreamSynchronize(g.s_comm));

@@ -194,20 +194,56 @@ void rank_ordered_combine(const double* all, int P, int count, int op, double* o
 	}
 }
 
-// MPI_Allreduce on doubles (advection dt MIN, solve.hpp:317; sums): the
-// values all-gathered, then combined in rank order on every rank
+namespace {
+// the same rank-ordered combine on the device: one thread per value (the
+// host form above, operation for operation, so both give the same bits)
+__global__ void rank_combine_kernel(const double* __restrict__ all, int P, int count, int op, double* __restrict__ out) {
+#pragma clang fp contract(off)
+	const int k = int(blockIdx.x * blockDim.x + threadIdx.x);
+	if (k >= count) return;
+	double acc = all[k];
+	for (int p = 1; p < P; p++) {
+		const double x = all[size_t(p) * size_t(count) + size_t(k)];
+		if (op == 0) acc += x;
+		else if (op == 1) acc = fmin(acc, x);
+		else acc = fmax(acc, x);
+	}
+	out[k] = acc;
+}
+}  // namespace
+
+// MPI_Allreduce on device doubles, queued on `s`: the ranks' values
+// all-gathered into a device buffer, then combined in rank order by one small
+// kernel on every rank.  Over RCCL nothing waits on the host (the reduction
+// is stream-ordered and can sit between two kernels of an iteration); the
+// host exchange has to stage through the host and returns with the result
+// on the device.  d_in and d_out may be the same buffer.
+void comm_allreduce_f64_dev(Grid& g, const double* d_in, double* d_out, int count, int op, hipStream_t s) {
+	if (count <= 0) return;
+	const size_t bytes = size_t(count) * 8;
+	if (g.size == 1) {
+		if (d_in != d_out) HIP_CHECK(hipMemcpyAsync(d_out, d_in, bytes, hipMemcpyDeviceToDevice, s));
+		return;
+	}
+	comm_require(g, "allreduce");
+	DX_REQUIRE(op >= 0 && op <= 2, "allreduce: op must be 0 (sum), 1 (min) or 2 (max)");
+	g.red_all.reserve(size_t(count) * size_t(g.size));
+	comm_allgather_dev(g, d_in, bytes, reinterpret_cast<uint8_t*>(g.red_all.p), s);
+	rank_combine_kernel<<<unsigned((count + 63) / 64), 64, 0, s>>>(g.red_all.p, g.size, count, op, d_out);
+	HIP_CHECK(hipGetLastError());
+}
+
+// MPI_Allreduce on host doubles (advection dt MIN, solve.hpp:317; sums): up,
+// the device form, down
 void comm_allreduce_f64(Grid& g, double* v, int count, int op) {
 	if (g.size == 1 || count <= 0) return;
-	comm_require(g, "allreduce");
 	hipStream_t s = g.s_comm;
-	const size_t bytes = size_t(count) * 8;
-	DBuf<double> mine, all;
-	mine.alloc(size_t(count));
-	all.alloc(size_t(count) * size_t(g.size));
-	HIP_CHECK(hipMemcpyAsync(mine.p, v, bytes, hipMemcpyHostToDevice, s));
-	comm_allgather_dev(g, mine.p, bytes, reinterpret_cast<uint8_t*>(all.p), s);
-	const std::vector<double> h = download(all.p, all.n, s);
-	rank_ordered_combine(h.data(), g.size, count, op, v);
+	DBuf<double> d;
+	d.alloc(size_t(count));
+	HIP_CHECK(hipMemcpyAsync(d.p, v, size_t(count) * 8, hipMemcpyHostToDevice, s));
+	comm_allreduce_f64_dev(g, d.p, d.p, count, op, s);
+	HIP_CHECK(hipMemcpyAsync(v, d.p, size_t(count) * 8, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 uint64_t comm_allreduce_max_u64(Grid& g, uint64_t v) {

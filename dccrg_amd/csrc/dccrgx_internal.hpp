@@ -456,6 +456,8 @@ struct Grid {
 	DBuf<uint64_t> removed_ids_d;               // the same on the device when n > 0, else empty
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;
+	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev
+	DBuf<double> dt_part;  // block minima of dccrgx_advection_max_time_step_device
 
 	// local layout
 	size_t n_inner = 0, n_outer = 0, n_local = 0, n_recv = 0, n_slots = 0;
@@ -553,6 +555,8 @@ std::vector<std::vector<uint8_t>> comm_exchange(Grid& g, const std::vector<std::
 std::vector<std::vector<uint64_t>> comm_allgather_u64(Grid& g, const std::vector<uint64_t>& mine);
 std::vector<std::vector<uint64_t>> comm_alltoall_u64(Grid& g, const std::vector<std::vector<uint64_t>>& send);
 void comm_allreduce_f64(Grid& g, double* v, int count, int op);  // 0 sum, 1 min, 2 max
+// the same on device values, queued on s (stream-ordered over RCCL)
+void comm_allreduce_f64_dev(Grid& g, const double* d_in, double* d_out, int count, int op, hipStream_t s);
 uint64_t comm_allreduce_max_u64(Grid& g, uint64_t v);
 // device payloads: per peer one message of known size each way
 struct DevMsg {
@@ -736,6 +740,7 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 // (run 0 inner, 1 outer: tiles never straddle the two)
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
+void k_min_partials(const double* partial, size_t n, double* out, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
                         double diff_increase, double diff_threshold, uint64_t* out, hipStream_t s);
 // adaptation of tests/advection/adapter.hpp: per local cell band (2 refine,

@@ -488,8 +488,11 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
 	std::vector<uint64_t> D = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_refine_cells))));
-	g.dont_refine_cells.clear();
 	if (!D.empty()) close_set(g, D, true);
+	// cells_not_to_refine = old_donts (10039-10040): the spread set, the same
+	// on every rank, stays for the next stop_refining and refine_completely
+	// (2477-2491) until balance_load (3812)
+	g.dont_refine_cells = std::unordered_set<uint64_t>(D.begin(), D.end());
 	DX_LAP("sr.1_override_refines");
 	std::vector<uint64_t> mine;
 	{
@@ -774,6 +777,8 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 			if (po[i] != g.rank) dest[pc[i]] = po[i];
 	}
 	g.weights.clear();
+	g.dont_refine_cells.clear();    // cells_not_to_refine (3812)
+	g.dont_unrefine_cells.clear();  // cells_not_to_unrefine (3813)
 	g.removed_ids_h.clear();  // unrefined_cell_data (3811)
 	g.removed_ids_d.release();
 	for (auto& f : g.fields) {

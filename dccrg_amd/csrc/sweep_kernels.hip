@@ -1340,6 +1340,29 @@ void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblock
 	HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+// the minimum of n partial minima into out[0] (one block; fmin is exact, so
+// the order does not matter)
+__global__ __launch_bounds__(256) void min_partials_kernel(const double* __restrict__ part, size_t n,
+                                                           double* __restrict__ out) {
+	__shared__ double red[256];
+	double mn = 1.7976931348623157e308;
+	for (size_t i = threadIdx.x; i < n; i += 256) mn = fmin(mn, part[i]);
+	red[threadIdx.x] = mn;
+	__syncthreads();
+	for (int k = 128; k > 0; k >>= 1) {
+		if (int(threadIdx.x) < k) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + k]);
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) out[0] = red[0];
+}
+}  // namespace
+
+void k_min_partials(const double* partial, size_t n, double* out, hipStream_t s) {
+	min_partials_kernel<<<1, 256, 0, s>>>(partial, n, out);
+	HIP_CHECK(hipGetLastError());
+}
+
 void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
                  double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
                  hipStream_t s) {

@@ -28,6 +28,15 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
+def _dev_ptr(t):
+    """A device address: an int, or a CUDA (HIP) float64 torch tensor's data."""
+    if isinstance(t, int):
+        return C.c_void_p(t)
+    if not (getattr(t, "is_cuda", False) and str(t.dtype) == "torch.float64" and t.is_contiguous()):
+        raise TypeError("expected a contiguous float64 tensor on the GPU (or a device address)")
+    return C.c_void_p(t.data_ptr())
+
+
 class Field:
     """One SoA payload array over all slots (local cells, then remote copies)."""
 
@@ -841,6 +850,12 @@ class Dccrg:
         check(lib().dccrgx_advection_max_time_step(self.h, self._fids(fields), C.byref(v)))
         return self.allreduce(v.value, "min")
 
+    def advection_max_time_step_device(self, fields, out):
+        """max_time_step reduced over all ranks into device memory `out` (a
+        float64 torch tensor on the GPU, or a device address), queued on the
+        compute stream: no host round trip over RCCL."""
+        check(lib().dccrgx_advection_max_time_step_device(self.h, self._fids(fields), _dev_ptr(out)))
+
     def advection_layout(self):
         """Tile layout of the advection sweep and its algorithmic HBM bytes per
         sweep over all local cells (see include/dccrgx.h)."""
@@ -873,6 +888,17 @@ class Dccrg:
         v = C.c_double(float(value))
         check(lib().dccrgx_allreduce_f64(self.h, C.byref(v), 1, {"sum": 0, "min": 1, "max": 2}[op]))
         return v.value
+
+    def allreduce_device(self, src, dst=None, op="sum"):
+        """MPI_Allreduce of `count` device doubles (torch tensors or device
+        addresses; dst defaults to src), stream-ordered on the compute stream,
+        combined in rank order (bitwise allreduce()'s result)."""
+        n = int(src.numel()) if hasattr(src, "numel") else None
+        if n is None:
+            raise TypeError("allreduce_device needs a torch tensor (its element count)")
+        d = src if dst is None else dst
+        check(lib().dccrgx_allreduce_f64_device(self.h, _dev_ptr(src), _dev_ptr(d), n,
+                                                {"sum": 0, "min": 1, "max": 2}[op]))
 
     def barrier(self):
         check(lib().dccrgx_barrier(self.h))

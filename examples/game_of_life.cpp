@@ -42,34 +42,30 @@ int main(int argc, char* argv[])
 	{
 		dccrg::Dccrg<game_of_life_cell> grid;
 		grid.set_initial_length({500, 500, 1}).set_neighborhood_length(1).set_maximum_refinement_level(0);
+		grid.set_host_staging(false);  // the state lives in a device field, not in Cell_Data
 		grid.initialize(MPI_COMM_WORLD);
 		rank = grid.get_rank();
-		dccrgx_grid* g = grid.native();
-		const int state = grid.add_field<uint32_t>("is_alive", true);
-		// the device field in slot order
-		const auto slots = dccrg::detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) {
-			return dccrgx_get_slot_ids(g, o, c, n);
-		});
-		size_t ni = 0, no = 0;
-		dccrg::detail::check(dccrgx_get_counts(g, &ni, &no, nullptr, nullptr));
-		std::vector<uint32_t> alive(ni + no);
+		// the state as a device field (facade members, no raw C calls)
+		const auto state = grid.add_field<uint32_t>("is_alive", true);
+		const auto slots = grid.get_slot_ids();
+		std::vector<uint32_t> alive(grid.get_number_of_local_slots());
 		for (size_t s = 0; s < alive.size(); s++) alive[s] = alive0(slots[s]);
-		dccrg::detail::check(dccrgx_field_upload(g, state, 0, alive.size(), alive.data()));
+		state.set(alive);
 
 		MPI_Barrier(MPI_COMM_WORLD);
 		const auto t0 = std::chrono::high_resolution_clock::now();
 		for (int turn = 0; turn < turns; turn++) {
-			dccrg::detail::check(dccrgx_start_remote_neighbor_copy_updates(g));
-			dccrg::detail::check(dccrgx_gol_step(g, state, DCCRGX_REGION_INNER));
-			dccrg::detail::check(dccrgx_wait_remote_neighbor_copy_update_receives(g));
-			dccrg::detail::check(dccrgx_gol_step(g, state, DCCRGX_REGION_OUTER));
-			dccrg::detail::check(dccrgx_wait_remote_neighbor_copy_update_sends(g));
-			dccrg::detail::check(dccrgx_gol_commit(g, state));
+			grid.start_remote_neighbor_copy_updates();
+			grid.gol_step(state, DCCRGX_REGION_INNER);
+			grid.wait_remote_neighbor_copy_update_receives();
+			grid.gol_step(state, DCCRGX_REGION_OUTER);
+			grid.wait_remote_neighbor_copy_update_sends();
+			grid.gol_commit(state);
 		}
-		dccrg::detail::check(dccrgx_synchronize(g));
+		grid.synchronize();
 		MPI_Barrier(MPI_COMM_WORLD);
 		seconds = std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
-		dccrg::detail::check(dccrgx_field_download(g, state, 0, alive.size(), alive.data()));
+		alive = state.get(alive.size());
 		uint64_t mine = 0, n = alive.size();
 		for (auto a : alive) mine += a;
 		MPI_Reduce(&mine, &live, 1, MPI_UINT64_T, MPI_SUM, 0, MPI_COMM_WORLD);

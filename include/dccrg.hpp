@@ -62,6 +62,7 @@
 #include <utility>
 #include <vector>
 
+#include "dccrg_get_cell_datatype.hpp"
 #include "dccrgx.h"
 
 namespace dccrg {
@@ -91,36 +92,19 @@ std::vector<uint64_t> fetch_u64(F&& f) {
 	return v;
 }
 
-// get_mpi_datatype dispatch (dccrg_get_cell_datatype.hpp:40-340): the
-// zero-argument member, or the five-argument one, or the whole object
+// get_mpi_datatype dispatch: the reference's get_cell_mpi_datatype
+// (include/dccrg_get_cell_datatype.hpp): a five-argument member before a
+// zero-argument one, a named MPI type for arithmetic cells, else the bytes
 template <class T>
-auto call_datatype(T& c, int) -> decltype(c.get_mpi_datatype()) {
-	return c.get_mpi_datatype();
-}
-template <class T>
-auto call_datatype(T& c, long) -> decltype(c.get_mpi_datatype(uint64_t(0), 0, 0, false, 0)) {
-	return c.get_mpi_datatype(error_cell, 0, 0, false, default_neighborhood_id);
-}
-template <class T>
-std::tuple<void*, int, MPI_Datatype> call_datatype(T& c, ...) {
-	return std::make_tuple((void*)&c, int(sizeof(T)), MPI_BYTE);
+mpi_transfer_t call_datatype(T& c, int) {
+	return get_cell_mpi_datatype(c, error_cell, 0, 0, false, default_neighborhood_id);
 }
 
 // the datatype of one cell for a transfer (the five-argument member gets the
 // cell, the processes and the direction, dccrg_get_cell_datatype.hpp:68-340)
 template <class T>
-auto cell_datatype(T& c, uint64_t, int, int, bool, int, int) -> decltype(c.get_mpi_datatype()) {
-	return c.get_mpi_datatype();
-}
-template <class T>
-auto cell_datatype(T& c, uint64_t cell, int sender, int receiver, bool receiving, int hood, long)
-    -> decltype(c.get_mpi_datatype(uint64_t(0), 0, 0, false, 0)) {
-	return c.get_mpi_datatype(cell, sender, receiver, receiving, hood);
-}
-
-template <class T>
-std::tuple<void*, int, MPI_Datatype> cell_datatype(T& c, uint64_t, int, int, bool, int, ...) {
-	return std::make_tuple((void*)&c, int(sizeof(T)), MPI_BYTE);
+mpi_transfer_t cell_datatype(T& c, uint64_t cell, int sender, int receiver, bool receiving, int hood, int) {
+	return get_cell_mpi_datatype(c, cell, sender, receiver, receiving, hood);
 }
 
 inline bool is_named_datatype(MPI_Datatype t) {
@@ -338,6 +322,16 @@ public:
 	struct Parameters {};
 	static constexpr int geometry_id = 0;
 	void attach(dccrgx_grid* g) { g_ = g; }
+	Parameters get() const { return {}; }
+	// parameters the library read from a grid file (load_grid_data)
+	void sync_from_library() {}
+	// the grid's length in level-0 cells and its periodicity, for geometries
+	// that size their parameters by them (Stretched_Cartesian_Geometry, whose
+	// parameters may be set before initialize)
+	void attach_parts(const Grid_Length* l, const Grid_Topology* t) {
+		length_ = l;
+		topology_ = t;
+	}
 	bool set(const Parameters&) { return true; }
 	std::array<double, 3> get_length(uint64_t cell) const { return batch(cell, false); }
 	std::array<double, 3> get_center(uint64_t cell) const { return batch(cell, true); }
@@ -349,6 +343,8 @@ protected:
 		return center ? c : L;
 	}
 	dccrgx_grid* g_ = nullptr;
+	const Grid_Length* length_ = nullptr;
+	const Grid_Topology* topology_ = nullptr;
 };
 
 struct Cartesian_Geometry_Parameters {
@@ -364,6 +360,9 @@ public:
 		return !g_ || dccrgx_set_geometry(g_, p.start.data(), p.level_0_cell_length.data()) == DCCRGX_OK;
 	}
 	const Parameters& get() const { return p_; }
+	void sync_from_library() {
+		if (g_) dccrgx_get_geometry(g_, p_.start.data(), p_.level_0_cell_length.data());
+	}
 	std::array<double, 3> get_start() const { return p_.start; }
 	std::array<double, 3> get_level_0_cell_length() const { return p_.level_0_cell_length; }
 	std::array<double, 3> get_min(uint64_t cell) const {
@@ -386,6 +385,49 @@ struct Iterator_Storage {  // dccrg.hpp:7279-7285
 	typename std::vector<T>::const_iterator cbegin() const { return begin_; }
 	typename std::vector<T>::const_iterator end() const { return end_; }
 	typename std::vector<T>::const_iterator cend() const { return end_; }
+};
+
+// A device-resident SoA field of the library (one T per slot: local cells in
+// slot order, then the copies of remote neighbors), the form the device
+// sweeps read and write.  Handles are cheap values; the array itself moves
+// on a structural change (refinement, balance_load), so data() asks the
+// library each time.  Converts to the field id of the C ABI.
+template <class T>
+class Device_Field {
+public:
+	Device_Field() = default;
+	Device_Field(dccrgx_grid* g, int id) : g_(g), id_(id) {}
+	int id() const { return id_; }
+	operator int() const { return id_; }
+	// the device array (valid until the next structural change)
+	T* data() const {
+		void* p = nullptr;
+		detail::check(dccrgx_field_device_ptr(g_, id_, &p));
+		return static_cast<T*>(p);
+	}
+	// slots [slot0, slot0 + n) to / from the host
+	void upload(const T* host, size_t n, size_t slot0 = 0) const {
+		detail::check(dccrgx_field_upload(g_, id_, slot0, n, host));
+	}
+	void download(T* host, size_t n, size_t slot0 = 0) const {
+		detail::check(dccrgx_field_download(g_, id_, slot0, n, host));
+	}
+	void set(const std::vector<T>& v, size_t slot0 = 0) const { upload(v.data(), v.size(), slot0); }
+	std::vector<T> get(size_t n, size_t slot0 = 0) const {
+		std::vector<T> v(n);
+		if (n) download(v.data(), n, slot0);
+		return v;
+	}
+
+private:
+	dccrgx_grid* g_ = nullptr;
+	int id_ = -1;
+};
+
+// dccrgx_poisson_solve's outcome (Poisson_Solve::solve, poisson_solve.hpp:251-522)
+struct Poisson_Result {
+	unsigned iterations = 0;
+	double residual = 0;
 };
 
 template <class Cell_Data, class Geometry = No_Geometry, class Additional_Cell_Items = std::tuple<>,
@@ -439,7 +481,7 @@ public:
 	const std::vector<Cells_Item>& cells = cells_rw;
 	const std::vector<Neighbors_Item>& neighbors = neighbors_rw;
 
-	Dccrg() = default;
+	Dccrg() { geometry_rw.attach_parts(&mapping_rw.length, &topology_rw); }
 	Dccrg(const Dccrg&) = delete;
 	Dccrg& operator=(const Dccrg&) = delete;
 	~Dccrg() {
@@ -662,18 +704,14 @@ public:
 
 	// ---- halo (966-1000, 5010-5367) -------------------------------------------------
 	bool update_copies_of_remote_neighbors(const int neighborhood_id = default_neighborhood_id) {
-		dump_initial();
-		sync_window();
-		upload_local();
+		stage_up();
 		if (dccrgx_update_copies_of_remote_neighbors_hood(g_, neighborhood_id) != DCCRGX_OK) return false;
-		download_remote();
+		if (staging_) download_remote();
 		return true;
 	}
 	bool start_remote_neighbor_copy_updates(const int neighborhood_id = default_neighborhood_id) {
 		if (neighborhood_id != default_neighborhood_id) return update_copies_of_remote_neighbors(neighborhood_id);
-		dump_initial();
-		sync_window();
-		upload_local();
+		stage_up();
 		return dccrgx_start_remote_neighbor_copy_updates(g_) == DCCRGX_OK;
 	}
 	bool start_remote_neighbor_copy_receives(const int neighborhood_id = default_neighborhood_id) {
@@ -682,9 +720,19 @@ public:
 	bool start_remote_neighbor_copy_sends(const int = default_neighborhood_id) { return true; }
 	bool wait_remote_neighbor_copy_update_receives(const int = default_neighborhood_id) {
 		if (dccrgx_wait_remote_neighbor_copy_update_receives(g_) != DCCRGX_OK) return false;
-		download_remote();
+		if (staging_) download_remote();
 		return true;
 	}
+	// The halo calls stage the host Cell_Data (every local payload up, the
+	// received copies down; default on, the reference's semantics).  A
+	// program whose per-cell state lives in device fields turns it off: the
+	// halo then moves only the transferred device fields, with no host copy.
+	Dccrg& set_host_staging(const bool on) {
+		staging_ = on;
+		if (g_ && payload_ >= 0) detail::check(dccrgx_set_field_transfer(g_, payload_, on ? 1 : 0));
+		return *this;
+	}
+	bool get_host_staging() const { return staging_; }
 	bool wait_remote_neighbor_copy_update_sends(const int = default_neighborhood_id) {
 		return dccrgx_wait_remote_neighbor_copy_update_sends(g_) == DCCRGX_OK;
 	}
@@ -988,19 +1036,119 @@ public:
 		return true;
 	}
 
-	// ---- device SoA fields --------------------------------------------------------------
+	// ---- device SoA fields and the device sweeps -------------------------------------------
+	// The host-staged Cell_Data path above moves every local payload to the
+	// device and back at each halo; a program whose per-cell loops run on the
+	// GPU keeps its state in device fields instead and calls the sweeps below
+	// (no native() or raw C calls needed).  A transferred field takes part in
+	// every halo of the default neighborhood.
 	template <class T>
-	int add_field(const std::string& name, bool transfer) {
+	Device_Field<T> add_field(const std::string& name, bool transfer) {
 		int id = -1;
 		detail::check(dccrgx_add_field(g_, name.c_str(), sizeof(T), transfer ? 1 : 0, &id));
-		return id;
+		return Device_Field<T>(g_, id);
 	}
 	int payload_field() const { return payload_; }
 	// host Cell_Data <-> device payload field
 	void upload() { upload_all(); }
 	void download() { download_all(); }
+	// slot -> cell id of every slot (local cells first, in slot order)
+	std::vector<uint64_t> get_slot_ids() const {
+		return detail::fetch_u64([&](uint64_t* o, size_t c, size_t* n) { return dccrgx_get_slot_ids(g_, o, c, n); });
+	}
+	size_t get_number_of_local_slots() const { return n_local_; }
+	// the compute stream's work done
+	void synchronize() const { detail::check(dccrgx_synchronize(g_)); }
+
+	// game of life over cell.neighbors_of (examples/game_of_life.cpp:54-79):
+	// `region` DCCRGX_REGION_ALL / _INNER / _OUTER; commit makes the new
+	// states current
+	void gol_step(const Device_Field<uint32_t>& state, const int region = DCCRGX_REGION_ALL) {
+		detail::check(dccrgx_gol_step(g_, state.id(), region));
+	}
+	void gol_commit(const Device_Field<uint32_t>& state) { detail::check(dccrgx_gol_commit(g_, state.id())); }
+	// one turn of the refined game (tests/game_of_life/solve.hpp:37-170);
+	// list: 8 x uint64 per cell (Cell_Data::data[1..8])
+	void get_live_neighbors(const Device_Field<uint32_t>& state, const Device_Field<std::array<uint64_t, 8>>& list) {
+		detail::check(dccrgx_get_live_neighbors(g_, state.id(), list.id()));
+	}
+
+	// advection (tests/advection): fields density, vx, vy, vz, lx, ly, lz
+	using Advection_Fields = std::array<Device_Field<double>, 7>;
+	void advection_initialize(const Advection_Fields& f) {  // initialize.hpp:36-82
+		const auto id = ids(f);
+		detail::check(dccrgx_advection_initialize(g_, id.data()));
+	}
+	double advection_max_time_step(const Advection_Fields& f) {  // solve.hpp:289-333, MIN over processes
+		const auto id = ids(f);
+		double v = 0;
+		detail::check(dccrgx_advection_max_time_step(g_, id.data(), &v));
+		detail::check(dccrgx_allreduce_f64(g_, &v, 1, 1));
+		return v;
+	}
+	// the same into device memory, stream-ordered (no host round trip over RCCL)
+	void advection_max_time_step(const Advection_Fields& f, double* device_out) {
+		const auto id = ids(f);
+		detail::check(dccrgx_advection_max_time_step_device(g_, id.data(), device_out));
+	}
+	void advection_step(const Advection_Fields& f, const double dt, const int region = DCCRGX_REGION_ALL) {
+		const auto id = ids(f);  // calculate_fluxes + apply_fluxes (solve.hpp:44-279)
+		detail::check(dccrgx_advection_step(g_, id.data(), dt, region));
+	}
+	void advection_commit(const Device_Field<double>& density) {
+		detail::check(dccrgx_advection_commit(g_, density.id()));
+	}
+	// check_for_adaptation + adapt_grid (adapter.hpp:47-309); returns the
+	// accepted (refines, dont_unrefines, unrefines) and (created, removed)
+	std::array<uint64_t, 3> advection_check_adaptation(const Device_Field<double>& density, const double diff_increase,
+	                                                   const double diff_threshold = 0.25,
+	                                                   const double unrefine_sensitivity = 0.5) {
+		std::array<uint64_t, 3> c{{0, 0, 0}};
+		detail::check(dccrgx_advection_check_adaptation(g_, density.id(), diff_increase, diff_threshold,
+		                                                unrefine_sensitivity, c.data()));
+		return c;
+	}
+	std::array<uint64_t, 2> advection_adapt(const Advection_Fields& f) {
+		const auto id = ids(f);
+		std::array<uint64_t, 2> out{{0, 0}};
+		detail::check(dccrgx_advection_adapt(g_, id.data(), out.data()));
+		after_device_change();
+		return out;
+	}
+
+	// Poisson (tests/poisson/poisson_solve.hpp): cache_system_info (827-971)
+	// for the given cells, then solve (251-522) or solve_failsafe (531-634)
+	void poisson_cache(const Device_Field<double>& rhs, const Device_Field<double>& solution,
+	                   const std::vector<uint64_t>& solve_cells, const std::vector<uint64_t>& skip_cells = {}) {
+		detail::check(dccrgx_poisson_cache(g_, rhs.id(), solution.id(), solve_cells.data(), solve_cells.size(),
+		                                   skip_cells.data(), skip_cells.size()));
+	}
+	Poisson_Result poisson_solve(const unsigned max_iterations = 1000, const unsigned min_iterations = 0,
+	                             const double stop_residual = 1e-15, const double p_of_norm = 2,
+	                             const double stop_after_residual_increase = 10, const bool failsafe = false) {
+		Poisson_Result r;
+		detail::check(dccrgx_poisson_solve(g_, max_iterations, min_iterations, stop_residual, p_of_norm,
+		                                   stop_after_residual_increase, failsafe ? 1 : 0, &r.iterations, &r.residual));
+		return r;
+	}
 
 private:
+	void stage_up() {
+		if (!staging_) return;
+		dump_initial();
+		sync_window();
+		upload_local();
+	}
+	static std::array<int, 7> ids(const std::array<Device_Field<double>, 7>& f) {
+		std::array<int, 7> r;
+		for (size_t k = 0; k < 7; k++) r[k] = f[k].id();
+		return r;
+	}
+	// the mesh changed under a device call (adaptation): the host side follows
+	void after_device_change() {
+		clear_removed();
+		refresh();
+	}
 	// DCCRGX_DUMP_CELLS=<path>: every rank writes its local cells (uint64 id +
 	// Cell_Data bytes, ascending id) to <path>.initial.<rank> at the first
 	// remote neighbor update and to <path>.final.<rank> when the grid is
@@ -1045,6 +1193,21 @@ private:
 		int R = 0;
 		detail::check(dccrgx_get_maximum_refinement_level(g_, &R));
 		max_ref_ = R;
+		// the neighborhood length stored in the file: the
+		// default neighborhood's offsets follow it
+		unsigned L = 0;
+		detail::check(dccrgx_get_neighborhood_length(g_, &L));
+		hood_ = L;
+		hood_set_ = ~0u;
+		{
+			int per[3] = {0, 0, 0};
+			detail::check(dccrgx_get_periodic(g_, per));
+			for (size_t d = 0; d < 3; d++) topology_rw.set_periodicity(d, per[d] != 0);
+			uint64_t len[3] = {1, 1, 1};
+			detail::check(dccrgx_get_initial_length(g_, len));
+			mapping_rw.length.set({{len[0], len[1], len[2]}});
+		}
+		geometry_rw.sync_from_library();
 		refresh();
 		return true;
 	}
@@ -1086,10 +1249,10 @@ private:
 	}
 	void add_payload_field() {
 		if constexpr (serialized_) {
-			detail::check(dccrgx_add_variable_field(g_, "Cell_Data", 1, &payload_));
+			detail::check(dccrgx_add_variable_field(g_, "Cell_Data", staging_ ? 1 : 0, &payload_));
 			return;
 		}
-		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), 1, &payload_));
+		detail::check(dccrgx_add_field(g_, "Cell_Data", sizeof(Cell_Data), staging_ ? 1 : 0, &payload_));
 		const auto w = detail::datatype_window<Cell_Data>();
 		detail::check(dccrgx_set_field_window(g_, payload_, w.first, w.second));
 		window_ = w;
@@ -1419,13 +1582,15 @@ private:
 		rg[2] = {cat(0), cat(nl)};
 		rg[3] = {cat(nl), cat(ns)};
 		rg[4] = {cat(0), cat(ns)};
-		// Additional_*_Items hooks (7318-7339, 7387-7401)
-		for (size_t k = 0; k < nl; k++) {
+		// Additional_*_Items hooks (7318-7339, 7387-7401), for every item the
+		// reference builds one for (local and remote cells, 11405-11409, and
+		// each neighbor item, 11504-11516), with default-constructed arguments
+		for (size_t k = 0; k < ns; k++) {
 			Cells_Item& c = items[k];
-			c.update_caller(*this, static_cast<const Additional_Cell_Items&>(c)...);
+			c.update_caller(*this, Additional_Cell_Items()...);
 			for (size_t i = size_t(c.all_neighbors.begin_ - nbrs.cbegin()); i < size_t(c.all_neighbors.end_ - nbrs.cbegin());
 			     i++)
-				nbrs[i].update_caller(*this, c, hood, static_cast<const Additional_Neighbor_Items&>(nbrs[i])...);
+				nbrs[i].update_caller(*this, c, hood, Additional_Neighbor_Items()...);
 		}
 	}
 
@@ -1509,6 +1674,10 @@ private:
 	// geometry parameters survive create() (set_geometry may come first)
 	struct GeometryHolder : Geometry {
 		typename Geometry::Parameters get_params_or_default() const { return params_; }
+		void sync_from_library() {
+			Geometry::sync_from_library();
+			params_ = Geometry::get();
+		}
 		bool set(const typename Geometry::Parameters& p) {
 			params_ = p;
 			return Geometry::set(p);
@@ -1523,6 +1692,7 @@ private:
 	unsigned hood_ = 1;
 	std::string lb_method_ = "RCB";
 	bool send_single_cells_ = false;
+	bool staging_ = true;  // set_host_staging
 	std::pair<size_t, size_t> window_{0, sizeof(Cell_Data)};
 	Grid_Topology topology_rw;
 	Mapping mapping_rw;

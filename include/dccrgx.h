@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 7 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 8 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -90,6 +90,13 @@ int dccrgx_set_maximum_refinement_level(dccrgx_grid* g, int level);        /* 81
 int dccrgx_set_periodic(dccrgx_grid* g, int x, int y, int z);              /* 8183 */
 int dccrgx_set_neighborhood_length(dccrgx_grid* g, unsigned length);       /* 8206 */
 int dccrgx_get_maximum_refinement_level(dccrgx_grid* g, int* level);
+/* the setup as the library holds it, e.g. after load_grid_data read it from
+ * a file: length in level-0 cells, periodicity (ABI 8) */
+int dccrgx_get_initial_length(dccrgx_grid* g, uint64_t length[3]);
+int dccrgx_get_periodic(dccrgx_grid* g, int periodic[3]);
+/* get_neighborhood_length (6725): the length set, or read from a grid file
+ * by load_grid_data (ABI 8) */
+int dccrgx_get_neighborhood_length(dccrgx_grid* g, unsigned* length);
 /* initialize(): level-0 cells, block partition (create_level_0_cells
  * 7967-8102), device neighbor build (initialize_neighbors 8240-8289 and
  * update_remote_neighbor_info / send-receive lists 8590-9309).  472 */
@@ -100,6 +107,9 @@ int dccrgx_set_geometry(dccrgx_grid* g, const double start[3], const double leve
 /* Cartesian_Geometry::get_center / get_length (dccrg_cartesian_geometry.hpp:
  * 282-362) of n cells: 3 doubles per cell each (either output may be NULL);
  * NaN for invalid ids */
+/* Cartesian_Geometry::get_start / get_level_0_cell_length (ABI 8); either
+ * output may be NULL */
+int dccrgx_get_geometry(dccrgx_grid* g, double start[3], double level_0_cell_length[3]);
 int dccrgx_geometry_batch(dccrgx_grid* g, const uint64_t* ids, size_t n, double* center, double* length);
 
 /* ---- mapping (dccrg_mapping.hpp) — host-side scalar queries -------------- */
@@ -262,7 +272,11 @@ int dccrgx_load_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, siz
  * field its window (sizes NULL), a variable-size field sizes[s] bytes for
  * local slot s (its cells take those sizes); a request beyond a record's end
  * returns DCCRGX_EINVAL.  bytes_left: per local slot, the unread bytes of its
- * record.  Nothing else may change the grid between start and finish. */
+ * record.  Nothing else may change the grid between start and finish.
+ * save_grid_data does not truncate the file (the reference does not
+ * either), so the last record of a file is bounded by the end of the file:
+ * bytes after the grid data (an older, longer file at the same path, or the
+ * caller's own) count toward that record's bytes_left. */
 int dccrgx_start_loading_grid_data(dccrgx_grid* g, const char* path, uint64_t offset, size_t header_bytes);
 int dccrgx_continue_loading_grid_data(dccrgx_grid* g, int field_id, const uint64_t* sizes);
 int dccrgx_finish_loading_grid_data(dccrgx_grid* g);
@@ -321,6 +335,13 @@ int dccrgx_set_field_transfer(dccrgx_grid* g, int field_id, int transfer);
 /* the bytes of each element the halo carries: [offset, offset + bytes) (what
  * Cell_Data::get_mpi_datatype describes; default: the whole element) */
 int dccrgx_set_field_window(dccrgx_grid* g, int field_id, size_t offset, size_t bytes);
+/* the field's device array (slot order).  The pointer stays valid until the
+ * next structural change (refinement, balance_load, loading a file).  Writes
+ * made through it are seen by every call; the library's own bookkeeping of a
+ * field's contents (e.g. dccrgx_get_live_neighbors' record that the list
+ * field's inner rows are already zero) is reset only when this function is
+ * called, so a program that writes through a pointer it fetched earlier
+ * fetches it again after such writes. */
 int dccrgx_field_device_ptr(dccrgx_grid* g, int field_id, void** ptr);
 /* host <-> device copies of whole slot ranges [slot0, slot0+n) */
 int dccrgx_field_upload(dccrgx_grid* g, int field_id, size_t slot0, size_t n, const void* host);
@@ -418,6 +439,11 @@ int dccrgx_advection_commit(dccrgx_grid* g, int density_field);
  * and max_time_step (solve.hpp:289-333, local part; caller reduces MIN) */
 int dccrgx_advection_initialize(dccrgx_grid* g, const int fields[7]);
 int dccrgx_advection_max_time_step(dccrgx_grid* g, const int fields[7], double* local_min);
+/* the same, reduced over all processes (MIN in rank order, solve.hpp:317),
+ * written to DEVICE memory d_out[0] in stream order on the compute stream:
+ * no host synchronization over RCCL, so an adaptive loop can take dt
+ * without a round trip (ABI 8) */
+int dccrgx_advection_max_time_step_device(dccrgx_grid* g, const int fields[7], double* d_out);
 /* refine candidates of check_for_adaptation (tests/advection/adapter.hpp:47-178):
  * local cells whose max face relative difference exceeds (lvl+1)*diff_increase */
 int dccrgx_advection_refine_candidates(dccrgx_grid* g, int density_field, double diff_increase,
@@ -468,6 +494,13 @@ int dccrgx_poisson_field(dccrgx_grid* g, const char* name, int* field_id);
 
 /* ---- collectives for user kernels (MPI_Allreduce in solve.hpp:317) ------- */
 int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 sum, 1 min, 2 max */);
+/* MPI_Allreduce on DEVICE doubles (dccrg_mpi_support.hpp All_Reduce's role
+ * for fp64), queued on the compute stream: the processes' values are
+ * all-gathered on the device and combined in rank order by one kernel, so
+ * the result is bitwise dccrgx_allreduce_f64's and, over RCCL, nothing waits
+ * on the host (a host exchange transport stages through the host).  d_in may
+ * equal d_out (ABI 8) */
+int dccrgx_allreduce_f64_device(dccrgx_grid* g, const double* d_in, double* d_out, int count, int op);
 int dccrgx_barrier(dccrgx_grid* g);
 
 /* Transport check (no reference counterpart): the bytes of a fixed-size

@@ -505,10 +505,19 @@ struct Grid {
 		}
 	}
 
-	// dccrg.hpp:2434-2520
+	// dccrg.hpp:2434-2520: at the maximum level dont_unrefine (2472-2475);
+	// refused for a cell in cells_not_to_refine or with a coarser neighbor
+	// there (2477-2491; the set persists between stop_refining calls)
 	bool refine_completely(uint64_t c) {
 		if (c == error_cell || !exists(c)) return false;
-		if (m.level(c) == m.R) return true;
+		if (m.level(c) == m.R) {
+			dont_unrefine(c);
+			return true;
+		}
+		if (not_to_refine.count(c)) return false;
+		if (nof.count(c))
+			for (const auto& n : nof.at(c))
+				if (m.level(n.first) < m.level(c) && not_to_refine.count(n.first)) return false;
 		to_refine.insert(c);
 		return true;
 	}
@@ -604,6 +613,7 @@ struct Grid {
 			old_donts.insert(donts.begin(), donts.end());
 			donts.clear();
 		} while (!new_donts.empty());
+		not_to_refine = old_donts;  // 10039: kept for the next stop_refining
 		for (const uint64_t c : old_donts) to_refine.erase(c);
 	}
 

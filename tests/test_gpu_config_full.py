@@ -6,6 +6,9 @@
   tests/golden/make_config3.py from oracle/dccrg_oracle.cpp), dt is bitwise
   the oracle's, and after 3 steps the density at ~17.8 K sampled leaves of
   every level is within 1e-12 x max|rho| of the oracle's.
+* After 100 steps the same samples are within 1e-12 x
+  max|rho| of the oracle's and the total mass sum(rho * volume) is within
+  1e-13 (relative) of the initial mass and of the oracle's.
 * The same mesh split into 4 z-slabs (block partition of the level-0 cells,
   children inherit, dccrg.hpp:7981-8013 / 10228-10237) on detached views with
   the density halo moved by the library's pack / place: every cell bitwise
@@ -115,3 +118,38 @@ def test_config3_four_slabs_bitwise(gpu):
         assert np.array_equal(g.fields["density"].get(0, g.n_local), rrho[pos])
     for g in gs + [ref]:
         g.close()
+
+
+def _mass(rho, lx, ly, lz):
+    import math
+
+    return math.fsum((rho * (lx * ly * lz)).tolist())
+
+
+def test_config3_hundred_steps_and_mass(gpu, golden):
+    """SURVEY §8(d) config 3's parity depth: 100 steps at full size."""
+    long = golden.get("steps_long")
+    assert long == 100, "regenerate tests/golden/config3_adv.json (make_config3.py)"
+    g, f = gpu_grid(BASE, R)
+    prerefine(g, f, R)
+    dt = g.advection_max_time_step(f)
+    assert dt == golden["dt"]
+    n = g.n_local
+    lx, ly, lz = (f[k].get(0, n) for k in (4, 5, 6))
+    m0 = _mass(f[0].get(0, n), lx, ly, lz)
+    assert m0 == pytest.approx(golden["mass_0"], rel=1e-15)
+    for _ in range(long):
+        g.advection_step(f, 0.5 * dt)
+        g.advection_commit(f[0])
+    sl = g.slot_ids()[:n]
+    rho = f[0].get(0, n)
+    m1 = _mass(rho, lx, ly, lz)
+    assert abs(m1 - m0) <= 1e-13 * m0, (m0, m1)
+    assert abs(m1 - golden["mass_long"]) <= 1e-13 * m0, (m1, golden["mass_long"])
+    order = np.argsort(sl)
+    want = np.array(golden["sample_ids"], np.uint64)
+    pos = np.searchsorted(sl[order], want)
+    assert np.array_equal(sl[order][pos], want)
+    exp = np.array(golden["sample_rho_long"])
+    assert np.max(np.abs(rho[order][pos] - exp)) <= TOL * np.max(np.abs(exp))
+    g.close()

@@ -204,7 +204,24 @@ def test_turn_equals_split_phases_and_clears_lists(gpu):
     st.set(a0)
     hst.set(a0)
     ls.set(np.full((g.n_slots, 8), 5, np.uint64))
-    for step in range(12):
+    for step in range(18):
+        if step == 9:
+            # the mesh changes between turns: three level-0
+            # leaves refined, one level-1 family merged, on both grids; the
+            # rebuild drops the record that the inner lists are zero, and the
+            # list field is filled with garbage again
+            sl = g.slot_ids()[: g.n_local]
+            lv0 = sl[sl <= np.uint64(480)][:3]
+            lv1 = sl[sl > np.uint64(480)][:1]
+            for x in (g, h):
+                for c in lv0:
+                    x.refine_completely(int(c))
+                for c in lv1:
+                    x.unrefine_completely(int(c))
+                x.stop_refining()
+            assert np.array_equal(g.slot_ids(), h.slot_ids())
+            assert not np.array_equal(g.slot_ids()[: g.n_local], sl), "the mesh did not change"
+            ls.set(np.full((g.n_slots, 8), 7, np.uint64))
         g.get_live_neighbors(st, ls)
         h.gol_amr_collect(hst, hls)
         h.update_copies_of_remote_neighbors()

@@ -212,27 +212,42 @@ def test_variable_payload_file_empty_records(gpu, tmp_path):
 
 
 def test_save_over_longer_file(gpu, tmp_path):
-    """save_grid_data over an older, longer file at the same path:
-    the file ends where the last record ends, so the last cell of a
-    variable-size field gets exactly its own bytes back."""
+    """save_grid_data over an older, longer file at the same path: like the
+    reference (MPI_MODE_CREATE | MPI_MODE_WRONLY, dccrg.hpp:1131) the file is
+    not truncated, so bytes past the new grid data stay (a
+    caller's own bytes there survive).  The split load with the sizes the
+    program knows (the reference's way, tests/restart/variable_cell_data.cpp)
+    restores every cell exactly; the old tail only widens the last record's
+    bytes_left."""
     path = tmp_path / "reuse.dc"
     big, _ = make_pair((9, 2, 1), 0, (False, False, False), 1, 0, 0.0, 1)
     d = big.add_variable_field("data", np.int32)
     d.set([np.full(40, 3, np.int32) for _ in range(big.n_local)])
     big.save_grid_data(path)
-    long_size = os.path.getsize(path)
+    old = open(path, "rb").read()
     g, _ = make_pair((6, 1, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    size = g.add_field("size", np.uint64)
     data = g.add_variable_field("data", np.int32)
     ids = g.slot_ids()[: g.n_local]
     cnt = _counts(ids)
+    size.set(cnt)
     data.set([np.arange(int(k), dtype=np.int32) + 7 for k in cnt])
     g.save_grid_data(path)
-    assert os.path.getsize(path) < long_size
+    new = open(path, "rb").read()
+    assert len(new) == len(old)  # not truncated
+    used = 8 + 87 + 8 + 16 * ids.size + int(8 * ids.size + 4 * cnt.sum())
+    assert new[used:] == old[used:]  # the bytes past the grid data are untouched
     h = dccrg_amd.Dccrg(0, 1, 0)
-    e = h.add_variable_field("data", np.int32)
-    h.load_grid_data(path)
+    hs = h.add_field("size", np.uint64)
+    hd = h.add_variable_field("data", np.int32)
+    h.start_loading_grid_data(path)
+    h.continue_loading_grid_data(hs)
+    k = hs.get(0, h.n_local)
     hid = h.slot_ids()[: h.n_local]
-    got = e.get(0, h.n_local)
-    assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, _counts(hid)))
+    assert np.array_equal(k, _counts(hid))
+    h.continue_loading_grid_data(hd, k)
+    h.finish_loading_grid_data()
+    got = hd.get(0, h.n_local)
+    assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, k))
     for x in (big, g, h):
         x.close()

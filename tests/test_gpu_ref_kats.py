@@ -13,6 +13,18 @@ reference-held assertions rather than the oracle:
   get_face_neighbors/test1.cpp   face neighbor counts, periodicity, pins (a11)
   get_neighbors_/test1.cpp       the face-neighbor cache, refined grids (a4)
   user_neighborhood/neighbor_list_length.cpp   user-hood list lengths (f4)
+Round 5 (VERDICT r04 "next" #1):
+  game_of_life/scalability.cpp   Dccrg<_, Stretched_Cartesian_Geometry>, the
+                                 2-D periodic line KAT (1000 x 1000, 16 turns,
+                                 the start / wait-receives / wait-sends split)
+  game_of_life/scalability1d.cpp 1e6 x 1 x 1, 100 turns, the same split
+  refine/dont_refine.cpp         dont_refine against direct, face and further
+                                 induced refinement (f1), All_Reduce of
+                                 dccrg_mpi_support.hpp
+  additional_cell_data/*.cpp     Additional_Cell_Items / _Neighbor_Items
+                                 defaults and update hooks, also after
+                                 balance_load (a10)
+  examples/simple_game_of_life.cpp   the blinker, 100 turns
 The reference's makefiles run every test at 1 process and under mpiexec
 (makefiles/homedir: -n 3); so does this file (get_cells needs >= 2).  Ranks
 share the one GPU through the library's host exchange over MPI."""
@@ -27,7 +39,9 @@ BIN = os.path.join(ROOT, "examples", "bin")
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
 KATS = ["get_cells", "proc_bdy_cells", "iterators1", "iterators2", "iterators3", "iterators4", "iterators5",
-        "get_face_neighbors", "get_neighbors_", "neighbor_list_length"]
+        "get_face_neighbors", "get_neighbors_", "neighbor_list_length",
+        "scalability", "scalability1d", "dont_refine", "acd_test1", "acd_test2", "acd_neighbor_data1",
+        "acd_neighbor_data2", "simple_game_of_life"]
 CASES = [(k, p) for k in KATS for p in ((2, 3) if k == "get_cells" else (1, 3))]
 
 

@@ -218,6 +218,21 @@ def sc_advection(rank, world):
     _prerefine(g, f, R)
     leaves = np.sort(np.concatenate(_gather(g.local_cells())))
     dt = 0.5 * g.advection_max_time_step(f)
+    # the stream-ordered forms: dt reduced on the device, and sum / min / max
+    # of rank-dependent values, bitwise the host allreduce's
+    import torch
+
+    ddt = torch.zeros(1, dtype=torch.float64, device="cuda")
+    g.advection_max_time_step_device(f, ddt)
+    vals = [1.0 / (3 + rank), -2.5 * rank, 1e-17 * (rank + 1)]
+    dev = {}
+    for op in ("sum", "min", "max"):
+        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        g.allreduce_device(t, op=op)
+        g.synchronize()
+        dev[op] = t.cpu().tolist() == [g.allreduce(v, op) for v in vals]
+    g.synchronize()
+    device_dt = 0.5 * float(ddt.cpu()[0]) == dt and all(dev.values())
     for _ in range(steps):
         g.start_remote_neighbor_copy_updates()
         g.advection_step(f, dt, "inner")
@@ -230,7 +245,7 @@ def sc_advection(rank, world):
     got = {}
     for d in _gather(mine):
         got.update(d)
-    res = {"outer": g.counts["outer"], "mesh": True, "bitwise": True, "oracle": True}
+    res = {"outer": g.counts["outer"], "mesh": True, "bitwise": True, "oracle": True, "device_dt": device_dt}
     if rank == 0:
         o = O.Grid(base, R, per, 0, 1)
         o.set_geometry((0, 0, 0), tuple(1.0 / b for b in base))
@@ -1130,7 +1145,7 @@ def test_config1_two_ranks(transport_results):
 
 
 def test_advection_distributed_refine_and_halo(transport_results):
-    _check(transport_results, "sc_advection", ["mesh", "bitwise", "oracle", "outer"])
+    _check(transport_results, "sc_advection", ["mesh", "bitwise", "oracle", "outer", "device_dt"])
 
 
 def test_migration_library_transport(transport_results):

@@ -2293,6 +2293,29 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		const bool lean = g.gola.mask_path;
 		if (lean && !ls.local_zero && g.n_inner) HIP_CHECK(hipMemsetAsync(L, 0, g.n_inner * 64, g.s_comp));
 		k_time_begin(g);
+		// one process: the level-0 game (gol_amr.hip), the exact collect and
+		// spread only behind it (gated on the device) when a family disagrees
+		const bool level0_game = lean && g.gola.geo && g.size == 1 && g.n_slots == nl && g.n_inner == nl &&
+		                         !std::getenv("DCCRGX_GOL_NO_L0GAME");
+		if (level0_game) {
+			k_gol_amr_level0_game(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, err.p, g.s_comp);
+			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 1, g.s_comp, g.n_inner,
+			          err.p);
+			k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp, 0, err.p);
+			k_time_end(g);
+			int h[3] = {0, 0, 0};
+			HIP_CHECK(hipMemcpyAsync(h, err.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+			// every level-0 cell of a one-process grid has a known leaf
+			DX_REQUIRE(!(h[0] & 8), "internal error: the level-0 game met a level-0 cell without a known leaf");
+			const int collect = (h[0] & 4) ? h[1] : h[0];
+			for (int e : {collect, h[2]}) {
+				DX_REQUIRE(!(e & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
+				DX_REQUIRE(!(e & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
+			}
+			ls.local_zero = true;
+			return 0;
+		}
 		if (lean && g.gola.geo) {
 			// the geometric collect; the exact per-entry one (gated on the
 			// device) when a family's leaves disagree or a reached level-0 cell
@@ -2331,12 +2354,24 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		region_range(g, region, s0, s1);
 		if (s1 <= s0) return 0;
 		DX_LAPS(g.s_comp);
-		ensure_tiles(g);
+		// tiles for a mesh already swept once (DCCRGX_TILES=always / never
+		// overrides): building them costs ~10 sweeps, so the first step on a
+		// freshly adapted mesh sweeps the face table (bitwise the same
+		// densities)
+		static const char* tp = std::getenv("DCCRGX_TILES");
+		const bool tiles = g.tiles_valid || (tp && std::strcmp(tp, "always") == 0) ||
+		                   (!(tp && std::strcmp(tp, "never") == 0) && g.adv_commits_on_mesh > 0);
+		if (tiles) ensure_tiles(g);
+		else ensure_face(g);
 		DX_LAP("step.0_ensure_tiles");
 		k_time_begin(g);
-		// tiles never straddle the inner / outer runs
-		if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
-		if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
+		if (tiles) {
+			// tiles never straddle the inner / outer runs
+			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
+			if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
+		} else {
+			k_advection_ell(f, (double*)rho.scratch.p, g.face_ell.p, g.face_fine.p, s0, s1, dt, g.s_comp);
+		}
 		k_time_end(g);
 		DX_LAP("step.1_sweep");
 		return 0;
@@ -2372,6 +2407,7 @@ int dccrgx_advection_commit(dccrgx_grid* gp, int df) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		commit(g, field(g, df));
+		g.adv_commits_on_mesh++;
 		return 0;
 	});
 }

@@ -481,6 +481,10 @@ struct Grid {
 	DBuf<int32_t> nof_off, nof_slot, it_slot, it_off;
 	// face CSR (built lazily): entry = slot * 8 + dir (dir 0..5 = -x,+x,-y,+y,-z,+z)
 	bool face_valid = false;
+	// advection sweeps committed on the current mesh (rebuild resets it): the
+	// first step on a new mesh sweeps the face table, tiles are built for the
+	// second (a mesh that changes every step never pays for them)
+	unsigned adv_commits_on_mesh = 0;
 	DBuf<uint32_t> face_ptr;
 	DBuf<int32_t> face_ent;
 	DBuf<int32_t> face_ell, face_fine;  // fixed-width form used by the advection sweep
@@ -739,6 +743,8 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 // tiled advection sweep over the regular and the irregular tiles of one run
 // (run 0 inner, 1 outer: tiles never straddle the two)
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
+void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
+                     size_t s1, double dt, hipStream_t s);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 void k_min_partials(const double* partial, size_t n, double* out, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
@@ -800,6 +806,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 // caller runs the exact collect instead
 void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t* state, size_t n_local, size_t n_state,
                    uint64_t* lst, size_t list_from, int* err, hipStream_t s);
+void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, int* err, hipStream_t s);
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0,
                const int* gate = nullptr);

@@ -453,7 +453,9 @@ __global__ __launch_bounds__(kCollectRows) void gol_amr_collect_mask_kernel(
 }
 
 __global__ void gol_amr_spread0_mask_kernel(const uint32_t* __restrict__ lvl0, size_t n0, uint32_t* __restrict__ state,
-                                            const uint32_t* __restrict__ mask, size_t s0, size_t s1) {
+                                            const uint32_t* __restrict__ mask, size_t s0, size_t s1,
+                                            const int* __restrict__ gate) {
+	if (gate && (*gate & (4 | 8)) == 0) return;  // block-uniform: the level-0 game did the turn
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n0; i += size_t(gridDim.x) * blockDim.x) {
 		const size_t s = lvl0[i];
 		if (s < s0 || s >= s1) continue;
@@ -490,7 +492,9 @@ __global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ g
                                                   const uint32_t* __restrict__ gslot, uint32_t* __restrict__ state,
                                                   const uint32_t* __restrict__ mask, const uint64_t* __restrict__ lst,
                                                   const uint32_t* __restrict__ l0c, L0Geom G, size_t n_local,
-                                                  size_t s0, size_t s1, int* __restrict__ err) {
+                                                  size_t s0, size_t s1, int* __restrict__ err,
+                                                  const int* __restrict__ gate) {
+	if (gate && (*gate & (4 | 8)) == 0) return;  // block-uniform: the level-0 game did the turn
 	const size_t t = size_t(xcd_block()) * blockDim.x + threadIdx.x;
 	const size_t gi = t >> 3;
 	const uint32_t m = uint32_t(t & 7u);
@@ -709,6 +713,126 @@ __global__ __launch_bounds__(256) void geo_collect_kernel(const uint32_t* __rest
 	ulonglong2* o = reinterpret_cast<ulonglong2*>(lst + s * kList);
 #pragma unroll
 	for (int i = 0; i < kList / 2; i++) o[i] = make_ulonglong2(out[2 * i], out[2 * i + 1]);
+}
+
+// ---- the level-0 game -------------------------------------------------------
+// On one process with at most one refinement level every leaf is local and a
+// refined level-0 cell's whole family is: the union of the children's reaches
+// (each its octant's corner) is the parent's own 3 x 3 x 3 (or 6-face) reach,
+// so the spread's count for every leaf of a level-0 cell is the number of
+// live level-0 cells around that cell.  One "entity" per level-0 cell - a
+// level-0 leaf (T.lvl0) or a family (T.gptr / T.gslot) - instead of one row
+// per leaf: the table pass writes each level-0 cell's byte from its leaves
+// (the families' OR, disagreement flagged as the geometric collect does),
+// the game pass counts the entity's live neighbors in the table once and
+// applies the rule (solve.hpp:150-167) to its leaves.  Blocks [0, nb0) take
+// the level-0 leaves (a thread each), the rest the families (eight lanes
+// each, OR / sums by shuffles).  Same table, same error bits; no masks and
+// no lists (none leave this process).
+__global__ __launch_bounds__(256) void lg_table_kernel(const uint32_t* __restrict__ lvl0, size_t n0, unsigned nb0,
+                                                       const uint32_t* __restrict__ gptr, size_t ng,
+                                                       const uint32_t* __restrict__ gslot,
+                                                       const uint32_t* __restrict__ l0c,
+                                                       const uint32_t* __restrict__ state, L0Geom G, GeoBox B,
+                                                       uint8_t* __restrict__ tab, int* __restrict__ err) {
+	if (blockIdx.x < nb0) {
+		const size_t e = size_t(blockIdx.x) * 256 + threadIdx.x;
+		if (e >= n0) return;
+		const uint32_t s = lvl0[e];
+		int x, y, z;
+		l0_unpack(l0c[s], G, x, y, z);
+		uint32_t k;
+		if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = state[s] ? 1u : 2u;
+		return;
+	}
+	const size_t t = size_t(blockIdx.x - nb0) * 256 + threadIdx.x;
+	const size_t gi = t >> 3;
+	const uint32_t m = uint32_t(t & 7u);
+	const bool live = gi < ng;  // the eight lanes of a family share a wave: no early exit
+	const uint32_t b = live ? gptr[gi] : 0u, e = live ? gptr[gi + 1] : 0u;
+	uint32_t v = 0;
+	for (uint32_t j = b + m; j < e; j += 8) v |= state[gslot[j]] ? 1u : 2u;
+#pragma unroll
+	for (int o = 1; o < 8; o <<= 1) v |= __shfl_xor(v, o, 8);
+	if (!live || m != 0 || e == b) return;
+	if (v == 3u) atomicOr(err, 4);
+	int x, y, z;
+	l0_unpack(l0c[gslot[b]], G, x, y, z);
+	uint32_t k;
+	if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = uint8_t(v);
+}
+
+// live level-0 cells among the reach items [t0, t1) (step dt) around (px, py,
+// pz); bit 3 of `e` for a reached cell without a known leaf
+template <bool CUBE>
+__device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, const L0Geom& G, const GeoBox& B, int px,
+                                             int py, int pz, int t0, int dt, uint32_t& e) {
+	constexpr int K = CUBE ? 27 : 7;
+	uint32_t cnt = 0;
+	for (int t = t0; t < K; t += dt) {
+		int a, b, d;
+		if (CUBE) {
+			a = t % 3;
+			b = (t / 3) % 3;
+			d = t / 9;
+		} else {  // the centre, then -x, +x, -y, +y, -z, +z
+			a = t == 1 ? 0 : (t == 2 ? 2 : 1);
+			b = t == 3 ? 0 : (t == 4 ? 2 : 1);
+			d = t == 5 ? 0 : (t == 6 ? 2 : 1);
+		}
+		if (a == 1 && b == 1 && d == 1) continue;  // the own level-0 cell (solve.hpp:72-74)
+		uint32_t k;
+		if (!B.index(G, px + a - 1, py + b - 1, pz + d - 1, k)) continue;  // beyond a non-periodic boundary
+		const uint32_t v = k == 0xffffffffu ? 0u : uint32_t(tab[k]);
+		if (v == 0u) e |= 8u;
+		cnt += v == 1u ? 1u : 0u;
+	}
+	return cnt;
+}
+
+// gated on err[0]: a disagreeing family (bit 2, from the table pass) leaves
+// every state to the exact collect + spread that run instead
+template <bool CUBE>
+__global__ __launch_bounds__(256) void lg_game_kernel(const uint32_t* __restrict__ lvl0, size_t n0, unsigned nb0,
+                                                      const uint32_t* __restrict__ gptr, size_t ng,
+                                                      const uint32_t* __restrict__ gslot,
+                                                      const uint32_t* __restrict__ l0c, uint32_t* __restrict__ state,
+                                                      const uint8_t* __restrict__ tab, L0Geom G, GeoBox B,
+                                                      int* __restrict__ err) {
+	if (__builtin_nontemporal_load(err) & 4) return;  // block-uniform
+	uint32_t e = 0;
+	if (blockIdx.x < nb0) {
+		const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+		if (i >= n0) return;
+		const uint32_t s = lvl0[i];
+		int x, y, z;
+		l0_unpack(l0c[s], G, x, y, z);
+		const uint32_t n = lg_count<CUBE>(tab, G, B, x, y, z, 0, 1, e);
+		if (n > uint32_t(kList)) e |= 1u;
+		if (e) atomicOr(err, int(e));
+		gol_rule(state, s, int(n));
+		return;
+	}
+	const size_t t = size_t(blockIdx.x - nb0) * 256 + threadIdx.x;
+	const size_t gi = t >> 3;
+	const uint32_t m = uint32_t(t & 7u);
+	const bool live = gi < ng;  // eight lanes per family, one wave: no early exit before the shuffles
+	const uint32_t b = live ? gptr[gi] : 0u, en = live ? gptr[gi + 1] : 0u;
+	uint32_t n = 0;
+	if (live && en > b) {
+		int x, y, z;
+		l0_unpack(l0c[gslot[b]], G, x, y, z);
+		n = lg_count<CUBE>(tab, G, B, x, y, z, int(m), 8, e);
+	}
+#pragma unroll
+	for (int o = 1; o < 8; o <<= 1) {
+		n += uint32_t(__shfl_xor(int(n), o, 8));
+		e |= uint32_t(__shfl_xor(int(e), o, 8));
+	}
+	if (!live) return;
+	if (n > uint32_t(kList)) e |= 1u;
+	if (e && m == 0) atomicOr(err, int(e));
+	for (uint32_t j = b + m; j < en; j += 8) gol_rule(state, gslot[j], int(n));
 }
 
 // per local slot: the child octant of a level-1 leaf, bit 7 for a level-0 leaf
@@ -948,10 +1072,40 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
 	}
 }
 
+// the level-0 game (one process): table + game, two launches
+void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, int* err, hipStream_t s) {
+	DX_REQUIRE(T.geo && (nh == 26 || nh == 6), "level-0 game not available");
+	const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
+	const GeoBox B{T.box0[0],
+	               T.box0[1],
+	               T.box0[2],
+	               T.boxn[0],
+	               T.boxn[1],
+	               T.boxn[2],
+	               T.per[0],
+	               T.per[1],
+	               T.per[2],
+	               {T.geo_lb[0], T.geo_lb[1], T.geo_lb[2]},
+	               {T.geo_bstride[0], T.geo_bstride[1], T.geo_bstride[2]},
+	               {T.geo_istride[0], T.geo_istride[1], T.geo_istride[2]}};
+	const unsigned nb0 = unsigned((T.n_lvl0 + 255) / 256), nb1 = unsigned((8 * T.ng + 255) / 256);
+	if (nb0 + nb1 == 0) return;
+	lg_table_kernel<<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state, G, B,
+	                                         T.l0tab.p, err);
+	HIP_CHECK(hipGetLastError());
+	if (nh == 26)
+		lg_game_kernel<true><<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state,
+		                                              T.l0tab.p, G, B, err);
+	else
+		lg_game_kernel<false><<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state,
+		                                               T.l0tab.p, G, B, err);
+	HIP_CHECK(hipGetLastError());
+}
+
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from, const int* gate) {
 	if (s1 <= s0) return;
-	DX_REQUIRE(!gate || (T.mask_path && phase == 0), "internal error: gated refined-game launch off the mask path");
+	DX_REQUIRE(!gate || T.mask_path, "internal error: gated refined-game launch off the mask path");
 	if (T.mask_path) {
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
@@ -962,10 +1116,10 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 		} else {
 			if (T.n_lvl0)
 				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,
-				                                                                   s0, s1);
+				                                                                   s0, s1, gate);
 			if (T.ng)
 				gol_amr_spread_groups_mask_kernel<<<xcd_grid((8 * T.ng + 255) / 256), 256, 0, s>>>(
-				    T.gptr.p, T.ng, T.gslot.p, state, T.mask.p, lst, T.l0c.p, G, n_local, s0, s1, err);
+				    T.gptr.p, T.ng, T.gslot.p, state, T.mask.p, lst, T.l0c.p, G, n_local, s0, s1, err, gate);
 		}
 		HIP_CHECK(hipGetLastError());
 		return;

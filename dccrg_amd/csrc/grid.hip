@@ -777,6 +777,10 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 			if (po[i] != g.rank) dest[pc[i]] = po[i];
 	}
 	g.weights.clear();
+	g.refine_bulk.clear();
+	g.unrefine_bulk.clear();
+	g.refine_requests.clear();      // cells_to_refine (3808)
+	g.unrefine_requests.clear();    // cells_to_unrefine (3810)
 	g.dont_refine_cells.clear();    // cells_not_to_refine (3812)
 	g.dont_unrefine_cells.clear();  // cells_not_to_unrefine (3813)
 	g.removed_ids_h.clear();  // unrefined_cell_data (3811)

@@ -527,6 +527,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	g.csr_valid = false;
 	g.face_valid = false;
 	g.tiles_valid = false;
+	g.adv_commits_on_mesh = 0;
 	g.slot_ids_h_valid = false;
 	g.index_h_valid = false;
 	g.po.valid = false;

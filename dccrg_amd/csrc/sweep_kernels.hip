@@ -281,6 +281,58 @@ __global__ void advection_kernel(const double* __restrict__ rho, const double* _
 	}
 }
 
+// The same sweep over the fixed-width face table of ensure_face
+// (face_fill_kernel: ell[6 r + d] = the neighbor's slot, -1 none, -2 - f the
+// four finer neighbors fine[4 f ..] in the reference's order): the sweep of a
+// mesh that has just changed, before (and instead of) building its tiles.
+// One thread per cell, the row's six codes as three 8-B loads, the same face
+// fluxes summed in the same face order as advection_kernel and the tile
+// sweeps, so the new density is bitwise theirs.
+__global__ __launch_bounds__(256) void advection_ell_kernel(const double* __restrict__ rho, const double* __restrict__ vx,
+                                                            const double* __restrict__ vy, const double* __restrict__ vz,
+                                                            const double* __restrict__ lx, const double* __restrict__ ly,
+                                                            const double* __restrict__ lz, double* __restrict__ rho_out,
+                                                            const int32_t* __restrict__ ell,
+                                                            const int32_t* __restrict__ fine, size_t s0, size_t s1,
+                                                            double dt) {
+#pragma clang fp contract(off)
+	typedef int i2v __attribute__((ext_vector_type(2)));
+	typedef int i4v __attribute__((ext_vector_type(4)));
+	for (size_t s = s0 + blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < s1; s += size_t(gridDim.x) * blockDim.x) {
+		const double cd = rho[s];
+		const double clx = lx[s], cly = ly[s], clz = lz[s];
+		const double cvx = vx[s], cvy = vy[s], cvz = vz[s];
+		int32_t e6[6];
+		const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
+#pragma unroll
+		for (int j = 0; j < 3; j++) {
+			const i2v v = ev[j];
+			e6[2 * j] = v.x;
+			e6[2 * j + 1] = v.y;
+		}
+		auto nb = [&](int32_t n, int dir) {
+			const double nv = dir < 2 ? vx[n] : (dir < 4 ? vy[n] : vz[n]);
+			return AdvNb{rho[n], lx[n], ly[n], lz[n], nv};
+		};
+		double acc = 0;
+#pragma unroll
+		for (int dir = 0; dir < 6; dir++) {
+			const int32_t c = e6[dir];
+			if (c == -1) continue;
+			if (c >= 0) {
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(c, dir), dt);
+			} else {
+				const i4v q = *reinterpret_cast<const i4v*>(fine + 4 * size_t(-2 - c));
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.x, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.y, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.z, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.w, dir), dt);
+			}
+		}
+		rho_out[s] = cd + acc / (clx * cly * clz);
+	}
+}
+
 // 32-bit byte offsets from a uniform base: global_load v, voff, s[base]
 // (halves the address registers of a gather; slots < 2^29, checked on the host)
 __device__ __forceinline__ double ldo(const double* __restrict__ p, uint32_t off) {
@@ -566,6 +618,162 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		tn = tk.next(tn);
 	}
 #endif
+}
+
+// The regular sweep with a compact LDS footprint, three blocks per CU
+// (VERDICT r04 lever (a): more tiles in flight per XCD at the same L2
+// footprint).  Own fields 7 x 512, the out-of-tile layers only the five
+// values each side's faces read (6 x 5 x 64), and the +x / +y / +z face
+// fluxes written over the layers once pass 1 has read them (one more
+// barrier): 45.5 KB per block instead of 64 KB, 80 VGPRs (6 waves per SIMD).
+// Same faces, same expressions, same summation order: bitwise the kernel
+// above.  Selected at run time (DCCRGX_REG3=1) for paired A/Bs.
+template <int MINW>
+__global__ __launch_bounds__(512, MINW) void advection_regular3_kernel(AdvPtrs P, double* __restrict__ rho_out,
+                                                                       const RegTileMeta* __restrict__ meta,
+                                                                       uint32_t ntiles, double dt) {
+#pragma clang fp contract(off)
+	constexpr uint32_t OWN = 0, EXT = 7 * 512, SHM = EXT + 6 * 5 * 64;  // double offsets
+	__shared__ double sh[SHM + 3 * 64];
+	const StaticTiles tk(ntiles);
+	const uint32_t t1 = tk.t1;
+	uint32_t t = tk.first();
+	if (t >= t1) return;  // block-uniform
+	const uint32_t tid = threadIdx.x;
+	const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+	const uint32_t l[3] = {(tid & 1u) | ((tid >> 2) & 2u) | ((tid >> 4) & 4u),
+	                       ((tid >> 1) & 1u) | ((tid >> 3) & 2u) | ((tid >> 5) & 4u),
+	                       ((tid >> 2) & 1u) | ((tid >> 4) & 2u) | ((tid >> 6) & 4u)};
+	const uint32_t fi[3] = {l[1] + 8 * l[2], l[0] + 8 * l[2], l[0] + 8 * l[1]};
+	const uint32_t bu = lane & 7u, bv = lane >> 3;
+	const uint32_t bcell = w == 0 ? m9(0, bu, bv) : (w == 1 ? m9(bu, 0, bv) : m9(bu, bv, 0));
+	const double* __restrict__ rho = P.p[0];
+	const double* __restrict__ lx = P.p[1];
+	const double* __restrict__ ly = P.p[2];
+	const double* __restrict__ lz = P.p[3];
+	const double* __restrict__ vx = P.p[4];
+	const double* __restrict__ vy = P.p[5];
+	const double* __restrict__ vz = P.p[6];
+	// own rows: 0 rho, 1 vx, 2 vy, 3 vz, 4 lx, 5 ly, 6 lz
+	auto own = [&](uint32_t row, uint32_t c) -> double& { return sh[OWN + row * 512 + c]; };
+	// layer of side d: values 0 rho, 1 lx, 2 ly, 3 lz, 4 the velocity along d's axis
+	auto ext = [&](uint32_t d, uint32_t val, uint32_t c) -> double& { return sh[EXT + (d * 5 + val) * 64 + c]; };
+	struct RegSet {
+		double c[7], e[4];
+	};
+	struct RM {
+		uint32_t ts, rec;
+		__device__ __forceinline__ int32_t nst(uint32_t d) const { return int32_t(word_of(rec, int(1 + d))); }
+	};
+	auto unpack = [&](uint32_t v) { return RM{word_of(v, 0), v}; };
+	auto load = [&](const RM& mt, RegSet& r) {
+		const uint32_t o = (mt.ts + tid) << 3;
+		r.c[0] = ldo(rho, o); r.c[1] = ldo(vx, o); r.c[2] = ldo(vy, o);
+		r.c[3] = ldo(vz, o); r.c[4] = ldo(lx, o); r.c[5] = ldo(ly, o);
+		r.c[6] = ldo(lz, o);
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
+			r.e[i] = 0;
+			if (row >= 30u) continue;
+			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
+			const int32_t st = mt.nst(d);
+			if (st < 0) continue;
+			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
+			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
+			r.e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+		}
+	};
+	auto stage = [&](const RegSet& r) {
+#pragma unroll
+		for (int k = 0; k < 7; k++) own(uint32_t(k), tid) = r.c[k];
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			const uint32_t row = w + 8u * uint32_t(i);
+			if (row < 30u) sh[EXT + row * 64 + lane] = r.e[i];  // row = d * 5 + val
+		}
+	};
+	// the +a neighbor of this cell: inside the tile (its own column) or on
+	// the +a layer; value `val` 0 rho, 1 lx, 2 ly, 3 lz, 4 velocity along a
+	auto nbr = [&](int a) -> AdvNb {
+		if (l[a] < 7) {
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] += 1;
+			const uint32_t c = m9(q[0], q[1], q[2]);
+			return AdvNb{own(0, c), own(4, c), own(5, c), own(6, c), own(1 + uint32_t(a), c)};
+		}
+		const uint32_t d = uint32_t(2 * a + 1);
+		return AdvNb{ext(d, 0, fi[a]), ext(d, 1, fi[a]), ext(d, 2, fi[a]), ext(d, 3, fi[a]), ext(d, 4, fi[a])};
+	};
+	auto compute = [&](const RM& mc) {
+		const uint32_t ts = mc.ts;
+		const double cd = own(0, tid), clx = own(4, tid), cly = own(5, tid), clz = own(6, tid);
+		const double cva[3] = {own(1, tid), own(2, tid), own(3, tid)};
+		double g[3];
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			const double ga = adv_face_g(a, cd, clx, cly, clz, cva[a], nbr(a), dt);
+			const bool has = l[a] < 7 || mc.nst(2 * a + 1) >= 0;
+			g[a] = has ? ga : 0.0;
+		}
+		double gmv = 0;
+		const bool bnd = w < 3 && mc.nst(2 * w) >= 0;  // wave-uniform
+		if (bnd) {
+			const uint32_t d = 2u * w;
+			const AdvNb self{own(0, bcell), own(4, bcell), own(5, bcell), own(6, bcell), own(1 + w, bcell)};
+			const double md = ext(d, 0, lane), mlx = ext(d, 1, lane), mly = ext(d, 2, lane), mlz = ext(d, 3, lane),
+			             mv = ext(d, 4, lane);
+			if (w == 0) gmv = adv_face_g(0, md, mlx, mly, mlz, mv, self, dt);
+			else if (w == 1) gmv = adv_face_g(1, md, mlx, mly, mlz, mv, self, dt);
+			else gmv = adv_face_g(2, md, mlx, mly, mlz, mv, self, dt);
+		}
+		__syncthreads();  // every layer value has been read: the fluxes go over them
+		double* shg = sh + EXT;  // [3][512]
+#pragma unroll
+		for (int a = 0; a < 3; a++) shg[a * 512 + tid] = g[a];
+		if (bnd) sh[SHM + w * 64 + lane] = gmv;
+		__syncthreads();
+		// nothing but indices stays live across the barriers: the fluxes and
+		// the cell's own values are read back from LDS
+		double acc = 0;
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			uint32_t q[3] = {l[0], l[1], l[2]};
+			q[a] -= 1;
+			double gm = 0;
+			if (l[a] > 0) gm = shg[a * 512 + m9(q[0] & 7u, q[1] & 7u, q[2] & 7u)];
+			else if (mc.nst(2 * a) >= 0) gm = sh[SHM + a * 64 + fi[a]];
+			acc += gm;
+			acc += -shg[a * 512 + tid];
+		}
+		st_nt(rho_out, ts + tid, own(0, tid) + acc / (own(4, tid) * own(5, tid) * own(6, tid)));
+	};
+	// no register prefetch of the next tile (its 22 VGPRs would spill at 80):
+	// with three blocks per CU the other blocks' loads overlap this one's
+	// compute.  The next record is still read one tile ahead.
+	RM cur = unpack(tile_record_word(meta, t, lane));
+	uint32_t tn = tk.next(t);
+	uint32_t rec = tn < t1 ? tile_record_word(meta, tn, lane) : 0u;
+	for (;;) {
+		{
+			RegSet ra;
+			load(cur, ra);
+			__syncthreads();  // the previous tile's fluxes have been read from LDS
+			stage(ra);
+		}
+		__syncthreads();
+		const bool more = tn < t1;
+		RM nxt = cur;
+		if (more) {
+			nxt = unpack(rec);
+			const uint32_t tnn = tk.next(tn);
+			rec = tnn < t1 ? tile_record_word(meta, tnn, lane) : 0u;
+		}
+		compute(cur);
+		if (!more) break;
+		cur = nxt;
+		tn = tk.next(tn);
+	}
 }
 
 // Persistent, software-pipelined form of advection_tiles_kernel for any tile
@@ -1294,6 +1502,14 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 // both persistent with two blocks per CU (r01k: one / two tiles in flight per
 // block, dynamic tickets and a second stream for the general sweep all tie
 // or lose against this schedule).
+void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
+                     size_t s1, double dt, hipStream_t s) {
+	if (s1 <= s0) return;
+	advection_ell_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6],
+	                                                                     rho_out, ell, fine, s0, s1, dt);
+	HIP_CHECK(hipGetLastError());
+}
+
 void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s) {
 	const size_t n_reg = g.tcount[run], n_irr = g.tcount[2 + run];
 	const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
@@ -1319,8 +1535,14 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 #endif
 	if (n_reg) {
 		const RegTileMeta* meta = g.tregmeta.p + (run == 0 ? 0 : g.tcount[0]);
-		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_reg + 7) / 8 * 8));
-		advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		static const bool reg3 = std::getenv("DCCRGX_REG3") && std::atoi(std::getenv("DCCRGX_REG3")) == 1;
+		if (reg3) {
+			const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 3, (n_reg + 7) / 8 * 8));
+			advection_regular3_kernel<6><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		} else {
+			const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_reg + 7) / 8 * 8));
+			advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+		}
 		HIP_CHECK(hipGetLastError());
 	}
 	if (n_irr) {

@@ -1373,10 +1373,16 @@ void* or_grid_create(const uint64_t* len, int R, int px, int py, int pz, unsigne
 
 void or_grid_destroy(void* h) { delete static_cast<OracleHandle*>(h); }
 
-/* replace the leaf set wholesale (ids + owners) and rebuild */
+/* replace the leaf set wholesale (ids + owners) and rebuild: a repartition
+ * (balance_load), which drops the pending requests and the dont sets
+ * (dccrg.hpp:3808-3813) */
 int or_grid_set_cells(void* hp, const uint64_t* ids, const int32_t* owners, size_t n) {
 	OR_TRY({
 		auto* h = static_cast<OracleHandle*>(hp);
+		h->g.to_refine.clear();
+		h->g.to_unrefine.clear();
+		h->g.not_to_refine.clear();
+		h->g.not_to_unrefine.clear();
 		h->g.cell_process.clear();
 		for (size_t i = 0; i < n; i++) h->g.cell_process[ids[i]] = owners[i];
 		h->g.rebuild();

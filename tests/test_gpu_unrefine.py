@@ -30,7 +30,9 @@ def _round(g, o, rng, p_unref, p_dont_unref, p_ref, p_dont_ref):
         elif l > 0 and u < p_unref + p_dont_unref:
             assert g.dont_unrefine(c) and o.dont_unrefine(c)
         elif l < R and u < p_unref + p_dont_unref + p_ref:
-            assert g.refine_completely(c) and o.refine_completely(c)
+            # both refuse a cell in, or next to a coarser one in, the dont_refine
+            # set kept from the last stop_refining (2477-2491)
+            assert g.refine_completely(c) == o.refine_completely(c)
         elif u < p_unref + p_dont_unref + p_ref + p_dont_ref:
             assert g.dont_refine(c) and o.dont_refine(c)
 

@@ -1166,7 +1166,7 @@ int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, 
 			}
 			return 0;
 		}
-		ensure_face(g);
+		ensure_face_csr(g);
 		uint32_t be[2];
 		HIP_CHECK(hipMemcpy(be, g.face_ptr.p + s, 8, hipMemcpyDeviceToHost));
 		const size_t k = be[1] - be[0];
@@ -1191,7 +1191,7 @@ int dccrgx_download_csr(dccrgx_grid* gp, int kind, uint32_t* ptr, uint64_t* ids,
 		const size_t nl = g.n_local;
 		const uint32_t* dptr = nullptr;
 		if (kind == 2) {
-			ensure_face(g);
+			ensure_face_csr(g);
 			dptr = g.face_ptr.p;
 		} else {
 			ensure_csr(g);
@@ -2295,10 +2295,10 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		k_time_begin(g);
 		// one process: the level-0 game (gol_amr.hip), the exact collect and
 		// spread only behind it (gated on the device) when a family disagrees
-		const bool level0_game = lean && g.gola.geo && g.size == 1 && g.n_slots == nl && g.n_inner == nl &&
-		                         !std::getenv("DCCRGX_GOL_NO_L0GAME");
+		const bool level0_game = lean && g.gola.geo && g.gola.lg_layout && g.size == 1 && g.n_slots == nl &&
+		                         g.n_inner == nl && !std::getenv("DCCRGX_GOL_NO_L0GAME");
 		if (level0_game) {
-			k_gol_amr_level0_game(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, err.p, g.s_comp);
+			k_gol_amr_level0_game(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, nl, err.p, g.s_comp);
 			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 1, g.s_comp, g.n_inner,
 			          err.p);
 			k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp, 0, err.p);
@@ -2642,7 +2642,18 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		const double* cf[7];
 		adv_fields(g, fids, cf);
 		DX_LAPS(g.s_comp);
-		g.last_new_cells = stop_refining_impl(g);
+		// velocities and lengths are reset for every local cell below
+		// (adapter.hpp:292-309): the rebuild need not carry them (the removed
+		// store still gets them, packed before the rebuild)
+		for (int k = 1; k < 7; k++)
+			if (fids[k] != fids[0]) field(g, fids[k]).no_carry = true;
+		try {
+			g.last_new_cells = stop_refining_impl(g);
+		} catch (...) {
+			for (int k = 1; k < 7; k++) field(g, fids[k]).no_carry = false;
+			throw;
+		}
+		for (int k = 1; k < 7; k++) field(g, fids[k]).no_carry = false;  // no rebuild ran (nothing changed)
 		DX_LAP("adapt.1_stop_refining");
 		hipStream_t s = g.s_comp;
 		double* f[7];

@@ -79,7 +79,56 @@ __global__ void hash_insert_kernel(HashEntry* tab, uint64_t mask, uint32_t shift
 	}
 }
 
+// per refinement level the smallest and largest id of a list (one atomic
+// per block and bound, the block's bounds reduced in LDS first)
+__global__ __launch_bounds__(256) void level_ranges_kernel(MapCtx m, const uint64_t* __restrict__ ids, size_t n,
+                                                           unsigned long long* lo, unsigned long long* hi) {
+	__shared__ unsigned long long slo[kRangeLevels], shi[kRangeLevels];
+	if (threadIdx.x < kRangeLevels) {
+		slo[threadIdx.x] = ~0ull;
+		shi[threadIdx.x] = 0ull;
+	}
+	__syncthreads();
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[i];
+		const int L = map_level(m, id);
+		if (L < 0 || L >= kRangeLevels) continue;
+		atomicMin(&slo[L], (unsigned long long)id);
+		atomicMax(&shi[L], (unsigned long long)id);
+	}
+	__syncthreads();
+	if (threadIdx.x < kRangeLevels && shi[threadIdx.x]) {
+		atomicMin(lo + threadIdx.x, slo[threadIdx.x]);
+		atomicMax(hi + threadIdx.x, shi[threadIdx.x]);
+	}
+}
+
+// every id of the list written by one thread: no atomics
+__global__ void range_insert_kernel(int2* __restrict__ rmap, DevMesh M, const uint64_t* __restrict__ ids,
+                                    const int32_t* __restrict__ owners, size_t n, size_t slot_upto) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const int64_t k = dm_range_index(M, ids[i]);
+		if (k >= 0) rmap[k] = make_int2(owners ? owners[i] : -2, i < slot_upto ? int32_t(i) : -1);
+	}
+}
+
+__global__ void range_clear_kernel(int2* __restrict__ rmap, DevMesh M, const uint64_t* __restrict__ ids, size_t n) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const int64_t k = dm_range_index(M, ids[i]);
+		if (k >= 0) rmap[k] = make_int2(-1, -1);
+	}
+}
+
 __global__ void hash_set_slots_kernel(DevMesh M, const uint64_t* slot_ids, size_t n, int32_t* err) {
+	if (M.rmap) {
+		int2* rmap = const_cast<int2*>(M.rmap);
+		for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+			const int64_t k = dm_range_index(M, slot_ids[i]);
+			if (k < 0 || rmap[k].x < 0) atomicExch(err, 1);
+			else rmap[k].y = int32_t(i);
+		}
+		return;
+	}
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = slot_ids[i];
 		uint64_t h = hash_home(id, M.shift);
@@ -379,12 +428,14 @@ __global__ void iterator_fill_kernel(const uint32_t* nof_ptr, const uint64_t* no
 	}
 }
 
-// face lists (get_face_neighbors_of semantics), one thread per local slot,
-// in two passes.  Pass 0 counts the entries of each row and keeps, per
-// direction, what the probes found: the slot of a single (same-size or
-// coarser) neighbor, -1 none, -2 four finer ones, -3 a single neighbor
-// without a slot.  Pass 1 writes the rows from those hints and probes again
-// only in the directions with finer neighbors.
+// The fixed-width face table (get_face_neighbors_of semantics), one thread
+// per local slot: ell[6 r + d] = the slot of the single (same-size or
+// coarser) face neighbor in direction d, -1 none, or -2 - f for the finer
+// face f whose 4 slots are fine[4 f ..] in the reference's order.  Finer faces
+// are numbered in (row, direction) order: face_table_kernel writes the
+// directions with one neighbor and appends the finer ones' keys
+// (row << 3 | d); after a sort of the keys face_fine_kernel probes those again.
+// A single neighbor without a slot sets *err.
 struct SlotExists {
 	DevMesh M;
 	mutable int32_t slot = -1;
@@ -424,125 +475,132 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // leaf between the two has that size - and taken when the row holds its id:
 // a same-size leaf is the one face neighbor in that direction (no finer or
 // coarser probe needed).  Otherwise, and for the misses, the probes of
-// face_dir.  The hints are the same either way.
-__global__ void face_hints_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1, bool morton,
-                                  uint64_t* cnt, int32_t* hint) {
+// face_dir.  The table is the same either way.  The loop runs whole waves
+// (wave_reserve needs every lane).
+__global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1,
+                                  bool morton, int32_t* ell, unsigned long long* n_fine, uint64_t* fine_keys,
+                                  int32_t* err) {
 	const SlotExists ex{M};
-	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
-		uint64_t c[3];
-		int lvl;
-		const uint64_t id = slot_ids[r];
-		cell_coords(m, id, c, lvl);
-		uint32_t k = 0, kf = 0;  // entries, finer faces
-		// the six predictions first, their six row loads in flight together
-		int32_t h[6];
-		uint64_t want[6], got[6];
-		bool probe[6];
-		if (morton) {
-			const int sh = 3 * (m.R - lvl);
-			const uint64_t len = uint64_t(1) << (m.R - lvl);
-			const int64_t key = int64_t(morton3(c) >> sh);
-			const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
+	const size_t stride = size_t(gridDim.x) * blockDim.x;
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r - lane_id() < nrows; r += stride) {
+		const bool live = r < nrows;
+		int32_t o6[6];
+		uint32_t kf = 0;  // finer faces
+		if (live) {
+			uint64_t c[3];
+			int lvl;
+			const uint64_t id = slot_ids[r];
+			cell_coords(m, id, c, lvl);
+			// the six predictions first, their six row loads in flight together
+			int32_t h[6];
+			uint64_t want[6], got[6];
+			bool probe[6];
+			if (morton) {
+				const int sh = 3 * (m.R - lvl);
+				const uint64_t len = uint64_t(1) << (m.R - lvl);
+				const int64_t key = int64_t(morton3(c) >> sh);
+				const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
+#pragma unroll
+				for (int dir = 0; dir < 6; dir++) {
+					uint64_t p[3];
+					h[dir] = -1;
+					want[dir] = ~uint64_t(0);
+					probe[dir] = face_probe(m, c, lvl, dir, p);
+					if (!probe[dir]) continue;
+					for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
+					const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
+					if (q >= lo && q < hi) {
+						h[dir] = int32_t(q);
+						want[dir] = map_from_indices(m, p[0], p[1], p[2], lvl);
+					}
+				}
+#pragma unroll
+				for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
+			}
 #pragma unroll
 			for (int dir = 0; dir < 6; dir++) {
-				uint64_t p[3];
-				h[dir] = -1;
-				want[dir] = ~uint64_t(0);
-				probe[dir] = face_probe(m, c, lvl, dir, p);
-				if (!probe[dir]) continue;
-				for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
-				const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
-				if (q >= lo && q < hi) {
-					h[dir] = int32_t(q);
-					want[dir] = map_from_indices(m, p[0], p[1], p[2], lvl);
+				if (morton) {
+					if (!probe[dir]) {
+						o6[dir] = -1;
+						continue;
+					}
+					if (h[dir] >= 0 && got[dir] == want[dir]) {
+						o6[dir] = h[dir];
+						continue;
+					}
 				}
+				uint64_t out[4];
+				const int nf = face_dir(m, c, lvl, dir, ex, out);
+				// a single neighbor was the last cell found (face_dir returns on it)
+				if (nf == 1 && ex.slot < 0) atomicExch(err, 1);
+				o6[dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -1));
+				kf += nf == 4 ? 1u : 0u;
 			}
+			typedef int i2v __attribute__((ext_vector_type(2)));
+			i2v* ev = reinterpret_cast<i2v*>(ell + 6 * r);
 #pragma unroll
-			for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
+			for (int j = 0; j < 3; j++) ev[j] = i2v{o6[2 * j], o6[2 * j + 1]};
 		}
-		int32_t o6[6];
-#pragma unroll
-		for (int dir = 0; dir < 6; dir++) {
-			if (morton) {
-				if (!probe[dir]) {
-					o6[dir] = -1;
-					continue;
-				}
-				if (h[dir] >= 0 && got[dir] == want[dir]) {
-					o6[dir] = h[dir];
-					k += 1;
-					continue;
-				}
-			}
-			uint64_t out[4];
-			const int nf = face_dir(m, c, lvl, dir, ex, out);
-			// a single neighbor was the last cell found (face_dir returns on it)
-			o6[dir] = nf == 0 ? -1 : (nf == 4 ? -2 : (ex.slot >= 0 ? ex.slot : -3));
-			k += uint32_t(nf);
-			kf += nf == 4 ? 1u : 0u;
-		}
-		typedef int i2v __attribute__((ext_vector_type(2)));
-		i2v* hv = reinterpret_cast<i2v*>(hint + 6 * r);
-#pragma unroll
-		for (int j = 0; j < 3; j++) hv[j] = i2v{o6[2 * j], o6[2 * j + 1]};
-		cnt[r] = (uint64_t(kf) << 32) | k;
+		if (__ballot(kf != 0) == 0) continue;
+		unsigned long long at = wave_reserve(n_fine, kf);
+		if (live)
+			for (int dir = 0; dir < 6; dir++)
+				if (o6[dir] == -2) fine_keys[at++] = (uint64_t(r) << 3) | uint64_t(dir);
 	}
 }
 
-// pass 1: the rows from the hints (finer directions probed again), with the
-// fixed-width table: ell[6 r + d] = the neighbor's slot (same size or
-// coarser), -1 none, or -2 - f for the finer face f whose 4 slots are
-// fine[4 f ..] (reference order); pos = the scan of pass 0's counts (finer
-// faces numbered in row order)
-__global__ void face_fill_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, const int32_t* hint,
-                                 const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
-                                 int32_t* err) {
+// the finer faces in key order: f = the key's position
+__global__ void face_fine_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, const uint64_t* fine_keys, size_t n,
+                                 int32_t* ell, int32_t* fine, int32_t* err) {
 	const DevExists ex{M};
-	typedef int i2v __attribute__((ext_vector_type(2)));
+	for (size_t f = blockIdx.x * size_t(blockDim.x) + threadIdx.x; f < n; f += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t key = fine_keys[f];
+		const size_t r = size_t(key >> 3);
+		const int dir = int(key & 7);
+		uint64_t c[3];
+		int lvl;
+		cell_coords(m, slot_ids[r], c, lvl);
+		uint64_t out[4];
+		const int nf = face_dir(m, c, lvl, dir, ex, out);
+		if (nf != 4) atomicExch(err, 1);
+		int32_t sl[4];
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			sl[i] = i < nf ? dm_slot(M, out[i]) : -1;
+			if (sl[i] < 0) atomicExch(err, 1);
+		}
+		reinterpret_cast<int4*>(fine)[f] = int4{sl[0], sl[1], sl[2], sl[3]};
+		ell[6 * r + dir] = -2 - int32_t(f);
+	}
+}
+
+// the CSR form of the table (rows of slot * 8 + direction entries, a row's
+// directions ascending, a finer face's four slots in table order): counts,
+// then entries from the scan
+__global__ void face_csr_count_kernel(const int32_t* ell, size_t nrows, uint32_t* cnt) {
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
-		const uint64_t pr = pos[r];
-		uint32_t k = uint32_t(pr), f = uint32_t(pr >> 32);
-		ptr[r] = k;
-		if (r + 1 == nrows) ptr[nrows] = uint32_t(pos[nrows]);
-		// the row's hints and table entries as three 8-B words
-		int32_t h6[6], e6[6];
-		const i2v* hv = reinterpret_cast<const i2v*>(hint + 6 * r);
-#pragma unroll
-		for (int j = 0; j < 3; j++) {
-			const i2v v = hv[j];
-			h6[2 * j] = v.x;
-			h6[2 * j + 1] = v.y;
+		uint32_t k = 0;
+		for (int d = 0; d < 6; d++) {
+			const int32_t e = ell[6 * r + d];
+			k += e >= 0 ? 1u : (e <= -2 ? 4u : 0u);
 		}
-#pragma unroll
-		for (int dir = 0; dir < 6; dir++) {
-			const int32_t h = h6[dir];
-			if (h == -1) {
-				e6[dir] = -1;
-				continue;
+		cnt[r] = k;
+	}
+}
+
+__global__ void face_csr_fill_kernel(const int32_t* ell, const int32_t* fine, size_t nrows, const uint32_t* ptr,
+                                     int32_t* ent) {
+	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
+		uint32_t k = ptr[r];
+		for (int d = 0; d < 6; d++) {
+			const int32_t e = ell[6 * r + d];
+			if (e >= 0) {
+				ent[k++] = e * 8 + d;
+			} else if (e <= -2) {
+				const size_t f = size_t(-2 - e);
+				for (int i = 0; i < 4; i++) ent[k++] = fine[4 * f + i] * 8 + d;
 			}
-			if (h != -2) {
-				if (h == -3) atomicExch(err, 1);
-				ent[k++] = (h == -3 ? -1 : h) * 8 + dir;
-				e6[dir] = h == -3 ? -1 : h;
-				continue;
-			}
-			uint64_t c[3];
-			int lvl;
-			cell_coords(m, slot_ids[r], c, lvl);
-			uint64_t out[4];
-			const int nf = face_dir(m, c, lvl, dir, ex, out);
-			for (int i = 0; i < nf; i++) {
-				const int32_t sl = dm_slot(M, out[i]);
-				if (sl < 0) atomicExch(err, 1);
-				ent[k++] = sl * 8 + dir;
-				fine[4 * size_t(f) + i] = sl;
-			}
-			e6[dir] = -2 - int32_t(f);
-			f++;
 		}
-		i2v* ev = reinterpret_cast<i2v*>(ell + 6 * r);
-#pragma unroll
-		for (int j = 0; j < 3; j++) ev[j] = i2v{e6[2 * j], e6[2 * j + 1]};
 	}
 }
 
@@ -933,6 +991,43 @@ void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t
 	HIP_CHECK(hipGetLastError());
 }
 
+bool k_level_ranges(const MapCtx& m, const uint64_t* ids, size_t n, uint64_t* lo, uint64_t* hi, hipStream_t s) {
+	if (m.R >= kRangeLevels) return false;
+	DBuf<unsigned long long> d;
+	d.alloc(2 * kRangeLevels);
+	std::vector<unsigned long long> h(2 * kRangeLevels);
+	for (int L = 0; L < kRangeLevels; L++) {
+		h[size_t(L)] = ~0ull;
+		h[size_t(kRangeLevels + L)] = 0ull;
+	}
+	HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+	if (n) {
+		level_ranges_kernel<<<std::min<unsigned>(grid_for(n, 256), 2048), 256, 0, s>>>(m, ids, n, d.p,
+		                                                                              d.p + kRangeLevels);
+		HIP_CHECK(hipGetLastError());
+	}
+	HIP_CHECK(hipMemcpyAsync(h.data(), d.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+	for (int L = 0; L < kRangeLevels; L++) {
+		lo[L] = h[size_t(L)];
+		hi[L] = h[size_t(kRangeLevels + L)];
+	}
+	return true;
+}
+
+void k_range_insert(int2* rmap, const DevMesh& M, const uint64_t* ids, const int32_t* owners, size_t n, size_t slot_upto,
+                    hipStream_t s) {
+	if (!n) return;
+	range_insert_kernel<<<grid_for(n, 256), 256, 0, s>>>(rmap, M, ids, owners, n, slot_upto);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_range_clear(int2* rmap, const DevMesh& M, const uint64_t* ids, size_t n, hipStream_t s) {
+	if (!n) return;
+	range_clear_kernel<<<grid_for(n, 256), 256, 0, s>>>(rmap, M, ids, n);
+	HIP_CHECK(hipGetLastError());
+}
+
 void k_hash_set_slots(const DevMesh& M, const uint64_t* slot_ids, size_t n, int32_t* err, hipStream_t s) {
 	if (!n) return;
 	hash_set_slots_kernel<<<grid_for(n, 256), 256, 0, s>>>(M, slot_ids, n, err);
@@ -1060,15 +1155,15 @@ void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s) {
 	v = download(d.p, n, s);
 }
 
-void sort_u64(uint64_t* keys, size_t n, hipStream_t s) {
+void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	if (n < 2) return;
 	DBuf<uint64_t> tmp;
 	tmp.alloc(n);
 	size_t b1 = 0;
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys, tmp.p, n, 0, end_bit, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(b1);
-	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, end_bit, s));
 	HIP_CHECK(hipMemcpyAsync(keys, tmp.p, n * 8, hipMemcpyDeviceToDevice, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -1122,16 +1217,39 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint64_t* cnt,
-                  int32_t* hint, const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
-                  int32_t* err_flag, int pass, hipStream_t s, bool morton, size_t run1) {
-	if (!nrows) return;
-	if (pass == 0)
-		face_hints_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, cnt,
-		                                                       hint);
-	else
-		face_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, hint, pos, ptr, ent, ell, fine,
-		                                                      err_flag);
+size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, size_t run1,
+                    bool morton, int32_t* ell, DBuf<int32_t>& fine, int32_t* err, hipStream_t s) {
+	DBuf<unsigned long long> n_fine;
+	n_fine.alloc(1);
+	HIP_CHECK(hipMemsetAsync(n_fine.p, 0, 8, s));
+	// finer faces: at most 6 per row, in practice a few percent of the rows
+	DBuf<uint64_t> keys;
+	keys.alloc(6 * nrows + 1);
+	if (nrows)
+		face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, ell,
+		                                                       n_fine.p, keys.p, err);
+	HIP_CHECK(hipGetLastError());
+	const size_t nf = size_t(read_counter(n_fine, s));
+	fine.alloc(4 * nf + 4);
+	if (!nf) return 0;
+	int bits = 4;
+	while (bits < 64 && (uint64_t(nrows) << 3) >> bits) bits++;
+	sort_u64(keys.p, nf, s, bits);
+	face_fine_kernel<<<grid_for(nf, 256), 256, 0, s>>>(m, M, slot_ids, keys.p, nf, ell, fine.p, err);
+	HIP_CHECK(hipGetLastError());
+	return nf;
+}
+
+void k_face_csr(const int32_t* ell, const int32_t* fine, size_t nrows, DBuf<uint32_t>& ptr, DBuf<int32_t>& ent,
+                hipStream_t s) {
+	DBuf<uint32_t> cnt;
+	cnt.alloc(nrows + 1);
+	ptr.alloc(nrows + 1);
+	if (nrows) face_csr_count_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(ell, nrows, cnt.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t t = scan_exclusive_u32(cnt.p, ptr.p, nrows, s);
+	ent.alloc(t + 1);
+	if (nrows) face_csr_fill_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(ell, fine, nrows, ptr.p, ent.p);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -242,6 +242,11 @@ struct Field {
 	// of life turn, which leaves each local list error_cell-cleared as the
 	// reference does; dropped by anything that may write local payloads)
 	bool local_zero = false;
+	// the next rebuild does not carry this field's payloads (its caller
+	// rewrites every local element right after, e.g. advection_adapt's
+	// velocity / length reset): the local part is left unwritten, the rest
+	// zeroed; the flag is dropped by that rebuild
+	bool no_carry = false;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
@@ -336,6 +341,15 @@ struct Mesh {
 	DBuf<HashEntry> tab;
 	uint64_t mask = 0;
 	uint32_t shift = 63;
+	// the range map instead of `tab` (dccrgx_mesh.hpp DevMesh::rmap)
+	DBuf<int2> rmap;
+	DBuf<RangeLevel> rl;
+	int rlev = 0;
+	// the grid's persistent full-level map (Grid::rmap_full) instead of an
+	// owned one: not freed with the mesh, cleared entry by entry by the next
+	// rebuild
+	const int2* rmap_shared = nullptr;
+	const RangeLevel* rl_shared = nullptr;
 	BlockPart bp;
 	DevMesh dev(uint64_t last) const {
 		DevMesh d{};
@@ -345,6 +359,9 @@ struct Mesh {
 		d.implicit = implicit ? 1 : 0;
 		d.bp = bp;
 		d.last = last;
+		d.rmap = rmap_shared ? rmap_shared : rmap.p;
+		d.rl = rmap_shared ? rl_shared : rl.p;
+		d.rlev = d.rmap ? rlev : 0;
 		return d;
 	}
 };
@@ -398,6 +415,9 @@ struct GolAmrTables {
 	// known region's bounding box a byte (bit 0: a known leaf there alive,
 	// bit 1: one dead)
 	bool geo = false;
+	bool lg_layout = false;  // every family eight consecutive slots (the level-0 game)
+	DBuf<uint32_t> lg_rows;  // its rows: level-0 leaves' and families' first slots, ascending
+	size_t n_lg_rows = 0;
 	DBuf<uint8_t> corner, l0tab;
 	uint32_t box0[3] = {0, 0, 0}, boxn[3] = {0, 0, 0};
 	uint32_t geo_lb[3] = {0, 0, 0}, geo_bstride[3] = {1, 1, 1}, geo_istride[3] = {1, 1, 1};  // table blocks
@@ -456,6 +476,13 @@ struct Grid {
 	DBuf<uint64_t> removed_ids_d;               // the same on the device when n > 0, else empty
 	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
 	Migration mig;
+	// the range map over the full id range of every level (one process,
+	// Morton-ordered own leaves: rebuild's "direct" mode), kept across
+	// rebuilds: each rebuild clears the previous mesh's entries and writes its
+	// own instead of clearing the whole map
+	DBuf<int2> rmap_full;
+	DBuf<RangeLevel> rl_full;
+	bool rmap_full_clean = true;  // every entry {-1, -1}
 	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev
 	DBuf<double> dt_part;  // block minima of dccrgx_advection_max_time_step_device
 
@@ -479,8 +506,10 @@ struct Grid {
 	DBuf<uint32_t> nof_ptr, nto_ptr, it_ptr;
 	DBuf<uint64_t> nof_id, nto_id;
 	DBuf<int32_t> nof_off, nof_slot, it_slot, it_off;
-	// face CSR (built lazily): entry = slot * 8 + dir (dir 0..5 = -x,+x,-y,+y,-z,+z)
-	bool face_valid = false;
+	// face table (built lazily, ensure_face) and its CSR form (built from the
+	// table when a consumer needs it, ensure_face_csr): entry = slot * 8 + dir
+	// (dir 0..5 = -x,+x,-y,+y,-z,+z)
+	bool face_valid = false, face_csr_valid = false;
 	// advection sweeps committed on the current mesh (rebuild resets it): the
 	// first step on a new mesh sweeps the face table, tiles are built for the
 	// second (a mesh that changes every step never pays for them)
@@ -589,11 +618,18 @@ void mesh_materialize(Grid& g, Mesh& out);
 // after a repartition: own leaves known, ghosts fetched from their owners
 void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n_local);
 // (entries i < slot_upto get slot i, the others -1)
+void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
+                      size_t slot_upto);
+bool k_level_ranges(const MapCtx& m, const uint64_t* ids, size_t n, uint64_t* lo, uint64_t* hi, hipStream_t s);
+void k_range_insert(int2* rmap, const DevMesh& M, const uint64_t* ids, const int32_t* owners, size_t n, size_t slot_upto,
+                    hipStream_t s);
+void k_range_clear(int2* rmap, const DevMesh& M, const uint64_t* ids, size_t n, hipStream_t s);
 void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
                      size_t slot_upto = 0);
 void rebuild(Grid& g, Mesh& new_mesh);  // new_mesh is moved into g.mesh
 void ensure_csr(Grid& g);
 void ensure_face(Grid& g);
+void ensure_face_csr(Grid& g);  // ensure_face + face_ptr / face_ent
 void ensure_tiles(Grid& g);
 const std::vector<uint64_t>& slot_ids_host(Grid& g);
 // batch lookups of known leaves: owner (-1 unknown) and slot (-1 none)
@@ -649,7 +685,7 @@ size_t k_extract_remote(const uint64_t* ids, size_t n, const DevMesh& M, int ran
 size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
                       size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s);
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit = 64);  // in place; keys < 2^end_bit
-void sort_u64(uint64_t* keys, size_t n, hipStream_t s);           // in place
+void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit = 64);  // in place; keys < 2^end_bit
 void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s);  // host list, device radix sort when large
 // (id, slot) of every slot sorted by id
 void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
@@ -665,9 +701,13 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
                       uint8_t* cls, uint32_t* it_cnt, const uint32_t* it_ptr, int32_t* it_slot, int32_t* it_off,
                       int pass, hipStream_t s);
 void k_slot_levels(const MapCtx& m, const uint64_t* slot_ids, size_t n, uint8_t* lvl, hipStream_t s);
-void k_face_lists(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, uint64_t* cnt,
-                  int32_t* hint, const uint64_t* pos, uint32_t* ptr, int32_t* ent, int32_t* ell, int32_t* fine,
-                  int32_t* err_flag, int pass, hipStream_t s, bool morton = false, size_t run1 = 0);
+// the fixed-width face table of rows [0, nrows) (ensure_face); fine is
+// allocated here; returns the number of finer faces
+size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, size_t run1,
+                    bool morton, int32_t* ell, DBuf<int32_t>& fine, int32_t* err, hipStream_t s);
+// its CSR rows (ensure_face_csr)
+void k_face_csr(const int32_t* ell, const int32_t* fine, size_t nrows, DBuf<uint32_t>& ptr, DBuf<int32_t>& ent,
+                hipStream_t s);
 void k_carry_src(const uint64_t* slot_ids, size_t n_slots, size_t nl, const MapCtx& m, const DevMesh& oldM,
                  size_t old_n_local, int32_t* src, hipStream_t s);
 void k_gather_rows(const uint8_t* old_data, const int32_t* src, size_t n, size_t elem, uint8_t* out, hipStream_t s);
@@ -806,7 +846,8 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 // caller runs the exact collect instead
 void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t* state, size_t n_local, size_t n_state,
                    uint64_t* lst, size_t list_from, int* err, hipStream_t s);
-void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, int* err, hipStream_t s);
+void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, size_t n_local, int* err,
+                           hipStream_t s);
 void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint32_t* state, uint64_t* lst, const uint32_t* ptr,
                const int32_t* nslot, size_t s0, size_t s1, int* err, hipStream_t s, size_t list_from = 0,
                const int* gate = nullptr);

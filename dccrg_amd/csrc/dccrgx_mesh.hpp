@@ -61,6 +61,19 @@ struct BlockPart {
 	}
 };
 
+// Range map: an explicit mesh whose known ids span few ids per refinement
+// level (one process, or z-slab partitions: the known leaves of level L lie
+// in [rlo[L], rhi[L]) and that range is not much larger than the known set)
+// keeps one 8-byte entry {owner, slot} per id of those ranges instead of the
+// hash table: no probing, no atomics to build (every id is written by one
+// thread), one load per lookup.  Absent = {-1, -1}.
+constexpr int kRangeLevels = 8;
+
+// one level's id range [lo, hi) and its first entry in the map
+struct RangeLevel {
+	uint64_t lo, hi, off;
+};
+
 struct DevMesh {
 	const HashEntry* tab;  // nullptr: no table
 	uint64_t mask;
@@ -68,13 +81,34 @@ struct DevMesh {
 	int implicit;
 	BlockPart bp;
 	uint64_t last;
+	const int2* rmap;       // non-null: the range map replaces the table
+	const RangeLevel* rl;   // rlev ranges (device memory: a DevMesh stays small)
+	int rlev;
 };
 
 DX_HD uint64_t hash_home(uint64_t id, uint32_t shift) { return (id * kHashMul) >> shift; }
 
 #if defined(__HIPCC__)
+// index of `id` in the range map, -1 outside its ranges
+__device__ __forceinline__ int64_t dm_range_index(const DevMesh& M, uint64_t id) {
+	for (int L = 0; L < M.rlev; L++) {
+		const RangeLevel q = M.rl[L];
+		if (id >= q.lo && id < q.hi) return int64_t(q.off + (id - q.lo));
+	}
+	return -1;
+}
+
 // one probe sequence; returns true and the entry's owner / slot if present
 __device__ __forceinline__ bool dm_lookup(const DevMesh& M, uint64_t id, int32_t& owner, int32_t& slot) {
+	if (M.rmap) {
+		const int64_t k = dm_range_index(M, id);
+		if (k < 0) return false;
+		const int2 e = M.rmap[k];
+		if (e.x < 0) return false;
+		owner = e.x;
+		slot = e.y;
+		return true;
+	}
 	if (!M.tab) return false;
 	uint64_t h = hash_home(id, M.shift);
 	for (;;) {

@@ -720,57 +720,61 @@ __global__ __launch_bounds__(256) void geo_collect_kernel(const uint32_t* __rest
 // refined level-0 cell's whole family is: the union of the children's reaches
 // (each its octant's corner) is the parent's own 3 x 3 x 3 (or 6-face) reach,
 // so the spread's count for every leaf of a level-0 cell is the number of
-// live level-0 cells around that cell.  One "entity" per level-0 cell - a
-// level-0 leaf (T.lvl0) or a family (T.gptr / T.gslot) - instead of one row
-// per leaf: the table pass writes each level-0 cell's byte from its leaves
-// (the families' OR, disagreement flagged as the geometric collect does),
-// the game pass counts the entity's live neighbors in the table once and
-// applies the rule (solve.hpp:150-167) to its leaves.  Blocks [0, nb0) take
-// the level-0 leaves (a thread each), the rest the families (eight lanes
-// each, OR / sums by shuffles).  Same table, same error bits; no masks and
-// no lists (none leave this process).
-__global__ __launch_bounds__(256) void lg_table_kernel(const uint32_t* __restrict__ lvl0, size_t n0, unsigned nb0,
-                                                       const uint32_t* __restrict__ gptr, size_t ng,
-                                                       const uint32_t* __restrict__ gslot,
+// live level-0 cells around that cell.  One row per level-0 cell instead of
+// one per leaf: a level-0 leaf, or a family - the eight children of a refined
+// level-0 cell are eight consecutive slots in Morton order, octant 0 first.
+// Both passes run over the slots (coalesced reads of the octant byte, the
+// packed level-0 coordinates and the states); the first slot of a family
+// speaks for it.  The table pass writes each level-0 cell's byte (the
+// family's OR, a disagreement flagged as the geometric collect does), the
+// game pass counts the row's live neighbors in the table once and applies
+// the rule (solve.hpp:150-167) to its leaves.  Same table, same error bits;
+// no masks, no lists (none leave the process).
+__global__ __launch_bounds__(256) void lg_table_kernel(const uint32_t* __restrict__ rows, size_t nrows,
+                                                       const uint8_t* __restrict__ corner,
                                                        const uint32_t* __restrict__ l0c,
                                                        const uint32_t* __restrict__ state, L0Geom G, GeoBox B,
                                                        uint8_t* __restrict__ tab, int* __restrict__ err) {
-	if (blockIdx.x < nb0) {
-		const size_t e = size_t(blockIdx.x) * 256 + threadIdx.x;
-		if (e >= n0) return;
-		const uint32_t s = lvl0[e];
-		int x, y, z;
-		l0_unpack(l0c[s], G, x, y, z);
-		uint32_t k;
-		if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = state[s] ? 1u : 2u;
-		return;
-	}
-	const size_t t = size_t(blockIdx.x - nb0) * 256 + threadIdx.x;
-	const size_t gi = t >> 3;
-	const uint32_t m = uint32_t(t & 7u);
-	const bool live = gi < ng;  // the eight lanes of a family share a wave: no early exit
-	const uint32_t b = live ? gptr[gi] : 0u, e = live ? gptr[gi + 1] : 0u;
-	uint32_t v = 0;
-	for (uint32_t j = b + m; j < e; j += 8) v |= state[gslot[j]] ? 1u : 2u;
+	const size_t r = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	if (r >= nrows) return;
+	const uint32_t s = rows[r];
+	const uint32_t c = corner[s];
+	uint32_t v;
+	if (c & 0x80u) {
+		v = state[s] ? 1u : 2u;
+	} else {
+		v = 0;
 #pragma unroll
-	for (int o = 1; o < 8; o <<= 1) v |= __shfl_xor(v, o, 8);
-	if (!live || m != 0 || e == b) return;
-	if (v == 3u) atomicOr(err, 4);
+		for (int k = 0; k < 8; k++) v |= state[s + k] ? 1u : 2u;
+		if (v == 3u) atomicOr(err, 4);
+	}
 	int x, y, z;
-	l0_unpack(l0c[gslot[b]], G, x, y, z);
+	l0_unpack(l0c[s], G, x, y, z);
 	uint32_t k;
 	if (B.index(G, x, y, z, k) && k != 0xffffffffu) tab[k] = uint8_t(v);
 }
 
-// live level-0 cells among the reach items [t0, t1) (step dt) around (px, py,
-// pz); bit 3 of `e` for a reached cell without a known leaf
-template <bool CUBE>
+// live level-0 cells among the reach items t = t0, t0 + DT, ... (< 27, or 7
+// for the faces) around the level-0 cell (px, py, pz): the three axes'
+// offsets into the table first (geo_axis, a level-0 reach), then every item's
+// byte in flight at once; bit 3 of `e` for a reached cell without a known
+// leaf
+template <bool CUBE, int T0MAX, int DT>
 __device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, const L0Geom& G, const GeoBox& B, int px,
-                                             int py, int pz, int t0, int dt, uint32_t& e) {
+                                             int py, int pz, int t0, uint32_t& e) {
 	constexpr int K = CUBE ? 27 : 7;
-	uint32_t cnt = 0;
-	for (int t = t0; t < K; t += dt) {
-		int a, b, d;
+	constexpr int N = (K + DT - 1) / DT;  // items per caller
+	bool rx[3], ry[3], rz[3], ix[3], iy[3], iz[3];
+	uint32_t ox[3], oy[3], oz[3];
+	geo_axis(px, G.lx, B.x0, B.nx, B.px, true, 0, B, 0, rx, ix, ox);
+	geo_axis(py, G.ly, B.y0, B.ny, B.py, true, 0, B, 1, ry, iy, oy);
+	geo_axis(pz, G.lz, B.z0, B.nz, B.pz, true, 0, B, 2, rz, iz, oz);
+	uint32_t v[N];
+	bool r[N];
+#pragma unroll
+	for (int j = 0; j < N; j++) {
+		const int t = (T0MAX == 0 ? 0 : t0) + j * DT;
+		int a = 1, b = 1, d = 1;
 		if (CUBE) {
 			a = t % 3;
 			b = (t / 3) % 3;
@@ -780,59 +784,79 @@ __device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, co
 			b = t == 3 ? 0 : (t == 4 ? 2 : 1);
 			d = t == 5 ? 0 : (t == 6 ? 2 : 1);
 		}
-		if (a == 1 && b == 1 && d == 1) continue;  // the own level-0 cell (solve.hpp:72-74)
-		uint32_t k;
-		if (!B.index(G, px + a - 1, py + b - 1, pz + d - 1, k)) continue;  // beyond a non-periodic boundary
-		const uint32_t v = k == 0xffffffffu ? 0u : uint32_t(tab[k]);
-		if (v == 0u) e |= 8u;
-		cnt += v == 1u ? 1u : 0u;
+		const bool centre = a == 1 && b == 1 && d == 1;  // the own level-0 cell (solve.hpp:72-74)
+		// a, b, d in 0..2 (clamped for the lanes past the last item)
+		a = min(max(a, 0), 2);
+		b = min(max(b, 0), 2);
+		d = min(max(d, 0), 2);
+		r[j] = t < K && !centre && rx[a] && ry[b] && rz[d];
+		const bool inb = ix[a] && iy[b] && iz[d];
+		v[j] = r[j] ? (inb ? uint32_t(tab[ox[a] + oy[b] + oz[d]]) : 0u) : 0u;
+	}
+	uint32_t cnt = 0;
+#pragma unroll
+	for (int j = 0; j < N; j++) {
+		e |= (r[j] && v[j] == 0u) ? 8u : 0u;
+		cnt += (r[j] && v[j] == 1u) ? 1u : 0u;
 	}
 	return cnt;
+}
+
+// whether every family is eight consecutive slots, octant 0 first (the
+// level-0 game's layout): bad = 1 otherwise
+__global__ void lg_layout_check_kernel(const uint8_t* __restrict__ corner, const uint32_t* __restrict__ l0c, size_t n,
+                                       int* __restrict__ bad) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		const uint32_t c = corner[s];
+		if (c & 0x80u) continue;
+		if (c != 0u) {
+			if (s < c || corner[s - c] != 0u || l0c[s - c] != l0c[s]) atomicExch(bad, 1);
+			continue;
+		}
+		for (uint32_t k = 1; k < 8; k++)
+			if (s + k >= n || corner[s + k] != k || l0c[s + k] != l0c[s]) {
+				atomicExch(bad, 1);
+				break;
+			}
+	}
+}
+
+// the level-0 game's rows: the slots of level-0 leaves and of families'
+// first children, ascending (flags, then the scan's positions)
+__global__ void lg_row_flags_kernel(const uint8_t* __restrict__ corner, size_t n, uint32_t* __restrict__ flag) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		const uint32_t c = corner[s];
+		flag[s] = ((c & 0x80u) || c == 0u) ? 1u : 0u;
+	}
+}
+
+__global__ void lg_row_fill_kernel(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos, size_t n,
+                                   uint32_t* __restrict__ rows) {
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x)
+		if (flag[s]) rows[pos[s]] = uint32_t(s);
 }
 
 // gated on err[0]: a disagreeing family (bit 2, from the table pass) leaves
 // every state to the exact collect + spread that run instead
 template <bool CUBE>
-__global__ __launch_bounds__(256) void lg_game_kernel(const uint32_t* __restrict__ lvl0, size_t n0, unsigned nb0,
-                                                      const uint32_t* __restrict__ gptr, size_t ng,
-                                                      const uint32_t* __restrict__ gslot,
+__global__ __launch_bounds__(256) void lg_game_kernel(const uint32_t* __restrict__ rows, size_t nrows,
+                                                      const uint8_t* __restrict__ corner,
                                                       const uint32_t* __restrict__ l0c, uint32_t* __restrict__ state,
                                                       const uint8_t* __restrict__ tab, L0Geom G, GeoBox B,
                                                       int* __restrict__ err) {
-	if (__builtin_nontemporal_load(err) & 4) return;  // block-uniform
+	if (__builtin_nontemporal_load(err) & 4) return;  // uniform
+	const size_t r = size_t(xcd_block()) * blockDim.x + threadIdx.x;
+	if (r >= nrows) return;
+	const uint32_t s = rows[r];
+	const uint32_t c = corner[s];
+	int x, y, z;
+	l0_unpack(l0c[s], G, x, y, z);
 	uint32_t e = 0;
-	if (blockIdx.x < nb0) {
-		const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
-		if (i >= n0) return;
-		const uint32_t s = lvl0[i];
-		int x, y, z;
-		l0_unpack(l0c[s], G, x, y, z);
-		const uint32_t n = lg_count<CUBE>(tab, G, B, x, y, z, 0, 1, e);
-		if (n > uint32_t(kList)) e |= 1u;
-		if (e) atomicOr(err, int(e));
-		gol_rule(state, s, int(n));
-		return;
-	}
-	const size_t t = size_t(blockIdx.x - nb0) * 256 + threadIdx.x;
-	const size_t gi = t >> 3;
-	const uint32_t m = uint32_t(t & 7u);
-	const bool live = gi < ng;  // eight lanes per family, one wave: no early exit before the shuffles
-	const uint32_t b = live ? gptr[gi] : 0u, en = live ? gptr[gi + 1] : 0u;
-	uint32_t n = 0;
-	if (live && en > b) {
-		int x, y, z;
-		l0_unpack(l0c[gslot[b]], G, x, y, z);
-		n = lg_count<CUBE>(tab, G, B, x, y, z, int(m), 8, e);
-	}
-#pragma unroll
-	for (int o = 1; o < 8; o <<= 1) {
-		n += uint32_t(__shfl_xor(int(n), o, 8));
-		e |= uint32_t(__shfl_xor(int(e), o, 8));
-	}
-	if (!live) return;
-	if (n > uint32_t(kList)) e |= 1u;
-	if (e && m == 0) atomicOr(err, int(e));
-	for (uint32_t j = b + m; j < en; j += 8) gol_rule(state, gslot[j], int(n));
+	const uint32_t cnt = lg_count<CUBE, 0, 1>(tab, G, B, x, y, z, 0, e);
+	if (cnt > uint32_t(kList)) e |= 1u;
+	if (e) atomicOr(err, int(e));
+	const int nm = (c & 0x80u) ? 1 : 8;
+	for (int k = 0; k < nm; k++) gol_rule(state, size_t(s) + size_t(k), int(cnt));
 }
 
 // per local slot: the child octant of a level-1 leaf, bit 7 for a level-0 leaf
@@ -979,6 +1003,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 	// geometric collect: maximum refinement level <= 1 on the mask path, the
 	// level-0 cells of the known region's bounding box in one table
 	T.geo = false;
+	T.lg_layout = false;
 	T.corner.release();
 	T.l0tab.release();
 	if (T.mask_path && m.R <= 1 && n_slots) {
@@ -1028,6 +1053,30 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 				geo_corner_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(m, slot_ids, n_local, T.corner.p);
 				HIP_CHECK(hipGetLastError());
 			}
+			// the level-0 game's layout (families as eight consecutive slots)
+			T.lg_layout = false;
+			if (n_local) {
+				DBuf<int> bad;
+				bad.alloc(1);
+				HIP_CHECK(hipMemsetAsync(bad.p, 0, 4, s));
+				lg_layout_check_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(T.corner.p, T.l0c.p, n_local, bad.p);
+				HIP_CHECK(hipGetLastError());
+				int hb = 1;
+				HIP_CHECK(hipMemcpyAsync(&hb, bad.p, 4, hipMemcpyDeviceToHost, s));
+				HIP_CHECK(hipStreamSynchronize(s));
+				T.lg_layout = hb == 0;
+			}
+			if (T.lg_layout) {
+				DBuf<uint32_t> flag, pos;
+				flag.alloc(n_local + 1);
+				pos.alloc(n_local + 1);
+				lg_row_flags_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(T.corner.p, n_local, flag.p);
+				HIP_CHECK(hipGetLastError());
+				T.n_lg_rows = scan_exclusive_u32(flag.p, pos.p, n_local, s);
+				T.lg_rows.alloc(T.n_lg_rows + 1);
+				lg_row_fill_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(flag.p, pos.p, n_local, T.lg_rows.p);
+				HIP_CHECK(hipGetLastError());
+			}
 			HIP_CHECK(hipStreamSynchronize(s));
 			T.geo = true;
 		}
@@ -1072,9 +1121,11 @@ void k_gol_amr_geo(GolAmrTables& T, const int32_t* hood, int nh, const uint32_t*
 	}
 }
 
-// the level-0 game (one process): table + game, two launches
-void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, int* err, hipStream_t s) {
-	DX_REQUIRE(T.geo && (nh == 26 || nh == 6), "level-0 game not available");
+// the level-0 game (one process): table + game, two launches over the slots
+void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_t* state, size_t n_local, int* err,
+                           hipStream_t s) {
+	DX_REQUIRE(T.geo && T.lg_layout && (nh == 26 || nh == 6), "level-0 game not available");
+	if (!n_local) return;
 	const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 	const GeoBox B{T.box0[0],
 	               T.box0[1],
@@ -1088,17 +1139,15 @@ void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_
 	               {T.geo_lb[0], T.geo_lb[1], T.geo_lb[2]},
 	               {T.geo_bstride[0], T.geo_bstride[1], T.geo_bstride[2]},
 	               {T.geo_istride[0], T.geo_istride[1], T.geo_istride[2]}};
-	const unsigned nb0 = unsigned((T.n_lvl0 + 255) / 256), nb1 = unsigned((8 * T.ng + 255) / 256);
-	if (nb0 + nb1 == 0) return;
-	lg_table_kernel<<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state, G, B,
-	                                         T.l0tab.p, err);
+	const size_t nr = T.n_lg_rows;
+	if (!nr) return;
+	const unsigned nb = xcd_grid((nr + 255) / 256);
+	lg_table_kernel<<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, G, B, T.l0tab.p, err);
 	HIP_CHECK(hipGetLastError());
 	if (nh == 26)
-		lg_game_kernel<true><<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state,
-		                                              T.l0tab.p, G, B, err);
+		lg_game_kernel<true><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
 	else
-		lg_game_kernel<false><<<nb0 + nb1, 256, 0, s>>>(T.lvl0.p, T.n_lvl0, nb0, T.gptr.p, T.ng, T.gslot.p, T.l0c.p, state,
-		                                               T.l0tab.p, G, B, err);
+		lg_game_kernel<false><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
 	HIP_CHECK(hipGetLastError());
 }
 

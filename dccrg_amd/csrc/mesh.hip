@@ -81,7 +81,81 @@ void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t
 	k_hash_insert(M.tab.p, M.mask, M.shift, ids, owners, -2, n, s, slot_upto);
 }
 
+// The range map (dccrgx_mesh.hpp) when the known ids' per-level ranges hold
+// at most 32 ids per known leaf (+16 M) - one process, or slab partitions -
+// else the hash table.  DCCRGX_RANGE_MAP=0 forces the table.
+void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
+                      size_t slot_upto) {
+	static const char* env = std::getenv("DCCRGX_RANGE_MAP");
+	const bool allowed = !(env && env[0] == '0');
+	uint64_t lo[kRangeLevels], hi[kRangeLevels];
+	M.rmap.release();
+	M.rl.release();
+	M.rlev = 0;
+	if (allowed && n && k_level_ranges(m, ids, n, lo, hi, s)) {
+		uint64_t total = 0;
+		std::vector<RangeLevel> rl;
+		for (int L = 0; L < kRangeLevels; L++) {
+			if (hi[L] == 0) continue;  // no id of this level
+			rl.push_back(RangeLevel{lo[L], hi[L] + 1, total});
+			total += hi[L] + 1 - lo[L];
+		}
+		if (total <= 32 * uint64_t(n) + (uint64_t(1) << 24) && total < (uint64_t(1) << 31)) {
+			M.rlev = int(rl.size());
+			upload(M.rl, rl, s);
+			M.rmap.alloc(size_t(total));
+			HIP_CHECK(hipMemsetAsync(M.rmap.p, 0xff, size_t(total) * sizeof(int2), s));
+			M.tab.release();
+			M.mask = 0;
+			k_range_insert(M.rmap.p, M.dev(m.last), ids, owners, n, slot_upto, s);
+			return;
+		}
+	}
+	mesh_build_hash(M, ids, owners, n, s, slot_upto);
+}
+
+// rebuild's direct mode (one process, the own leaves in slot order): the
+// grid's persistent map over every level's whole id range when that is at
+// most 32 entries per known leaf (+16 M); the previous mesh's entries are
+// cleared one by one (its known list), not the whole map
+static bool mesh_build_range_full(Grid& g, Mesh& M, const Mesh& old, size_t slot_upto, hipStream_t s) {
+	static const char* env = std::getenv("DCCRGX_RANGE_MAP");
+	if (env && env[0] == '0') return false;
+	const MapCtx& m = g.m;
+	if (m.R >= kRangeLevels || !M.n_known) return false;
+	const uint64_t total = m.last;  // ids 1..last, entry id - 1
+	if (total > 32 * uint64_t(M.n_known) + (uint64_t(1) << 24) || total >= (uint64_t(1) << 31)) return false;
+	if (!g.rmap_full.p || g.rmap_full.n != size_t(total)) {
+		std::vector<RangeLevel> rl;
+		for (int L = 0; L <= m.R; L++) rl.push_back(RangeLevel{m.first[L], m.first[L + 1], m.first[L] - 1});
+		upload(g.rl_full, rl, s);
+		g.rmap_full.alloc(size_t(total));
+		g.rmap_full_clean = false;
+	}
+	Mesh probe;
+	probe.rmap_shared = g.rmap_full.p;
+	probe.rl_shared = g.rl_full.p;
+	probe.rlev = m.R + 1;
+	const DevMesh pd = probe.dev(m.last);
+	if (old.rmap_shared == g.rmap_full.p && old.kid.p && old.n_known) {
+		k_range_clear(g.rmap_full.p, pd, old.kid.p, old.n_known, s);  // the entries the previous mesh wrote
+	} else if (!g.rmap_full_clean) {
+		HIP_CHECK(hipMemsetAsync(g.rmap_full.p, 0xff, g.rmap_full.n * sizeof(int2), s));
+	}
+	g.rmap_full_clean = false;
+	M.tab.release();
+	M.rmap.release();
+	M.rl.release();
+	M.mask = 0;
+	M.rmap_shared = g.rmap_full.p;
+	M.rl_shared = g.rl_full.p;
+	M.rlev = m.R + 1;
+	k_range_insert(g.rmap_full.p, pd, M.kid.p, M.kown.p, M.n_known, slot_upto, s);
+	return true;
+}
+
 void mesh_init_implicit(Grid& g) {
+	if (g.mesh.rmap_shared) g.rmap_full_clean = false;
 	g.mesh = Mesh{};
 	g.mesh.implicit = true;
 	g.mesh.bp.init(g.m.first[1] - 1, uint64_t(g.size));
@@ -287,6 +361,10 @@ void rebuild(Grid& g, Mesh& nm) {
 	g.mesh = std::move(nm);
 	Mesh& M = g.mesh;
 	M.tab.release();
+	M.rmap.release();
+	M.rl.release();
+	M.rmap_shared = nullptr;
+	M.rl_shared = nullptr;
 
 	// slot order: Morton order of the min corner on refined grids (step 2)
 	int order = g.slot_order;
@@ -310,7 +388,12 @@ void rebuild(Grid& g, Mesh& nm) {
 		// one process, own leaves already in Morton order: the prefix is the
 		// slot order, so the table gets its slots as it is built
 		direct = g.size == 1 && M.n_prefix && g.morton_slots && M.prefix_run1 == M.n_prefix && M.n_known == M.n_prefix;
-		mesh_build_hash(M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
+		if (!(direct && mesh_build_range_full(g, M, old, M.n_prefix, s))) {
+			// a mesh of its own; the shared map (if the previous mesh used it)
+			// keeps that mesh's entries
+			if (old.rmap_shared) g.rmap_full_clean = false;
+			mesh_build_range(m, M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
+		}
 		DX_LAP("rb.1a_hash");
 		if (M.n_prefix && g.morton_slots) {
 			// the own leaves are kid's prefix, in (at most two runs of) Morton order
@@ -486,8 +569,14 @@ void rebuild(Grid& g, Mesh& nm) {
 		}
 		DBuf<uint8_t> nd;
 		nd.alloc(g.n_slots * f.elem);
-		if (f.data.p && old_slot_ids.p) k_gather_rows(f.data.p, src.p, g.n_slots, f.elem, nd.p, s);  // zeros where no source
-		else if (nd.n) HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
+		if (f.no_carry && nd.n) {
+			if (g.n_slots > nl) HIP_CHECK(hipMemsetAsync(nd.p + nl * f.elem, 0, (g.n_slots - nl) * f.elem, s));
+		} else if (f.data.p && old_slot_ids.p) {
+			k_gather_rows(f.data.p, src.p, g.n_slots, f.elem, nd.p, s);  // zeros where no source
+		} else if (nd.n) {
+			HIP_CHECK(hipMemsetAsync(nd.p, 0, nd.n, s));
+		}
+		f.no_carry = false;
 		f.data.swap(nd);
 		f.scratch.release();
 	}
@@ -583,29 +672,12 @@ void ensure_face(Grid& g) {
 	hipStream_t s = g.s_comp;
 	DX_PHASE("face.build", s);
 	const size_t nl = g.n_local;
-	const DevMesh dm = g.dm();
-	// pass 0: per row (finer faces << 32 | entries) and per direction a hint;
-	// pass 1: CSR rows and the fixed-width table from the scan
-	DBuf<uint64_t> cnt, pos;
-	cnt.alloc(nl + 1);
-	pos.alloc(nl + 1);
-	g.face_ptr.alloc(nl + 1);
 	DBuf<int32_t> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
-	DBuf<int32_t> hint;  // per row and direction what pass 0 found (build_kernels.hip)
-	hint.alloc(6 * nl + 6);
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, cnt.p, hint.p, nullptr, nullptr, nullptr, nullptr, nullptr, err.p, 0, s,
-	             g.morton_slots, g.n_inner);
-	const uint64_t tot = nl ? scan_exclusive_u64(cnt.p, pos.p, nl, s) : 0;
-	const size_t t = size_t(tot & 0xffffffffu);
-	g.n_fine_faces = size_t(tot >> 32);
-	g.face_ent.alloc(t + 1);
 	g.face_ell.alloc(6 * nl + 6);
-	g.face_fine.alloc(4 * g.n_fine_faces + 4);
-	if (!nl) HIP_CHECK(hipMemsetAsync(g.face_ptr.p, 0, 4, s));
-	k_face_lists(g.m, dm, g.slot_ids.p, nl, nullptr, hint.p, pos.p, g.face_ptr.p, g.face_ent.p, g.face_ell.p,
-	             g.face_fine.p, err.p, 1, s);
+	g.n_fine_faces = k_face_table(g.m, g.dm(), g.slot_ids.p, nl, g.n_inner, g.morton_slots, g.face_ell.p,
+	                              g.face_fine, err.p, s);
 	g.slot_lvl.alloc(g.n_slots + 1);
 	k_slot_levels(g.m, g.slot_ids.p, g.n_slots, g.slot_lvl.p, s);
 	int32_t herr = 0;
@@ -613,10 +685,20 @@ void ensure_face(Grid& g) {
 	HIP_CHECK(hipStreamSynchronize(s));
 	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
 	g.face_valid = true;
+	g.face_csr_valid = false;
+}
+
+void ensure_face_csr(Grid& g) {
+	ensure_face(g);
+	if (g.face_csr_valid) return;
+	k_face_csr(g.face_ell.p, g.face_fine.p, g.n_local, g.face_ptr, g.face_ent, g.s_comp);
+	// consumers read the rows with blocking copies on the null stream
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	g.face_csr_valid = true;
 }
 
 void ensure_tiles(Grid& g) {
-	ensure_face(g);
+	ensure_face_csr(g);
 	if (g.tiles_valid) return;
 	DX_LAPS(g.s_comp);
 	const int T = g.tile;

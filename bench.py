@@ -219,13 +219,8 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
     halo between them is a no-op).
 
-    Roofline bytes per leaf and step: the minimum any implementation moves
-    from HBM - the leaf's state (4 B), its neighbors_of row (4 B per entry +
-    4 B row pointer) and the collected list it writes (data[1..8], 64 B):
-    4 + (4 k + 4) + 64, at or below the PMC-measured traffic.  The
-    per-gather count (every neighbor's parent and state, the siblings'
-    lists) is reported beside it as `logical_bytes_per_leaf`, not as HBM
-    traffic."""
+    One process, so the turn is the level-0 game (gol_amr.hip): the
+    roofline bytes are the ones its two passes move (below)."""
     n = 2048
     g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
     g.set_maximum_refinement_level(1).initialize()
@@ -251,17 +246,24 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     nl = g.n_local
     kbar = g.neighbor_entries("of") / nl
     f1 = float(np.mean(lvl == 1))
-    # roofline: the bytes the turn's kernels must move per leaf (the geometric
-    # collect, gol_amr.hip: level-0 coordinates 4 B, octant 1 B, state read 4 B
-    # and written 4 B, mask written 4 B and read back 4 B) over the turn's
-    # kernel time: `achieved` / `frac` are a share of HBM bandwidth.  SURVEY
-    # §8(d)'s fixed CSR/AMR figure (8 B + 4 B per neighbor entry + 4 B row
-    # pointer) counts neighbor-entry reads this path does not make; it is
-    # reported beside it as model_throughput_GBs / frac_model, a throughput
-    # figure, not bandwidth.
+    # roofline: the bytes the turn's kernels must move over the turn's kernel
+    # time, so `achieved` / `frac` are a share of HBM bandwidth.  The grid is
+    # one process (a replica per GPU), so the turn is the level-0 game
+    # (gol_amr.hip lg_table_kernel + lg_game_kernel, one row per level-0
+    # cell): per leaf its state read by the table pass and read + written by
+    # the game pass (12 B), per level-0 cell the row's slot, octant byte and
+    # packed level-0 coordinates read by both passes (2 x 9 B) and its table
+    # byte written once and read once (2 B).  SURVEY §8(d)'s fixed CSR/AMR
+    # figure (8 B + 4 B per neighbor entry + 4 B row pointer) counts
+    # neighbor-entry reads this path does not make; it is reported beside it
+    # as model_throughput_GBs / frac_model, a throughput figure, not
+    # bandwidth.
     per_cell = 8 + 4 * kbar + 4
-    moved = 4 + 1 + 4 + 4 + 4 + 4
-    ach = moved * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
+    moved_step = 12 * nl + 20 * n * n
+    kern = "lg_table_kernel + lg_game_kernel (+ the gated exact collect / spread, which exit at once)"
+    moved_model = "level-0 game: 12 B per leaf (state) + 20 B per level-0 cell (row, octant, coordinates, table)"
+    moved = moved_step / nl
+    ach = moved_step * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     model = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
                      nl * a.steps / el, 1, a, el / a.steps * 1e3, "u32",
@@ -270,11 +272,10 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                       "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
     line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS if ach else None,
-                        "traffic": measured_traffic("gol_amr", nl, moved * nl, 1),
-                        "kernel": "geo_l0_leaves + geo_l0_groups + geo_collect + gol_amr_spread0_mask + "
-                                  "gol_amr_spread_groups_mask",
-                        "alg_bytes_per_leaf": moved, "alg_bytes_per_step": moved * nl,
-                        "alg_bytes_model": "bytes the geometric collect moves per leaf",
+                        "traffic": measured_traffic("gol_amr", nl, moved_step, 1),
+                        "kernel": kern,
+                        "alg_bytes_per_leaf": moved, "alg_bytes_per_step": moved_step,
+                        "alg_bytes_model": moved_model,
                         "model_bytes_per_leaf": per_cell, "model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
                         "model_throughput_GBs": model, "frac_model": model / PEAK_HBM_GBS if model else None,
                         "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}

@@ -14,7 +14,7 @@ for w in $WORKLOADS; do
     advection) re='advection_(regular|tiles)'; args="--steps 10 --warmup 1" ;;
     gol) re='gol_structured'; args="--workload gol --steps 10 --warmup 1" ;;
     scalability) re='gol_structured'; args="--workload scalability --steps 10 --warmup 1" ;;
-    gol_amr) re='gol_amr_(values|collect|spread)'; args="--workload gol_amr --steps 10 --warmup 1" ;;
+    gol_amr) re='lg_(table|game)_kernel|gol_amr_spread|geo_collect'; args="--workload gol_amr --steps 10 --warmup 1" ;;
     poisson) re='po_(phase|reduce)'; args="--workload poisson --steps 10 --warmup 1" ;;
     *) echo "unknown workload $w"; exit 2 ;;
   esac

@@ -2084,9 +2084,9 @@ int dccrgx_get_migration_cells(dccrgx_grid* gp, int peer, int incoming, uint64_t
 	});
 }
 
-// set_send_single_cells 6677 / get_send_single_cells 6684: accepted and
-// reported; the wire message is always one per peer and field (message
-// boundaries carry no data here, so the received payloads are the same)
+// set_send_single_cells 6677 / get_send_single_cells 6684: on, the halo's
+// fixed-size payloads go on the wire one cell at a time (comm.hip
+// wire_pieces); the received payloads are the same either way
 int dccrgx_set_send_single_cells(dccrgx_grid* gp, int on) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);

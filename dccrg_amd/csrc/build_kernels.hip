@@ -315,26 +315,48 @@ __global__ void fill_nto_kernel(MapCtx m, const int32_t* hood_to, int nh, DevMes
 }
 
 // --------------------------------------------------------------------------
+// owned-elsewhere entries as keys owner * stride + id, or (owners != nullptr,
+// ids too deep for such keys) as the id in keys[] and the owner in owners[]
 __global__ void extract_remote_kernel(const uint64_t* ids, size_t n, DevMesh M, int rank, uint64_t stride,
-                                      uint64_t* keys, unsigned long long* counter) {
+                                      uint64_t* keys, uint32_t* owners, unsigned long long* counter) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = ids[i];
 		if (id == error_cell) continue;
 		const int32_t o = dm_owner(M, id);
-		if (o >= 0 && o != rank) keys[atomicAdd(counter, 1ull)] = uint64_t(o) * stride + id;
+		if (o < 0 || o == rank) continue;
+		const unsigned long long at = atomicAdd(counter, 1ull);
+		if (owners) {
+			keys[at] = id;
+			owners[at] = uint32_t(o);
+		} else {
+			keys[at] = uint64_t(o) * stride + id;
+		}
 	}
 }
 
 __global__ void extract_send_kernel(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids,
                                     size_t row0, size_t nrows, DevMesh M, int rank, uint64_t stride, uint64_t* keys,
-                                    unsigned long long* counter) {
+                                    uint32_t* owners, unsigned long long* counter) {
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r < nrows; r += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t self = slot_ids[row0 + r];
 		for (uint32_t e = nto_ptr[r]; e < nto_ptr[r + 1]; e++) {
 			const int32_t o = dm_owner(M, nto_id[e]);
-			if (o >= 0 && o != rank) keys[atomicAdd(counter, 1ull)] = uint64_t(o) * stride + self;
+			if (o < 0 || o == rank) continue;
+			const unsigned long long at = atomicAdd(counter, 1ull);
+			if (owners) {
+				keys[at] = self;
+				owners[at] = uint32_t(o);
+			} else {
+				keys[at] = uint64_t(o) * stride + self;
+			}
 		}
 	}
+}
+
+// 1 where a (owner, id) pair differs from the one before it
+__global__ void pair_heads_kernel(const uint64_t* ids, const uint32_t* owners, size_t n, uint8_t* head) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		head[i] = (i == 0 || ids[i] != ids[i - 1] || owners[i] != owners[i - 1]) ? 1 : 0;
 }
 
 __global__ void lookup_slots_kernel(const uint64_t* ids, size_t n, DevMesh M, int32_t* out, int32_t* err) {
@@ -1094,25 +1116,80 @@ static void zero_counter(DBuf<unsigned long long>& ctr, hipStream_t s) {
 	HIP_CHECK(hipMemsetAsync(ctr.p, 0, sizeof(unsigned long long), s));
 }
 
-size_t k_extract_remote(const uint64_t* ids, size_t n, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out,
-                        hipStream_t s) {
-	if (!n) return 0;
-	DBuf<unsigned long long> ctr;
-	zero_counter(ctr, s);
-	extract_remote_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, rank, stride, keys_out, ctr.p);
+// the n extracted entries grouped by owner, each group's ids ascending and
+// unique: one 64-bit key sort, or for pairs a sort by id then a stable sort
+// by owner and a select of the pair heads
+static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t stride, int size,
+                           std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
+	out.clear();
+	if (!n) return;
+	if (!owners) {
+		n = sort_unique_u64(keys, n, s);
+		for (uint64_t k : download(keys, n, s)) out[int(k / stride)].push_back(k % stride);
+		return;
+	}
+	DBuf<uint64_t> k2;
+	DBuf<uint32_t> o2;
+	k2.alloc(n);
+	o2.alloc(n);
+	int obits = 1;
+	while (obits < 32 && (uint64_t(size) >> obits)) obits++;
+	size_t b1 = 0, b2 = 0, b3 = 0;
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, keys, k2.p, owners, o2.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, o2.p, owners, k2.p, keys, n, 0, obits, s));
+	DBuf<uint8_t> head;
+	head.alloc(n);
+	DBuf<unsigned long long> nsel;
+	nsel.alloc(1);
+	HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, b3, keys, head.p, k2.p, nsel.p, n, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(std::max(b1, std::max(b2, b3)));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, b1, keys, k2.p, owners, o2.p, n, 0, 64, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, b2, o2.p, owners, k2.p, keys, n, 0, obits, s));
+	pair_heads_kernel<<<grid_for(n, 256), 256, 0, s>>>(keys, owners, n, head.p);
 	HIP_CHECK(hipGetLastError());
-	return read_counter(ctr, s);
+	HIP_CHECK(hipcub::DeviceSelect::Flagged(temp.p, b3, keys, head.p, k2.p, nsel.p, n, s));
+	HIP_CHECK(hipcub::DeviceSelect::Flagged(temp.p, b3, owners, head.p, o2.p, nsel.p, n, s));
+	const size_t u = read_counter(nsel, s);
+	const std::vector<uint64_t> ids = download(k2.p, u, s);
+	const std::vector<uint32_t> own = download(o2.p, u, s);
+	for (size_t i = 0; i < u; i++) out[int(own[i])].push_back(ids[i]);
 }
 
-size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
-                      size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s) {
-	if (!nrows) return 0;
+void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size,
+                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
+	out.clear();
+	if (!n) return;
+	const uint64_t stride = M.last + 1;
+	const bool pairs = uint64_t(size) > ~uint64_t(0) / stride;
+	DBuf<uint64_t> keys;
+	DBuf<uint32_t> owners;
+	keys.alloc(n);
+	if (pairs) owners.alloc(n);
+	DBuf<unsigned long long> ctr;
+	zero_counter(ctr, s);
+	extract_remote_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, rank, stride, keys.p, owners.p, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	group_by_owner(keys.p, owners.p, read_counter(ctr, s), stride, size, out, s);
+}
+
+void k_send_by_owner(const uint64_t* nto_id, const uint32_t* nto_ptr, size_t n_entries, const uint64_t* slot_ids,
+                     size_t row0, size_t nrows, const DevMesh& M, int rank, int size,
+                     std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
+	out.clear();
+	if (!nrows || !n_entries) return;
+	const uint64_t stride = M.last + 1;
+	const bool pairs = uint64_t(size) > ~uint64_t(0) / stride;
+	DBuf<uint64_t> keys;
+	DBuf<uint32_t> owners;
+	keys.alloc(n_entries);
+	if (pairs) owners.alloc(n_entries);
 	DBuf<unsigned long long> ctr;
 	zero_counter(ctr, s);
 	extract_send_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(nto_id, nto_ptr, slot_ids, row0, nrows, M, rank, stride,
-	                                                         keys_out, ctr.p);
+	                                                         keys.p, owners.p, ctr.p);
 	HIP_CHECK(hipGetLastError());
-	return read_counter(ctr, s);
+	group_by_owner(keys.p, owners.p, read_counter(ctr, s), stride, size, out, s);
 }
 
 __global__ void iota_i32_kernel(int32_t* out, size_t n) {

@@ -30,27 +30,69 @@ void comm_require(const Grid& g, const char* what) {
 		                               " needs a communicator (grid created without an RCCL id or an exchange function)");
 }
 
-// The byte mover.  Messages to / from one peer keep their list order (the
-// wire order): RCCL matches a pair's sends and receives in posting order,
-// the host exchange concatenates them in list order.  Returns with the
-// transfer queued on `s` (RCCL) or completed (host exchange).
+// The wire: per direction a list of (peer, pointer, bytes) pieces.  A
+// message is one piece each way, except under send_single_cells (6658-6681,
+// start_user_data_transfers 10613-10692: one MPI message per cell, in the
+// cells' order): then the consecutive messages of a peer that are runs of
+// cells (DevMsg::cell) go out cell by cell, each cell's pieces in message
+// (field) order, so the wire carries the reference's per-cell sequence.  The
+// pieces land where their messages point, so the bytes placed are the same
+// either way.
+struct Piece {
+	int peer;
+	uint8_t* p;
+	size_t n;
+};
+
+static void wire_pieces(const std::vector<DevMsg>& msgs, bool single, std::vector<Piece>& snd, std::vector<Piece>& rcv) {
+	for (size_t i = 0; i < msgs.size();) {
+		size_t j = i;
+		while (j < msgs.size() && msgs[j].peer == msgs[i].peer) j++;
+		for (int dir = 0; dir < 2; dir++) {
+			auto bytes = [&](const DevMsg& m) { return dir == 0 ? m.send_bytes : m.recv_bytes; };
+			auto ptr = [&](const DevMsg& m) {
+				return dir == 0 ? const_cast<uint8_t*>(m.send) : m.recv;
+			};
+			std::vector<Piece>& out = dir == 0 ? snd : rcv;
+			// cells per message of the run, when every message is a run of as many
+			size_t cells = 0;
+			bool split = single;
+			for (size_t k = i; k < j && split; k++) {
+				const DevMsg& m = msgs[k];
+				split = m.cell > 0 && bytes(m) % m.cell == 0 && (k == i || bytes(m) / m.cell == cells);
+				if (split) cells = bytes(m) / m.cell;
+			}
+			if (split) {
+				for (size_t c = 0; c < cells; c++)
+					for (size_t k = i; k < j; k++) out.push_back({msgs[k].peer, ptr(msgs[k]) + c * msgs[k].cell, msgs[k].cell});
+			} else {
+				for (size_t k = i; k < j; k++)
+					if (bytes(msgs[k])) out.push_back({msgs[k].peer, ptr(msgs[k]), bytes(msgs[k])});
+			}
+		}
+		i = j;
+	}
+}
+
+// The byte mover.  Pieces to / from one peer keep their order (the wire
+// order): RCCL matches a pair's sends and receives in posting order, the host
+// exchange concatenates them in that order.  Returns with the transfer
+// queued on `s` (RCCL) or completed (host exchange).
 static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) {
+	std::vector<Piece> snd, rcv;
+	wire_pieces(msgs, g.send_single_cells, snd, rcv);
 	if (g.nccl && !g.xfn) {
 		NCCL_CHECK(ncclGroupStart());
-		for (const auto& m : msgs) {
-			if (m.send_bytes) NCCL_CHECK(ncclSend(m.send, m.send_bytes, ncclUint8, m.peer, g.nccl, s));
-			if (m.recv_bytes) NCCL_CHECK(ncclRecv(m.recv, m.recv_bytes, ncclUint8, m.peer, g.nccl, s));
-		}
+		for (const auto& m : snd) NCCL_CHECK(ncclSend(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
+		for (const auto& m : rcv) NCCL_CHECK(ncclRecv(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
 		NCCL_CHECK(ncclGroupEnd());
 		return;
 	}
 	const size_t P = size_t(g.size);
 	std::vector<size_t> sb(P, 0), rb(P, 0);
-	for (const auto& m : msgs) {
-		DX_REQUIRE(m.peer >= 0 && m.peer < g.size && m.peer != g.rank, "message to an invalid peer");
-		sb[size_t(m.peer)] += m.send_bytes;
-		rb[size_t(m.peer)] += m.recv_bytes;
-	}
+	for (const auto& m : msgs) DX_REQUIRE(m.peer >= 0 && m.peer < g.size && m.peer != g.rank, "message to an invalid peer");
+	for (const auto& m : snd) sb[size_t(m.peer)] += m.n;
+	for (const auto& m : rcv) rb[size_t(m.peer)] += m.n;
 	std::vector<std::vector<uint8_t>> hs(P), hr(P);
 	std::vector<size_t> so(P, 0), ro(P, 0);
 	for (size_t p = 0; p < P; p++) {
@@ -58,10 +100,10 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 		hr[p].resize(rb[p]);
 	}
 	HIP_CHECK(hipStreamSynchronize(s));  // the send buffers are complete
-	for (const auto& m : msgs) {
+	for (const auto& m : snd) {
 		const size_t p = size_t(m.peer);
-		if (m.send_bytes) HIP_CHECK(hipMemcpyAsync(hs[p].data() + so[p], m.send, m.send_bytes, hipMemcpyDefault, s));
-		so[p] += m.send_bytes;
+		HIP_CHECK(hipMemcpyAsync(hs[p].data() + so[p], m.p, m.n, hipMemcpyDefault, s));
+		so[p] += m.n;
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 	std::vector<const void*> sp(P, nullptr);
@@ -71,10 +113,10 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 		rp[p] = hr[p].data();
 	}
 	DX_REQUIRE(g.xfn(g.xctx, sp.data(), sb.data(), rp.data(), rb.data()) == 0, "exchange function failed");
-	for (const auto& m : msgs) {
+	for (const auto& m : rcv) {
 		const size_t p = size_t(m.peer);
-		if (m.recv_bytes) HIP_CHECK(hipMemcpyAsync(m.recv, hr[p].data() + ro[p], m.recv_bytes, hipMemcpyDefault, s));
-		ro[p] += m.recv_bytes;
+		HIP_CHECK(hipMemcpyAsync(m.p, hr[p].data() + ro[p], m.n, hipMemcpyDefault, s));
+		ro[p] += m.n;
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 }

@@ -439,7 +439,7 @@ struct Grid {
 	hipStream_t s_comp = nullptr, s_comm = nullptr;
 	hipEvent_t ev_comp = nullptr, ev_halo = nullptr;
 	bool halo_in_flight = false;
-	bool send_single_cells = false;  // set_send_single_cells (6677), reported only
+	bool send_single_cells = false;  // set_send_single_cells (6677): halo messages one cell at a time
 
 	// setup (dccrg.hpp:8120-8230)
 	uint64_t len[3] = {1, 1, 1};
@@ -591,13 +591,16 @@ void comm_allreduce_f64(Grid& g, double* v, int count, int op);  // 0 sum, 1 min
 // the same on device values, queued on s (stream-ordered over RCCL)
 void comm_allreduce_f64_dev(Grid& g, const double* d_in, double* d_out, int count, int op, hipStream_t s);
 uint64_t comm_allreduce_max_u64(Grid& g, uint64_t v);
-// device payloads: per peer one message of known size each way
+// device payloads: per peer one message of known size each way.  cell > 0:
+// the message is a run of cells of `cell` bytes each way, which
+// send_single_cells (6677) puts on the wire one cell at a time (comm.hip)
 struct DevMsg {
 	int peer;
 	const uint8_t* send;
 	size_t send_bytes;
 	uint8_t* recv;
 	size_t recv_bytes;
+	size_t cell = 0;
 };
 // one grouped point-to-point round of device messages (the same message list
 // for every transport; see comm.hip)
@@ -634,10 +637,6 @@ void ensure_tiles(Grid& g);
 const std::vector<uint64_t>& slot_ids_host(Grid& g);
 // batch lookups of known leaves: owner (-1 unknown) and slot (-1 none)
 void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot);
-void lists_on_host(Grid& g, const std::vector<uint64_t>& of_id, const std::vector<uint64_t>& to_id,
-                   const std::vector<uint32_t>& to_ptr, const std::vector<uint64_t>& self,
-                   std::map<int, std::vector<uint64_t>>& recv_ids, std::map<int, std::vector<uint64_t>>& send_ids,
-                   std::vector<uint64_t>* extra_remote);
 int32_t lookup_owner(Grid& g, uint64_t id);
 bool is_local_cell(Grid& g, uint64_t id);
 int64_t lookup_slot(Grid& g, uint64_t id);
@@ -677,13 +676,16 @@ void k_count_rows(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, 
                   const uint64_t* slot_ids, size_t row0, size_t nrows, uint32_t* nof_cnt, uint32_t* nto_cnt,
                   hipStream_t s);
 int max_hood_items();  // largest stencil the neighbors_to dedupe can hold in LDS
-// remote (owner != rank) entries of an id array as composite keys owner*(last+1)+id
-size_t k_extract_remote(const uint64_t* ids, size_t n, const DevMesh& M, int rank, uint64_t stride,
-                        uint64_t* keys_out, hipStream_t s);
-// keys for the send side: for each neighbors_to entry with a remote owner,
-// owner*(last+1) + the row's own id
-size_t k_extract_send(const uint64_t* nto_id, const uint32_t* nto_ptr, const uint64_t* slot_ids, size_t row0,
-                      size_t nrows, const DevMesh& M, int rank, uint64_t stride, uint64_t* keys_out, hipStream_t s);
+// the entries of an id array owned by another process, grouped by owner
+// (each group ascending, unique); device sorts of owner * (last + 1) + id
+// keys, or of (owner, id) pairs when the ids leave no room for the owner
+void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size,
+                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s);
+// the send side: for each neighbors_to entry (n_entries in all) with a remote
+// owner, the row's own id under that owner
+void k_send_by_owner(const uint64_t* nto_id, const uint32_t* nto_ptr, size_t n_entries, const uint64_t* slot_ids,
+                     size_t row0, size_t nrows, const DevMesh& M, int rank, int size,
+                     std::map<int, std::vector<uint64_t>>& out, hipStream_t s);
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit = 64);  // in place; keys < 2^end_bit
 void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit = 64);  // in place; keys < 2^end_bit
 void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s);  // host list, device radix sort when large

@@ -235,7 +235,8 @@ static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 	// one message per peer and field (field order): the send slice of the
 	// packed buffer, received straight into the peer's run of halo slots for
 	// a whole-element field of a direct plan, else into the receive buffer
-	// and placed; the same list for RCCL and the host exchange
+	// and placed; the same list for RCCL and the host exchange (cell by cell
+	// on the wire under send_single_cells, comm.hip)
 	std::vector<DevMsg> msgs;
 	for (int p : H.peers()) {
 		const size_t ns = count_of(H.send_ids, p), nr = count_of(H.recv_ids, p);
@@ -244,7 +245,8 @@ static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 			Field* f = tf[k];
 			uint8_t* dst = direct && f->full_window() ? f->data.p + (g.n_local + ro) * f->elem
 			                                          : H.recvbuf.p + L.rfo[k] + ro * f->win_len;
-			msgs.push_back({p, H.sendbuf.p + L.sfo[k] + so * f->win_len, ns * f->win_len, dst, nr * f->win_len});
+			msgs.push_back({p, H.sendbuf.p + L.sfo[k] + so * f->win_len, ns * f->win_len, dst, nr * f->win_len,
+			                f->win_len});
 		}
 	}
 	comm_device_transfer(g, msgs, s);
@@ -302,20 +304,9 @@ UserHood& ensure_uhood(Grid& g, int id) {
 	HaloPlan& P = h.plan;
 	P.send_ids.clear();
 	P.recv_ids.clear();
-	if (g.size > 1 && uint64_t(g.size) > ~uint64_t(0) / (g.m.last + 1)) {
-		// ids too large for owner * (last + 1) + id keys (mesh.hip rebuild)
-		lists_on_host(g, download(h.nof_id.p, t_of, s), download(h.nto_id.p, t_to, s), download(h.nto_ptr.p, nl + 1, s),
-		              download(g.slot_ids.p, nl, s), P.recv_ids, P.send_ids, nullptr);
-	} else if (g.size > 1) {
-		const uint64_t stride = g.m.last + 1;
-		DBuf<uint64_t> keys;
-		keys.alloc(std::max(t_of, t_to) + 1);
-		size_t nk = k_extract_remote(h.nof_id.p, t_of, dm, g.rank, stride, keys.p, s);
-		nk = sort_unique_u64(keys.p, nk, s);
-		for (uint64_t k : download(keys.p, nk, s)) P.recv_ids[int(k / stride)].push_back(k % stride);
-		nk = k_extract_send(h.nto_id.p, h.nto_ptr.p, g.slot_ids.p, 0, nl, dm, g.rank, stride, keys.p, s);
-		nk = sort_unique_u64(keys.p, nk, s);
-		for (uint64_t k : download(keys.p, nk, s)) P.send_ids[int(k / stride)].push_back(k % stride);
+	if (g.size > 1) {
+		k_remote_by_owner(h.nof_id.p, t_of, dm, g.rank, g.size, P.recv_ids, s);
+		k_send_by_owner(h.nto_id.p, h.nto_ptr.p, t_to, g.slot_ids.p, 0, nl, dm, g.rank, g.size, P.send_ids, s);
 	}
 	std::vector<uint64_t> sall, rall;
 	P.send_off.clear();

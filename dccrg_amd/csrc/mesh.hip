@@ -293,57 +293,6 @@ void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n) {
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 
-// send / receive lists (and the neighbors_to-only remote cells) of rows
-// `self` from their neighbors_of / neighbors_to ids, grouped by owner on the
-// host: the fallback of the device key sort (owner * (last + 1) + id) for
-// grids whose ids leave no room for the owner in 64 bits
-void lists_on_host(Grid& g, const std::vector<uint64_t>& of_id, const std::vector<uint64_t>& to_id,
-                   const std::vector<uint32_t>& to_ptr, const std::vector<uint64_t>& self,
-                   std::map<int, std::vector<uint64_t>>& recv_ids, std::map<int, std::vector<uint64_t>>& send_ids,
-                   std::vector<uint64_t>* extra_remote) {
-	std::vector<uint64_t> u(of_id);
-	u.insert(u.end(), to_id.begin(), to_id.end());
-	std::sort(u.begin(), u.end());
-	u.erase(std::unique(u.begin(), u.end()), u.end());
-	std::vector<int32_t> own(u.size());
-	lookup_batch(g, u.data(), u.size(), own.data(), nullptr);
-	const auto owner = [&](uint64_t id) {
-		const auto it = std::lower_bound(u.begin(), u.end(), id);
-		return it != u.end() && *it == id ? own[size_t(it - u.begin())] : -1;
-	};
-	std::map<int, std::set<uint64_t>> recv, send, rem_to;
-	for (uint64_t id : of_id) {
-		const int o = owner(id);
-		if (o >= 0 && o != g.rank) recv[o].insert(id);
-	}
-	for (size_t r = 0; r < self.size(); r++)
-		for (uint32_t e = to_ptr[r]; e < to_ptr[r + 1]; e++) {
-			const int o = owner(to_id[e]);
-			if (o >= 0 && o != g.rank) {
-				send[o].insert(self[r]);
-				rem_to[o].insert(to_id[e]);
-			}
-		}
-	recv_ids.clear();
-	send_ids.clear();
-	for (auto& kv : recv) recv_ids[kv.first].assign(kv.second.begin(), kv.second.end());
-	for (auto& kv : send) send_ids[kv.first].assign(kv.second.begin(), kv.second.end());
-	if (!extra_remote) return;
-	std::vector<uint64_t> extra;
-	for (auto& kv : rem_to) {
-		const auto it = recv_ids.find(kv.first);
-		for (uint64_t id : kv.second)
-			if (it == recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id)) extra.push_back(id);
-	}
-	std::sort(extra.begin(), extra.end());
-	*extra_remote = extra;
-}
-
-static void decode_keys(const std::vector<uint64_t>& keys, uint64_t stride, std::map<int, std::vector<uint64_t>>& out) {
-	out.clear();
-	for (uint64_t k : keys) out[int(k / stride)].push_back(k % stride);
-}
-
 // ---------------------------------------------------------------------------
 // (Re)build every local structure from `nm`.  Field payloads of cells that
 // stay on this rank are carried over (old slot -> new slot); freshly created
@@ -446,11 +395,6 @@ void rebuild(Grid& g, Mesh& nm) {
 	H.send_ids.clear();
 	H.recv_ids.clear();
 	g.extra_remote.clear();
-	// the lists are sorted as 64-bit keys owner * (last + 1) + id; a grid at
-	// the id space's deepest levels (set_maximum_refinement_level(-1)) leaves
-	// no room for the owner, and its lists are grouped on the host instead
-	const bool packed = uint64_t(g.size) <= ~uint64_t(0) / (m.last + 1);
-	const uint64_t stride = packed ? m.last + 1 : 0;
 	if (g.n_outer > 0) {
 		const size_t no = g.n_outer;
 		DBuf<uint32_t> c_of, c_to, p_of, p_to;
@@ -461,40 +405,26 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, c_of.p, c_to.p, s);
 		const size_t t_of = scan_exclusive_u32(c_of.p, p_of.p, no, s);
 		const size_t t_to = scan_exclusive_u32(c_to.p, p_to.p, no, s);
-		DBuf<uint64_t> of_id, to_id, keys;
+		DBuf<uint64_t> of_id, to_id;
 		DBuf<int32_t> of_off;
 		of_id.alloc(t_of + 1);
 		of_off.alloc(3 * t_of + 3);
 		to_id.alloc(t_to + 1);
-		keys.alloc(std::max(t_of, t_to) + 1);
 		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, local_slots.p, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
 		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, p_to.p, to_id.p, s);
-		if (!packed) {
-			const std::vector<uint64_t> hof = download(of_id.p, t_of, s), hto = download(to_id.p, t_to, s),
-			                            self = download(local_slots.p + g.n_inner, no, s);
-			const std::vector<uint32_t> hpto = download(p_to.p, no + 1, s);
-			lists_on_host(g, hof, hto, hpto, self, H.recv_ids, H.send_ids, &g.extra_remote);
-		} else {
-			size_t nk = k_extract_remote(of_id.p, t_of, dm, g.rank, stride, keys.p, s);
-			nk = sort_unique_u64(keys.p, nk, s);
-			decode_keys(download(keys.p, nk, s), stride, H.recv_ids);
-			nk = k_extract_send(to_id.p, p_to.p, local_slots.p, g.n_inner, no, dm, g.rank, stride, keys.p, s);
-			nk = sort_unique_u64(keys.p, nk, s);
-			decode_keys(download(keys.p, nk, s), stride, H.send_ids);
-			nk = k_extract_remote(to_id.p, t_to, dm, g.rank, stride, keys.p, s);
-			nk = sort_unique_u64(keys.p, nk, s);
-			std::map<int, std::vector<uint64_t>> rem_to;
-			decode_keys(download(keys.p, nk, s), stride, rem_to);
-			std::vector<uint64_t> extra;
-			for (auto& kv : rem_to) {
-				const auto it = H.recv_ids.find(kv.first);
-				for (uint64_t id : kv.second)
-					if (it == H.recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id))
-						extra.push_back(id);
-			}
-			std::sort(extra.begin(), extra.end());
-			g.extra_remote = extra;
+		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s);
+		k_send_by_owner(to_id.p, p_to.p, t_to, local_slots.p, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
+		std::map<int, std::vector<uint64_t>> rem_to;
+		k_remote_by_owner(to_id.p, t_to, dm, g.rank, g.size, rem_to, s);
+		std::vector<uint64_t> extra;
+		for (auto& kv : rem_to) {
+			const auto it = H.recv_ids.find(kv.first);
+			for (uint64_t id : kv.second)
+				if (it == H.recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id))
+					extra.push_back(id);
 		}
+		std::sort(extra.begin(), extra.end());
+		g.extra_remote = extra;
 	}
 	g.peers = H.peers();
 	DX_LAP("rb.3_lists");

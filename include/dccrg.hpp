@@ -522,8 +522,8 @@ public:
 		return *this;
 	}
 	const std::string& get_load_balancing_method() const { return lb_method_; }  // 8228
-	// set / get_send_single_cells (6658-6681): the flag is kept and reported;
-	// the wire stays one message per peer (the same bytes in the same order)
+	// set / get_send_single_cells (6658-6681): on, remote neighbor updates
+	// send each cell's fixed-size payload as its own message (dccrgx.h)
 	Dccrg& set_send_single_cells(const bool given) {
 		send_single_cells_ = given;
 		if (g_) detail::check(dccrgx_set_send_single_cells(g_, given ? 1 : 0));

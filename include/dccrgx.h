@@ -379,10 +379,13 @@ int dccrgx_variable_field_device_ptr(dccrgx_grid* g, int field_id, void** data, 
 int dccrgx_removed_variable_field_download(dccrgx_grid* g, int field_id, uint64_t* sizes, void* bytes, size_t cap,
                                            size_t* nbytes);
 /* set_send_single_cells 6677 / get_send_single_cells 6684: one message per
- * cell (tag = position + 1) instead of one per process.  Accepted and
- * reported; the library always sends one message per peer and field, which
- * carries the same bytes in the same order (message boundaries hold no data
- * here), so the received payloads are identical. */
+ * cell (tag = position + 1) instead of one per process.  On, the remote
+ * neighbor updates put each cell's fixed-size payload on the wire as its own
+ * message (per cell in the send list's order, a cell's fields in field
+ * order; RCCL posts them in that order, which is how its point-to-point
+ * matches them); off, one message per peer and field.  Variable-size fields,
+ * migrations and removed-cell payloads keep one message per peer.  The
+ * received payloads are identical either way. */
 int dccrgx_set_send_single_cells(dccrgx_grid* g, int on);
 int dccrgx_get_send_single_cells(dccrgx_grid* g, int* on);
 

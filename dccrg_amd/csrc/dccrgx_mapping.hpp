@@ -30,6 +30,7 @@ struct MapCtx {
 	uint64_t glen[3];         // grid length in finest-level indices: len << R
 	uint64_t first[kMaxLevels + 1];  // first id of level l (first[R+1] = last_cell + 1)
 	uint64_t last;            // last valid cell id
+	int lg[2];                // log2 of len[0], len[1] when both are powers of two, else -1
 };
 
 DX_HD void map_init(MapCtx& m, const uint64_t len[3], int R, const int per[3]) {
@@ -39,6 +40,12 @@ DX_HD void map_init(MapCtx& m, const uint64_t len[3], int R, const int per[3]) {
 		m.glen[d] = len[d] << R;
 	}
 	m.R = R;
+	m.lg[0] = m.lg[1] = -1;
+	if (len[0] && len[1] && !(len[0] & (len[0] - 1)) && !(len[1] & (len[1] - 1))) {
+		m.lg[0] = m.lg[1] = 0;
+		while ((uint64_t(1) << m.lg[0]) < len[0]) m.lg[0]++;
+		while ((uint64_t(1) << m.lg[1]) < len[1]) m.lg[1]++;
+	}
 	const uint64_t g = len[0] * len[1] * len[2];
 	uint64_t c = 1;
 	for (int l = 0; l <= R; l++) {
@@ -83,6 +90,15 @@ DX_HD int map_indices(const MapCtx& m, uint64_t cell, uint64_t& x, uint64_t& y, 
 	}
 	uint64_t c = cell - m.first[l];
 	const int sh = m.R - l;
+	if (m.lg[0] >= 0) {
+		// power-of-two x and y lengths: the divisions are shifts
+		const int bx = m.lg[0] + l, by = m.lg[1] + l;
+		x = (c & ((uint64_t(1) << bx) - 1)) << sh;
+		const uint64_t q = c >> bx;
+		y = (q & ((uint64_t(1) << by) - 1)) << sh;
+		z = (q >> by) << sh;
+		return l;
+	}
 	const uint64_t lx = m.len[0] << l, ly = m.len[1] << l;
 	if (((c | lx | ly) >> 32) == 0) {
 		// 32-bit division when the operands fit (exact, a fraction of the

@@ -687,8 +687,11 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	}
 
 	DX_LAP("sr.5_removed_payloads");
-	Mesh known, nm;
-	mesh_materialize(g, known);
+	// the known leaves: the current explicit list itself (read only), or the
+	// implicit initial mesh written out
+	Mesh materialized, nm;
+	if (g.mesh.implicit) mesh_materialize(g, materialized);
+	const Mesh& known = g.mesh.implicit ? materialized : g.mesh;
 	nm.implicit = false;
 	nm.bp = known.bp;
 	{

@@ -327,6 +327,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	DBuf<uint64_t> d_local;
 	bool prefix_sorted = false;  // d_local already in Morton order
 	bool direct = false;         // ... and slot i = d_local[i] (table slots set on insert)
+	bool solo = false;           // ... on one process: the slots are kid itself (no copies)
 	if (M.implicit) {
 		uint64_t f, c;
 		M.bp.range(uint64_t(g.rank), f, c);
@@ -344,7 +345,12 @@ void rebuild(Grid& g, Mesh& nm) {
 			mesh_build_range(m, M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
 		}
 		DX_LAP("rb.1a_hash");
-		if (M.n_prefix && g.morton_slots) {
+		solo = direct && g.size == 1;
+		if (solo) {
+			// every known leaf is an own leaf, kid in slot order: read in place
+			g.n_local = M.n_prefix;
+			prefix_sorted = true;
+		} else if (M.n_prefix && g.morton_slots) {
 			// the own leaves are kid's prefix, in (at most two runs of) Morton order
 			g.n_local = M.n_prefix;
 			d_local.alloc(g.n_local + 1);
@@ -372,17 +378,23 @@ void rebuild(Grid& g, Mesh& nm) {
 	DX_LAP("rb.1_local");
 
 	// 2. inner / outer classification (update_remote_neighbor_info 8992-9095)
-	DBuf<uint32_t> flag, scan;
-	flag.alloc(nl + 1);
-	scan.alloc(nl + 1);
-	HIP_CHECK(hipMemsetAsync(flag.p, 0, (nl + 1) * sizeof(uint32_t), s));
-	if (g.size > 1) k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.rank, d_local.p, nl, flag.p, s);
-	g.n_outer = scan_exclusive_u32(flag.p, scan.p, nl, s);
-	g.n_inner = nl - g.n_outer;
 	DBuf<uint64_t> local_slots;
-	local_slots.alloc(nl + 1);
-	k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
-	d_local.release();
+	if (solo) {
+		g.n_outer = 0;
+		g.n_inner = nl;
+	} else {
+		DBuf<uint32_t> flag, scan;
+		flag.alloc(nl + 1);
+		scan.alloc(nl + 1);
+		HIP_CHECK(hipMemsetAsync(flag.p, 0, (nl + 1) * sizeof(uint32_t), s));
+		if (g.size > 1) k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.rank, d_local.p, nl, flag.p, s);
+		g.n_outer = scan_exclusive_u32(flag.p, scan.p, nl, s);
+		g.n_inner = nl - g.n_outer;
+		local_slots.alloc(nl + 1);
+		k_assign_slots2(flag.p, scan.p, nl, g.n_inner, d_local.p, local_slots.p, s);
+		d_local.release();
+	}
+	const uint64_t* lsp = solo ? M.kid.p : local_slots.p;  // the own leaves in slot order
 	if (g.morton_slots && !prefix_sorted) {
 		// (a Morton-ordered d_local stays so in both runs: the split is stable)
 		k_morton_sort(m, local_slots.p, g.n_inner, s);
@@ -402,7 +414,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		c_to.alloc(no + 1);
 		p_of.alloc(no + 1);
 		p_to.alloc(no + 1);
-		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, c_of.p, c_to.p, s);
+		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, c_of.p, c_to.p, s);
 		const size_t t_of = scan_exclusive_u32(c_of.p, p_of.p, no, s);
 		const size_t t_to = scan_exclusive_u32(c_to.p, p_to.p, no, s);
 		DBuf<uint64_t> of_id, to_id;
@@ -410,10 +422,10 @@ void rebuild(Grid& g, Mesh& nm) {
 		of_id.alloc(t_of + 1);
 		of_off.alloc(3 * t_of + 3);
 		to_id.alloc(t_to + 1);
-		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, local_slots.p, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
-		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, local_slots.p, g.n_inner, no, p_to.p, to_id.p, s);
+		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, lsp, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
+		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, p_to.p, to_id.p, s);
 		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s);
-		k_send_by_owner(to_id.p, p_to.p, t_to, local_slots.p, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
+		k_send_by_owner(to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
 		std::map<int, std::vector<uint64_t>> rem_to;
 		k_remote_by_owner(to_id.p, t_to, dm, g.rank, g.size, rem_to, s);
 		std::vector<uint64_t> extra;
@@ -441,7 +453,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	halo.insert(halo.end(), g.extra_remote.begin(), g.extra_remote.end());
 	g.n_slots = nl + halo.size();
 	g.slot_ids.alloc(g.n_slots + 1);
-	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, local_slots.p, nl * 8, hipMemcpyDeviceToDevice, s));
+	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, lsp, nl * 8, hipMemcpyDeviceToDevice, s));
 	if (!halo.empty())
 		HIP_CHECK(hipMemcpyAsync(g.slot_ids.p + nl, halo.data(), halo.size() * 8, hipMemcpyHostToDevice, s));
 	DBuf<int32_t> err;
@@ -515,7 +527,10 @@ void rebuild(Grid& g, Mesh& nm) {
 	// the known list as [own leaves in slot order | the others] for the next
 	// refinement (Mesh::n_prefix)
 	M.n_prefix = M.prefix_run1 = 0;
-	if (!M.implicit && g.morton_slots && nl) {
+	if (solo) {
+		// kid is already [slot order], every owner this rank
+		M.n_prefix = M.prefix_run1 = nl;
+	} else if (!M.implicit && g.morton_slots && nl) {
 		DBuf<uint64_t> kid;
 		DBuf<int32_t> kown;
 		kid.alloc(M.n_known + 1);

@@ -333,6 +333,82 @@ __global__ __launch_bounds__(256) void advection_ell_kernel(const double* __rest
 	}
 }
 
+// advection_ell_kernel with the block's own 256 cells staged in LDS: a
+// block sweeps 256 consecutive slots (Morton order: a compact box, where
+// about five in six face neighbors are cells of the same block), reads its
+// cells' seven values once, coalesced, and takes every neighbor inside the
+// block from LDS; the others are gathered as before.  The same values in the
+// same order: bitwise the densities of advection_ell_kernel.
+__global__ __launch_bounds__(256) void advection_ell_lds_kernel(
+    const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
+    const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
+    const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
+    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt) {
+#pragma clang fp contract(off)
+	typedef int i2v __attribute__((ext_vector_type(2)));
+	typedef int i4v __attribute__((ext_vector_type(4)));
+	__shared__ double sd[256], svx[256], svy[256], svz[256], slx[256], sly[256], slz[256];
+	const unsigned t = threadIdx.x;
+	for (size_t b0 = s0 + blockIdx.x * size_t(256); b0 < s1; b0 += size_t(gridDim.x) * 256) {
+		const size_t s = b0 + t;
+		const bool live = s < s1;
+		const uint32_t nb_in = uint32_t(min(size_t(256), s1 - b0));
+		double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
+		int32_t e6[6] = {-1, -1, -1, -1, -1, -1};
+		if (live) {
+			cd = rho[s];
+			clx = lx[s];
+			cly = ly[s];
+			clz = lz[s];
+			cvx = vx[s];
+			cvy = vy[s];
+			cvz = vz[s];
+			const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
+#pragma unroll
+			for (int j = 0; j < 3; j++) {
+				const i2v v = ev[j];
+				e6[2 * j] = v.x;
+				e6[2 * j + 1] = v.y;
+			}
+		}
+		__syncthreads();  // the previous chunk's readers are done with LDS
+		sd[t] = cd;
+		svx[t] = cvx;
+		svy[t] = cvy;
+		svz[t] = cvz;
+		slx[t] = clx;
+		sly[t] = cly;
+		slz[t] = clz;
+		__syncthreads();
+		if (!live) continue;
+		auto nb = [&](int32_t n, int dir) {
+			const uint32_t k = uint32_t(int64_t(n) - int64_t(b0));
+			if (k < nb_in) {
+				const double nv = dir < 2 ? svx[k] : (dir < 4 ? svy[k] : svz[k]);
+				return AdvNb{sd[k], slx[k], sly[k], slz[k], nv};
+			}
+			const double nv = dir < 2 ? vx[n] : (dir < 4 ? vy[n] : vz[n]);
+			return AdvNb{rho[n], lx[n], ly[n], lz[n], nv};
+		};
+		double acc = 0;
+#pragma unroll
+		for (int dir = 0; dir < 6; dir++) {
+			const int32_t c = e6[dir];
+			if (c == -1) continue;
+			if (c >= 0) {
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(c, dir), dt);
+			} else {
+				const i4v q = *reinterpret_cast<const i4v*>(fine + 4 * size_t(-2 - c));
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.x, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.y, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.z, dir), dt);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.w, dir), dt);
+			}
+		}
+		rho_out[s] = cd + acc / (clx * cly * clz);
+	}
+}
+
 // 32-bit byte offsets from a uniform base: global_load v, voff, s[base]
 // (halves the address registers of a gather; slots < 2^29, checked on the host)
 __device__ __forceinline__ double ldo(const double* __restrict__ p, uint32_t off) {
@@ -1505,8 +1581,13 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
                      size_t s1, double dt, hipStream_t s) {
 	if (s1 <= s0) return;
-	advection_ell_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5], f[6],
-	                                                                     rho_out, ell, fine, s0, s1, dt);
+	static const bool plain = std::getenv("DCCRGX_ELL_LDS") && std::atoi(std::getenv("DCCRGX_ELL_LDS")) == 0;
+	if (plain)
+		advection_ell_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5],
+		                                                                     f[6], rho_out, ell, fine, s0, s1, dt);
+	else
+		advection_ell_lds_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5],
+		                                                                         f[6], rho_out, ell, fine, s0, s1, dt);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -500,7 +500,7 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // face_dir.  The table is the same either way.  The loop runs whole waves
 // (wave_reserve needs every lane).
 __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1,
-                                  bool morton, int32_t* ell, unsigned long long* n_fine, uint64_t* fine_keys,
+                                  bool morton, int32_t* ell, unsigned long long* n_fine, uint32_t* fine_keys,
                                   int32_t* err) {
 	const SlotExists ex{M};
 	const size_t stride = size_t(gridDim.x) * blockDim.x;
@@ -567,16 +567,16 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 		unsigned long long at = wave_reserve(n_fine, kf);
 		if (live)
 			for (int dir = 0; dir < 6; dir++)
-				if (o6[dir] == -2) fine_keys[at++] = (uint64_t(r) << 3) | uint64_t(dir);
+				if (o6[dir] == -2) fine_keys[at++] = (uint32_t(r) << 3) | uint32_t(dir);
 	}
 }
 
 // the finer faces in key order: f = the key's position
-__global__ void face_fine_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, const uint64_t* fine_keys, size_t n,
+__global__ void face_fine_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, const uint32_t* fine_keys, size_t n,
                                  int32_t* ell, int32_t* fine, int32_t* err) {
 	const DevExists ex{M};
 	for (size_t f = blockIdx.x * size_t(blockDim.x) + threadIdx.x; f < n; f += size_t(gridDim.x) * blockDim.x) {
-		const uint64_t key = fine_keys[f];
+		const uint32_t key = fine_keys[f];
 		const size_t r = size_t(key >> 3);
 		const int dir = int(key & 7);
 		uint64_t c[3];
@@ -1141,15 +1141,17 @@ static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t 
 	head.alloc(n);
 	DBuf<unsigned long long> nsel;
 	nsel.alloc(1);
+	size_t b4 = 0;
 	HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, b3, keys, head.p, k2.p, nsel.p, n, s));
+	HIP_CHECK(hipcub::DeviceSelect::Flagged(nullptr, b4, owners, head.p, o2.p, nsel.p, n, s));
 	DBuf<uint8_t> temp;
-	temp.alloc(std::max(b1, std::max(b2, b3)));
+	temp.alloc(std::max(std::max(b1, b2), std::max(b3, b4)));
 	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, b1, keys, k2.p, owners, o2.p, n, 0, 64, s));
 	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, b2, o2.p, owners, k2.p, keys, n, 0, obits, s));
 	pair_heads_kernel<<<grid_for(n, 256), 256, 0, s>>>(keys, owners, n, head.p);
 	HIP_CHECK(hipGetLastError());
 	HIP_CHECK(hipcub::DeviceSelect::Flagged(temp.p, b3, keys, head.p, k2.p, nsel.p, n, s));
-	HIP_CHECK(hipcub::DeviceSelect::Flagged(temp.p, b3, owners, head.p, o2.p, nsel.p, n, s));
+	HIP_CHECK(hipcub::DeviceSelect::Flagged(temp.p, b4, owners, head.p, o2.p, nsel.p, n, s));
 	const size_t u = read_counter(nsel, s);
 	const std::vector<uint64_t> ids = download(k2.p, u, s);
 	const std::vector<uint32_t> own = download(o2.p, u, s);
@@ -1296,11 +1298,13 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 
 size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, size_t run1,
                     bool morton, int32_t* ell, DBuf<int32_t>& fine, int32_t* err, hipStream_t s) {
+	DX_REQUIRE(nrows < (size_t(1) << 29), "too many local cells for the face keys");
 	DBuf<unsigned long long> n_fine;
 	n_fine.alloc(1);
 	HIP_CHECK(hipMemsetAsync(n_fine.p, 0, 8, s));
-	// finer faces: at most 6 per row, in practice a few percent of the rows
-	DBuf<uint64_t> keys;
+	// finer faces: at most 6 per row, in practice a few percent of the rows;
+	// keys row << 3 | direction
+	DBuf<uint32_t> keys;
 	keys.alloc(6 * nrows + 1);
 	if (nrows)
 		face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, ell,
@@ -1310,8 +1314,17 @@ size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids,
 	fine.alloc(4 * nf + 4);
 	if (!nf) return 0;
 	int bits = 4;
-	while (bits < 64 && (uint64_t(nrows) << 3) >> bits) bits++;
-	sort_u64(keys.p, nf, s, bits);
+	while (bits < 32 && (uint64_t(nrows) << 3) >> bits) bits++;
+	if (nf > 1) {
+		DBuf<uint32_t> sorted;
+		sorted.alloc(nf);
+		size_t b1 = 0;
+		HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys.p, sorted.p, nf, 0, bits, s));
+		DBuf<uint8_t> temp;
+		temp.alloc(b1);
+		HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys.p, sorted.p, nf, 0, bits, s));
+		keys.swap(sorted);
+	}
 	face_fine_kernel<<<grid_for(nf, 256), 256, 0, s>>>(m, M, slot_ids, keys.p, nf, ell, fine.p, err);
 	HIP_CHECK(hipGetLastError());
 	return nf;

@@ -216,8 +216,7 @@ static void po_reduce(Grid& g, int k, unsigned nb, const PoParams& prm, int stag
 
 static PoScalars po_read_scalars(Grid& g) {
 	PoScalars h{};
-	HIP_CHECK(hipMemcpyAsync(&h, g.po.st.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
-	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	d2h_small(&h, g.po.st.p, sizeof(h), g.s_comp);
 	return h;
 }
 
@@ -1020,8 +1019,7 @@ int dccrgx_mapping_batch(dccrgx_grid* gp, const uint64_t* ids, size_t n, int32_t
 		mapping_batch_kernel<<<grid_for(n, 256), 256, 0, g.s_comp>>>(m, d_ids.p, n, d_lvl.p, d_out.p);
 		HIP_CHECK(hipGetLastError());
 		HIP_CHECK(hipMemcpyAsync(level, d_lvl.p, n * 4, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipMemcpyAsync(out, d_out.p, 15 * n * 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		d2h_small(out, d_out.p, 15 * n * 8, g.s_comp);
 		return 0;
 	});
 }
@@ -2013,8 +2011,7 @@ int dccrgx_variable_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t 
 		Field& f = var_field(g, fid, slot0, n);
 		uint64_t a = 0, b = 0;
 		HIP_CHECK(hipMemcpyAsync(&a, f.voff.p + slot0, 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipMemcpyAsync(&b, f.voff.p + slot0 + n, 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		d2h_small(&b, f.voff.p + slot0 + n, 8, g.s_comp);
 		DX_REQUIRE(nbytes == b - a, "byte count differs from the cells' sizes (resize them first)");
 		if (nbytes) HIP_CHECK(hipMemcpy(f.data.p + a, bytes, nbytes, hipMemcpyHostToDevice));
 		return 0;
@@ -2028,8 +2025,7 @@ int dccrgx_variable_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_
 		Field& f = var_field(g, fid, slot0, n);
 		uint64_t a = 0, b = 0;
 		HIP_CHECK(hipMemcpyAsync(&a, f.voff.p + slot0, 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipMemcpyAsync(&b, f.voff.p + slot0 + n, 8, hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		d2h_small(&b, f.voff.p + slot0 + n, 8, g.s_comp);
 		if (nbytes) *nbytes = size_t(b - a);
 		if (b - a > cap) return DCCRGX_ERANGE;
 		if (b > a) HIP_CHECK(hipMemcpy(bytes, f.data.p + a, b - a, hipMemcpyDeviceToHost));
@@ -2242,8 +2238,7 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 		k_time_end(g);
 		if (phase == 0) ls.local_zero = false;
 		int h = 0;
-		HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		d2h_small(&h, err.p, sizeof(int), g.s_comp);
 		DX_REQUIRE(!(h & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
 		DX_REQUIRE(!(h & 2), "a dead neighbor's level-0 parent was recorded alive (siblings disagree)");
 		return 0;
@@ -2260,8 +2255,7 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 // 8), err[2] the spread - in the order the reference would have aborted
 static void check_gol_turn_err(Grid& g, DBuf<int>& err) {
 	int h[3] = {0, 0, 0};
-	HIP_CHECK(hipMemcpyAsync(h, err.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
-	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	d2h_small(h, err.p, sizeof(h), g.s_comp);
 	const int collect = (h[0] & (4 | 8)) ? h[1] : h[0];
 	for (int e : {collect, h[2]}) {
 		DX_REQUIRE(!(e & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");
@@ -2304,8 +2298,7 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 			k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp, 0, err.p);
 			k_time_end(g);
 			int h[3] = {0, 0, 0};
-			HIP_CHECK(hipMemcpyAsync(h, err.p, sizeof(h), hipMemcpyDeviceToHost, g.s_comp));
-			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+			d2h_small(h, err.p, sizeof(h), g.s_comp);
 			// every level-0 cell of a one-process grid has a known leaf
 			DX_REQUIRE(!(h[0] & 8), "internal error: the level-0 game met a level-0 cell without a known leaf");
 			const int collect = (h[0] & 4) ? h[1] : h[0];

@@ -1028,8 +1028,7 @@ bool k_level_ranges(const MapCtx& m, const uint64_t* ids, size_t n, uint64_t* lo
 		                                                                              d.p + kRangeLevels);
 		HIP_CHECK(hipGetLastError());
 	}
-	HIP_CHECK(hipMemcpyAsync(h.data(), d.p, h.size() * 8, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(h.data(), d.p, h.size() * 8, s);
 	for (int L = 0; L < kRangeLevels; L++) {
 		lo[L] = h[size_t(L)];
 		hi[L] = h[size_t(kRangeLevels + L)];
@@ -1106,8 +1105,7 @@ void k_fill_neighbors_to(const MapCtx& m, const int32_t* hood_to, int nh, const 
 
 static size_t read_counter(const DBuf<unsigned long long>& ctr, hipStream_t s) {
 	unsigned long long h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, ctr.p, sizeof(h), s);
 	return size_t(h);
 }
 
@@ -1271,8 +1269,7 @@ uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStre
 	temp.alloc(bytes);
 	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in, out, n + 1, s));
 	uint32_t h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, out + n, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, out + n, sizeof(h), s);
 	return h;
 }
 
@@ -1498,8 +1495,7 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 	{
 		// the level-0 requests' marker sorts last
 		uint64_t last = 0;
-		if (n) HIP_CHECK(hipMemcpyAsync(&last, par.p + n - 1, 8, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		if (n) d2h_small(&last, par.p + n - 1, 8, s);
 		if (n && last == ~uint64_t(0)) n--;
 	}
 	if (!n) return {};
@@ -1551,8 +1547,7 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 	// where input positions at[k] land (the expanded list's run boundaries)
 	for (int k = 0; k < n_at; k++) {
 		uint32_t v = 0;
-		HIP_CHECK(hipMemcpyAsync(&v, pos.p + at[k], 4, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		d2h_small(&v, pos.p + at[k], 4, s);
 		pos_at[k] = v;
 	}
 	out_id.alloc(n_out + 1);

@@ -284,8 +284,7 @@ void comm_allreduce_f64(Grid& g, double* v, int count, int op) {
 	d.alloc(size_t(count));
 	HIP_CHECK(hipMemcpyAsync(d.p, v, size_t(count) * 8, hipMemcpyHostToDevice, s));
 	comm_allreduce_f64_dev(g, d.p, d.p, count, op, s);
-	HIP_CHECK(hipMemcpyAsync(v, d.p, size_t(count) * 8, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(v, d.p, size_t(count) * 8, s);
 }
 
 uint64_t comm_allreduce_max_u64(Grid& g, uint64_t v) {

@@ -172,6 +172,11 @@ struct DBuf {
 	}
 };
 
+// bytes from the device into host memory, s drained first (copy + sync);
+// reads of up to kSmallRead bytes go through a pinned staging buffer
+constexpr size_t kSmallRead = 64 * 1024;
+void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s);
+
 template <class T>
 inline void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
 	d.alloc(h.size());
@@ -181,10 +186,7 @@ inline void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
 template <class T>
 inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
 	std::vector<T> h(n);
-	if (n) {
-		HIP_CHECK(hipMemcpyAsync(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
-	}
+	if (n) d2h_small(h.data(), d, n * sizeof(T), s);
 	return h;
 }
 

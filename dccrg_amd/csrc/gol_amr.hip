@@ -495,27 +495,34 @@ __global__ void gol_amr_spread_groups_mask_kernel(const uint32_t* __restrict__ g
                                                   size_t s0, size_t s1, int* __restrict__ err,
                                                   const int* __restrict__ gate) {
 	if (gate && (*gate & (4 | 8)) == 0) return;  // block-uniform: the level-0 game did the turn
-	const size_t t = size_t(xcd_block()) * blockDim.x + threadIdx.x;
-	const size_t gi = t >> 3;
-	const uint32_t m = uint32_t(t & 7u);
-	const bool live_group = gi < ng;  // lanes of one group share a wave (8 | 64): no early exit
-	const uint32_t b = live_group ? gptr[gi] : 0u, e = live_group ? gptr[gi + 1] : 0u;
-	uint32_t u = 0, any = 0;
-	for (uint32_t j = b + m; j < e; j += 8) {
-		const uint32_t gs = gslot[j];
-		any |= (gs >= s0 && gs < s1) ? 1u : 0u;
-		u |= gs < n_local ? mask[gs] : remote_mask(lst, l0c, G, gs, err);
-	}
+	// an ungated launch has a thread per group member; a gated one (mostly
+	// exiting at once) a capped grid walking the groups
+	const size_t stride = size_t(gridDim.x) * blockDim.x;  // a multiple of 64: lanes keep their place
+	for (size_t t = size_t(gate ? blockIdx.x : xcd_block()) * blockDim.x + threadIdx.x;; t += stride) {
+		const size_t gi = t >> 3;
+		if ((t - (t & 63u)) >> 3 >= ng) break;  // the wave's first group is past the end (wave-uniform)
+		const uint32_t m = uint32_t(t & 7u);
+		const bool live_group = gi < ng;  // lanes of one group share a wave (8 | 64): no early exit
+		const uint32_t b = live_group ? gptr[gi] : 0u, e = live_group ? gptr[gi + 1] : 0u;
+		uint32_t u = 0, any = 0;
+		for (uint32_t j = b + m; j < e; j += 8) {
+			const uint32_t gs = gslot[j];
+			any |= (gs >= s0 && gs < s1) ? 1u : 0u;
+			u |= gs < n_local ? mask[gs] : remote_mask(lst, l0c, G, gs, err);
+		}
 #pragma unroll
-	for (int o = 1; o < 8; o <<= 1) {
-		u |= __shfl_xor(u, o, 8);
-		any |= __shfl_xor(any, o, 8);
+		for (int o = 1; o < 8; o <<= 1) {
+			u |= __shfl_xor(u, o, 8);
+			any |= __shfl_xor(any, o, 8);
+		}
+		if (any) {
+			const int n = __popc(u);
+			if (n > kList && m == 0) atomicOr(err, 1);
+			for (uint32_t j = b + m; j < e; j += 8)
+				if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
+		}
+		if (!gate) break;  // ungated: one group member per thread
 	}
-	if (!any) return;
-	const int n = __popc(u);
-	if (n > kList && m == 0) atomicOr(err, 1);
-	for (uint32_t j = b + m; j < e; j += 8)
-		if (gslot[j] >= s0 && gslot[j] < s1) gol_rule(state, gslot[j], n);
 }
 
 // ---- geometric collect ------------------------------------------------------
@@ -954,8 +961,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		HIP_CHECK(hipGetLastError());
 	}
 	unsigned long long h[2] = {0, 0};
-	HIP_CHECK(hipMemcpyAsync(h, cnt.p, 16, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(h, cnt.p, 16, s);
 	// the level-0 slots' keys sort last: the groups end where they begin
 	const uint32_t grouped = uint32_t(n_slots - size_t(h[0]));
 	HIP_CHECK(hipMemcpyAsync(T.gptr.p + ng, &grouped, 4, hipMemcpyHostToDevice, s));
@@ -979,8 +985,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		T.l0c.alloc(n_slots + 1);
 		T.mask.alloc(n_slots + 1);
 		uint32_t total = 0;
-		if (n_local) HIP_CHECK(hipMemcpyAsync(&total, ptr + n_local, 4, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		if (n_local) d2h_small(&total, ptr + n_local, 4, s);
 		T.ent.alloc(size_t(total) + 4);  // whole 16-byte words for the values pass
 		T.n_ent = total;
 		HIP_CHECK(hipMemsetAsync(T.ent.p, 0xff, T.ent.n * 4, s));  // padding = no slot
@@ -996,8 +1001,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 			HIP_CHECK(hipGetLastError());
 		}
 		int hb = 0;
-		HIP_CHECK(hipMemcpyAsync(&hb, bad.p, 4, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		d2h_small(&hb, bad.p, 4, s);
 		T.mask_path = hb == 0;
 	}
 	// geometric collect: maximum refinement level <= 1 on the mask path, the
@@ -1015,8 +1019,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		geo_bbox_kernel<<<std::min<unsigned>(grid_for(n_slots, 256), 1024), 256, 0, s>>>(T.l0c.p, n_slots, G, mm.p);
 		HIP_CHECK(hipGetLastError());
 		int h[6];
-		HIP_CHECK(hipMemcpyAsync(h, mm.p, sizeof(h), hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		d2h_small(h, mm.p, sizeof(h), s);
 		const uint32_t L[3] = {T.lx, T.ly, T.lz};
 		for (int d = 0; d < 3; d++) {
 			T.per[d] = m.periodic[d];
@@ -1062,8 +1065,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 				lg_layout_check_kernel<<<grid_for(n_local, 256), 256, 0, s>>>(T.corner.p, T.l0c.p, n_local, bad.p);
 				HIP_CHECK(hipGetLastError());
 				int hb = 1;
-				HIP_CHECK(hipMemcpyAsync(&hb, bad.p, 4, hipMemcpyDeviceToHost, s));
-				HIP_CHECK(hipStreamSynchronize(s));
+				d2h_small(&hb, bad.p, 4, s);
 				T.lg_layout = hb == 0;
 			}
 			if (T.lg_layout) {
@@ -1159,15 +1161,17 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 		const L0Geom G{T.lx, T.ly, T.lz, T.bx, T.by};
 		if (phase == 0) {
 			const size_t nchunk = (s1 - s0 + kCollectRows - 1) / kCollectRows;
-			gol_amr_collect_mask_kernel<<<gate ? unsigned(std::min<size_t>(nchunk, 1024)) : xcd_grid(nchunk), kCollectRows, 0,
+			gol_amr_collect_mask_kernel<<<gate ? unsigned(std::min<size_t>(nchunk, 256)) : xcd_grid(nchunk), kCollectRows, 0,
 			                              s>>>(
 			    state, T.ent.p, ptr, T.l0c.p, G, lst, T.mask.p, s0, s1, list_from < s0 ? s0 : list_from, err, gate);
 		} else {
 			if (T.n_lvl0)
-				gol_amr_spread0_mask_kernel<<<grid_for(T.n_lvl0, 256), 256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p,
-				                                                                   s0, s1, gate);
+				gol_amr_spread0_mask_kernel<<<gate ? std::min(grid_for(T.n_lvl0, 256), 256u) : grid_for(T.n_lvl0, 256),
+				                              256, 0, s>>>(T.lvl0.p, T.n_lvl0, state, T.mask.p, s0, s1, gate);
 			if (T.ng)
-				gol_amr_spread_groups_mask_kernel<<<xcd_grid((8 * T.ng + 255) / 256), 256, 0, s>>>(
+				gol_amr_spread_groups_mask_kernel<<<gate ? std::min(xcd_grid((8 * T.ng + 255) / 256), 256u)
+				                                         : xcd_grid((8 * T.ng + 255) / 256),
+				                                    256, 0, s>>>(
 				    T.gptr.p, T.ng, T.gslot.p, state, T.mask.p, lst, T.l0c.p, G, n_local, s0, s1, err, gate);
 		}
 		HIP_CHECK(hipGetLastError());

@@ -332,8 +332,7 @@ UserHood& ensure_uhood(Grid& g, int id) {
 	k_lookup_slots(d1.p, P.n_send, dm, P.send_slots.p, err.p, s);
 	k_lookup_slots(d2.p, P.n_recv, dm, P.recv_slots.p, err.p, s);
 	int herr = 0;
-	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&herr, err.p, 4, s);
 	DX_REQUIRE(herr == 0, "user neighborhood references a cell without a local slot or remote copy");
 	h.valid = true;
 	return h;
@@ -742,8 +741,7 @@ static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids) {
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, g.s_comp));
 	k_lookup_slots(d.p, ids.size(), g.dm(), sl.p, err.p, g.s_comp);
 	int32_t h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, err.p, 4, hipMemcpyDeviceToHost, g.s_comp));
-	HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	d2h_small(&h, err.p, 4, g.s_comp);
 	DX_REQUIRE(h == 0, "migrating cell without a slot");
 	return sl;
 }
@@ -910,8 +908,7 @@ void finish_balance_load_impl(Grid& g) {
 		HIP_CHECK(hipGetLastError());
 	}
 	unsigned long long kept = 0;
-	HIP_CHECK(hipMemcpyAsync(&kept, ctr.p, 8, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&kept, ctr.p, 8, s);
 	if (!arrived.empty())
 		HIP_CHECK(hipMemcpyAsync(local.p + kept, arrived.data(), arrived.size() * 8, hipMemcpyHostToDevice, s));
 	const size_t n_new = size_t(kept) + arrived.size();

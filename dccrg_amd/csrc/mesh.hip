@@ -367,8 +367,7 @@ void rebuild(Grid& g, Mesh& nm) {
 				HIP_CHECK(hipGetLastError());
 			}
 			unsigned long long hn = 0;
-			HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipStreamSynchronize(s));
+			d2h_small(&hn, ctr.p, 8, s);
 			g.n_local = size_t(hn);
 			if (!g.morton_slots) sort_u64(d_local.p, g.n_local, s);
 		}
@@ -484,8 +483,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		H.send_slots.alloc(sids.size() + 1);
 		k_lookup_slots(d.p, sids.size(), dm, H.send_slots.p, err.p, s);
 		int32_t herr = 0;
-		HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		d2h_small(&herr, err.p, 4, s);
 		DX_REQUIRE(herr == 0, "internal error: slot of a local, halo or send cell missing from the mesh table");
 	}
 
@@ -546,8 +544,7 @@ void rebuild(Grid& g, Mesh& nm) {
 			                                                          kown.p + nl, ctr.p);
 			HIP_CHECK(hipGetLastError());
 			unsigned long long hn = 0;
-			HIP_CHECK(hipMemcpyAsync(&hn, ctr.p, 8, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipStreamSynchronize(s));
+			d2h_small(&hn, ctr.p, 8, s);
 			ng = size_t(hn);
 		}
 		DX_REQUIRE(nl + ng == M.n_known, "internal error: known leaves are not own + others");
@@ -606,8 +603,7 @@ void ensure_csr(Grid& g) {
 	k_iterator_lists(g.nof_ptr.p, g.nof_id.p, g.nof_off.p, g.nof_slot.p, g.nto_ptr.p, g.nto_id.p, nl, cls.p, nullptr,
 	                 g.it_ptr.p, g.it_slot.p, g.it_off.p, 1, s);
 	int32_t herr = 0;
-	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&herr, err.p, 4, s);
 	DX_REQUIRE(herr == 0, "neighbor list references a cell unknown to this rank (unbalanced mesh?)");
 	g.csr_valid = true;
 }
@@ -626,8 +622,7 @@ void ensure_face(Grid& g) {
 	g.slot_lvl.alloc(g.n_slots + 1);
 	k_slot_levels(g.m, g.slot_ids.p, g.n_slots, g.slot_lvl.p, s);
 	int32_t herr = 0;
-	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&herr, err.p, 4, s);
 	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
 	g.face_valid = true;
 	g.face_csr_valid = false;
@@ -686,8 +681,7 @@ void ensure_tiles(Grid& g) {
 		const size_t nr = g.tcount[0] + g.tcount[1];
 		const auto lr = download(g.tlists.p, nr, g.s_comp);
 		std::vector<RegTileMeta> rm(nr);
-		if (nr) HIP_CHECK(hipMemcpyAsync(rm.data(), g.tregmeta.p, nr * sizeof(RegTileMeta), hipMemcpyDeviceToHost, g.s_comp));
-		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		if (nr) d2h_small(rm.data(), g.tregmeta.p, nr * sizeof(RegTileMeta), g.s_comp);
 		std::vector<int64_t> where(nt, -1);  // tile -> regular list index (>= 0) or -(irregular index) - 2
 		for (size_t i = 0; i < nr; i++) where[lr[i]] = int64_t(i);
 		for (size_t i = 0; i < ni; i++) where[li[i]] = -int64_t(i) - 2;
@@ -733,8 +727,7 @@ void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_
 	sl.alloc(n);
 	k_lookup(g.dm(), d.p, n, o.p, sl.p, s);
 	if (owner) HIP_CHECK(hipMemcpyAsync(owner, o.p, n * 4, hipMemcpyDeviceToHost, s));
-	if (slot) HIP_CHECK(hipMemcpyAsync(slot, sl.p, n * 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	if (slot) d2h_small(slot, sl.p, n * 4, s);
 }
 
 // slot of a slotted id from the host index, -1 if it has no slot

@@ -1705,8 +1705,7 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, con
 	check_rows_kernel<<<grid_for(np, 256), 256, 0, s>>>(cidx.p, pslot.p, np, n_local, err.p);
 	HIP_CHECK(hipGetLastError());
 	int h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, err.p, sizeof(int), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, err.p, sizeof(int), s);
 	DX_REQUIRE(h == 0, "merged parent is not local or a removed child's payload is missing");
 	k_adv_parent_density(rho, pslot.p, cidx.p, removed_rho, np, s);
 }
@@ -1741,8 +1740,7 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	                                                                        unref.p, part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
-	HIP_CHECK(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(h, cnt.p, sizeof(h), s);
 	out.refine = download(ref.p, size_t(h[0]), s);
 	out.unrefine = download(unref.p, size_t(h[1]), s);
 	out.kept = size_t(h[2]);
@@ -1788,8 +1786,7 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, c
 	                                                       diff_threshold, out, ctr.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, ctr.p, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, ctr.p, sizeof(h), s);
 	return size_t(h);
 }
 

@@ -622,8 +622,7 @@ static size_t device_cut(const DBuf<uint8_t>& al, size_t n_inner, size_t n_local
 	chain_expand_kernel<<<(cap_anchor + 63) / 64, 64, 0, s>>>(next.p, anchors.p, cnt.p, n, starts.p);
 	HIP_CHECK(hipGetLastError());
 	uint32_t na = 0;
-	HIP_CHECK(hipMemcpyAsync(&na, cnt.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&na, cnt.p, 4, s);
 	DX_REQUIRE(na >= 1 && na < cap_anchor, "internal error: tile chain longer than its bound");
 	// the starts before the terminal: the sequence is increasing, so the
 	// count of each run is a count of values below its end
@@ -685,8 +684,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		return out;
 	}
 	uint32_t n_ent = 0;
-	HIP_CHECK(hipMemcpyAsync(&n_ent, face_ptr + n_local, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&n_ent, face_ptr + n_local, 4, s);
 	// (DCCRGX_TILE_GLOBAL=1: always the global build below, the fallback,
 	// so that tests compare the two)
 	if (T <= kXT && ntiles && !std::getenv("DCCRGX_TILE_GLOBAL")) {
@@ -752,8 +750,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 		temp.alloc(bytes + 1);
 		HIP_CHECK(hipcub::DeviceSelect::If(temp.p, bytes, all.p, keys.p, nsel.p, size_t(n_ent), OutOfTile(), s));
 		unsigned long long h = 0;
-		HIP_CHECK(hipMemcpyAsync(&h, nsel.p, sizeof(h), hipMemcpyDeviceToHost, s));
-		HIP_CHECK(hipStreamSynchronize(s));
+		d2h_small(&h, nsel.p, sizeof(h), s);
 		m0 = size_t(h);
 	}
 	all.release();
@@ -798,8 +795,7 @@ TileBuild k_build_tiles(const uint32_t* face_ptr, const int32_t* face_ent, const
 	pack_ext_kernel<<<grid_for(m, 256), 256, 0, s>>>(ext.p, ext_ax.p, m, ext_pk.p);
 	HIP_CHECK(hipGetLastError());
 	int herr = 0;
-	HIP_CHECK(hipMemcpyAsync(&herr, err.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&herr, err.p, 4, s);
 	DX_REQUIRE(herr == 0, "internal error: face neighbor missing from its tile's external list");
 	{
 		const std::vector<uint32_t> fbh = download(fine_base.p, ntiles, s);

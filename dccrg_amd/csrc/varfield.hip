@@ -118,8 +118,7 @@ uint64_t scan_exclusive_u64(const uint64_t* in, uint64_t* out, size_t n, hipStre
 	temp.alloc(bytes + 1);
 	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in, out, n + 1, s));
 	uint64_t h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, out + n, sizeof(h), hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, out + n, sizeof(h), s);
 	return h;
 }
 
@@ -132,8 +131,7 @@ void var_reset(Field& f, size_t n_slots, hipStream_t s) {
 
 uint64_t var_total(const Field& f, size_t n_slots, hipStream_t s) {
 	uint64_t h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, f.voff.p + n_slots, 8, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, f.voff.p + n_slots, 8, s);
 	return h;
 }
 
@@ -194,8 +192,7 @@ uint64_t var_place(Field& f, size_t n_slots, const int32_t* slots, size_t n, con
 		HIP_CHECK(hipGetLastError());
 	}
 	int32_t h = 0;
-	HIP_CHECK(hipMemcpyAsync(&h, flag.p, 4, hipMemcpyDeviceToHost, s));
-	HIP_CHECK(hipStreamSynchronize(s));
+	d2h_small(&h, flag.p, 4, s);
 	if (h) var_resize(f, n_slots, want.p, s);
 	DBuf<uint64_t> in_off;
 	in_off.alloc(n + 1);

@@ -178,7 +178,7 @@ static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns
 		if (!n) continue;
 		DBuf<uint64_t> d;
 		d.alloc(n);
-		HIP_CHECK(hipMemcpyAsync(d.p, ids, n * 8, hipMemcpyHostToDevice, s));
+		h2d(d.p, ids, n * 8, s);
 		po_classify_kernel<<<grid_for(n, 256), 256, 0, s>>>(type, g.dm(), d.p, n, nl, pass == 0 ? 2 : 0);
 		HIP_CHECK(hipGetLastError());
 		HIP_CHECK(hipStreamSynchronize(s));
@@ -577,7 +577,7 @@ static void continue_load_impl(Grid& g, int fid, const uint64_t* sizes) {
 		DBuf<uint64_t> all;
 		all.alloc(g.n_slots + 1);
 		var_sizes(f, nullptr, 0, g.n_slots, all.p, g.s_comp);
-		if (nl) HIP_CHECK(hipMemcpyAsync(all.p, bytes.data(), nl * 8, hipMemcpyHostToDevice, g.s_comp));
+		if (nl) h2d(all.p, bytes.data(), nl * 8, g.s_comp);
 		var_resize(f, g.n_slots, all.p, g.s_comp);
 		if (at[nl]) HIP_CHECK(hipMemcpy(f.data.p, got.data(), got.size(), hipMemcpyHostToDevice));
 	} else if (nl && f.win_len) {
@@ -1015,7 +1015,7 @@ int dccrgx_mapping_batch(dccrgx_grid* gp, const uint64_t* ids, size_t n, int32_t
 		d_ids.alloc(n);
 		d_out.alloc(15 * n);
 		d_lvl.alloc(n);
-		HIP_CHECK(hipMemcpyAsync(d_ids.p, ids, n * 8, hipMemcpyHostToDevice, g.s_comp));
+		h2d(d_ids.p, ids, n * 8, g.s_comp);
 		mapping_batch_kernel<<<grid_for(n, 256), 256, 0, g.s_comp>>>(m, d_ids.p, n, d_lvl.p, d_out.p);
 		HIP_CHECK(hipGetLastError());
 		HIP_CHECK(hipMemcpyAsync(level, d_lvl.p, n * 4, hipMemcpyDeviceToHost, g.s_comp));
@@ -1999,7 +1999,7 @@ int dccrgx_variable_field_resize(dccrgx_grid* gp, int fid, size_t slot0, size_t 
 		DBuf<uint64_t> all;
 		all.alloc(g.n_slots + 1);
 		var_sizes(f, nullptr, 0, g.n_slots, all.p, g.s_comp);
-		if (n) HIP_CHECK(hipMemcpyAsync(all.p + slot0, sizes, n * 8, hipMemcpyHostToDevice, g.s_comp));
+		if (n) h2d(all.p + slot0, sizes, n * 8, g.s_comp);
 		var_resize(f, g.n_slots, all.p, g.s_comp);
 		return 0;
 	});

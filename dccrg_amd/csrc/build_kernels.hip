@@ -15,6 +15,9 @@
 // the block-partition formula on the initial level-0 grid).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <functional>
+
 #include "dccrgx_internal.hpp"
 
 namespace dccrgx {
@@ -1022,7 +1025,7 @@ bool k_level_ranges(const MapCtx& m, const uint64_t* ids, size_t n, uint64_t* lo
 		h[size_t(L)] = ~0ull;
 		h[size_t(kRangeLevels + L)] = 0ull;
 	}
-	HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, s));
+	h2d(d.p, h.data(), h.size() * 8, s);
 	if (n) {
 		level_ranges_kernel<<<std::min<unsigned>(grid_for(n, 256), 2048), 256, 0, s>>>(m, ids, n, d.p,
 		                                                                              d.p + kRangeLevels);
@@ -1221,6 +1224,10 @@ void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_
 // a host list sorted (and deduplicated): by the device radix sort above a few
 // thousand ids (std::sort of 200 K ids takes 5-15 ms on the host), else here
 void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s) {
+	// already in order (lists that arrive sorted: one rank's own, merged runs)
+	if (unique ? std::adjacent_find(v.begin(), v.end(), std::greater_equal<uint64_t>()) == v.end()
+	           : std::is_sorted(v.begin(), v.end()))
+		return;
 	if (v.size() < 8192) {
 		std::sort(v.begin(), v.end());
 		if (unique) v.erase(std::unique(v.begin(), v.end()), v.end());

@@ -182,7 +182,7 @@ std::vector<std::vector<uint8_t>> comm_exchange(Grid& g, const std::vector<std::
 	DBuf<uint8_t> ds, dr;
 	ds.alloc(stot + 1);
 	dr.alloc(rtot + 1);
-	if (stot) HIP_CHECK(hipMemcpyAsync(ds.p, hs.data(), stot, hipMemcpyHostToDevice, s));
+	if (stot) h2d(ds.p, hs.data(), stot, s);
 	msgs.clear();
 	for (int p = 0; p < P; p++)
 		if (ssz[size_t(p)] || rsz[size_t(p)])
@@ -282,7 +282,7 @@ void comm_allreduce_f64(Grid& g, double* v, int count, int op) {
 	hipStream_t s = g.s_comm;
 	DBuf<double> d;
 	d.alloc(size_t(count));
-	HIP_CHECK(hipMemcpyAsync(d.p, v, size_t(count) * 8, hipMemcpyHostToDevice, s));
+	h2d(d.p, v, size_t(count) * 8, s);
 	comm_allreduce_f64_dev(g, d.p, d.p, count, op, s);
 	d2h_small(v, d.p, size_t(count) * 8, s);
 }

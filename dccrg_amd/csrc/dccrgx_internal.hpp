@@ -176,11 +176,15 @@ struct DBuf {
 // reads of up to kSmallRead bytes go through a pinned staging buffer
 constexpr size_t kSmallRead = 64 * 1024;
 void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s);
+// bytes from host memory to the device, queued on s (list-sized ones staged
+// through pinned memory); the host buffer may be reused on return
+constexpr size_t kStageUp = 256 * 1024;
+void h2d(void* dev, const void* host, size_t bytes, hipStream_t s);
 
 template <class T>
 inline void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
 	d.alloc(h.size());
-	if (!h.empty()) HIP_CHECK(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s));
+	if (!h.empty()) h2d(d.p, h.data(), h.size() * sizeof(T), s);
 }
 
 template <class T>

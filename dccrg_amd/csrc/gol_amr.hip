@@ -964,7 +964,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 	d2h_small(h, cnt.p, 16, s);
 	// the level-0 slots' keys sort last: the groups end where they begin
 	const uint32_t grouped = uint32_t(n_slots - size_t(h[0]));
-	HIP_CHECK(hipMemcpyAsync(T.gptr.p + ng, &grouped, 4, hipMemcpyHostToDevice, s));
+	h2d(T.gptr.p + ng, &grouped, 4, s);
 	HIP_CHECK(hipStreamSynchronize(s));
 	T.ng = ng;
 	T.n_lvl0 = size_t(h[1]);
@@ -1015,7 +1015,7 @@ void k_gol_amr_tables(const MapCtx& m, const uint64_t* slot_ids, size_t n_slots,
 		DBuf<int> mm;
 		mm.alloc(6);
 		const int init[6] = {1 << 30, 1 << 30, 1 << 30, -1, -1, -1};
-		HIP_CHECK(hipMemcpyAsync(mm.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+		h2d(mm.p, init, sizeof(init), s);
 		geo_bbox_kernel<<<std::min<unsigned>(grid_for(n_slots, 256), 1024), 256, 0, s>>>(T.l0c.p, n_slots, G, mm.p);
 		HIP_CHECK(hipGetLastError());
 		int h[6];

@@ -910,7 +910,7 @@ void finish_balance_load_impl(Grid& g) {
 	unsigned long long kept = 0;
 	d2h_small(&kept, ctr.p, 8, s);
 	if (!arrived.empty())
-		HIP_CHECK(hipMemcpyAsync(local.p + kept, arrived.data(), arrived.size() * 8, hipMemcpyHostToDevice, s));
+		h2d(local.p + kept, arrived.data(), arrived.size() * 8, s);
 	const size_t n_new = size_t(kept) + arrived.size();
 	Mesh nm;
 	mesh_from_local(g, nm, local, n_new);

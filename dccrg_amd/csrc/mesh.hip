@@ -247,8 +247,8 @@ void mesh_materialize(Grid& g, Mesh& out) {
 		HIP_CHECK(hipGetLastError());
 	}
 	if (!ring.empty()) {
-		HIP_CHECK(hipMemcpyAsync(out.kid.p + c, ring.data(), ring.size() * 8, hipMemcpyHostToDevice, s));
-		HIP_CHECK(hipMemcpyAsync(out.kown.p + c, rown.data(), ring.size() * 4, hipMemcpyHostToDevice, s));
+		h2d(out.kid.p + c, ring.data(), ring.size() * 8, s);
+		h2d(out.kown.p + c, rown.data(), ring.size() * 4, s);
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -287,8 +287,8 @@ void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n) {
 		HIP_CHECK(hipGetLastError());
 	}
 	if (!gid.empty()) {
-		HIP_CHECK(hipMemcpyAsync(out.kid.p + n, gid.data(), gid.size() * 8, hipMemcpyHostToDevice, s));
-		HIP_CHECK(hipMemcpyAsync(out.kown.p + n, gown.data(), gid.size() * 4, hipMemcpyHostToDevice, s));
+		h2d(out.kid.p + n, gid.data(), gid.size() * 8, s);
+		h2d(out.kown.p + n, gown.data(), gid.size() * 4, s);
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -454,7 +454,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	g.slot_ids.alloc(g.n_slots + 1);
 	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, lsp, nl * 8, hipMemcpyDeviceToDevice, s));
 	if (!halo.empty())
-		HIP_CHECK(hipMemcpyAsync(g.slot_ids.p + nl, halo.data(), halo.size() * 8, hipMemcpyHostToDevice, s));
+		h2d(g.slot_ids.p + nl, halo.data(), halo.size() * 8, s);
 	DBuf<int32_t> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
@@ -721,7 +721,7 @@ void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_
 	hipStream_t s = g.s_comp;
 	DBuf<uint64_t> d;
 	d.alloc(n);
-	HIP_CHECK(hipMemcpyAsync(d.p, ids, n * 8, hipMemcpyHostToDevice, s));
+	h2d(d.p, ids, n * 8, s);
 	DBuf<int32_t> o, sl;
 	o.alloc(n);
 	sl.alloc(n);

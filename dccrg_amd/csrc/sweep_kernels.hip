@@ -1741,6 +1741,10 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	d2h_small(h, cnt.p, sizeof(h), s);
+	// ascending ids (the lists the host merges and stop_refining sorts), sorted
+	// here before they leave the device
+	sort_u64(ref.p, size_t(h[0]), s);
+	sort_u64(unref.p, size_t(h[1]), s);
 	out.refine = download(ref.p, size_t(h[0]), s);
 	out.unrefine = download(unref.p, size_t(h[1]), s);
 	out.kept = size_t(h[2]);

@@ -907,7 +907,7 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 	counts[1] = reg[1].size();
 	counts[2] = irr[0].size();
 	counts[3] = irr[1].size();
-	HIP_CHECK(hipMemcpyAsync(lists.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, s));
+	h2d(lists.p, all.data(), all.size() * 4, s);
 	// per regular tile, in list order: start slot + neighbor-box starts
 	const std::vector<uint32_t> hts = download(tstart, nt + 1, s);
 	const std::vector<int32_t> hnb = download(tnb.p, 6 * nt, s);
@@ -921,7 +921,7 @@ void k_classify_tiles(const MapCtx& m, const uint32_t* tstart, size_t n_tiles_in
 		}
 	regmeta.alloc(meta.size() + 1);
 	if (!meta.empty())
-		HIP_CHECK(hipMemcpyAsync(regmeta.p, meta.data(), meta.size() * sizeof(RegTileMeta), hipMemcpyHostToDevice, s));
+		h2d(regmeta.p, meta.data(), meta.size() * sizeof(RegTileMeta), s);
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 

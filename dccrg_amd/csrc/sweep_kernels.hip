@@ -282,7 +282,7 @@ __global__ void advection_kernel(const double* __restrict__ rho, const double* _
 }
 
 // The same sweep over the fixed-width face table of ensure_face
-// (face_fill_kernel: ell[6 r + d] = the neighbor's slot, -1 none, -2 - f the
+// (face_table_kernel: ell[6 r + d] = the neighbor's slot, -1 none, -2 - f the
 // four finer neighbors fine[4 f ..] in the reference's order): the sweep of a
 // mesh that has just changed, before (and instead of) building its tiles.
 // One thread per cell, the row's six codes as three 8-B loads, the same face

@@ -176,8 +176,9 @@ struct DBuf {
 // reads of up to kSmallRead bytes go through a pinned staging buffer
 constexpr size_t kSmallRead = 64 * 1024;
 void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s);
-// bytes from host memory to the device, queued on s (list-sized ones staged
-// through pinned memory); the host buffer may be reused on return
+// bytes from host memory to the device on s (list-sized ones staged through
+// pinned memory and completed on return); the host buffer may be reused on
+// return
 constexpr size_t kStageUp = 256 * 1024;
 void h2d(void* dev, const void* host, size_t bytes, hipStream_t s);
 

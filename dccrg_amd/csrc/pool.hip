@@ -159,35 +159,24 @@ void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s) {
 }
 
 // Host -> device copies of list-sized buffers (256 B .. 256 KiB) through a
-// ring of four pinned staging buffers per host thread: a pageable 64-KiB
-// upload costs 85 us against 21 from pinned memory on MI355X
+// pinned staging buffer per host thread: a pageable 64-KiB upload costs
+// 85 us against 21 from pinned memory on MI355X, the stream sync included
 // (scripts/microbench/h2d_small.hip); smaller and larger ones go directly
-// (pageable is as fast there).  The host buffer may be reused on return, as
-// with a pageable hipMemcpyAsync; a slot is refilled once its last copy is
-// done (its event).
+// (pageable is as fast there).  The staged copy is waited for before
+// returning (the buffer is reused by the next upload; an event per staging
+// slot instead is unsafe here: grids destroy their streams, and HIP refuses
+// to wait on an event last recorded on a destroyed stream).
 void h2d(void* dev, const void* host, size_t bytes, hipStream_t s) {
 	if (!bytes) return;
 	if (bytes < 256 || bytes > kStageUp) {
 		HIP_CHECK(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s));
 		return;
 	}
-	struct Ring {
-		void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
-		hipEvent_t ev[4] = {};
-		int next = 0;
-	};
-	thread_local Ring R;
-	const int i = R.next;
-	R.next = (i + 1) & 3;
-	if (!R.buf[i]) {
-		HIP_CHECK(hipHostMalloc(&R.buf[i], kStageUp, hipHostMallocDefault));
-		HIP_CHECK(hipEventCreateWithFlags(&R.ev[i], hipEventDisableTiming));
-	} else {
-		HIP_CHECK(hipEventSynchronize(R.ev[i]));
-	}
-	std::memcpy(R.buf[i], host, bytes);
-	HIP_CHECK(hipMemcpyAsync(dev, R.buf[i], bytes, hipMemcpyHostToDevice, s));
-	HIP_CHECK(hipEventRecord(R.ev[i], s));
+	thread_local void* stage = nullptr;
+	if (!stage) HIP_CHECK(hipHostMalloc(&stage, kStageUp, hipHostMallocDefault));
+	std::memcpy(stage, host, bytes);
+	HIP_CHECK(hipMemcpyAsync(dev, stage, bytes, hipMemcpyHostToDevice, s));
+	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace dccrgx

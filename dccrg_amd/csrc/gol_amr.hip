@@ -766,7 +766,10 @@ __global__ __launch_bounds__(256) void lg_table_kernel(const uint32_t* __restric
 // offsets into the table first (geo_axis, a level-0 reach), then every item's
 // byte in flight at once; bit 3 of `e` for a reached cell without a known
 // leaf
-template <bool CUBE, int T0MAX, int DT>
+// FLAT: a one-cell-thick, non-periodic z axis (a 2-D game such as
+// unrefined2d.cpp): only the own plane is reached, so the items off it are
+// dropped at compile time (the same count: they were unreached)
+template <bool CUBE, int T0MAX, int DT, bool FLAT = false>
 __device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, const L0Geom& G, const GeoBox& B, int px,
                                              int py, int pz, int t0, uint32_t& e) {
 	constexpr int K = CUBE ? 27 : 7;
@@ -775,7 +778,16 @@ __device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, co
 	uint32_t ox[3], oy[3], oz[3];
 	geo_axis(px, G.lx, B.x0, B.nx, B.px, true, 0, B, 0, rx, ix, ox);
 	geo_axis(py, G.ly, B.y0, B.ny, B.py, true, 0, B, 1, ry, iy, oy);
-	geo_axis(pz, G.lz, B.z0, B.nz, B.pz, true, 0, B, 2, rz, iz, oz);
+	if (FLAT) {
+#pragma unroll
+		for (int i = 0; i < 3; i++) {
+			rz[i] = i == 1;
+			iz[i] = i == 1;
+			oz[i] = i == 1 ? B.part(2, uint32_t(pz) - B.z0) : 0u;
+		}
+	} else {
+		geo_axis(pz, G.lz, B.z0, B.nz, B.pz, true, 0, B, 2, rz, iz, oz);
+	}
 	uint32_t v[N];
 	bool r[N];
 #pragma unroll
@@ -792,6 +804,11 @@ __device__ __forceinline__ uint32_t lg_count(const uint8_t* __restrict__ tab, co
 			d = t == 5 ? 0 : (t == 6 ? 2 : 1);
 		}
 		const bool centre = a == 1 && b == 1 && d == 1;  // the own level-0 cell (solve.hpp:72-74)
+		if (FLAT && d != 1) {  // off the own plane: never reached
+			r[j] = false;
+			v[j] = 0;
+			continue;
+		}
 		// a, b, d in 0..2 (clamped for the lanes past the last item)
 		a = min(max(a, 0), 2);
 		b = min(max(b, 0), 2);
@@ -845,7 +862,7 @@ __global__ void lg_row_fill_kernel(const uint32_t* __restrict__ flag, const uint
 
 // gated on err[0]: a disagreeing family (bit 2, from the table pass) leaves
 // every state to the exact collect + spread that run instead
-template <bool CUBE>
+template <bool CUBE, bool FLAT>
 __global__ __launch_bounds__(256) void lg_game_kernel(const uint32_t* __restrict__ rows, size_t nrows,
                                                       const uint8_t* __restrict__ corner,
                                                       const uint32_t* __restrict__ l0c, uint32_t* __restrict__ state,
@@ -859,7 +876,7 @@ __global__ __launch_bounds__(256) void lg_game_kernel(const uint32_t* __restrict
 	int x, y, z;
 	l0_unpack(l0c[s], G, x, y, z);
 	uint32_t e = 0;
-	const uint32_t cnt = lg_count<CUBE, 0, 1>(tab, G, B, x, y, z, 0, e);
+	const uint32_t cnt = lg_count<CUBE, 0, 1, FLAT>(tab, G, B, x, y, z, 0, e);
 	if (cnt > uint32_t(kList)) e |= 1u;
 	if (e) atomicOr(err, int(e));
 	const int nm = (c & 0x80u) ? 1 : 8;
@@ -1146,10 +1163,19 @@ void k_gol_amr_level0_game(GolAmrTables& T, const int32_t* hood, int nh, uint32_
 	const unsigned nb = xcd_grid((nr + 255) / 256);
 	lg_table_kernel<<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, G, B, T.l0tab.p, err);
 	HIP_CHECK(hipGetLastError());
-	if (nh == 26)
-		lg_game_kernel<true><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
+	// a one-cell-thick non-periodic z axis: the 2-D form of the count
+	// (DCCRGX_LG_FLAT=0: the general one)
+	static const bool no_flat = std::getenv("DCCRGX_LG_FLAT") && std::atoi(std::getenv("DCCRGX_LG_FLAT")) == 0;
+	const bool flat = !no_flat && T.lz == 1 && !T.per[2];
+	if (nh == 26 && flat)
+		lg_game_kernel<true, true><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
+	else if (nh == 26)
+		lg_game_kernel<true, false><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
+	else if (flat)
+		lg_game_kernel<false, true><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
 	else
-		lg_game_kernel<false><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B, err);
+		lg_game_kernel<false, false><<<nb, 256, 0, s>>>(T.lg_rows.p, nr, T.corner.p, T.l0c.p, state, T.l0tab.p, G, B,
+		                                                err);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -2293,14 +2293,21 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		                         g.n_inner == nl && !std::getenv("DCCRGX_GOL_NO_L0GAME");
 		if (level0_game) {
 			k_gol_amr_level0_game(g.gola, g.d_hood.p, int(g.hood.size() / 3), S, nl, err.p, g.s_comp);
-			k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 1, g.s_comp, g.n_inner,
-			          err.p);
-			k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp, 0, err.p);
 			k_time_end(g);
 			int h[3] = {0, 0, 0};
 			d2h_small(h, err.p, sizeof(h), g.s_comp);
 			// every level-0 cell of a one-process grid has a known leaf
 			DX_REQUIRE(!(h[0] & 8), "internal error: the level-0 game met a level-0 cell without a known leaf");
+			if (h[0] & 4) {
+				// a family's leaves disagree (the game pass did not run): the
+				// exact collect and spread, whose abort order is the reference's
+				k_time_begin(g);
+				k_gol_amr(0, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 1, g.s_comp,
+				          g.n_inner);
+				k_gol_amr(1, g.gola, g.n_slots, nl, S, L, g.nof_ptr.p, g.nof_slot.p, 0, nl, err.p + 2, g.s_comp, 0);
+				k_time_end(g);
+				d2h_small(h, err.p, sizeof(h), g.s_comp);
+			}
 			const int collect = (h[0] & 4) ? h[1] : h[0];
 			for (int e : {collect, h[2]}) {
 				DX_REQUIRE(!(e & 1), "No more room in live neighbor list (more than 8 live level-0 neighbors)");

@@ -26,3 +26,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gola_${TAG
     python -u bench.py --workload gol_amr --steps 20 --warmup 2 --no-cpu-baseline \
     > gpurun_out/prof_gola_${TAG}.json 2> gpurun_out/prof_gola_${TAG}.err || exit $?
 python scripts/step_breakdown.py gpurun_out/prof_gola_${TAG}/run_kernel_trace.csv lg_table 2 12
+# the adaptive step's phase table from the phase-timing build, when present
+if [ -f dccrg_amd/libdccrgx_pt.so ]; then
+  DCCRGX_LIB=libdccrgx_pt.so timeout -k 10 300 python -u bench.py --workload advection_adapt --steps 20 --warmup 3 \
+      --no-cpu-baseline > gpurun_out/${TAG}_adapt_phases.json 2> gpurun_out/${TAG}_adapt_phases.txt || exit $?
+  grep phase gpurun_out/${TAG}_adapt_phases.txt | sort -k4 -n -r | head -25
+fi

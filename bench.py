@@ -260,7 +260,7 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     # bandwidth.
     per_cell = 8 + 4 * kbar + 4
     moved_step = 12 * nl + 20 * n * n
-    kern = "lg_table_kernel + lg_game_kernel (+ the gated exact collect / spread, which exit at once)"
+    kern = "lg_table_kernel + lg_game_kernel"
     moved_model = "level-0 game: 12 B per leaf (state) + 20 B per level-0 cell (row, octant, coordinates, table)"
     moved = moved_step / nl
     ach = moved_step * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None

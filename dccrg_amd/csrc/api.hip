@@ -1542,7 +1542,7 @@ int dccrgx_dont_refine(dccrgx_grid* gp, uint64_t cell) {
 int dccrgx_get_removed_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		return copy_out_u64(g.removed_ids_h, out, cap, n);
+		return copy_out_u64(g.removed_ids.host(g.s_comp), out, cap, n);
 	});
 }
 
@@ -1550,7 +1550,7 @@ int dccrgx_removed_field_download(dccrgx_grid* gp, int fid, void* host, size_t c
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		Field& f = fixed_field(g, fid);
-		const size_t bytes = g.removed_ids_h.size() * f.elem;
+		const size_t bytes = g.removed_ids.size() * f.elem;
 		DX_REQUIRE(cap_bytes >= bytes, "buffer too small for the removed cells' payloads");
 		if (bytes) HIP_CHECK(hipMemcpy(host, f.removed.p, bytes, hipMemcpyDeviceToHost));
 		return 0;
@@ -1561,7 +1561,7 @@ int dccrgx_removed_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(ptr, "null pointer");
-		*ptr = g.removed_ids_h.empty() ? nullptr : fixed_field(g, fid).removed.p;
+		*ptr = g.removed_ids.empty() ? nullptr : fixed_field(g, fid).removed.p;
 		return 0;
 	});
 }
@@ -1570,19 +1570,19 @@ int dccrgx_stop_refining(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) 
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(g.initialized, "not initialized");
-		g.last_new_cells = stop_refining_impl(g);
+		stop_refining_impl(g);
 		if (!out) {
-			if (n) *n = g.last_new_cells.size();
+			if (n) *n = g.new_cells.size();
 			return 0;
 		}
-		return copy_out_u64(g.last_new_cells, out, cap, n);
+		return copy_out_u64(g.new_cells.host(g.s_comp), out, cap, n);
 	});
 }
 
 int dccrgx_get_new_cells(dccrgx_grid* gp, uint64_t* out, size_t cap, size_t* n) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		return copy_out_u64(g.last_new_cells, out, cap, n);
+		return copy_out_u64(g.new_cells.host(g.s_comp), out, cap, n);
 	});
 }
 
@@ -2049,7 +2049,7 @@ int dccrgx_removed_variable_field_download(dccrgx_grid* gp, int fid, uint64_t* s
 		GRID_OR_FAIL(gp);
 		Field& f = field(g, fid);
 		DX_REQUIRE(f.var, "not a variable-size field");
-		const size_t n = g.removed_ids_h.size();
+		const size_t n = g.removed_ids.size();
 		if (!n || !f.rm_off.p) {
 			if (nbytes) *nbytes = 0;
 			return 0;
@@ -2648,7 +2648,7 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		for (int k = 1; k < 7; k++)
 			if (fids[k] != fids[0]) field(g, fids[k]).no_carry = true;
 		try {
-			g.last_new_cells = stop_refining_impl(g);
+			stop_refining_impl(g);
 		} catch (...) {
 			for (int k = 1; k < 7; k++) field(g, fids[k]).no_carry = false;
 			throw;
@@ -2660,9 +2660,7 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
 		// merged parents (adapter.hpp:260-290): the removed children grouped by
 		// parent on the device, each parent's mean of its eight children
-		const auto& rm = g.removed_ids_h;
-		k_adv_merge_parents(g.m, g.dm(), g.n_local, rm, f[0], (const double*)field(g, fids[0]).removed.p, s,
-		                    g.removed_ids_d.n >= rm.size() ? g.removed_ids_d.p : nullptr);
+		k_adv_merge_parents(g.m, g.dm(), g.n_local, g.removed_ids, f[0], (const double*)field(g, fids[0]).removed.p, s);
 		DX_LAP("adapt.2_parents");
 		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
 		HIP_CHECK(hipStreamSynchronize(s));
@@ -2684,8 +2682,8 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		for (int k = 0; k < 7; k++) field(g, fids[k]).transfer = saved[k];
 		DX_LAP("adapt.4_halo");
 		if (out) {
-			out[0] = g.last_new_cells.size();
-			out[1] = rm.size();
+			out[0] = g.new_cells.size();
+			out[1] = g.removed_ids.size();
 		}
 		return 0;
 	});

@@ -1576,10 +1576,10 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 
-std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                                         hipStream_t s) {
-	if (S.empty()) return {};
-	DBuf<uint64_t> dS, out;
+size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
+                          DBuf<uint64_t>& out, hipStream_t s) {
+	if (S.empty()) return 0;
+	DBuf<uint64_t> dS;
 	upload(dS, S, s);
 	out.alloc(8 * S.size() + 1);
 	DBuf<unsigned long long> ctr;
@@ -1589,14 +1589,14 @@ std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int 
 	HIP_CHECK(hipGetLastError());
 	const size_t n = read_counter(ctr, s);
 	sort_u64(out.p, n, s);
-	return download(out.p, n, s);
+	return n;
 }
 
-void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, DBuf<uint64_t>* ids_dev) {
-	ids.clear();
+size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s) {
+	ids.release();
 	slots.release();
-	if (F.empty()) return;
+	if (F.empty()) return 0;
 	DBuf<uint64_t> dF, k1, k2;
 	DBuf<int32_t> v1;
 	upload(dF, F, s);
@@ -1617,9 +1617,9 @@ void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vec
 		DBuf<uint8_t> temp;
 		temp.alloc(bytes + 1);
 		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
-		ids = download(k2.p, n, s);
-		if (ids_dev) ids_dev->swap(k2);
+		ids.swap(k2);
 	}
+	return n;
 }
 
 void k_slot_levels(const MapCtx& m, const uint64_t* slot_ids, size_t n, uint8_t* lvl, hipStream_t s) {

@@ -24,7 +24,7 @@ size_t halo_pack_peer(Grid& g, int hood, int peer, uint8_t* buf, size_t cap);
 void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t bytes);
 void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb);
 
-std::vector<uint64_t> stop_refining_impl(Grid& g);
+void stop_refining_impl(Grid& g);  // the created cells in Grid::new_cells
 
 void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t* cells, const int32_t* procs,
                                   size_t n);

@@ -182,6 +182,37 @@ void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s);
 constexpr size_t kStageUp = 256 * 1024;
 void h2d(void* dev, const void* host, size_t bytes, hipStream_t s);
 
+// an id list made on the device, read on the host only when asked (the
+// adaptive step never reads its created / removed cells on the host)
+struct LazyIds {
+	DBuf<uint64_t> d;
+	std::vector<uint64_t> h;
+	size_t n = 0;
+	bool host_valid = true;
+	void clear() {
+		d.release();
+		h.clear();
+		n = 0;
+		host_valid = true;
+	}
+	void set_host(std::vector<uint64_t> v) {
+		d.release();
+		h = std::move(v);
+		n = h.size();
+		host_valid = true;
+	}
+	void set_device(DBuf<uint64_t>&& buf, size_t count) {
+		h.clear();
+		d = std::move(buf);
+		n = count;
+		host_valid = count == 0;
+	}
+	size_t size() const { return n; }
+	bool empty() const { return n == 0; }
+	const uint64_t* dev() const { return n && d.n >= n ? d.p : nullptr; }
+	inline const std::vector<uint64_t>& host(hipStream_t s);
+};
+
 template <class T>
 inline void upload(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
 	d.alloc(h.size());
@@ -192,6 +223,14 @@ template <class T>
 inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
 	std::vector<T> h(n);
 	if (n) d2h_small(h.data(), d, n * sizeof(T), s);
+	return h;
+}
+
+inline const std::vector<uint64_t>& LazyIds::host(hipStream_t s) {
+	if (!host_valid) {
+		h = download(d.p, n, s);
+		host_valid = true;
+	}
 	return h;
 }
 
@@ -238,7 +277,7 @@ struct Field {
 	DBuf<uint8_t> data;     // n_slots * elem
 	DBuf<uint8_t> scratch;  // double buffer for sweeps (allocated on demand)
 	// payloads of the cells removed by the last stop_refining whose parent is
-	// local (unrefined_cell_data 7250), in the order of Grid::removed_ids_h
+	// local (unrefined_cell_data 7250), in the order of Grid::removed_ids
 	DBuf<uint8_t> removed;
 	// variable-size payloads (varfield.hip): elem == 0, `data` is a byte pool
 	// and slot s owns [voff[s], voff[s + 1]); the removed store likewise
@@ -479,9 +518,8 @@ struct Grid {
 	} load;
 	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
 	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
-	std::vector<uint64_t> removed_ids_h;        // get_removed_cells 3497 (order of Field::removed)
-	DBuf<uint64_t> removed_ids_d;               // the same on the device when n > 0, else empty
-	std::vector<uint64_t> last_new_cells;  // local cells created by the last stop_refining
+	LazyIds removed_ids;  // get_removed_cells 3497 (order of Field::removed)
+	LazyIds new_cells;    // local cells created by the last stop_refining (ascending)
 	Migration mig;
 	// the range map over the full id range of every level (one process,
 	// Morton-ordered own leaves: rebuild's "direct" mode), kept across
@@ -748,11 +786,14 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 // stop_refining on the device: the children of the refined cells owned by
 // `rank`, ascending; the children of merged families staying on `rank`
 // (owned here, like the family's first child), ascending, and their slots
-std::vector<uint64_t> k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                                         hipStream_t s);
-void k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                     std::vector<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s,
-                     DBuf<uint64_t>* ids_dev = nullptr);
+// the local children of the refined cells S, ascending, into out; returns
+// their count
+size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
+                          DBuf<uint64_t>& out, hipStream_t s);
+// the children of the merged families F held here, ascending, into ids with
+// their slots; returns their count
+size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s);
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
                      hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0,
@@ -817,8 +858,9 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
                  double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
                  hipStream_t s);
-void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
-                         double* rho, const double* removed_rho, hipStream_t s, const uint64_t* rm_dev = nullptr);
+// rm: the removed cells (on the device when it holds them, else uploaded)
+void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, LazyIds& rm, double* rho,
+                         const double* removed_rho, hipStream_t s);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
                           size_t np, hipStream_t s);
 void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],

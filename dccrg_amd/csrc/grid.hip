@@ -463,8 +463,8 @@ static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
 //    removed children's payloads go to the parent's process (10360-10410,
 //    get_removed_cells 3497), the parents start zeroed (cell_data[parent],
 //    10475) and every structure is rebuilt.
-// Returns the local cells created by refinement.
-std::vector<uint64_t> stop_refining_impl(Grid& g) {
+// The local cells created by refinement go to Grid::new_cells.
+void stop_refining_impl(Grid& g) {
 	if (g.size > 1) comm_require(g, "stop_refining");
 	const int nh = int(g.hood.size() / 3);
 	hipStream_t s = g.s_comp;
@@ -473,8 +473,8 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		f.removed.release();
 		f.rm_off.release();
 	}
-	g.removed_ids_h.clear();
-	g.removed_ids_d.release();
+	g.removed_ids.clear();
+	g.new_cells.clear();
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
 	std::vector<uint64_t> D = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_refine_cells))));
@@ -511,11 +511,15 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s);
 	const std::vector<uint64_t> F = union_sorted(g, comm_allgather_u64(g, fmine));
 	DX_LAP("sr.3_override_unrefines");
-	if (S.empty() && F.empty()) return {};
+	if (S.empty() && F.empty()) return;
 
-	// local refined cells -> the new local cells (on the device); weights and
-	// pins follow (6199-6200, 10239-10251)
-	std::vector<uint64_t> created = k_created_children(g.m, g.dm(), g.rank, S, s);
+	// local refined cells -> the new local cells (on the device, read on the
+	// host only when asked); weights and pins follow (6199-6200, 10239-10251)
+	{
+		DBuf<uint64_t> created;
+		const size_t nc = k_created_children(g.m, g.dm(), g.rank, S, created, s);
+		g.new_cells.set_device(std::move(created), nc);
+	}
 	if (!g.weights.empty() || !g.pins.empty()) {
 		std::vector<int32_t> own(S.size());
 		lookup_batch(g, S.data(), S.size(), own.data(), nullptr);
@@ -542,10 +546,11 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 
 	// merged families: the children's payloads to the parent's new process
 	std::map<int, std::vector<uint64_t>> send_ids, recv_ids;
-	std::vector<uint64_t> keep_ids;  // removed children staying on this rank
-	DBuf<int32_t> ksl;               // and their slots (device)
+	DBuf<uint64_t> keep_ids;  // removed children staying on this rank (device, ascending)
+	DBuf<int32_t> ksl;        // and their slots
+	size_t n_keep = 0;
 	if (!F.empty()) {
-		k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, &g.removed_ids_d);
+		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s);
 		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
 		if (g.size > 1 || attrs) {
@@ -580,7 +585,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		for (auto& kv : recv_ids) k += kv.second.size();
 		return k;
 	}();
-	const size_t n_rm = keep_ids.size() + n_recv;
+	const size_t n_rm = n_keep + n_recv;
 	// every rank takes part when any family merges (the host transport's
 	// exchanges are collective)
 	if (!F.empty()) {
@@ -589,9 +594,8 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		for (auto& f : g.fields) {
 			if (f.var) continue;
 			f.removed.alloc(n_rm * f.elem + 1);
-			if (!keep_ids.empty()) k_pack(f.data.p, f.elem, 0, f.elem, ksl.p, keep_ids.size(), f.removed.p, s);
+			if (n_keep) k_pack(f.data.p, f.elem, 0, f.elem, ksl.p, n_keep, f.removed.p, s);
 		}
-		g.removed_ids_h = keep_ids;
 		std::vector<size_t> soff, roff;
 		size_t so = 0, ro = 0;
 		for (auto& kv : send_ids) {
@@ -601,8 +605,14 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		for (auto& kv : recv_ids) {
 			roff.push_back(ro);
 			ro += kv.second.size() * bpc;
-			g.removed_ids_h.insert(g.removed_ids_h.end(), kv.second.begin(), kv.second.end());
-			g.removed_ids_d.release();  // the device copy holds the kept ones only
+		}
+		if (recv_ids.empty()) {
+			g.removed_ids.set_device(std::move(keep_ids), n_keep);
+		} else {
+			// the kept children, then the received ones per source process
+			std::vector<uint64_t> all = download(keep_ids.p, n_keep, s);
+			for (auto& kv : recv_ids) all.insert(all.end(), kv.second.begin(), kv.second.end());
+			g.removed_ids.set_host(std::move(all));
 		}
 		DBuf<uint8_t> sbuf, rbuf;
 		sbuf.alloc(so + 1);
@@ -637,7 +647,7 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 		if (g.size > 1) comm_device_transfer(g, msgs, s);
 		// field-major messages -> the removed store after the kept children
 		j = 0;
-		size_t at = keep_ids.size();
+		size_t at = n_keep;
 		for (auto& kv : recv_ids) {
 			size_t o = roff[j++];
 			for (auto& f : g.fields) {
@@ -666,10 +676,10 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 			for (auto& f : g.fields) {
 				if (!f.var) continue;
 				VarMsg K, X;
-				var_pack(f, ksl.p, keep_ids.size(), K, s);
+				var_pack(f, ksl.p, n_keep, K, s);
 				var_pack(f, osl.p, out_all.size(), X, s);
 				if (g.size > 1) var_transfer(g, X, R, ro2, s);
-				const size_t nk = keep_ids.size();
+				const size_t nk = n_keep;
 				DBuf<uint64_t> sizes;
 				sizes.alloc(n_rm + 1);
 				if (nk) HIP_CHECK(hipMemcpyAsync(sizes.p, K.ssz.p, nk * 8, hipMemcpyDeviceToDevice, s));
@@ -708,7 +718,6 @@ std::vector<uint64_t> stop_refining_impl(Grid& g) {
 	DX_LAP("sr.6_apply");
 	rebuild(g, nm);
 	DX_LAP("sr.7_rebuild");
-	return created;
 }
 
 // --------------------------------------------------------------------------- load balance
@@ -775,8 +784,7 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 	g.unrefine_requests.clear();    // cells_to_unrefine (3810)
 	g.dont_refine_cells.clear();    // cells_not_to_refine (3812)
 	g.dont_unrefine_cells.clear();  // cells_not_to_unrefine (3813)
-	g.removed_ids_h.clear();  // unrefined_cell_data (3811)
-	g.removed_ids_d.release();
+	g.removed_ids.clear();  // unrefined_cell_data (3811)
 	for (auto& f : g.fields) {
 		f.removed.release();
 		f.rm_off.release();

@@ -1678,13 +1678,14 @@ void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const ui
 // adapt_grid's merged parents (adapter.hpp:260-290) from the removed store's
 // ids `rm` (store order): parents grouped, their eight children in ascending
 // id, the parents' local slots, then the mean density
-void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, const std::vector<uint64_t>& rm,
-                         double* rho, const double* removed_rho, hipStream_t s, const uint64_t* rm_dev) {
+void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, LazyIds& rm, double* rho,
+                         const double* removed_rho, hipStream_t s) {
 	if (rm.empty()) return;
 	const size_t n = rm.size();
 	DBuf<uint64_t> up, par;
+	const uint64_t* rm_dev = rm.dev();
 	if (!rm_dev) {
-		upload(up, rm, s);
+		upload(up, rm.host(s), s);
 		rm_dev = up.p;
 	}
 	par.alloc(n);

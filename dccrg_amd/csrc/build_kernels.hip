@@ -1489,11 +1489,12 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 
 std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
                                           const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
-                                          const std::vector<uint64_t>& DU, hipStream_t s) {
+                                          const std::vector<uint64_t>& DU, hipStream_t s, const uint64_t* dS_given) {
 	if (req.empty()) return {};
 	DBuf<uint64_t> dr, par, dS, dDU;
 	upload(dr, req, s);
-	upload(dS, S, s);
+	if (!dS_given) upload(dS, S, s);
+	const uint64_t* dSp = dS_given ? dS_given : dS.p;
 	upload(dDU, DU, s);
 	par.alloc(req.size() + 1);
 	request_parents_kernel<<<grid_for(req.size(), 256), 256, 0, s>>>(m, dr.p, req.size(), par.p);
@@ -1509,9 +1510,9 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 	DBuf<uint32_t> ok;
 	ok.alloc(n);
 	k_fill_i32(reinterpret_cast<int32_t*>(ok.p), n, 1, s);
-	family_blocked_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, par.p, n, dS.p, S.size(), dDU.p, DU.size(), ok.p);
+	family_blocked_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, par.p, n, dSp, S.size(), dDU.p, DU.size(), ok.p);
 	if (nh > 0)
-		unrefine_check_kernel<<<grid_for(n * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, par.p, n, dS.p, S.size(),
+		unrefine_check_kernel<<<grid_for(n * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, par.p, n, dSp, S.size(),
 		                                                                    ok.p);
 	HIP_CHECK(hipGetLastError());
 	const std::vector<uint64_t> cand = download(par.p, n, s);
@@ -1525,10 +1526,13 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
                      hipStream_t s, const size_t* at, size_t* pos_at, int n_at, size_t n_prefix, const DevMesh* dm,
-                     DBuf<int32_t>* src) {
-	DBuf<uint64_t> dS, dF;
-	upload(dS, S, s);
-	upload(dF, F, s);
+                     DBuf<int32_t>* src, const uint64_t* dS_given, const uint64_t* dF_given) {
+	DBuf<uint64_t> dS_own, dF_own;
+	if (!dS_given) upload(dS_own, S, s);
+	if (!dF_given) upload(dF_own, F, s);
+	struct {
+		const uint64_t* p;
+	} dS{dS_given ? dS_given : dS_own.p}, dF{dF_given ? dF_given : dF_own.p};
 	DBuf<uint32_t> cnt, pos;
 	cnt.alloc(n + 1);
 	pos.alloc(n + 1);
@@ -1577,10 +1581,13 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 }
 
 size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                          DBuf<uint64_t>& out, hipStream_t s) {
+                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS_given) {
 	if (S.empty()) return 0;
-	DBuf<uint64_t> dS;
-	upload(dS, S, s);
+	DBuf<uint64_t> dS_own;
+	if (!dS_given) upload(dS_own, S, s);
+	struct {
+		const uint64_t* p;
+	} dS{dS_given ? dS_given : dS_own.p};
 	out.alloc(8 * S.size() + 1);
 	DBuf<unsigned long long> ctr;
 	ctr.alloc(1);
@@ -1593,13 +1600,16 @@ size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std
 }
 
 size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s) {
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF_given) {
 	ids.release();
 	slots.release();
 	if (F.empty()) return 0;
-	DBuf<uint64_t> dF, k1, k2;
+	DBuf<uint64_t> dF_own, k1, k2;
 	DBuf<int32_t> v1;
-	upload(dF, F, s);
+	if (!dF_given) upload(dF_own, F, s);
+	struct {
+		const uint64_t* p;
+	} dF{dF_given ? dF_given : dF_own.p};
 	const size_t cap = 8 * F.size();
 	k1.alloc(cap + 1);
 	k2.alloc(cap + 1);

@@ -776,28 +776,30 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 // set S (sorted): none of the children refined or marked dont_unrefine (DU,
 // sorted), and no finer leaf or refined same-level leaf in the parent's
 // neighborhood (unrefine_check_kernel)
+// (stop_refining's sets S and F are sorted host lists; dS / dF, when given,
+// are their device copies, uploaded once by the caller)
 std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
                                           const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
-                                          const std::vector<uint64_t>& DU, hipStream_t s);
+                                          const std::vector<uint64_t>& DU, hipStream_t s,
+                                          const uint64_t* dS = nullptr);
+// the children of the refined cells S owned by `rank`, ascending, into out;
+// returns their count
+size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
+                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS = nullptr);
+// the children of the merged families F staying on `rank` (owned here, like
+// the family's first child), ascending, into ids with their slots; returns
+// their count
+size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF = nullptr);
 // known list after refining the sorted set S and merging the families under
 // the sorted parents F: every known leaf in S is replaced by its 8 children
 // (same owner), the children of a parent in F by the parent (owner of the
 // first child)
-// stop_refining on the device: the children of the refined cells owned by
-// `rank`, ascending; the children of merged families staying on `rank`
-// (owned here, like the family's first child), ascending, and their slots
-// the local children of the refined cells S, ascending, into out; returns
-// their count
-size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                          DBuf<uint64_t>& out, hipStream_t s);
-// the children of the merged families F held here, ascending, into ids with
-// their slots; returns their count
-size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s);
 void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n, const std::vector<uint64_t>& S,
                      const std::vector<uint64_t>& F, DBuf<uint64_t>& out_id, DBuf<int32_t>& out_own, size_t& n_out,
                      hipStream_t s, const size_t* at = nullptr, size_t* pos_at = nullptr, int n_at = 0,
-                     size_t n_prefix = 0, const DevMesh* dm = nullptr, DBuf<int32_t>* src = nullptr);
+                     size_t n_prefix = 0, const DevMesh* dm = nullptr, DBuf<int32_t>* src = nullptr,
+                     const uint64_t* dS = nullptr, const uint64_t* dF = nullptr);
 
 // --- launchers implemented in tile_build.hip --------------------------------
 struct TileBuild {

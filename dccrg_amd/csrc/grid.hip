@@ -508,8 +508,13 @@ void stop_refining_impl(Grid& g) {
 	const std::vector<uint64_t> DU = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_unrefine_cells))));
 	g.dont_unrefine_cells.clear();
 	DX_LAP("sr.3a_requests");
-	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s);
+	// S is final: one device copy for the passes below
+	DBuf<uint64_t> dS;
+	upload(dS, S, s);
+	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p);
 	const std::vector<uint64_t> F = union_sorted(g, comm_allgather_u64(g, fmine));
+	DBuf<uint64_t> dF;
+	upload(dF, F, s);
 	DX_LAP("sr.3_override_unrefines");
 	if (S.empty() && F.empty()) return;
 
@@ -517,7 +522,7 @@ void stop_refining_impl(Grid& g) {
 	// host only when asked); weights and pins follow (6199-6200, 10239-10251)
 	{
 		DBuf<uint64_t> created;
-		const size_t nc = k_created_children(g.m, g.dm(), g.rank, S, created, s);
+		const size_t nc = k_created_children(g.m, g.dm(), g.rank, S, created, s, dS.p);
 		g.new_cells.set_device(std::move(created), nc);
 	}
 	if (!g.weights.empty() || !g.pins.empty()) {
@@ -550,7 +555,7 @@ void stop_refining_impl(Grid& g) {
 	DBuf<int32_t> ksl;        // and their slots
 	size_t n_keep = 0;
 	if (!F.empty()) {
-		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s);
+		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, dF.p);
 		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
 		if (g.size > 1 || attrs) {
@@ -711,7 +716,8 @@ void stop_refining_impl(Grid& g) {
 		size_t pos_at[2] = {0, 0};
 		const DevMesh dm = g.dm();
 		k_apply_refines(g.m, known.kid.p, known.kown.p, known.n_known, S, F, nm.kid, nm.kown, nm.n_known, s, at, pos_at,
-		                known.n_prefix ? 2 : 0, known.n_prefix, &dm, g.size == 1 && known.n_prefix ? &nm.carry : nullptr);
+		                known.n_prefix ? 2 : 0, known.n_prefix, &dm, g.size == 1 && known.n_prefix ? &nm.carry : nullptr,
+		                dS.p, dF.p);
 		nm.prefix_run1 = pos_at[0];
 		nm.n_prefix = pos_at[1];
 	}

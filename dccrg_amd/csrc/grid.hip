@@ -413,6 +413,16 @@ static std::vector<uint64_t> union_sorted(Grid& g, const std::vector<std::vector
 	return u;
 }
 
+// every rank's sorted list merged (All_Gather + union); one process: its own
+// list, without the copies of the exchange
+static std::vector<uint64_t> gather_union(Grid& g, std::vector<uint64_t> mine) {
+	if (g.size == 1) {
+		host_sort_u64(mine, true, g.s_comp);  // a no-op for the sorted lists given here
+		return mine;
+	}
+	return union_sorted(g, comm_allgather_u64(g, mine));
+}
+
 static DBuf<int32_t> slots_of(Grid& g, const std::vector<uint64_t>& ids);
 
 static std::vector<uint64_t> sorted_unique(Grid& g, std::vector<uint64_t> v) {
@@ -435,7 +445,7 @@ static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
 		    k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp, finer);
 		std::vector<uint64_t> mine_new;
 		std::set_difference(found.begin(), found.end(), S.begin(), S.end(), std::back_inserter(mine_new));
-		const std::vector<uint64_t> all = union_sorted(g, comm_allgather_u64(g, mine_new));
+		const std::vector<uint64_t> all = gather_union(g, std::move(mine_new));
 		fresh.clear();
 		std::set_difference(all.begin(), all.end(), S.begin(), S.end(), std::back_inserter(fresh));
 		if (fresh.empty()) break;
@@ -477,7 +487,7 @@ void stop_refining_impl(Grid& g) {
 	g.new_cells.clear();
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
-	std::vector<uint64_t> D = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_refine_cells))));
+	std::vector<uint64_t> D = gather_union(g, sorted_unique(g, vec(g.dont_refine_cells)));
 	if (!D.empty()) close_set(g, D, true);
 	// cells_not_to_refine = old_donts (10039-10040): the spread set, the same
 	// on every rank, stays for the next stop_refining and refine_completely
@@ -494,7 +504,7 @@ void stop_refining_impl(Grid& g) {
 	}
 	g.refine_requests.clear();
 	g.refine_bulk.clear();
-	std::vector<uint64_t> S = union_sorted(g, comm_allgather_u64(g, mine));
+	std::vector<uint64_t> S = gather_union(g, std::move(mine));
 	if (!S.empty()) close_set(g, S, false);
 	DX_LAP("sr.2_induce_refines");
 
@@ -505,14 +515,14 @@ void stop_refining_impl(Grid& g) {
 	req.insert(req.end(), g.unrefine_bulk.begin(), g.unrefine_bulk.end());
 	g.unrefine_requests.clear();
 	g.unrefine_bulk.clear();
-	const std::vector<uint64_t> DU = union_sorted(g, comm_allgather_u64(g, sorted_unique(g, vec(g.dont_unrefine_cells))));
+	const std::vector<uint64_t> DU = gather_union(g, sorted_unique(g, vec(g.dont_unrefine_cells)));
 	g.dont_unrefine_cells.clear();
 	DX_LAP("sr.3a_requests");
 	// S is final: one device copy for the passes below
 	DBuf<uint64_t> dS;
 	upload(dS, S, s);
 	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p);
-	const std::vector<uint64_t> F = union_sorted(g, comm_allgather_u64(g, fmine));
+	const std::vector<uint64_t> F = gather_union(g, fmine);
 	DBuf<uint64_t> dF;
 	upload(dF, F, s);
 	DX_LAP("sr.3_override_unrefines");

@@ -86,6 +86,28 @@ def test_config1_driver_matches_oracle(gpu, P):
     assert int(m.group(3)) == int(o.gol_get(ids).sum())
 
 
+def test_advection_device_members(gpu):
+    """examples/advection_device.cpp: the reference's adaptive advection loop
+    (tests/advection/2d.cpp, adapt every step, cfl 0.5) through the facade's
+    device members only (add_field<double>, advection_initialize / _step /
+    _commit / _check_adaptation / _adapt, advection_max_time_step), at 1 and
+    2 processes: mass conserved over the steps (1e-13
+    relative), cells created and removed, and the same counts and mass at
+    both process counts."""
+    res = {}
+    for P in (1, 2):
+        out = mpirun("advection_device", P, [16, 12])
+        m = re.search(r"cells (\d+) steps (\d+) created (\d+) removed (\d+) mass0 (\S+) mass (\S+)", out)
+        assert m, out
+        res[P] = m.groups()
+    for P in (1, 2):
+        _, steps, created, removed, m0, m1 = res[P]
+        assert int(steps) == 12 and int(created) > 0 and int(removed) > 0
+        assert abs(float(m1) - float(m0)) <= 1e-13 * abs(float(m0)), (P, m0, m1)
+    assert res[1][:4] == res[2][:4]
+    assert abs(float(res[1][5]) - float(res[2][5])) <= 1e-13 * abs(float(res[1][5]))
+
+
 CELL_LINE = re.compile(r"Cell (\d+) data \(on process (\d+)\): ([-\d .e+]*)")
 
 

@@ -108,6 +108,28 @@ def test_advection_device_members(gpu):
     assert abs(float(res[1][5]) - float(res[2][5])) <= 1e-13 * abs(float(res[1][5]))
 
 
+@pytest.mark.parametrize("n", [64, 512])
+def test_poisson_device_members(gpu, tmp_path, n):
+    """examples/poisson_device.cpp: tests/poisson/poisson1d.cpp's solve through
+    the facade's poisson_cache / poisson_solve at 1 and 3 processes, within
+    the reference's 2-norm threshold (3e-7) of the reference's serial solver
+    (tests/golden/poisson1d_ref.npz) after the last-cell offset."""
+    from poisson_cases import POISSON1D_THRESHOLD, offset_last, p_norm, poisson1d_reference
+
+    ref, rhs = poisson1d_reference(n)
+    rf = tmp_path / "rhs.bin"
+    rhs.astype("<f8").tofile(rf)
+    sols = []
+    for P in (1, 3):
+        of = tmp_path / f"sol{P}.bin"
+        out = mpirun("poisson_device", P, [n, rf, of])
+        assert re.search(rf"cells {n} iterations \d+", out), out
+        sols.append(offset_last(np.fromfile(of, dtype="<f8")))
+    for s_ in sols:
+        assert p_norm(s_, ref) <= POISSON1D_THRESHOLD
+    assert p_norm(sols[0], sols[1]) <= POISSON1D_THRESHOLD
+
+
 CELL_LINE = re.compile(r"Cell (\d+) data \(on process (\d+)\): ([-\d .e+]*)")
 
 

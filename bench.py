@@ -242,8 +242,12 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     st.set(live0[par].astype(np.uint32))
     for _ in range(a.warmup):
         g.get_live_neighbors(st, ls)
-    el, kms, kn = timed(g, torch, dist, 1, lambda: g.get_live_neighbors(st, ls), a.steps)
+    # one process per grid: at N > 1 every rank plays its own replica, timed
+    # between the same barriers (value = all ranks' leaves / the slowest rank)
+    el, kms, kn = timed(g, torch, dist, world, lambda: g.get_live_neighbors(st, ls), a.steps)
     nl = g.n_local
+    mx, sm = reduce_stats(torch, dist, world, [el, float(nl)])
+    el, total = mx[0], int(sm[1])
     kbar = g.neighbor_entries("of") / nl
     f1 = float(np.mean(lvl == 1))
     # roofline: the bytes the turn's kernels must move over the turn's kernel
@@ -266,7 +270,7 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     ach = moved_step * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     model = per_cell * nl * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
     line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
-                     nl * a.steps / el, 1, a, el / a.steps * 1e3, "u32",
+                     total * a.steps / el, world, a, el / a.steps * 1e3, "u32",
                      "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
                      {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
                       "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
@@ -279,8 +283,9 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                         "model_bytes_per_leaf": per_cell, "model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
                         "model_throughput_GBs": model, "frac_model": model / PEAK_HBM_GBS if model else None,
                         "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}
-    line["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline("gol_amr", a.cpu_seconds)
-    print(json.dumps(line), flush=True)
+    line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("gol_amr", a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     g.close()
 
 

@@ -16,6 +16,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <functional>
 
 #include "dccrgx_internal.hpp"
@@ -504,7 +505,7 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // (wave_reserve needs every lane).
 __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1,
                                   bool morton, int32_t* ell, unsigned long long* n_fine, uint32_t* fine_keys,
-                                  int32_t* err) {
+                                  size_t key_cap, int32_t* err) {
 	const SlotExists ex{M};
 	const size_t stride = size_t(gridDim.x) * blockDim.x;
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r - lane_id() < nrows; r += stride) {
@@ -570,7 +571,10 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 		unsigned long long at = wave_reserve(n_fine, kf);
 		if (live)
 			for (int dir = 0; dir < 6; dir++)
-				if (o6[dir] == -2) fine_keys[at++] = (uint32_t(r) << 3) | uint32_t(dir);
+				if (o6[dir] == -2) {
+					if (at < key_cap) fine_keys[at] = (uint32_t(r) << 3) | uint32_t(dir);  // else counted only
+					at++;
+				}
 	}
 }
 
@@ -1307,14 +1311,24 @@ size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids,
 	n_fine.alloc(1);
 	HIP_CHECK(hipMemsetAsync(n_fine.p, 0, 8, s));
 	// finer faces: at most 6 per row, in practice a few percent of the rows;
-	// keys row << 3 | direction
+	// keys row << 3 | direction, room for a quarter of the rows first (the
+	// pass runs again with room for all of them if that was too little: it
+	// rewrites every row of the table)
 	DBuf<uint32_t> keys;
-	keys.alloc(6 * nrows + 1);
-	if (nrows)
-		face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, ell,
-		                                                       n_fine.p, keys.p, err);
-	HIP_CHECK(hipGetLastError());
-	const size_t nf = size_t(read_counter(n_fine, s));
+	const char* kc = std::getenv("DCCRGX_FACE_KEY_CAP");  // tests: a small first room forces the second pass
+	size_t cap = kc && *kc ? size_t(std::strtoull(kc, nullptr, 10)) : nrows / 4 + 1024;
+	size_t nf = 0;
+	for (;;) {
+		keys.alloc(cap);
+		if (nrows)
+			face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit,
+			                                                       ell, n_fine.p, keys.p, cap, err);
+		HIP_CHECK(hipGetLastError());
+		nf = size_t(read_counter(n_fine, s));
+		if (nf <= cap) break;
+		cap = nf;
+		HIP_CHECK(hipMemsetAsync(n_fine.p, 0, 8, s));
+	}
 	fine.alloc(4 * nf + 4);
 	if (!nf) return 0;
 	int bits = 4;

@@ -139,6 +139,33 @@ def test_face_table_sweep_bitwise_equals_tiles(gpu, base, R):
         assert np.array_equal(a, b)
 
 
+def test_face_table_second_pass_same_table(gpu, monkeypatch):
+    """The face table's finer-face keys get room for a quarter of the rows
+    first and the pass runs again with room for all of them when that was
+    too little (k_face_table): forced here with room for one key, the
+    densities of three table sweeps (which read the table, finer faces
+    included) are bitwise those of the one-pass build."""
+    out = []
+    for cap in (None, "1"):
+        if cap is None:
+            monkeypatch.delenv("DCCRGX_FACE_KEY_CAP", raising=False)
+        else:
+            monkeypatch.setenv("DCCRGX_FACE_KEY_CAP", cap)
+        g, f = gpu_grid((16, 16, 8), 2)
+        prerefine(g, f, 2)
+        dt = g.advection_max_time_step(f)
+        rho = []
+        for _ in range(3):
+            g.advection_step(f, 0.5 * dt)
+            g.advection_commit(f[0])
+            rho.append(f[0].get(0, g.n_local))
+        out.append(rho)
+        g.close()
+    monkeypatch.delenv("DCCRGX_FACE_KEY_CAP", raising=False)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+
+
 def _run_parity_grid(base=(32, 32, 8), R=2, steps=100):
     g, f = gpu_grid(base, R)
     prerefine(g, f, R)

@@ -2569,7 +2569,9 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		flush_bulk_requests(g);
 		if (g.unrefine_requests.empty() && n < (size_t(1) << 28)) {
 			// on the device: refine requests, whole-family decisions, partial runs
-			const AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, g.s_comp);
+			// one process with Morton-ordered slots: each family's leaves are one run
+			const bool solo = g.size == 1 && g.morton_slots;
+			const AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.s_comp);
 			// 2434-2520 (bulk lists: no set hashing of ~20 K ids per step)
 			g.refine_bulk.insert(g.refine_bulk.end(), q.refine.begin(), q.refine.end());
 			nref = q.refine.size();

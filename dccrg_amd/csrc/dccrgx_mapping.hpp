@@ -57,12 +57,21 @@ DX_HD void map_init(MapCtx& m, const uint64_t len[3], int R, const int per[3]) {
 	for (int l = R + 2; l <= kMaxLevels; l++) m.first[l] = c;
 }
 
-// dccrg_mapping.hpp:261-289
+// dccrg_mapping.hpp:261-289.  first[] is read at lane-uniform indices only: in
+// a kernel the MapCtx is a kernel argument, and an index that differs between
+// lanes turns each read into a dependent global load (scalar loads otherwise)
 DX_HD int map_level(const MapCtx& m, uint64_t cell) {
 	if (cell == error_cell || cell > m.last) return -1;
 	int l = 0;
-	while (l < m.R && cell >= m.first[l + 1]) l++;
+	for (int k = 1; k <= m.R; k++) l += cell >= m.first[k] ? 1 : 0;
 	return l;
+}
+
+// m.first[l] (0 <= l <= R + 1) by lane-uniform reads (see map_level)
+DX_HD uint64_t map_first(const MapCtx& m, int l) {
+	uint64_t f = m.first[0];
+	for (int k = 1; k <= m.R + 1; k++) f = k <= l ? m.first[k] : f;
+	return f;
 }
 
 // dccrg_mapping.hpp:297-310
@@ -78,7 +87,7 @@ DX_HD uint64_t map_from_indices(const MapCtx& m, uint64_t x, uint64_t y, uint64_
 	if (lvl < 0 || lvl > m.R) return error_cell;
 	const int sh = m.R - lvl;
 	const uint64_t lx = m.len[0] << lvl, ly = m.len[1] << lvl;
-	return m.first[lvl] + (x >> sh) + (y >> sh) * lx + (z >> sh) * lx * ly;
+	return map_first(m, lvl) + (x >> sh) + (y >> sh) * lx + (z >> sh) * lx * ly;
 }
 
 // dccrg_mapping.hpp:217-253; returns level (-1 on error) and fills indices
@@ -88,7 +97,7 @@ DX_HD int map_indices(const MapCtx& m, uint64_t cell, uint64_t& x, uint64_t& y, 
 		x = y = z = error_index;
 		return -1;
 	}
-	uint64_t c = cell - m.first[l];
+	uint64_t c = cell - map_first(m, l);
 	const int sh = m.R - l;
 	if (m.lg[0] >= 0) {
 		// power-of-two x and y lengths: the divisions are shifts

@@ -1341,86 +1341,156 @@ __global__ void adv_bands_kernel(MapCtx m, const double* __restrict__ rho, const
 // run goes to the host, which merges the runs of a parent (families split
 // between runs or processes).  Lists are appended through counters
 // cnt[0] refines, cnt[1] unrefines, cnt[2] kept families, cnt[3] partial runs.
-__global__ void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restrict__ ids,
-                                    const uint8_t* __restrict__ band, size_t n, uint64_t* __restrict__ ref,
-                                    uint64_t* __restrict__ unref, uint32_t* __restrict__ part,
-                                    unsigned long long* __restrict__ cnt) {
-	// each lane a run of kRun slots: classify them, reserve its positions in
-	// the three lists with one atomic per wave and list, then write.  The
-	// parents of slots s0 - 1 .. s0 + kRun + 6 (a family run starting at the
-	// lane's last slot reaches 7 further) are computed once each.
-	constexpr int kRun = 8;
-	constexpr int kWin = kRun + 8;  // window index w <-> slot s0 - 1 + w
-	const size_t s0 = (blockIdx.x * size_t(blockDim.x) + threadIdx.x) * kRun;
-	uint64_t par[kWin];  // parent id, or ~0 for a level-0 cell / outside [0, n)
+//
+// Coalesced: a wave covers 64 x kJ consecutive slots, lane l taking slots
+// base + 64 j + l (j < kJ) and the tail chunk base + 64 kJ + l (the runs that
+// start in the last chunk reach up to 7 slots past it); the neighbors'
+// parents and bands come from the other lanes by shuffles (slot + q is lane
+// l + q of the same chunk, or of the next one past lane 63).  List positions
+// are reserved per block (block_reserve4).  Every id and band load is issued
+// before the parents are computed.  (Round 5: 282 -> 136 us a config-3 step,
+// of which the per-block reservation took 277 -> 191, the solo shortcut
+// 191 -> 165 and lane-uniform MapCtx reads the rest)
+// Positions in the four request lists for a block of W waves: one atomic per
+// block and list (per-wave atomics on the same four counters serialise at the
+// device-coherent level - 4 x ~17000 of them a config-3 step).  c and the
+// result in counter order: refine, unrefine, kept, partial.
+template <int W>
+__device__ __forceinline__ void block_reserve4(unsigned long long* __restrict__ cnt, const unsigned c[4],
+                                               unsigned long long out[4]) {
+	__shared__ unsigned tot[W][4];
+	__shared__ unsigned long long at[W][4];
+	const int lane = int(threadIdx.x & 63u), w = int(threadIdx.x >> 6);
+	unsigned incl[4];
 #pragma unroll
-	for (int w = 0; w < kWin; w++) {
-		const size_t s = s0 + size_t(w) - 1;  // wraps to a huge value for s0 = 0, w = 0
-		par[w] = ~uint64_t(0);
-		if (s < n && (w > 0 || s0 > 0)) {
-			const uint64_t id = ids[s];
-			if (map_level(m, id) > 0) par[w] = map_parent(m, id);
+	for (int k = 0; k < 4; k++) {
+		incl[k] = c[k];
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const unsigned v = __shfl_up(incl[k], d, 64);
+			if (lane >= d) incl[k] += v;
+		}
+		if (lane == 63) tot[w][k] = incl[k];
+	}
+	__syncthreads();
+	if (threadIdx.x < 4) {
+		const int k = int(threadIdx.x);
+		unsigned run = 0;
+		for (int v = 0; v < W; v++) run += tot[v][k];
+		unsigned long long b = run ? atomicAdd(&cnt[k], static_cast<unsigned long long>(run)) : 0ull;
+		for (int v = 0; v < W; v++) {
+			at[v][k] = b;
+			b += tot[v][k];
 		}
 	}
-	uint8_t what[kRun];  // bit 0 refine, 1 partial run head, 2 kept family head, 3 unrefine family head
-	uint8_t runk[kRun];
+	__syncthreads();
+#pragma unroll
+	for (int k = 0; k < 4; k++) out[k] = at[w][k] + (incl[k] - c[k]);
+}
+
+// solo: every cell of the grid is local and the slots are in Morton order, so
+// a family's leaves are one run and a partial run (k < 8) always has a
+// sibling with children - no lookups needed to know it.
+template <int BS>
+__global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restrict__ ids,
+                                                               const uint8_t* __restrict__ band, size_t n, bool solo,
+                                                               uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
+                                                               uint32_t* __restrict__ part,
+                                                               unsigned long long* __restrict__ cnt) {
+	constexpr int kJ = 8;
+	const int lane = int(threadIdx.x & 63u);
+	const size_t wave = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+	const size_t base = wave * 64 * kJ;
+	uint64_t par[kJ + 1];
+	uint32_t bnd[kJ + 1];
+	// every load issued before the parents are computed (id 0 = none)
+#pragma unroll
+	for (int j = 0; j <= kJ; j++) {
+		const size_t sj = base + 64 * size_t(j) + size_t(lane);
+		par[j] = sj < n ? ids[sj] : 0;
+		bnd[j] = sj < n ? uint32_t(band[sj]) : 0u;
+	}
+	// the parent of the slot before the wave's first one
+	uint64_t before = base > 0 && base - 1 < n ? ids[base - 1] : 0;
+	before = map_level(m, before) > 0 ? map_parent(m, before) : ~uint64_t(0);
+#pragma unroll
+	for (int j = 0; j <= kJ; j++) par[j] = map_level(m, par[j]) > 0 ? map_parent(m, par[j]) : ~uint64_t(0);
+	uint32_t flags = 0;  // per j, 4 bits: 1 refine, 2 partial run head, 4 kept family head, 8 unrefine head
+	uint32_t runk = 0;   // per j, 4 bits: the run length of a partial run head
 	unsigned cr = 0, cp = 0, ck = 0, cu = 0;
 #pragma unroll
-	for (int j = 0; j < kRun; j++) {
-		what[j] = 0;
-		runk[j] = 0;
-		const size_t s = s0 + j;
-		if (s >= n) continue;
-		const uint64_t p = par[j + 1];
+	for (int j = 0; j < kJ; j++) {
+		const size_t sj = base + 64 * size_t(j) + size_t(lane);
+		const uint64_t p = par[j];
+		// the previous slot's parent: lane - 1, or lane 63 of the chunk before
+		const uint64_t prev_in = __shfl(par[j], (lane + 63) & 63, 64);
+		const uint64_t prev_last = j > 0 ? __shfl(par[j - 1], 63, 64) : before;
+		const uint64_t prev = lane > 0 ? prev_in : prev_last;
+		// the next seven slots' parents and bands (every lane takes part)
+		uint64_t nx[7];
+		uint32_t nb[7];
+#pragma unroll
+		for (int q = 1; q <= 7; q++) {
+			const int L = lane + q;
+			const uint64_t a = __shfl(par[j], L & 63, 64), b = __shfl(par[j + 1], L & 63, 64);
+			const uint32_t ba = __shfl(bnd[j], L & 63, 64), bb = __shfl(bnd[j + 1], L & 63, 64);
+			nx[q - 1] = L < 64 ? a : b;
+			nb[q - 1] = L < 64 ? ba : bb;
+		}
+		if (sj >= n) continue;
 		const int lvl = p == ~uint64_t(0) ? 0 : map_level(m, p) + 1;
-		if (band[s] == 2 && lvl < int(m.R)) {
-			what[j] |= 1;
+		uint32_t what = 0;
+		if (bnd[j] == 2 && lvl < int(m.R)) {
+			what |= 1;
 			cr++;
 		}
-		if (lvl == 0) continue;
-		// run head of a family: the first slot of a run of consecutive slots
-		// with one parent
-		if (par[j] == p) continue;
-		uint32_t k = 1;
-		bool keep = band[s] >= 1;
+		if (lvl > 0 && prev != p) {
+			uint32_t k = 1;
+			bool keep = bnd[j] >= 1;
 #pragma unroll
-		for (int q = 1; q < 8; q++) {
-			if (k != uint32_t(q)) break;
-			if (par[j + 1 + q] != p) break;
-			keep = keep || band[s + q] >= 1;
-			k++;
+			for (int q = 1; q < 8; q++) {
+				if (k != uint32_t(q)) break;
+				if (nx[q - 1] != p) break;
+				keep = keep || nb[q - 1] >= 1;
+				k++;
+			}
+			bool whole = !solo;  // every child of p is a leaf (some held elsewhere)
+			if (k < 8 && whole) {
+				uint64_t ch[8];
+				map_all_children(m, p, ch);
+				for (int i = 0; i < 8; i++) whole = whole && dm_owner(M, ch[i]) >= 0;
+			}
+			if (k < 8 && !whole) {
+				// a sibling has children: the family cannot be unrefined in
+				// this round (unrefine_completely refuses, a dont_unrefine mark
+				// changes nothing), so the host never sees it; counted as the
+				// host's decide() would count it
+				if (keep) ck++;
+			} else if (k < 8) {
+				what |= 2;
+				runk |= k << (4 * j);
+				cp++;
+			} else if (keep) {
+				ck++;
+			} else {
+				what |= 8;
+				cu++;
+			}
 		}
-		runk[j] = uint8_t(k);
-		bool whole = true;  // every child of p is a leaf (some of them held elsewhere)
-		if (k < 8) {
-			uint64_t ch[8];
-			map_all_children(m, p, ch);
-			for (int i = 0; i < 8; i++) whole = whole && dm_owner(M, ch[i]) >= 0;
-		}
-		if (k < 8 && !whole) {
-			// a sibling has children: the family cannot be unrefined in this
-			// round (unrefine_completely refuses, a dont_unrefine mark changes
-			// nothing), so the host never sees it; counted as the host's
-			// decide() would count it
-			if (keep) ck++;
-		} else if (k < 8) {
-			what[j] |= 2;
-			cp++;
-		} else if (keep) {
-			what[j] |= 4;
-			ck++;
-		} else {
-			what[j] |= 8;
-			cu++;
-		}
+		flags |= what << (4 * j);
 	}
-	unsigned long long ar = wave_reserve(&cnt[0], cr), ap = wave_reserve(&cnt[3], cp), au = wave_reserve(&cnt[1], cu);
-	(void)wave_reserve(&cnt[2], ck);
-	for (int j = 0; j < kRun; j++) {
-		const size_t s = s0 + j;
-		if (what[j] & 1) ref[ar++] = ids[s];
-		if (what[j] & 2) part[ap++] = uint32_t(s) | (uint32_t(runk[j]) << 28);
-		if (what[j] & 8) unref[au++] = ids[s];
+	const unsigned c[4] = {cr, cu, ck, cp};
+	unsigned long long b[4];
+	block_reserve4<BS / 64>(cnt, c, b);
+	unsigned long long ar = b[0], au = b[1], ap = b[3];
+#pragma unroll
+	for (int j = 0; j < kJ; j++) {
+		const uint32_t what = (flags >> (4 * j)) & 15u;
+		if (!what) continue;
+		const size_t sj = base + 64 * size_t(j) + size_t(lane);
+		if (what & 1) ref[ar++] = ids[sj];
+		if (what & 2) part[ap++] = uint32_t(sj) | (((runk >> (4 * j)) & 15u) << 28);
+		if (what & 8) unref[au++] = ids[sj];
 	}
 }
 
@@ -1725,7 +1795,7 @@ static void k_gather_ids_bands(const uint64_t* ids, const uint8_t* band, const u
 }
 
 AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
-                           hipStream_t s) {
+                           bool solo, hipStream_t s) {
 	AdvRequests out;
 	if (!n) return out;
 	DX_REQUIRE(n < (size_t(1) << 28), "too many local cells for the request runs");
@@ -1737,8 +1807,8 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	part.alloc(n);
 	cnt.alloc(4);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
-	adv_requests_kernel<<<unsigned((n + 256 * 8 - 1) / (256 * 8)), 256, 0, s>>>(m, dm, slot_ids, band, n, ref.p,
-	                                                                        unref.p, part.p, cnt.p);
+	adv_requests_kernel<1024><<<unsigned((n + 1024 * 8 - 1) / (1024 * 8)), 1024, 0, s>>>(m, dm, slot_ids, band, n, solo,
+	                                                                                    ref.p, unref.p, part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	d2h_small(h, cnt.p, sizeof(h), s);

@@ -524,20 +524,33 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 			if (morton) {
 				const int sh = 3 * (m.R - lvl);
 				const uint64_t len = uint64_t(1) << (m.R - lvl);
-				const int64_t key = int64_t(morton3(c) >> sh);
+				const uint64_t key = morton3(c) >> sh;
 				const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
+				// the neighbor's id and Morton key from this cell's: one step
+				// along d is +-stride[d] in the id and a dilated +-1 in the key
+				// (no re-interleave, no index -> id products); a periodic wrap
+				// takes the general form
+				const uint64_t lx = m.len[0] << lvl, ly = m.len[1] << lvl;
+				const uint64_t stride[3] = {1, lx, lx * ly};
 #pragma unroll
 				for (int dir = 0; dir < 6; dir++) {
+					const int d = dir >> 1;
 					uint64_t p[3];
 					h[dir] = -1;
 					want[dir] = ~uint64_t(0);
 					probe[dir] = face_probe(m, c, lvl, dir, p);
 					if (!probe[dir]) continue;
-					for (int d = 0; d < 3; d++) p[d] &= ~(len - 1);
-					const int64_t q = int64_t(r) + (int64_t(morton3(p) >> sh) - key);
+					p[d] &= ~(len - 1);  // the other two are c's, aligned
+					const uint64_t M = uint64_t(0x1249249249249249ull) << d, u = uint64_t(1) << d;
+					uint64_t nkey;
+					if ((dir & 1) ? p[d] == c[d] + len : p[d] + len == c[d])
+						nkey = (dir & 1) ? ((((key | ~M) + u) & M) | (key & ~M)) : ((((key & M) - u) & M) | (key & ~M));
+					else
+						nkey = morton3(p) >> sh;
+					const int64_t q = int64_t(r) + (int64_t(nkey) - int64_t(key));
 					if (q >= lo && q < hi) {
 						h[dir] = int32_t(q);
-						want[dir] = map_from_indices(m, p[0], p[1], p[2], lvl);
+						want[dir] = id + ((p[d] >> (m.R - lvl)) - (c[d] >> (m.R - lvl))) * stride[d];
 					}
 				}
 #pragma unroll

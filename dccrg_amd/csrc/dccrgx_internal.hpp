@@ -389,13 +389,12 @@ struct Mesh {
 	uint32_t shift = 63;
 	// the range map instead of `tab` (dccrgx_mesh.hpp DevMesh::rmap)
 	DBuf<int2> rmap;
-	DBuf<RangeLevel> rl;
+	RangeLevel rl[kRangeLevels] = {};
 	int rlev = 0;
 	// the grid's persistent full-level map (Grid::rmap_full) instead of an
 	// owned one: not freed with the mesh, cleared entry by entry by the next
 	// rebuild
 	const int2* rmap_shared = nullptr;
-	const RangeLevel* rl_shared = nullptr;
 	BlockPart bp;
 	DevMesh dev(uint64_t last) const {
 		DevMesh d{};
@@ -406,8 +405,8 @@ struct Mesh {
 		d.bp = bp;
 		d.last = last;
 		d.rmap = rmap_shared ? rmap_shared : rmap.p;
-		d.rl = rmap_shared ? rl_shared : rl.p;
 		d.rlev = d.rmap ? rlev : 0;
+		for (int L = 0; L < d.rlev; L++) d.rl[L] = rl[L];
 		return d;
 	}
 };
@@ -526,7 +525,6 @@ struct Grid {
 	// rebuilds: each rebuild clears the previous mesh's entries and writes its
 	// own instead of clearing the whole map
 	DBuf<int2> rmap_full;
-	DBuf<RangeLevel> rl_full;
 	bool rmap_full_clean = true;  // every entry {-1, -1}
 	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev
 	DBuf<double> dt_part;  // block minima of dccrgx_advection_max_time_step_device

@@ -82,7 +82,9 @@ struct DevMesh {
 	BlockPart bp;
 	uint64_t last;
 	const int2* rmap;       // non-null: the range map replaces the table
-	const RangeLevel* rl;   // rlev ranges (device memory: a DevMesh stays small)
+	// the rlev ranges, by value: a kernel reads them at lane-uniform indices
+	// from its arguments (scalar loads, no dependent global load per probe)
+	RangeLevel rl[kRangeLevels];
 	int rlev;
 };
 
@@ -91,7 +93,9 @@ DX_HD uint64_t hash_home(uint64_t id, uint32_t shift) { return (id * kHashMul) >
 #if defined(__HIPCC__)
 // index of `id` in the range map, -1 outside its ranges
 __device__ __forceinline__ int64_t dm_range_index(const DevMesh& M, uint64_t id) {
-	for (int L = 0; L < M.rlev; L++) {
+#pragma unroll
+	for (int L = 0; L < kRangeLevels; L++) {
+		if (L >= M.rlev) break;
 		const RangeLevel q = M.rl[L];
 		if (id >= q.lo && id < q.hi) return int64_t(q.off + (id - q.lo));
 	}

@@ -90,7 +90,6 @@ void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32
 	const bool allowed = !(env && env[0] == '0');
 	uint64_t lo[kRangeLevels], hi[kRangeLevels];
 	M.rmap.release();
-	M.rl.release();
 	M.rlev = 0;
 	if (allowed && n && k_level_ranges(m, ids, n, lo, hi, s)) {
 		uint64_t total = 0;
@@ -102,7 +101,7 @@ void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32
 		}
 		if (total <= 32 * uint64_t(n) + (uint64_t(1) << 24) && total < (uint64_t(1) << 31)) {
 			M.rlev = int(rl.size());
-			upload(M.rl, rl, s);
+			for (int L = 0; L < M.rlev; L++) M.rl[L] = rl[size_t(L)];
 			M.rmap.alloc(size_t(total));
 			HIP_CHECK(hipMemsetAsync(M.rmap.p, 0xff, size_t(total) * sizeof(int2), s));
 			M.tab.release();
@@ -126,16 +125,13 @@ static bool mesh_build_range_full(Grid& g, Mesh& M, const Mesh& old, size_t slot
 	const uint64_t total = m.last;  // ids 1..last, entry id - 1
 	if (total > 32 * uint64_t(M.n_known) + (uint64_t(1) << 24) || total >= (uint64_t(1) << 31)) return false;
 	if (!g.rmap_full.p || g.rmap_full.n != size_t(total)) {
-		std::vector<RangeLevel> rl;
-		for (int L = 0; L <= m.R; L++) rl.push_back(RangeLevel{m.first[L], m.first[L + 1], m.first[L] - 1});
-		upload(g.rl_full, rl, s);
 		g.rmap_full.alloc(size_t(total));
 		g.rmap_full_clean = false;
 	}
 	Mesh probe;
 	probe.rmap_shared = g.rmap_full.p;
-	probe.rl_shared = g.rl_full.p;
 	probe.rlev = m.R + 1;
+	for (int L = 0; L <= m.R; L++) probe.rl[L] = RangeLevel{m.first[L], m.first[L + 1], m.first[L] - 1};
 	const DevMesh pd = probe.dev(m.last);
 	if (old.rmap_shared == g.rmap_full.p && old.kid.p && old.n_known) {
 		k_range_clear(g.rmap_full.p, pd, old.kid.p, old.n_known, s);  // the entries the previous mesh wrote
@@ -145,11 +141,10 @@ static bool mesh_build_range_full(Grid& g, Mesh& M, const Mesh& old, size_t slot
 	g.rmap_full_clean = false;
 	M.tab.release();
 	M.rmap.release();
-	M.rl.release();
 	M.mask = 0;
 	M.rmap_shared = g.rmap_full.p;
-	M.rl_shared = g.rl_full.p;
 	M.rlev = m.R + 1;
+	for (int L = 0; L <= m.R; L++) M.rl[L] = probe.rl[L];
 	k_range_insert(g.rmap_full.p, pd, M.kid.p, M.kown.p, M.n_known, slot_upto, s);
 	return true;
 }
@@ -311,9 +306,7 @@ void rebuild(Grid& g, Mesh& nm) {
 	Mesh& M = g.mesh;
 	M.tab.release();
 	M.rmap.release();
-	M.rl.release();
 	M.rmap_shared = nullptr;
-	M.rl_shared = nullptr;
 
 	// slot order: Morton order of the min corner on refined grids (step 2)
 	int order = g.slot_order;

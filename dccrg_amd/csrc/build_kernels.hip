@@ -1266,7 +1266,6 @@ void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	temp.alloc(b1);
 	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, end_bit, s));
 	HIP_CHECK(hipMemcpyAsync(keys, tmp.p, n * 8, hipMemcpyDeviceToDevice, s));
-	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
@@ -1469,7 +1468,7 @@ std::vector<uint64_t> k_ghost_level0(const MapCtx& m, const DevMesh& M, int rank
 			cap = k;
 			continue;
 		}
-		const size_t u = sort_unique_u64(out.p, k, s);
+		const size_t u = sort_unique_u64(out.p, k, s, map_id_bits(m));
 		return download(out.p, u, s);
 	}
 }
@@ -1485,7 +1484,7 @@ std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size
 	cells_under_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, local, n, dl0.p, l0.size(), out.p, ctr.p);
 	HIP_CHECK(hipGetLastError());
 	const size_t k = read_counter(ctr, s);
-	sort_u64(out.p, k, s);
+	sort_u64(out.p, k, s, map_id_bits(m));
 	return download(out.p, k, s);
 }
 
@@ -1509,7 +1508,7 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 			cap = k;
 			continue;
 		}
-		const size_t u = sort_unique_u64(out.p, k, s);
+		const size_t u = sort_unique_u64(out.p, k, s, map_id_bits(m));
 		return download(out.p, u, s);
 	}
 }
@@ -1622,7 +1621,7 @@ size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std
 	created_children_kernel<<<unsigned((S.size() + 255) / 256), 256, 0, s>>>(m, M, rank, dS.p, S.size(), out.p, ctr.p);
 	HIP_CHECK(hipGetLastError());
 	const size_t n = read_counter(ctr, s);
-	sort_u64(out.p, n, s);
+	sort_u64(out.p, n, s, map_id_bits(m));
 	return n;
 }
 
@@ -1650,10 +1649,10 @@ size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::v
 	const size_t n = read_counter(ctr, s);
 	if (n) {
 		size_t bytes = 0;
-		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, map_id_bits(m), s));
 		DBuf<uint8_t> temp;
 		temp.alloc(bytes + 1);
-		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, 64, s));
+		HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, k1.p, k2.p, v1.p, slots.p, n, 0, map_id_bits(m), s));
 		ids.swap(k2);
 	}
 	return n;

@@ -67,6 +67,14 @@ DX_HD int map_level(const MapCtx& m, uint64_t cell) {
 	return l;
 }
 
+// bits of the largest cell id: every id is < 2^map_id_bits (radix sorts of
+// ids take only these bits)
+DX_HD int map_id_bits(const MapCtx& m) {
+	int b = 1;
+	while (b < 64 && (m.last >> b) != 0) b++;
+	return b;
+}
+
 // m.first[l] (0 <= l <= R + 1) by lane-uniform reads (see map_level)
 DX_HD uint64_t map_first(const MapCtx& m, int l) {
 	uint64_t f = m.first[0];

@@ -1761,7 +1761,7 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, Laz
 	par.alloc(n);
 	removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p);
 	HIP_CHECK(hipGetLastError());
-	const size_t np = sort_unique_u64(par.p, n, s);
+	const size_t np = sort_unique_u64(par.p, n, s, map_id_bits(m));
 	DX_REQUIRE(np * 8 == n, "a merged family's removed children are incomplete");
 	DBuf<int32_t> cidx, pslot;
 	DBuf<int> err;
@@ -1814,8 +1814,8 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	d2h_small(h, cnt.p, sizeof(h), s);
 	// ascending ids (the lists the host merges and stop_refining sorts), sorted
 	// here before they leave the device
-	sort_u64(ref.p, size_t(h[0]), s);
-	sort_u64(unref.p, size_t(h[1]), s);
+	sort_u64(ref.p, size_t(h[0]), s, map_id_bits(m));
+	sort_u64(unref.p, size_t(h[1]), s, map_id_bits(m));
 	out.refine = download(ref.p, size_t(h[0]), s);
 	out.unrefine = download(unref.p, size_t(h[1]), s);
 	out.kept = size_t(h[2]);

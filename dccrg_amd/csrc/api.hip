@@ -119,7 +119,7 @@ static int po_field(Grid& g, const char* name, size_t elem) {
 	g.fields.push_back(std::move(f));
 	Field& nf = g.fields.back();
 	nf.data.alloc(g.n_slots * elem);
-	if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+	if (nf.data.n) HIP_CHECK(hipMemsetAsync(nf.data.p, 0, nf.data.n, g.s_comp));
 	return int(g.fields.size() - 1);
 }
 
@@ -579,12 +579,18 @@ static void continue_load_impl(Grid& g, int fid, const uint64_t* sizes) {
 		var_sizes(f, nullptr, 0, g.n_slots, all.p, g.s_comp);
 		if (nl) h2d(all.p, bytes.data(), nl * 8, g.s_comp);
 		var_resize(f, g.n_slots, all.p, g.s_comp);
-		if (at[nl]) HIP_CHECK(hipMemcpy(f.data.p, got.data(), got.size(), hipMemcpyHostToDevice));
+		if (at[nl]) {
+			HIP_CHECK(hipMemcpyAsync(f.data.p, got.data(), got.size(), hipMemcpyHostToDevice, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		}
 	} else if (nl && f.win_len) {
 		// the window of every element; the rest of it keeps its bytes
 		std::vector<uint8_t> h = download(f.data.p, nl * f.elem, g.s_comp);
 		for (size_t s = 0; s < nl; s++) std::memcpy(&h[s * f.elem + f.win_off], &got[at[s]], f.win_len);
-		HIP_CHECK(hipMemcpy(f.data.p, h.data(), h.size(), hipMemcpyHostToDevice));
+		{
+			HIP_CHECK(hipMemcpyAsync(f.data.p, h.data(), h.size(), hipMemcpyHostToDevice, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		}
 	}
 	for (size_t s = 0; s < nl; s++) g.load.pos[s] += bytes[s];
 }
@@ -818,8 +824,8 @@ int dccrgx_download_user_csr(dccrgx_grid* gp, int hood, int kind, uint32_t* ptr,
 		if (tot > cap) return DCCRGX_ERANGE;
 		std::memcpy(ptr, hp.data(), (nl + 1) * 4);
 		if (!tot) return 0;
-		HIP_CHECK(hipMemcpy(ids, kind == 0 ? h.nof_id.p : h.nto_id.p, tot * 8, hipMemcpyDeviceToHost));
-		if (offs && kind == 0) HIP_CHECK(hipMemcpy(offs, h.nof_off.p, tot * 12, hipMemcpyDeviceToHost));
+		d2h_small(ids, kind == 0 ? h.nof_id.p : h.nto_id.p, tot * 8, g.s_comp);
+		if (offs && kind == 0) d2h_small(offs, h.nof_off.p, tot * 12, g.s_comp);
 		return 0;
 	});
 }
@@ -1092,13 +1098,13 @@ int dccrgx_get_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, int32
 		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
 		ensure_csr(g);
 		uint32_t be[2];
-		HIP_CHECK(hipMemcpy(be, g.nof_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		d2h_small(be, g.nof_ptr.p + s, 8, g.s_comp);
 		const size_t k = be[1] - be[0];
 		if (n) *n = k;
 		if (k > cap) return DCCRGX_ERANGE;
 		if (k) {
-			HIP_CHECK(hipMemcpy(ids, g.nof_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
-			if (offs) HIP_CHECK(hipMemcpy(offs, g.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+			d2h_small(ids, g.nof_id.p + be[0], k * 8, g.s_comp);
+			if (offs) d2h_small(offs, g.nof_off.p + 3 * size_t(be[0]), k * 12, g.s_comp);
 		}
 		return 0;
 	});
@@ -1111,11 +1117,11 @@ int dccrgx_get_neighbors_to(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, size_
 		if (s < 0 || size_t(s) >= g.n_local) return DCCRGX_ENOTFOUND;
 		ensure_csr(g);
 		uint32_t be[2];
-		HIP_CHECK(hipMemcpy(be, g.nto_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		d2h_small(be, g.nto_ptr.p + s, 8, g.s_comp);
 		const size_t k = be[1] - be[0];
 		if (n) *n = k;
 		if (k > cap) return DCCRGX_ERANGE;
-		if (k) HIP_CHECK(hipMemcpy(ids, g.nto_id.p + be[0], k * 8, hipMemcpyDeviceToHost));
+		if (k) d2h_small(ids, g.nto_id.p + be[0], k * 8, g.s_comp);
 		return 0;
 	});
 }
@@ -1166,12 +1172,12 @@ int dccrgx_get_face_neighbors_of(dccrgx_grid* gp, uint64_t cell, uint64_t* ids, 
 		}
 		ensure_face_csr(g);
 		uint32_t be[2];
-		HIP_CHECK(hipMemcpy(be, g.face_ptr.p + s, 8, hipMemcpyDeviceToHost));
+		d2h_small(be, g.face_ptr.p + s, 8, g.s_comp);
 		const size_t k = be[1] - be[0];
 		if (n) *n = k;
 		if (k > cap) return DCCRGX_ERANGE;
 		std::vector<int32_t> ent(k);
-		if (k) HIP_CHECK(hipMemcpy(ent.data(), g.face_ent.p + be[0], k * 4, hipMemcpyDeviceToHost));
+		if (k) d2h_small(ent.data(), g.face_ent.p + be[0], k * 4, g.s_comp);
 		const auto& sid = slot_ids_host(g);
 		for (size_t i = 0; i < k; i++) {
 			ids[i] = sid[size_t(ent[i] >> 3)];
@@ -1203,10 +1209,10 @@ int dccrgx_download_csr(dccrgx_grid* gp, int kind, uint32_t* ptr, uint64_t* ids,
 		if (!tot) return 0;
 		const auto& sid = slot_ids_host(g);
 		if (kind == 0) {
-			HIP_CHECK(hipMemcpy(ids, g.nof_id.p, tot * 8, hipMemcpyDeviceToHost));
-			if (aux) HIP_CHECK(hipMemcpy(aux, g.nof_off.p, tot * 12, hipMemcpyDeviceToHost));
+			d2h_small(ids, g.nof_id.p, tot * 8, g.s_comp);
+			if (aux) d2h_small(aux, g.nof_off.p, tot * 12, g.s_comp);
 		} else if (kind == 1) {
-			HIP_CHECK(hipMemcpy(ids, g.nto_id.p, tot * 8, hipMemcpyDeviceToHost));
+			d2h_small(ids, g.nto_id.p, tot * 8, g.s_comp);
 		} else if (kind == 2) {
 			std::vector<int32_t> ent = download(g.face_ent.p, tot, g.s_comp);
 			static const int dmap[6] = {-1, +1, -2, +2, -3, +3};
@@ -1217,7 +1223,7 @@ int dccrgx_download_csr(dccrgx_grid* gp, int kind, uint32_t* ptr, uint64_t* ids,
 		} else {
 			std::vector<int32_t> sl = download(g.it_slot.p, tot, g.s_comp);
 			for (size_t i = 0; i < tot; i++) ids[i] = sid[size_t(sl[i])];
-			if (aux) HIP_CHECK(hipMemcpy(aux, g.it_off.p, tot * 12, hipMemcpyDeviceToHost));
+			if (aux) d2h_small(aux, g.it_off.p, tot * 12, g.s_comp);
 		}
 		return 0;
 	});
@@ -1552,7 +1558,7 @@ int dccrgx_removed_field_download(dccrgx_grid* gp, int fid, void* host, size_t c
 		Field& f = fixed_field(g, fid);
 		const size_t bytes = g.removed_ids.size() * f.elem;
 		DX_REQUIRE(cap_bytes >= bytes, "buffer too small for the removed cells' payloads");
-		if (bytes) HIP_CHECK(hipMemcpy(host, f.removed.p, bytes, hipMemcpyDeviceToHost));
+		if (bytes) d2h_small(host, f.removed.p, bytes, g.s_comp);
 		return 0;
 	});
 }
@@ -1676,14 +1682,14 @@ int dccrgx_get_user_neighbors(dccrgx_grid* gp, int id, uint64_t cell, int kind, 
 		UserHood& h = ensure_uhood(g, id);
 		const DBuf<uint32_t>& ptr = kind == 0 ? h.nof_ptr : h.nto_ptr;
 		uint32_t be[2];
-		HIP_CHECK(hipMemcpy(be, ptr.p + s, 8, hipMemcpyDeviceToHost));
+		d2h_small(be, ptr.p + s, 8, g.s_comp);
 		const size_t k = be[1] - be[0];
 		if (n) *n = k;
 		if (k > cap) return DCCRGX_ERANGE;
 		if (k) {
-			HIP_CHECK(hipMemcpy(ids, (kind == 0 ? h.nof_id.p : h.nto_id.p) + be[0], k * 8, hipMemcpyDeviceToHost));
+			d2h_small(ids, (kind == 0 ? h.nof_id.p : h.nto_id.p) + be[0], k * 8, g.s_comp);
 			if (offs && kind == 0)
-				HIP_CHECK(hipMemcpy(offs, h.nof_off.p + 3 * size_t(be[0]), k * 12, hipMemcpyDeviceToHost));
+				d2h_small(offs, h.nof_off.p + 3 * size_t(be[0]), k * 12, g.s_comp);
 		}
 		return 0;
 	});
@@ -1949,7 +1955,7 @@ int dccrgx_add_field(dccrgx_grid* gp, const char* name, size_t elem, int transfe
 		Field& nf = g.fields.back();
 		if (g.initialized) {
 			nf.data.alloc(g.n_slots * elem);
-			if (nf.data.n) HIP_CHECK(hipMemset(nf.data.p, 0, nf.data.n));
+			if (nf.data.n) HIP_CHECK(hipMemsetAsync(nf.data.p, 0, nf.data.n, g.s_comp));
 		}
 		*fid = int(g.fields.size() - 1);
 		return 0;
@@ -2013,7 +2019,10 @@ int dccrgx_variable_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t 
 		HIP_CHECK(hipMemcpyAsync(&a, f.voff.p + slot0, 8, hipMemcpyDeviceToHost, g.s_comp));
 		d2h_small(&b, f.voff.p + slot0 + n, 8, g.s_comp);
 		DX_REQUIRE(nbytes == b - a, "byte count differs from the cells' sizes (resize them first)");
-		if (nbytes) HIP_CHECK(hipMemcpy(f.data.p + a, bytes, nbytes, hipMemcpyHostToDevice));
+		if (nbytes) {
+			HIP_CHECK(hipMemcpyAsync(f.data.p + a, bytes, nbytes, hipMemcpyHostToDevice, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		}
 		return 0;
 	});
 }
@@ -2028,7 +2037,7 @@ int dccrgx_variable_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_
 		d2h_small(&b, f.voff.p + slot0 + n, 8, g.s_comp);
 		if (nbytes) *nbytes = size_t(b - a);
 		if (b - a > cap) return DCCRGX_ERANGE;
-		if (b > a) HIP_CHECK(hipMemcpy(bytes, f.data.p + a, b - a, hipMemcpyDeviceToHost));
+		if (b > a) d2h_small(bytes, f.data.p + a, b - a, g.s_comp);
 		return 0;
 	});
 }
@@ -2059,7 +2068,7 @@ int dccrgx_removed_variable_field_download(dccrgx_grid* gp, int fid, uint64_t* s
 		if (sizes)
 			for (size_t i = 0; i < n; i++) sizes[i] = o[i + 1] - o[i];
 		if (o[n] > cap) return DCCRGX_ERANGE;
-		if (o[n] && bytes) HIP_CHECK(hipMemcpy(bytes, f.removed.p, o[n], hipMemcpyDeviceToHost));
+		if (o[n] && bytes) d2h_small(bytes, f.removed.p, o[n], g.s_comp);
 		return 0;
 	});
 }
@@ -2135,7 +2144,10 @@ int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const 
 		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
-		if (n) HIP_CHECK(hipMemcpy(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice));
+		if (n) {
+			HIP_CHECK(hipMemcpyAsync(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice, g.s_comp));
+			HIP_CHECK(hipStreamSynchronize(g.s_comp));
+		}
 		return 0;
 	});
 }
@@ -2146,7 +2158,7 @@ int dccrgx_field_download(dccrgx_grid* gp, int fid, size_t slot0, size_t n, void
 		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
-		if (n) HIP_CHECK(hipMemcpy(host, f.data.p + slot0 * f.elem, n * f.elem, hipMemcpyDeviceToHost));
+		if (n) d2h_small(host, f.data.p + slot0 * f.elem, n * f.elem, g.s_comp);
 		return 0;
 	});
 }
@@ -2385,7 +2397,7 @@ int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[10]) {
 		ensure_tiles(g);
 		const uint64_t nt = g.n_tiles_inner + g.n_tiles_outer;
 		uint32_t entries = 0;
-		HIP_CHECK(hipMemcpy(&entries, g.face_ptr.p + g.n_local, 4, hipMemcpyDeviceToHost));
+		d2h_small(&entries, g.face_ptr.p + g.n_local, 4, g.s_comp);
 		const uint64_t n = g.n_local;
 		out[0] = uint64_t(g.tile);
 		out[1] = nt;
@@ -2447,7 +2459,10 @@ int dccrgx_advection_initialize(dccrgx_grid* gp, const int fids[7]) {
 		for (int k = 0; k < 7; k++) {
 			Field& F = field(g, fids[k]);
 			DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
-			if (n) HIP_CHECK(hipMemcpy(F.data.p, a[k].data(), n * 8, hipMemcpyHostToDevice));
+			if (n) {
+				HIP_CHECK(hipMemcpyAsync(F.data.p, a[k].data(), n * 8, hipMemcpyHostToDevice, g.s_comp));
+				HIP_CHECK(hipStreamSynchronize(g.s_comp));
+			}
 		}
 		return 0;
 	});

@@ -372,9 +372,11 @@ size_t halo_pack_peer(Grid& g, int hood, int peer, uint8_t* buf, size_t cap) {
 	size_t o = 0;
 	for (size_t k = 0; k < tf.size(); k++) {
 		const size_t b = ns * tf[k]->win_len;
-		if (b) HIP_CHECK(hipMemcpy(buf + o, H.sendbuf.p + L.sfo[k] + so * tf[k]->win_len, b, hipMemcpyDefault));
+		if (b)
+			HIP_CHECK(hipMemcpyAsync(buf + o, H.sendbuf.p + L.sfo[k] + so * tf[k]->win_len, b, hipMemcpyDefault, g.s_comp));
 		o += b;
 	}
+	HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	return o;
 }
 
@@ -389,7 +391,8 @@ void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t byt
 	size_t o = 0;
 	for (size_t k = 0; k < tf.size(); k++) {
 		const size_t b = nr * tf[k]->win_len;
-		if (b) HIP_CHECK(hipMemcpy(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, buf + o, b, hipMemcpyDefault));
+		if (b)
+			HIP_CHECK(hipMemcpyAsync(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, buf + o, b, hipMemcpyDefault, g.s_comp));
 		k_place(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, tf[k]->elem, tf[k]->win_off, tf[k]->win_len,
 		        H.recv_slots.p + ro, nr, tf[k]->data.p, g.s_comp);
 		o += b;
@@ -975,7 +978,10 @@ void migration_pack_peer(Grid& g, int peer, uint8_t* buf, size_t cap) {
 	size_t sb, rb;
 	migration_message_size(g, peer, sb, rb);
 	DX_REQUIRE(cap >= sb, "buffer too small for the migration message");
-	if (sb) HIP_CHECK(hipMemcpy(buf, M.sendbuf.p + off_of(M.out_off, peer), sb, hipMemcpyDefault));
+	if (sb) {
+		HIP_CHECK(hipMemcpyAsync(buf, M.sendbuf.p + off_of(M.out_off, peer), sb, hipMemcpyDefault, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	}
 }
 
 void migration_place_peer(Grid& g, int peer, const uint8_t* buf, size_t bytes) {
@@ -983,7 +989,10 @@ void migration_place_peer(Grid& g, int peer, const uint8_t* buf, size_t bytes) {
 	size_t sb, rb;
 	migration_message_size(g, peer, sb, rb);
 	DX_REQUIRE(bytes == rb, "migration message has the wrong size");
-	if (rb) HIP_CHECK(hipMemcpy(M.recvbuf.p + off_of(M.in_off, peer), buf, rb, hipMemcpyDefault));
+	if (rb) {
+		HIP_CHECK(hipMemcpyAsync(M.recvbuf.p + off_of(M.in_off, peer), buf, rb, hipMemcpyDefault, g.s_comp));
+		HIP_CHECK(hipStreamSynchronize(g.s_comp));
+	}
 	M.transferred = true;
 }
 

@@ -1266,9 +1266,10 @@ void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	temp.alloc(b1);
 	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, end_bit, s));
 	HIP_CHECK(hipMemcpyAsync(keys, tmp.p, n * 8, hipMemcpyDeviceToDevice, s));
-	// kept: without it the three-process Poisson 1-D transport test missed its
-	// tolerance once (r05f; cause not identified - the callers found all stay
-	// on this stream or read back through it), and passed with it (r05ak)
+	// kept: the three-process Poisson 1-D transport test missed its tolerance
+	// once while this sync was out (r05f); the likelier cause, null-stream
+	// memsets racing the compute stream, was fixed later (DESIGN.md section 6,
+	// "Stream order"), and the sync stays as the cheap side of the doubt
 	HIP_CHECK(hipStreamSynchronize(s));
 }
 

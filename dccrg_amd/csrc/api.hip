@@ -1425,6 +1425,8 @@ int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* n
 }
 
 static void flush_bulk_requests(Grid& g) {
+	g.refine_dev_valid = false;
+	g.refine_dev.release();
 	g.refine_requests.insert(g.refine_bulk.begin(), g.refine_bulk.end());
 	g.unrefine_requests.insert(g.unrefine_bulk.begin(), g.unrefine_bulk.end());
 	g.refine_bulk.clear();
@@ -2586,9 +2588,14 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			// on the device: refine requests, whole-family decisions, partial runs
 			// one process with Morton-ordered slots: each family's leaves are one run
 			const bool solo = g.size == 1 && g.morton_slots;
-			const AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.s_comp);
+			AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.s_comp);
 			// 2434-2520 (bulk lists: no set hashing of ~20 K ids per step)
 			g.refine_bulk.insert(g.refine_bulk.end(), q.refine.begin(), q.refine.end());
+			if (g.refine_requests.empty() && !q.refine.empty()) {
+				// the whole refine request set: its device copy stays for stop_refining
+				g.refine_dev = std::move(q.refine_dev);
+				g.refine_dev_valid = true;
+			}
 			nref = q.refine.size();
 			nkeep = q.kept;
 			g.unrefine_bulk.insert(g.unrefine_bulk.end(), q.unrefine.begin(), q.unrefine.end());

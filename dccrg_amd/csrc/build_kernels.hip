@@ -1495,10 +1495,13 @@ std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size
 
 std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
                                         const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s,
-                                        bool finer) {
+                                        bool finer, const uint64_t* dreq_given) {
 	if (req.empty()) return {};
-	DBuf<uint64_t> dreq;
-	upload(dreq, req, s);
+	DBuf<uint64_t> dreq_own;
+	if (!dreq_given) upload(dreq_own, req, s);
+	struct {
+		const uint64_t* p;
+	} dreq{dreq_given ? dreq_given : dreq_own.p};
 	unsigned long long cap = req.size() * 16 + 1024;
 	for (;;) {
 		DBuf<uint64_t> out;

@@ -507,6 +507,11 @@ struct Grid {
 	// merged into the sets above by flush_bulk_requests() before any call
 	// that consults the sets, and read directly by stop_refining
 	std::vector<uint64_t> refine_bulk, unrefine_bulk;
+	// refine_bulk's device copy when it is exactly one device request list
+	// (check_for_adaptation's, sorted and unique) and nothing else was
+	// requested: stop_refining then skips its uploads of that list
+	DBuf<uint64_t> refine_dev;
+	bool refine_dev_valid = false;
 	// a grid file being loaded in parts (start / continue / finish_loading_
 	// grid_data 1795-2400): per local slot the next unread byte of the cell's
 	// record and the record's end
@@ -768,7 +773,7 @@ std::vector<uint64_t> k_cells_under(const MapCtx& m, const uint64_t* local, size
 // (the dont_refine spread of override_refines 9991-10038)
 std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh,
                                         const DevMesh& M, int rank, const std::vector<uint64_t>& req, hipStream_t s,
-                                        bool finer = false);
+                                        bool finer = false, const uint64_t* dreq_given = nullptr);
 // override_unrefines (9796-9898) on the device: the requested cells'
 // parents (sorted, unique) whose families may merge given the final refine
 // set S (sorted): none of the children refined or marked dont_unrefine (DU,
@@ -847,6 +852,7 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, c
 // length, members' ids and bands) for the host to merge by parent
 struct AdvRequests {
 	std::vector<uint64_t> refine, unrefine;
+	DBuf<uint64_t> refine_dev;  // `refine` on the device (sorted, unique)
 	size_t kept = 0;
 	std::vector<size_t> part_slot;
 	std::vector<uint32_t> part_len;

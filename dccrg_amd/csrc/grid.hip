@@ -439,13 +439,15 @@ static bool sorted_contains(const std::vector<uint64_t>& v, uint64_t x) {
 
 // closure of a sorted set under a rule every rank evaluates for its own
 // cells in `fresh`, the new cells all-gathered each round (the loops of
-// induce_refines 9591-9720 and of override_refines 9991-10038)
-static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
+// induce_refines 9591-9720 and of override_refines 9991-10038).  dS: S on
+// the device (the first round reads it there); returns whether S grew
+static bool close_set(Grid& g, std::vector<uint64_t>& S, bool finer, const uint64_t* dS = nullptr) {
 	const int nh = int(g.hood.size() / 3);
 	std::vector<uint64_t> fresh = S;
+	bool grew = false;
 	while (true) {
-		const std::vector<uint64_t> found =
-		    k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp, finer);
+		const std::vector<uint64_t> found = k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh,
+		                                                      g.s_comp, finer, grew ? nullptr : dS);
 		std::vector<uint64_t> mine_new;
 		std::set_difference(found.begin(), found.end(), S.begin(), S.end(), std::back_inserter(mine_new));
 		const std::vector<uint64_t> all = gather_union(g, std::move(mine_new));
@@ -455,7 +457,9 @@ static void close_set(Grid& g, std::vector<uint64_t>& S, bool finer) {
 		std::vector<uint64_t> merged;
 		std::merge(S.begin(), S.end(), fresh.begin(), fresh.end(), std::back_inserter(merged));
 		S.swap(merged);
+		grew = true;
 	}
+	return grew;
 }
 
 // stop_refining (3461-3485) = override_refines, induce_refines,
@@ -497,6 +501,13 @@ void stop_refining_impl(Grid& g) {
 	// (2477-2491) until balance_load (3812)
 	g.dont_refine_cells = std::unordered_set<uint64_t>(D.begin(), D.end());
 	DX_LAP("sr.1_override_refines");
+	// the request set is exactly check_for_adaptation's device list: S starts
+	// as it, on the device as well
+	DBuf<uint64_t> dS;
+	const bool dev_rq = g.refine_dev_valid && g.refine_requests.empty() && D.empty() && g.size == 1;
+	if (dev_rq) dS = std::move(g.refine_dev);
+	g.refine_dev_valid = false;
+	g.refine_dev.release();
 	std::vector<uint64_t> mine;
 	{
 		std::vector<uint64_t> rq = vec(g.refine_requests);
@@ -508,7 +519,8 @@ void stop_refining_impl(Grid& g) {
 	g.refine_requests.clear();
 	g.refine_bulk.clear();
 	std::vector<uint64_t> S = gather_union(g, std::move(mine));
-	if (!S.empty()) close_set(g, S, false);
+	bool s_on_dev = dev_rq && !S.empty();
+	if (!S.empty() && close_set(g, S, false, s_on_dev ? dS.p : nullptr)) s_on_dev = false;
 	DX_LAP("sr.2_induce_refines");
 
 	// unrefines: one family per requested parent, unless one of its children
@@ -522,8 +534,7 @@ void stop_refining_impl(Grid& g) {
 	g.dont_unrefine_cells.clear();
 	DX_LAP("sr.3a_requests");
 	// S is final: one device copy for the passes below
-	DBuf<uint64_t> dS;
-	upload(dS, S, s);
+	if (!s_on_dev) upload(dS, S, s);
 	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p);
 	const std::vector<uint64_t> F = gather_union(g, fmine);
 	DBuf<uint64_t> dF;
@@ -798,6 +809,8 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 	}
 	g.weights.clear();
 	g.refine_bulk.clear();
+	g.refine_dev_valid = false;
+	g.refine_dev.release();
 	g.unrefine_bulk.clear();
 	g.refine_requests.clear();      // cells_to_refine (3808)
 	g.unrefine_requests.clear();    // cells_to_unrefine (3810)

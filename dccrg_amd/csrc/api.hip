@@ -2684,7 +2684,8 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
 		// merged parents (adapter.hpp:260-290): the removed children grouped by
 		// parent on the device, each parent's mean of its eight children
-		k_adv_merge_parents(g.m, g.dm(), g.n_local, g.removed_ids, f[0], (const double*)field(g, fids[0]).removed.p, s);
+		k_adv_merge_parents(g.m, g.dm(), g.n_local, g.removed_ids, f[0], (const double*)field(g, fids[0]).removed.p, s,
+		                    g.merged_dev.p, g.n_merged);
 		DX_LAP("adapt.2_parents");
 		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
 		HIP_CHECK(hipStreamSynchronize(s));

@@ -512,6 +512,10 @@ struct Grid {
 	// requested: stop_refining then skips its uploads of that list
 	DBuf<uint64_t> refine_dev;
 	bool refine_dev_valid = false;
+	// the last stop_refining's merged parents on the device (one process:
+	// every removed cell's parent, sorted), for adapt_grid's parent means
+	DBuf<uint64_t> merged_dev;
+	size_t n_merged = 0;
 	// a grid file being loaded in parts (start / continue / finish_loading_
 	// grid_data 1795-2400): per local slot the next unread byte of the cell's
 	// record and the record's end
@@ -865,8 +869,10 @@ void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const ui
                  double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
                  hipStream_t s);
 // rm: the removed cells (on the device when it holds them, else uploaded)
+// (parents, np: the merged parents on the device, sorted, when known - one
+// process: exactly the removed cells' parents; used when 8 np removed cells)
 void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, LazyIds& rm, double* rho,
-                         const double* removed_rho, hipStream_t s);
+                         const double* removed_rho, hipStream_t s, const uint64_t* parents = nullptr, size_t np = 0);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
                           size_t np, hipStream_t s);
 void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],

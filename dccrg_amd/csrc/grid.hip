@@ -492,6 +492,8 @@ void stop_refining_impl(Grid& g) {
 	}
 	g.removed_ids.clear();
 	g.new_cells.clear();
+	g.merged_dev.release();
+	g.n_merged = 0;
 
 	auto vec = [](const std::unordered_set<uint64_t>& s) { return std::vector<uint64_t>(s.begin(), s.end()); };
 	std::vector<uint64_t> D = gather_union(g, sorted_unique(g, vec(g.dont_refine_cells)));
@@ -748,6 +750,10 @@ void stop_refining_impl(Grid& g) {
 	DX_LAP("sr.6_apply");
 	rebuild(g, nm);
 	DX_LAP("sr.7_rebuild");
+	if (g.size == 1 && !F.empty()) {
+		g.merged_dev = std::move(dF);
+		g.n_merged = F.size();
+	}
 }
 
 // --------------------------------------------------------------------------- load balance

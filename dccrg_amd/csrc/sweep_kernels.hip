@@ -1749,7 +1749,7 @@ void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const ui
 // ids `rm` (store order): parents grouped, their eight children in ascending
 // id, the parents' local slots, then the mean density
 void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, LazyIds& rm, double* rho,
-                         const double* removed_rho, hipStream_t s) {
+                         const double* removed_rho, hipStream_t s, const uint64_t* parents, size_t np_given) {
 	if (rm.empty()) return;
 	const size_t n = rm.size();
 	DBuf<uint64_t> up, par;
@@ -1758,10 +1758,18 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, Laz
 		upload(up, rm.host(s), s);
 		rm_dev = up.p;
 	}
-	par.alloc(n);
-	removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p);
-	HIP_CHECK(hipGetLastError());
-	const size_t np = sort_unique_u64(par.p, n, s, map_id_bits(m));
+	size_t np = np_given;
+	const uint64_t* parp = parents;
+	if (!(parents && np * 8 == n)) {
+		// the parents of the removed cells (the families' parents as
+		// stop_refining merged them, when given: sorted and unique, and
+		// removed_rows / check_rows below still verify every child maps to one)
+		par.alloc(n);
+		removed_parents_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p);
+		HIP_CHECK(hipGetLastError());
+		np = sort_unique_u64(par.p, n, s, map_id_bits(m));
+		parp = par.p;
+	}
 	DX_REQUIRE(np * 8 == n, "a merged family's removed children are incomplete");
 	DBuf<int32_t> cidx, pslot;
 	DBuf<int> err;
@@ -1770,9 +1778,9 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, Laz
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(cidx.p, 0xff, 8 * np * sizeof(int32_t), s));
 	HIP_CHECK(hipMemsetAsync(err.p, 0, sizeof(int), s));
-	removed_rows_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, par.p, np, cidx.p, err.p);
+	removed_rows_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, rm_dev, n, parp, np, cidx.p, err.p);
 	HIP_CHECK(hipGetLastError());
-	k_lookup_slots(par.p, np, dm, pslot.p, err.p, s);  // a missing parent sets err too
+	k_lookup_slots(parp, np, dm, pslot.p, err.p, s);  // a missing parent sets err too
 	check_rows_kernel<<<grid_for(np, 256), 256, 0, s>>>(cidx.p, pslot.p, np, n_local, err.p);
 	HIP_CHECK(hipGetLastError());
 	int h = 0;

@@ -1615,7 +1615,7 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 }
 
 size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS_given) {
+                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS_given, bool sorted) {
 	if (S.empty()) return 0;
 	DBuf<uint64_t> dS_own;
 	if (!dS_given) upload(dS_own, S, s);
@@ -1629,7 +1629,7 @@ size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std
 	created_children_kernel<<<unsigned((S.size() + 255) / 256), 256, 0, s>>>(m, M, rank, dS.p, S.size(), out.p, ctr.p);
 	HIP_CHECK(hipGetLastError());
 	const size_t n = read_counter(ctr, s);
-	sort_u64(out.p, n, s, map_id_bits(m));
+	if (sorted) sort_u64(out.p, n, s, map_id_bits(m));
 	return n;
 }
 

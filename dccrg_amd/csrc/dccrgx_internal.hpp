@@ -189,23 +189,27 @@ struct LazyIds {
 	std::vector<uint64_t> h;
 	size_t n = 0;
 	bool host_valid = true;
+	bool unsorted = false;  // the device list is sorted on the first host read
 	void clear() {
 		d.release();
 		h.clear();
 		n = 0;
 		host_valid = true;
+		unsorted = false;
 	}
 	void set_host(std::vector<uint64_t> v) {
 		d.release();
 		h = std::move(v);
 		n = h.size();
 		host_valid = true;
+		unsorted = false;
 	}
-	void set_device(DBuf<uint64_t>&& buf, size_t count) {
+	void set_device(DBuf<uint64_t>&& buf, size_t count, bool sorted = true) {
 		h.clear();
 		d = std::move(buf);
 		n = count;
 		host_valid = count == 0;
+		unsorted = !sorted && count > 1;
 	}
 	size_t size() const { return n; }
 	bool empty() const { return n == 0; }
@@ -226,8 +230,12 @@ inline std::vector<T> download(const T* d, size_t n, hipStream_t s) {
 	return h;
 }
 
+void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit);  // (declared with its default below)
+
 inline const std::vector<uint64_t>& LazyIds::host(hipStream_t s) {
 	if (!host_valid) {
+		if (unsorted) sort_u64(d.p, n, s, 64);
+		unsorted = false;
 		h = download(d.p, n, s);
 		host_valid = true;
 	}
@@ -527,7 +535,7 @@ struct Grid {
 	std::unordered_set<uint64_t> dont_unrefine_cells;  // dont_unrefine 2679
 	std::unordered_set<uint64_t> dont_refine_cells;    // dont_refine 2744
 	LazyIds removed_ids;  // get_removed_cells 3497 (order of Field::removed)
-	LazyIds new_cells;    // local cells created by the last stop_refining (ascending)
+	LazyIds new_cells;    // local cells created by the last stop_refining (ascending on the host)
 	Migration mig;
 	// the range map over the full id range of every level (one process,
 	// Morton-ordered own leaves: rebuild's "direct" mode), kept across
@@ -792,7 +800,7 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 // the children of the refined cells S owned by `rank`, ascending, into out;
 // returns their count
 size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
-                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS = nullptr);
+                          DBuf<uint64_t>& out, hipStream_t s, const uint64_t* dS = nullptr, bool sorted = true);
 // the children of the merged families F staying on `rank` (owned here, like
 // the family's first child), ascending, into ids with their slots; returns
 // their count

@@ -548,8 +548,9 @@ void stop_refining_impl(Grid& g) {
 	// host only when asked); weights and pins follow (6199-6200, 10239-10251)
 	{
 		DBuf<uint64_t> created;
-		const size_t nc = k_created_children(g.m, g.dm(), g.rank, S, created, s, dS.p);
-		g.new_cells.set_device(std::move(created), nc);
+		// ascending on the first host read (new_cells has no device reader)
+		const size_t nc = k_created_children(g.m, g.dm(), g.rank, S, created, s, dS.p, false);
+		g.new_cells.set_device(std::move(created), nc, false);
 	}
 	if (!g.weights.empty() || !g.pins.empty()) {
 		std::vector<int32_t> own(S.size());

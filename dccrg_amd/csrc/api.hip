@@ -1427,6 +1427,8 @@ int dccrgx_get_number_of_update_cells(dccrgx_grid* gp, uint64_t* ns, uint64_t* n
 static void flush_bulk_requests(Grid& g) {
 	g.refine_dev_valid = false;
 	g.refine_dev.release();
+	g.unrefine_dev_valid = false;
+	g.unrefine_dev.release();
 	g.refine_requests.insert(g.refine_bulk.begin(), g.refine_bulk.end());
 	g.unrefine_requests.insert(g.unrefine_bulk.begin(), g.unrefine_bulk.end());
 	g.refine_bulk.clear();
@@ -2595,6 +2597,10 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 				// the whole refine request set: its device copy stays for stop_refining
 				g.refine_dev = std::move(q.refine_dev);
 				g.refine_dev_valid = true;
+			}
+			if (solo && g.unrefine_requests.empty() && !q.unrefine.empty()) {
+				g.unrefine_dev = std::move(q.unrefine_dev);
+				g.unrefine_dev_valid = true;
 			}
 			nref = q.refine.size();
 			nkeep = q.kept;

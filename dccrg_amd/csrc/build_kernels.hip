@@ -1523,18 +1523,22 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 
 std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
                                           const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
-                                          const std::vector<uint64_t>& DU, hipStream_t s, const uint64_t* dS_given) {
+                                          const std::vector<uint64_t>& DU, hipStream_t s, const uint64_t* dS_given,
+                                          const uint64_t* dreq_heads) {
+	// dreq_heads: req on the device, ascending octant-0 children of level > 0,
+	// so their parents come out ascending and distinct (no sort, no marker)
 	if (req.empty()) return {};
-	DBuf<uint64_t> dr, par, dS, dDU;
-	upload(dr, req, s);
+	DBuf<uint64_t> dr_own, par, dS, dDU;
+	if (!dreq_heads) upload(dr_own, req, s);
+	const uint64_t* drp = dreq_heads ? dreq_heads : dr_own.p;
 	if (!dS_given) upload(dS, S, s);
 	const uint64_t* dSp = dS_given ? dS_given : dS.p;
 	upload(dDU, DU, s);
 	par.alloc(req.size() + 1);
-	request_parents_kernel<<<grid_for(req.size(), 256), 256, 0, s>>>(m, dr.p, req.size(), par.p);
+	request_parents_kernel<<<grid_for(req.size(), 256), 256, 0, s>>>(m, drp, req.size(), par.p);
 	HIP_CHECK(hipGetLastError());
-	size_t n = sort_unique_u64(par.p, req.size(), s);
-	{
+	size_t n = dreq_heads ? req.size() : sort_unique_u64(par.p, req.size(), s);
+	if (!dreq_heads) {
 		// the level-0 requests' marker sorts last
 		uint64_t last = 0;
 		if (n) d2h_small(&last, par.p + n - 1, 8, s);

@@ -520,6 +520,10 @@ struct Grid {
 	// requested: stop_refining then skips its uploads of that list
 	DBuf<uint64_t> refine_dev;
 	bool refine_dev_valid = false;
+	// the same for unrefine_bulk: check_for_adaptation's whole-family heads
+	// on one process (octant-0 children, ascending: their parents ascend too)
+	DBuf<uint64_t> unrefine_dev;
+	bool unrefine_dev_valid = false;
 	// the last stop_refining's merged parents on the device (one process:
 	// every removed cell's parent, sorted), for adapt_grid's parent means
 	DBuf<uint64_t> merged_dev;
@@ -796,7 +800,7 @@ std::vector<uint64_t> k_induced_refines(const MapCtx& m, const int32_t* hood, co
 std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, int nh, const DevMesh& M,
                                           const std::vector<uint64_t>& req, const std::vector<uint64_t>& S,
                                           const std::vector<uint64_t>& DU, hipStream_t s,
-                                          const uint64_t* dS = nullptr);
+                                          const uint64_t* dS = nullptr, const uint64_t* dreq_heads = nullptr);
 // the children of the refined cells S owned by `rank`, ascending, into out;
 // returns their count
 size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,
@@ -865,6 +869,7 @@ size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, c
 struct AdvRequests {
 	std::vector<uint64_t> refine, unrefine;
 	DBuf<uint64_t> refine_dev;  // `refine` on the device (sorted, unique)
+	DBuf<uint64_t> unrefine_dev;  // `unrefine` on the device (sorted; one process: octant-0 heads)
 	size_t kept = 0;
 	std::vector<size_t> part_slot;
 	std::vector<uint32_t> part_len;

@@ -528,6 +528,13 @@ void stop_refining_impl(Grid& g) {
 	// unrefines: one family per requested parent, unless one of its children
 	// is refined or marked dont_unrefine, or its neighborhood forbids it (on
 	// the device)
+	// (the requests exactly check_for_adaptation's device list of family
+	// heads: read there, no upload, no sort of their parents)
+	DBuf<uint64_t> dUR;
+	const bool dev_ur = g.unrefine_dev_valid && g.unrefine_requests.empty() && g.size == 1;
+	if (dev_ur) dUR = std::move(g.unrefine_dev);
+	g.unrefine_dev_valid = false;
+	g.unrefine_dev.release();
 	std::vector<uint64_t> req(g.unrefine_requests.begin(), g.unrefine_requests.end());
 	req.insert(req.end(), g.unrefine_bulk.begin(), g.unrefine_bulk.end());
 	g.unrefine_requests.clear();
@@ -537,7 +544,8 @@ void stop_refining_impl(Grid& g) {
 	DX_LAP("sr.3a_requests");
 	// S is final: one device copy for the passes below
 	if (!s_on_dev) upload(dS, S, s);
-	const std::vector<uint64_t> fmine = k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p);
+	const std::vector<uint64_t> fmine =
+	    k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p, dev_ur ? dUR.p : nullptr);
 	const std::vector<uint64_t> F = gather_union(g, fmine);
 	DBuf<uint64_t> dF;
 	upload(dF, F, s);
@@ -818,6 +826,8 @@ void initialize_balance_load_impl(Grid& g, bool use_partitioner, const uint64_t*
 	g.refine_bulk.clear();
 	g.refine_dev_valid = false;
 	g.refine_dev.release();
+	g.unrefine_dev_valid = false;
+	g.unrefine_dev.release();
 	g.unrefine_bulk.clear();
 	g.refine_requests.clear();      // cells_to_refine (3808)
 	g.unrefine_requests.clear();    // cells_to_unrefine (3810)

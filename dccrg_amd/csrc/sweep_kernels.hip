@@ -1825,8 +1825,9 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	sort_u64(ref.p, size_t(h[0]), s, map_id_bits(m));
 	sort_u64(unref.p, size_t(h[1]), s, map_id_bits(m));
 	out.refine = download(ref.p, size_t(h[0]), s);
-	out.refine_dev = std::move(ref);
 	out.unrefine = download(unref.p, size_t(h[1]), s);
+	out.refine_dev = std::move(ref);
+	out.unrefine_dev = std::move(unref);
 	out.kept = size_t(h[2]);
 	const std::vector<uint32_t> runs = download(part.p, size_t(h[3]), s);
 	// the partial runs' members: ids and bands

@@ -17,7 +17,16 @@ Other lines (--workload): gol (config 2), gol_amr, poisson
 of 1-B and 4-B payloads, game of life on the 4-B state, one half-shift
 repartition).
 
-    python bench.py [--gpus N --steps K --warmup W]   (N > 1 via torch.distributed.run)
+    python bench.py [--gpus N --steps K --warmup W]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process is only
+a launcher: it starts N rank processes of this script (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, one GPU each), touches
+no GPU itself, relays their output (rank 0 prints the JSON line) and exits
+non-zero if any rank fails - the reference's scalability harness launches its
+own ranks per process count the same way (tests/scalability/run_tests.py:
+27-30, 185-198).  Under an external launcher (torch.distributed.run) WORLD_SIZE
+must equal --gpus.
 """
 import argparse
 import json
@@ -37,7 +46,7 @@ XGMI_LINK_GBS = 153.0  # one xGMI link, one direction
 CPU_SHARE = 16         # host cores of one GPU's share on the bench box
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -52,7 +61,75 @@ def parse():
                    default="advection",
                    help="advection = BASELINE metric (default); gol = config 2; gol_amr = SURVEY a14; "
                         "poisson = config 4; scalability = config 5; advection_adapt = SURVEY f1")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------- rank launcher
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_commands(n, argv, port, base_env=None, child=None):
+    """(argv, env) of every rank process: this script with the same
+    arguments, one GPU per rank (LOCAL_RANK = RANK on one node)."""
+    base = dict(os.environ if base_env is None else base_env)
+    cmd = list(child) if child is not None else [sys.executable, "-u", os.path.abspath(__file__)]
+    out = []
+    for r in range(n):
+        env = dict(base)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append((cmd + list(argv), env))
+    return out
+
+
+def launch(n, argv, child=None, poll_s=0.2):
+    """Start n ranks, wait for all of them; when one fails the others are
+    stopped (they would wait forever in a collective).  Returns the exit code:
+    0 when every rank exited 0, else the first failing rank's code (1 if that
+    was a signal).  Ranks inherit stdout / stderr, so rank 0's JSON line is
+    this process's output."""
+    procs = [subprocess.Popen(c, env=e, cwd=ROOT) for c, e in rank_commands(n, argv, free_port(), child=child)]
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 1
+                sys.stderr.write(f"bench launcher: a rank exited with {bad[0]}; stopping the others\n")
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(poll_s)
+    except KeyboardInterrupt:
+        rc = 130
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc
+
+
+def world_check(a, env=None):
+    """None: run as a rank (or alone); 'launch': spawn --gpus ranks; else an
+    error message (WORLD_SIZE set by a launcher and different from --gpus)."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if a.gpus > 1 else None
+    if int(ws) != a.gpus:
+        return f"WORLD_SIZE={ws} from the launcher but --gpus {a.gpus}: pass --gpus {ws}"
+    return None
 
 
 # ---------------------------------------------------------------------------- CPU baseline
@@ -123,10 +200,14 @@ def alive_rule(ids):
     return (z < np.uint64(int(0.2 * 2 ** 64))).astype(np.uint32)
 
 
-def line_base(metric, value, world, a, ms, dtype, data, config, scaling="weak"):
-    return {"metric": metric, "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": a.steps,
+def line_base(metric, value, world, a, ms, dtype, data, config, scaling="weak", g=None):
+    line = {"metric": metric, "value": value, "unit": "cell-updates/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
             "dtype": dtype, "data": data, "config": config}
+    if g is not None:
+        kind, ranks = g.transport()
+        line["transport"] = {"kind": kind, "comm_ranks": ranks}
+    return line
 
 
 # Rehearsal of the N > 1 path on one GPU (DCCRG_BENCH_TRANSPORT=host): every
@@ -138,8 +219,14 @@ HOST_TRANSPORT = "host"
 
 def make_grid(mod, rank, world, uid):
     if uid == HOST_TRANSPORT:
-        return mod.Dccrg(rank, world, 0, exchange=mod.grid.TorchExchange())
-    return mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+        g = mod.Dccrg(rank, world, 0, exchange=mod.grid.TorchExchange())
+    else:
+        g = mod.Dccrg(rank, world, int(os.environ.get("LOCAL_RANK", rank)), uid)
+    if world > 1:
+        kind, ranks = g.transport()
+        if ranks != world:  # the library's communicator must span every rank
+            raise RuntimeError(f"rank {rank}: the grid's {kind} communicator has {ranks} ranks, expected {world}")
+    return g
 
 
 def reduce_stats(torch, dist, world, vals):
@@ -200,7 +287,7 @@ def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
         line = line_base("cell-updates/s, game of life 3D (BASELINE config 2)", sm[1] * a.steps / mx[0], world, a,
                          mx[0] / a.steps * 1e3, "u32", "synthetic: seeded alive(id) rule, p=0.2",
                          {"workload": f"game of life {nx}x{ny}x{nz}, neighborhood 1, non-periodic (config 2"
-                                      f"{', z slabs' if world > 1 else ''})", "cells_rank0": n})
+                                      f"{', z slabs' if world > 1 else ''})", "cells_rank0": n}, g=g)
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS, "traffic": measured_traffic("gol", n, 8 * n, world),
                             "kernel": "gol_structured_v3",
@@ -273,7 +360,7 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                      total * a.steps / el, world, a, el / a.steps * 1e3, "u32",
                      "synthetic: seeded level-0 states (p=0.3), a seeded quarter of the cells refined",
                      {"workload": "get_live_neighbors, 2048x2048x1 level-0, max_ref_lvl 1, neighborhood 1",
-                      "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s})
+                      "cells_rank0": nl, "neighbor_entries_per_leaf": kbar, "setup_s": setup_s}, g=g)
     line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS if ach else None,
                         "traffic": measured_traffic("gol_amr", nl, moved_step, 1),
@@ -344,7 +431,7 @@ def poisson_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                          {"workload": f"poisson3d BiCG, base {n}x{n}x{n * world}, periodic, refined twice at the "
                                       f"center, min = max = {a.steps} iterations",
                           "cells_rank0": n_solve, "setup_s": setup_s,
-                          "parallelism": f"domain decomposition x{world}"})
+                          "parallelism": f"domain decomposition x{world}"}, g=g)
         line["steps"] = it
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS if ach else None,
@@ -424,7 +511,7 @@ def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                          {"workload": f"tests/scalability 1024x1024x{nzr * world} uniform, neighborhood 1, "
                                       "block partition (z slabs), game of life on the 4-B payload",
                           "cells_total": int(sm[1]), "cells_rank0": int(n),
-                          "parallelism": f"domain decomposition x{world}"})
+                          "parallelism": f"domain decomposition x{world}"}, g=g)
         ach = 8.0 * n * a.steps / (kms / 1e3) / 1e9 if kms > 0 else None
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS if ach else None,
@@ -510,7 +597,7 @@ def advection_adapt_main(a, dccrg_amd, torch, dist, rank, world, uid):
                          {"workload": "advection3d, base 128x128x128 per GPU, max_ref_lvl 2, face neighbors, "
                                       "adapt every step (check_for_adaptation + adapt_grid), balance every 25",
                           "cells_rank0_first": cells0, "cells_rank0_last": g.n_local, "setup_s": setup_s,
-                          "parallelism": f"domain decomposition x{world}"})
+                          "parallelism": f"domain decomposition x{world}"}, g=g)
         ach = 64.0 * sm[1] / world / (kms / 1e3) / 1e9 if kms > 0 else None
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
@@ -607,7 +694,7 @@ def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
                           "base": [a.base, a.base, a.base * world], "max_ref_lvl": a.max_ref_lvl,
                           "cells_total": total_cells, "cells_rank0": n_local, "halo_cells_rank0": c["recv"],
                           "partition": "block (level-0 z-slabs, children inherit)",
-                          "parallelism": f"domain decomposition x{world}", "setup_s": setup_s})
+                          "parallelism": f"domain decomposition x{world}", "setup_s": setup_s}, g=g)
         line["roofline"] = {
             "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": (achieved / PEAK_HBM_GBS) if achieved else None, "traffic": traffic,
@@ -639,6 +726,13 @@ def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
 
 def main():
     a = parse()
+    wc = world_check(a)
+    if wc == "launch":
+        # before any torch / HIP call: this process never touches the GPU
+        sys.exit(launch(a.gpus, sys.argv[1:]))
+    if wc is not None:
+        sys.stderr.write(f"bench.py: {wc}\n")
+        sys.exit(2)
     if a.base is None:
         # Poisson at 256^3 per GPU: one phase's working set (~1.5 GB) is far
         # above the 256 MiB Infinity Cache, so its rate is an HBM rate

@@ -155,6 +155,7 @@ _SIGS = {
     "dccrgx_allreduce_f64": (C.c_int, [vp, P(C.c_double), C.c_int, C.c_int]),
     "dccrgx_allreduce_f64_device": (C.c_int, [vp, vp, vp, C.c_int, C.c_int]),
     "dccrgx_barrier": (C.c_int, [vp]),
+    "dccrgx_get_transport": (C.c_int, [vp, P(C.c_int), P(C.c_int)]),
     "dccrgx_comm_loopback": (C.c_int, [vp, C.c_int, sz, sz, sz]),
     "dccrgx_synchronize": (C.c_int, [vp]),
     "dccrgx_compute_stream": (vp, [vp]),

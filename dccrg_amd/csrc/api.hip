@@ -356,7 +356,7 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 	}
 	const uint64_t mine = std::accumulate(rec.begin(), rec.end(), uint64_t(0));
 	const auto cnt = comm_allgather_u64(g, {uint64_t(nl), mine});
-	uint64_t total = 0, before = 0, bytes_before = 0;
+	uint64_t total = 0, before = 0, bytes_before = 0, bytes_total = 0;
 	for (int p = 0; p < g.size; p++) {
 		const auto& c = cnt[size_t(p)];
 		DX_REQUIRE(c.size() == 2, "grid file: inconsistent cell counts");
@@ -365,6 +365,7 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 			bytes_before += c[1];
 		}
 		total += c[0];
+		bytes_total += c[1];
 	}
 	const int fd = ::open(path, O_CREAT | O_WRONLY, 0644);
 	DX_REQUIRE(fd >= 0, std::string("cannot open grid file ") + path);
@@ -406,9 +407,19 @@ static void save_grid_impl(Grid& g, const char* path, uint64_t offset, const voi
 	}
 	if (nl) pwrite_all(fd, list.data(), 16 * nl, list0 + 16 * before);
 	if (mine) pwrite_all(fd, data.data(), data.size(), data0);
-	// no truncation: like the reference (MPI_MODE_CREATE | MPI_MODE_WRONLY,
-	// dccrg.hpp:1131), bytes already in the file past the grid data stay
-	// (ADVICE r04); a loader bounds the last record by the end of the file
+	// Like the reference (MPI_MODE_CREATE | MPI_MODE_WRONLY, dccrg.hpp:1131)
+	// bytes already in the file past the grid data stay - except
+	// when a variable-size field is saved: the one-shot load_grid_data takes
+	// such a field's bytes up to the record's end, and the last record ends at
+	// the end of the file, so stale bytes of an older, longer file there would
+	// become the last cell's payload.  Then rank 0 cuts the file at
+	// the end of the grid data (every rank's records lie before it).
+	const uint64_t data_end = list0 + 16 * total + bytes_total;
+	if (g.rank == 0 && !var_transfer_fields(g).empty()) {
+		const off_t cur = ::lseek(fd, 0, SEEK_END);
+		DX_REQUIRE(cur >= 0, "grid file size unknown");
+		if (uint64_t(cur) > data_end) DX_REQUIRE(::ftruncate(fd, off_t(data_end)) == 0, "grid file: truncate failed");
+	}
 }
 
 // start_loading_grid_data (1795-2083): the grid block and the cell list; every
@@ -2743,6 +2754,23 @@ int dccrgx_barrier(dccrgx_grid* gp) {
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		double z = 0;
 		comm_allreduce_f64(g, &z, 1, 0);
+		return 0;
+	});
+}
+
+int dccrgx_get_transport(dccrgx_grid* gp, int* kind, int* comm_ranks) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		int k = DCCRGX_TRANSPORT_NONE, n = 1;
+		if (g.xfn) {
+			k = DCCRGX_TRANSPORT_HOST;
+			n = g.size;
+		} else if (g.nccl) {
+			k = DCCRGX_TRANSPORT_RCCL;
+			NCCL_CHECK(ncclCommCount(g.nccl, &n));
+		}
+		if (kind) *kind = k;
+		if (comm_ranks) *comm_ranks = n;
 		return 0;
 	});
 }

@@ -238,7 +238,9 @@ void rank_ordered_combine(const double* all, int P, int count, int op, double* o
 
 namespace {
 // the same rank-ordered combine on the device: one thread per value (the
-// host form above, operation for operation, so both give the same bits)
+// host form above, operation for operation - std::min / std::max are the
+// two comparisons below, which keep the first operand on NaN and on +-0 where
+// fmin / fmax would not - so both give the same bits)
 __global__ void rank_combine_kernel(const double* __restrict__ all, int P, int count, int op, double* __restrict__ out) {
 #pragma clang fp contract(off)
 	const int k = int(blockIdx.x * blockDim.x + threadIdx.x);
@@ -247,10 +249,18 @@ __global__ void rank_combine_kernel(const double* __restrict__ all, int P, int c
 	for (int p = 1; p < P; p++) {
 		const double x = all[size_t(p) * size_t(count) + size_t(k)];
 		if (op == 0) acc += x;
-		else if (op == 1) acc = fmin(acc, x);
-		else acc = fmax(acc, x);
+		else if (op == 1) acc = (x < acc) ? x : acc;
+		else acc = (acc < x) ? x : acc;
 	}
 	out[k] = acc;
+}
+
+// all-gather of count doubles into `gather` (P x count, rank-major) and the
+// rank-ordered combine into d_out, all queued on s
+void allreduce_through(Grid& g, double* gather, const double* d_in, double* d_out, int count, int op, hipStream_t s) {
+	comm_allgather_dev(g, d_in, size_t(count) * 8, reinterpret_cast<uint8_t*>(gather), s);
+	rank_combine_kernel<<<unsigned((count + 63) / 64), 64, 0, s>>>(gather, g.size, count, op, d_out);
+	HIP_CHECK(hipGetLastError());
 }
 }  // namespace
 
@@ -260,6 +270,15 @@ __global__ void rank_combine_kernel(const double* __restrict__ all, int P, int c
 // is stream-ordered and can sit between two kernels of an iteration); the
 // host exchange has to stage through the host and returns with the result
 // on the device.  d_in and d_out may be the same buffer.
+//
+// The gather buffer g.red_all belongs to the compute stream: only this
+// function writes it and callers pass s_comp (the combine kernel may still be
+// reading it when this returns).  The host form below runs on s_comm and
+// gathers into a buffer of its own, so a host allreduce (dccrgx_barrier,
+// dccrgx_allreduce_f64) right after a device one cannot overwrite the values
+// the device form's pending combine has yet to read.  A grow of red_all under
+// a pending reader is safe: the old block goes to the pool's pending list,
+// reused only after a device synchronisation (pool.hip).
 void comm_allreduce_f64_dev(Grid& g, const double* d_in, double* d_out, int count, int op, hipStream_t s) {
 	if (count <= 0) return;
 	const size_t bytes = size_t(count) * 8;
@@ -269,21 +288,23 @@ void comm_allreduce_f64_dev(Grid& g, const double* d_in, double* d_out, int coun
 	}
 	comm_require(g, "allreduce");
 	DX_REQUIRE(op >= 0 && op <= 2, "allreduce: op must be 0 (sum), 1 (min) or 2 (max)");
+	DX_REQUIRE(s == g.s_comp, "device allreduce: the compute stream owns the gather buffer");
 	g.red_all.reserve(size_t(count) * size_t(g.size));
-	comm_allgather_dev(g, d_in, bytes, reinterpret_cast<uint8_t*>(g.red_all.p), s);
-	rank_combine_kernel<<<unsigned((count + 63) / 64), 64, 0, s>>>(g.red_all.p, g.size, count, op, d_out);
-	HIP_CHECK(hipGetLastError());
+	allreduce_through(g, g.red_all.p, d_in, d_out, count, op, s);
 }
 
 // MPI_Allreduce on host doubles (advection dt MIN, solve.hpp:317; sums): up,
-// the device form, down
+// gathered and combined on s_comm in a buffer of this call (value slot +
+// P x count gather), down
 void comm_allreduce_f64(Grid& g, double* v, int count, int op) {
 	if (g.size == 1 || count <= 0) return;
+	comm_require(g, "allreduce");
+	DX_REQUIRE(op >= 0 && op <= 2, "allreduce: op must be 0 (sum), 1 (min) or 2 (max)");
 	hipStream_t s = g.s_comm;
 	DBuf<double> d;
-	d.alloc(size_t(count));
+	d.alloc(size_t(count) * size_t(g.size + 1));
 	h2d(d.p, v, size_t(count) * 8, s);
-	comm_allreduce_f64_dev(g, d.p, d.p, count, op, s);
+	allreduce_through(g, d.p + count, d.p, d.p, count, op, s);
 	d2h_small(v, d.p, size_t(count) * 8, s);
 }
 

@@ -547,7 +547,7 @@ struct Grid {
 	// own instead of clearing the whole map
 	DBuf<int2> rmap_full;
 	bool rmap_full_clean = true;  // every entry {-1, -1}
-	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev
+	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev (s_comp only)
 	DBuf<double> dt_part;  // block minima of dccrgx_advection_max_time_step_device
 
 	// local layout

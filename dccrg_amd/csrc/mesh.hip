@@ -719,7 +719,9 @@ void lookup_batch(Grid& g, const uint64_t* ids, size_t n, int32_t* owner, int32_
 	o.alloc(n);
 	sl.alloc(n);
 	k_lookup(g.dm(), d.p, n, o.p, sl.p, s);
-	if (owner) HIP_CHECK(hipMemcpyAsync(owner, o.p, n * 4, hipMemcpyDeviceToHost, s));
+	// both reads end in a stream sync (d2h_small): the callers read `owner` /
+	// `slot` on return
+	if (owner) d2h_small(owner, o.p, n * 4, s);
 	if (slot) d2h_small(slot, sl.p, n * 4, s);
 }
 

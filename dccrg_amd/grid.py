@@ -900,6 +900,13 @@ class Dccrg:
         check(lib().dccrgx_allreduce_f64_device(self.h, _dev_ptr(src), _dev_ptr(d), n,
                                                 {"sum": 0, "min": 1, "max": 2}[op]))
 
+    def transport(self):
+        """(kind, communicator ranks) the library holds: kind "none" (a
+        detached view), "rccl" (ranks = ncclCommCount) or "host"."""
+        k, n = C.c_int(), C.c_int()
+        check(lib().dccrgx_get_transport(self.h, C.byref(k), C.byref(n)))
+        return ("none", "rccl", "host")[k.value], n.value
+
     def barrier(self):
         check(lib().dccrgx_barrier(self.h))
 

@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 8 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 9 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -505,6 +505,17 @@ int dccrgx_allreduce_f64(dccrgx_grid* g, double* inout, int count, int op /* 0 s
  * equal d_out (ABI 8) */
 int dccrgx_allreduce_f64_device(dccrgx_grid* g, const double* d_in, double* d_out, int count, int op);
 int dccrgx_barrier(dccrgx_grid* g);
+
+/* The transport the grid was built on (no reference counterpart; the
+ * reference's MPI_Comm_size on its duplicated communicator): *kind is
+ * DCCRGX_TRANSPORT_NONE (a detached view), _RCCL or _HOST (an exchange
+ * function), *comm_ranks the ranks of the communicator the library holds -
+ * ncclCommCount of its RCCL communicator, the grid's size for a host exchange,
+ * 1 for a detached view (ABI 9) */
+#define DCCRGX_TRANSPORT_NONE 0
+#define DCCRGX_TRANSPORT_RCCL 1
+#define DCCRGX_TRANSPORT_HOST 2
+int dccrgx_get_transport(dccrgx_grid* g, int* kind, int* comm_ranks);
 
 /* Transport check (no reference counterpart): the bytes of a fixed-size
  * field's slots [slot0, slot0 + n) sent by this process to itself and

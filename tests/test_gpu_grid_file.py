@@ -211,14 +211,46 @@ def test_variable_payload_file_empty_records(gpu, tmp_path):
     h2.close()
 
 
-def test_save_over_longer_file(gpu, tmp_path):
-    """save_grid_data over an older, longer file at the same path: like the
-    reference (MPI_MODE_CREATE | MPI_MODE_WRONLY, dccrg.hpp:1131) the file is
-    not truncated, so bytes past the new grid data stay (a
-    caller's own bytes there survive).  The split load with the sizes the
-    program knows (the reference's way, tests/restart/variable_cell_data.cpp)
-    restores every cell exactly; the old tail only widens the last record's
-    bytes_left."""
+def test_save_over_longer_file_fixed_size(gpu, tmp_path):
+    """save_grid_data of fixed-size fields over an older, longer file at the
+    same path: like the reference (MPI_MODE_CREATE | MPI_MODE_WRONLY,
+    dccrg.hpp:1131) the file is not truncated, so bytes past the new grid data
+    stay (a caller's own bytes there survive), and the one-shot
+    load reads every cell exactly (fixed-size records never run to the end of
+    the file)."""
+    path = tmp_path / "reuse_fixed.dc"
+    big, _ = make_pair((9, 2, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    b = big.add_field("value", np.float64)
+    b.set(np.full(big.n_local, 3.5))
+    big.add_field("pad", np.float64).set(np.full(big.n_local, 9.0))
+    big.save_grid_data(path)
+    old = open(path, "rb").read()
+    g, _ = make_pair((6, 1, 1), 0, (False, False, False), 1, 0, 0.0, 1)
+    v = g.add_field("value", np.float64)
+    ids = g.slot_ids()[: g.n_local]
+    v.set(ids.astype(np.float64) * 0.25)
+    g.save_grid_data(path)
+    new = open(path, "rb").read()
+    assert len(new) == len(old)  # not truncated
+    used = 8 + 87 + 8 + 16 * ids.size + 8 * ids.size
+    assert new[used:] == old[used:]  # the bytes past the grid data are untouched
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    hv = h.add_field("value", np.float64)
+    h.load_grid_data(path)
+    hid = h.slot_ids()[: h.n_local]
+    assert np.array_equal(hv.get(0, h.n_local), hid.astype(np.float64) * 0.25)
+    for x in (big, g, h):
+        x.close()
+
+
+def test_save_over_longer_file_variable_size(gpu, tmp_path):
+    """The same with a variable-size field: the one-shot load infers such a
+    field's bytes from the record's end, and the last record ends at the end of
+    the file, so save_grid_data cuts the file at the end of its grid data
+    (stale bytes of the older file must not become the last cell's
+    payload).  Both the one-shot load (sizes inferred) and the split load with
+    the sizes the program knows (the reference's way,
+    tests/restart/variable_cell_data.cpp) restore every cell exactly."""
     path = tmp_path / "reuse.dc"
     big, _ = make_pair((9, 2, 1), 0, (False, False, False), 1, 0, 0.0, 1)
     d = big.add_variable_field("data", np.int32)
@@ -234,9 +266,18 @@ def test_save_over_longer_file(gpu, tmp_path):
     data.set([np.arange(int(k), dtype=np.int32) + 7 for k in cnt])
     g.save_grid_data(path)
     new = open(path, "rb").read()
-    assert len(new) == len(old)  # not truncated
     used = 8 + 87 + 8 + 16 * ids.size + int(8 * ids.size + 4 * cnt.sum())
-    assert new[used:] == old[used:]  # the bytes past the grid data are untouched
+    assert len(old) > used and len(new) == used  # cut at the end of the grid data
+    # one-shot: the variable field's sizes from the records
+    h1 = dccrg_amd.Dccrg(0, 1, 0)
+    h1s = h1.add_field("size", np.uint64)
+    h1d = h1.add_variable_field("data", np.int32)
+    h1.load_grid_data(path)
+    k1 = h1s.get(0, h1.n_local)
+    assert np.array_equal(k1, _counts(h1.slot_ids()[: h1.n_local]))
+    got1 = h1d.get(0, h1.n_local)
+    assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got1, k1))
+    # split load with the caller's sizes
     h = dccrg_amd.Dccrg(0, 1, 0)
     hs = h.add_field("size", np.uint64)
     hd = h.add_variable_field("data", np.int32)
@@ -249,5 +290,5 @@ def test_save_over_longer_file(gpu, tmp_path):
     h.finish_loading_grid_data()
     got = hd.get(0, h.n_local)
     assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, k))
-    for x in (big, g, h):
+    for x in (big, g, h, h1):
         x.close()

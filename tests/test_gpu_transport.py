@@ -984,9 +984,13 @@ def sc_poisson1d(rank, world):
             sols.append(offset_last(np.array([d_all[i] for i in range(1, n + 1)])))
             res[f"owners_{n}_{d}"] = bool(np.all(slots % world == rank))
             g.close()
-        res[f"n{n}"] = bool(all(p_norm(s_, ref) <= POISSON1D_THRESHOLD for s_ in sols) and
-                            all(p_norm(sols[a], sols[b]) <= POISSON1D_THRESHOLD for a in range(3)
-                                for b in range(a + 1, 3)))
+        # the 2-norms themselves go into the result, so a failure message
+        # carries the numbers
+        to_ref = [float(p_norm(s_, ref)) for s_ in sols]
+        between = [float(p_norm(sols[a], sols[b])) for a in range(3) for b in range(a + 1, 3)]
+        res[f"norm_ref_{n}"] = to_ref
+        res[f"norm_orient_{n}"] = between
+        res[f"n{n}"] = bool(all(v <= POISSON1D_THRESHOLD for v in to_ref + between))
     return res
 
 

@@ -701,6 +701,13 @@ def advection_main(a, dccrg_amd, torch, dist, rank, world, uid):
             "kernel": "advection_regular_pp_kernel + advection_tiles_pp_kernel", "layout": layout,
             "alg_bytes_per_step": alg_bytes_step, "alg_bytes_core_per_step": alg_core,
             "frac_core_64B": (alg_core * a.steps / kern_s / 1e9 / PEAK_HBM_GBS) if kern_s > 0 else None,
+            # the bytes the two kernels need, each value read once (layout
+            # bytes_needed: core + face codes + per out-of-tile neighbor its
+            # density and 24-B record + list entries + finer faces + tile
+            # records), beside SURVEY's CSR-inclusive count
+            "bytes_needed_per_step": layout["bytes_needed"],
+            "frac_bytes_needed": (layout["bytes_needed"] * a.steps / kern_s / 1e9 / PEAK_HBM_GBS) if kern_s > 0
+            else None,
             "kernel_ms_per_step": kern_ms / a.steps if a.steps else None,
             "timed_intervals_per_step": kern_n / a.steps if a.steps else 0}
         line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("advection", a.cpu_seconds)

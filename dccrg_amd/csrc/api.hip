@@ -159,6 +159,15 @@ static PoArrays po_arrays(Grid& g) {
 	return a;
 }
 
+// the fields a solve or a cache pass writes: the solution and the solver's own
+static void po_written(Grid& g) {
+	const PoissonState& P = g.po;
+	for (int id : {P.sol, P.type, P.best, P.p0, P.p1, P.r0, P.r1, P.ap0, P.sf})
+		if (id >= 0 && size_t(id) < g.fields.size()) field_written(g.fields[size_t(id)]);
+	for (int k = 0; k < 6; k++)
+		if (P.f[k] >= 0 && size_t(P.f[k]) < g.fields.size()) field_written(g.fields[size_t(P.f[k])]);
+}
+
 // cache_system_info 827-971
 static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns, const uint64_t* skip, size_t nk) {
 	DX_REQUIRE(field(g, rhs).elem == 8 && field(g, sol).elem == 8, "rhs and solution must be fp64 fields");
@@ -166,6 +175,7 @@ static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns
 	PoissonState& P = g.po;
 	P.rhs = rhs;
 	P.sol = sol;
+	po_written(g);
 	ensure_face(g);
 	hipStream_t s = g.s_comp;
 	const size_t nl = g.n_local;
@@ -227,6 +237,7 @@ static PoScalars po_read_scalars(Grid& g) {
 static PoScalars po_solve(Grid& g, const PoParams& prm, bool failsafe) {
 	PoissonState& P = g.po;
 	DX_REQUIRE(P.valid, "Poisson system not cached for the current mesh");
+	po_written(g);
 	hipStream_t s = g.s_comp;
 	const size_t n = g.n_local;
 	const unsigned nb = k_po_blocks(n);
@@ -604,6 +615,7 @@ static void continue_load_impl(Grid& g, int fid, const uint64_t* sizes) {
 		}
 	}
 	for (size_t s = 0; s < nl; s++) g.load.pos[s] += bytes[s];
+	field_written(f);
 }
 
 // finish_loading_grid_data (2380-2400)
@@ -647,6 +659,46 @@ static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
 		DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
 		f[k] = (const double*)F.data.p;
 	}
+}
+
+// The neighbor records of the tile sweeps (Grid::NbRecords) for the fields
+// fids: kept while the six velocity / length fields are the same fields with
+// the same write epochs and arrays and the tiles are the same; rebuilt
+// otherwise (one pass over the slots, 48 B read + 72 B written per slot, on
+// the compute stream, so it follows every queued write of those fields).
+// nullptr - the sweeps read the fields - when one of them is external (its
+// device pointer is out), when the slots exceed the records' 32-bit indexing,
+// and unless DCCRGX_NBREC=1: the records are an experiment that lost (paired
+// A/B, DESIGN §5: the record lines are touched by neighbor reads alone, so
+// they miss where the field lines hit because the neighbor tile's own reads
+// brought them into L2: 0.182 -> 0.235 ms of sweep kernels on config 3).
+const double* ensure_nbrec(Grid& g, const int fids[7]) {
+	const char* env = std::getenv("DCCRGX_NBREC");  // read per call: tests switch it
+	const bool off = !(env && std::atoi(env) == 1);
+	Grid::NbRecords& R = g.nbrec;
+	if (off || g.n_slots == 0 || g.n_slots >= (size_t(1) << 29)) return nullptr;
+	for (int k = 1; k < 7; k++)
+		if (field(g, fids[k]).external) return nullptr;
+	bool ok = R.valid && R.tiles_gen == g.tiles_gen && R.n_slots == g.n_slots;
+	for (int k = 1; k < 7 && ok; k++) {
+		const Field& F = field(g, fids[k]);
+		ok = R.fid[k - 1] == fids[k] && R.epoch[k - 1] == F.epoch && R.ptr[k - 1] == F.data.p;
+	}
+	if (ok) return R.r.p;
+	const double* f[7];
+	adv_fields(g, fids, f);
+	R.r.alloc(9 * g.n_slots);
+	k_nbrec(f, g.n_slots, R.r.p, g.s_comp);
+	for (int k = 1; k < 7; k++) {
+		const Field& F = field(g, fids[k]);
+		R.fid[k - 1] = fids[k];
+		R.epoch[k - 1] = F.epoch;
+		R.ptr[k - 1] = F.data.p;
+	}
+	R.tiles_gen = g.tiles_gen;
+	R.n_slots = g.n_slots;
+	R.valid = true;
+	return R.r.p;
 }
 
 static void gol_step_impl(Grid& g, Field& f, int region) {
@@ -2147,7 +2199,10 @@ int dccrgx_field_device_ptr(dccrgx_grid* gp, int fid, void** ptr) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		field(g, fid).local_zero = false;
-		*ptr = fixed_field(g, fid).data.p;
+		Field& f = fixed_field(g, fid);
+		field_written(f);
+		f.external = true;  // writes through the pointer are not seen
+		*ptr = f.data.p;
 		return 0;
 	});
 }
@@ -2158,6 +2213,7 @@ int dccrgx_field_upload(dccrgx_grid* gp, int fid, size_t slot0, size_t n, const 
 		field(g, fid).local_zero = false;
 		Field& f = fixed_field(g, fid);
 		DX_REQUIRE(slot0 + n <= g.n_slots, "slot range out of bounds");
+		field_written(f);
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));
 		if (n) {
 			HIP_CHECK(hipMemcpyAsync(f.data.p + slot0 * f.elem, host, n * f.elem, hipMemcpyHostToDevice, g.s_comp));
@@ -2248,6 +2304,8 @@ int dccrgx_gol_amr(dccrgx_grid* gp, int phase, int sf, int lf, int region) {
 		Field& st = field(g, sf);
 		Field& ls = field(g, lf);
 		DX_REQUIRE(st.elem == 4, "game of life state must be a 4-byte field");
+		field_written(st);
+		field_written(ls);
 		DX_REQUIRE(ls.elem == 64, "live level-0 neighbor list must be a 64-byte field (8 x uint64)");
 		size_t s0, s1;
 		region_range(g, region, s0, s1);
@@ -2296,6 +2354,8 @@ int dccrgx_get_live_neighbors(dccrgx_grid* gp, int sf, int lf) {
 		Field& st = field(g, sf);
 		Field& ls = field(g, lf);
 		DX_REQUIRE(st.elem == 4, "game of life state must be a 4-byte field");
+		field_written(st);
+		field_written(ls);
 		DX_REQUIRE(ls.elem == 64, "live level-0 neighbor list must be a 64-byte field (8 x uint64)");
 		const size_t nl = g.n_local;
 		if (!nl && g.size == 1) return 0;
@@ -2391,12 +2451,17 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 		if (tiles) ensure_tiles(g);
 		else ensure_face(g);
 		DX_LAP("step.0_ensure_tiles");
-		k_time_begin(g);
 		if (tiles) {
+			// (outside the timed interval: a rebuild happens once per mesh or
+			// field change, not per step)
+			const double* rec = ensure_nbrec(g, fids);
+			DX_LAP("step.0_nbrec");
+			k_time_begin(g);
 			// tiles never straddle the inner / outer runs
-			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp);
-			if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp);
+			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp, rec);
+			if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp, rec);
 		} else {
+			k_time_begin(g);
 			k_advection_ell(f, (double*)rho.scratch.p, g.face_ell.p, g.face_fine.p, s0, s1, dt, g.s_comp);
 		}
 		k_time_end(g);
@@ -2405,7 +2470,7 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 	});
 }
 
-int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[10]) {
+int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[12]) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(out, "null output");
@@ -2424,8 +2489,26 @@ int dccrgx_advection_layout(dccrgx_grid* gp, uint64_t out[10]) {
 		// the face CSR (4 B per entry + 4 B row pointer)
 		out[6] = 64 * n + 4 * (n + 1) + 4 * uint64_t(entries);
 		out[7] = 64 * n;
-		out[8] = g.tcount[0] + g.tcount[1];
-		out[9] = 512 * (g.tcount[0] + g.tcount[1]);
+		const size_t nreg = g.tcount[0] + g.tcount[1];
+		out[8] = nreg;
+		out[9] = 512 * nreg;
+		uint64_t ext_reg = 0;
+		if (nreg) {
+			std::vector<RegTileMeta> rm(nreg);
+			d2h_small(rm.data(), g.tregmeta.p, nreg * sizeof(RegTileMeta), g.s_comp);
+			for (const auto& r : rm)
+				for (int d = 0; d < 6; d++) ext_reg += r.nst[d] >= 0 ? 64 : 0;
+		}
+		out[10] = ext_reg;
+		// 40 B per out-of-tile neighbor from the fields (density, three
+		// lengths, the velocity along the face); 32 B with the records
+		// (DCCRGX_NBREC=1, ensure_nbrec)
+		const char* env = std::getenv("DCCRGX_NBREC");
+		const bool rec_off = !(env && std::atoi(env) == 1);
+		const uint64_t per_ext = rec_off ? 40 : 32;
+		const uint64_t n_irr_cells = n - out[9], ext_irr = g.total_ext - ext_reg;
+		out[11] = 64 * n + 12 * n_irr_cells + (per_ext + 4) * ext_irr + per_ext * ext_reg + 8 * uint64_t(g.n_fine_faces) +
+		          32 * nt;
 		return 0;
 	});
 }
@@ -2474,6 +2557,7 @@ int dccrgx_advection_initialize(dccrgx_grid* gp, const int fids[7]) {
 		for (int k = 0; k < 7; k++) {
 			Field& F = field(g, fids[k]);
 			DX_REQUIRE(F.elem == 8, "advection fields must be fp64");
+			field_written(F);
 			if (n) {
 				HIP_CHECK(hipMemcpyAsync(F.data.p, a[k].data(), n * 8, hipMemcpyHostToDevice, g.s_comp));
 				HIP_CHECK(hipStreamSynchronize(g.s_comp));
@@ -2698,7 +2782,10 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		DX_LAP("adapt.1_stop_refining");
 		hipStream_t s = g.s_comp;
 		double* f[7];
-		for (int k = 0; k < 7; k++) f[k] = (double*)field(g, fids[k]).data.p;
+		for (int k = 0; k < 7; k++) {
+			f[k] = (double*)field(g, fids[k]).data.p;
+			field_written(field(g, fids[k]));
+		}
 		// merged parents (adapter.hpp:260-290): the removed children grouped by
 		// parent on the device, each parent's mean of its eight children
 		k_adv_merge_parents(g.m, g.dm(), g.n_local, g.removed_ids, f[0], (const double*)field(g, fids[0]).removed.p, s,
@@ -2784,8 +2871,10 @@ int dccrgx_comm_loopback(dccrgx_grid* gp, int field_id, size_t slot0, size_t n, 
 		DX_REQUIRE(slot0 + n <= g.n_slots && dst_slot0 + n <= g.n_slots, "slot range beyond the field");
 		DX_REQUIRE(slot0 + n <= dst_slot0 || dst_slot0 + n <= slot0, "overlapping slot ranges");
 		f.local_zero = false;  // the receive may land in local slots
+		field_written(f);
 		HIP_CHECK(hipStreamSynchronize(g.s_comp));  // the field's producers
-		comm_loopback(g, f.data.p + slot0 * f.elem, f.data.p + dst_slot0 * f.elem, n * f.elem, g.s_comm);
+		comm_loopback(g, f.data.p + slot0 * f.elem, f.data.p + dst_slot0 * f.elem, n * f.elem,
+		              g.send_single_cells ? f.elem : 0, g.s_comm);
 		HIP_CHECK(hipStreamSynchronize(g.s_comm));
 		return 0;
 	});

@@ -74,6 +74,29 @@ static void wire_pieces(const std::vector<DevMsg>& msgs, bool single, std::vecto
 	}
 }
 
+// Pieces per peer and direction in one RCCL group.  Under send_single_cells
+// a config-5 face plane is ~10^6 pieces per peer; one group of that many
+// ncclSend / ncclRecv is past what RCCL is built for, so the pieces go out in
+// rounds: round j holds, for every peer and direction, that peer's pieces
+// [j K, (j + 1) K).  A pair's sends of round j are the peer's receives of round
+// j (both sides build the same wire), so every round completes on its own
+// and the posting order of a pair - the per-cell wire order - is kept.
+constexpr size_t kPiecesPerGroup = 4096;
+
+// consecutive pieces to one peer that continue each other in memory become
+// one piece (same bytes, same order)
+static void coalesce(std::vector<Piece>& v) {
+	size_t o = 0;
+	for (size_t i = 0; i < v.size(); i++) {
+		if (o && v[o - 1].peer == v[i].peer && v[o - 1].p + v[o - 1].n == v[i].p) {
+			v[o - 1].n += v[i].n;
+		} else {
+			v[o++] = v[i];
+		}
+	}
+	v.resize(o);
+}
+
 // The byte mover.  Pieces to / from one peer keep their order (the wire
 // order): RCCL matches a pair's sends and receives in posting order, the host
 // exchange concatenates them in that order.  Returns with the transfer
@@ -82,12 +105,44 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 	std::vector<Piece> snd, rcv;
 	wire_pieces(msgs, g.send_single_cells, snd, rcv);
 	if (g.nccl && !g.xfn) {
-		NCCL_CHECK(ncclGroupStart());
-		for (const auto& m : snd) NCCL_CHECK(ncclSend(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
-		for (const auto& m : rcv) NCCL_CHECK(ncclRecv(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
-		NCCL_CHECK(ncclGroupEnd());
+		// each piece's index among its peer's pieces of its direction
+		auto rank_in_peer = [&](const std::vector<Piece>& v, std::vector<size_t>& idx) {
+			std::vector<size_t> cnt(size_t(g.size), 0);
+			idx.resize(v.size());
+			size_t most = 0;
+			for (size_t i = 0; i < v.size(); i++) {
+				idx[i] = cnt[size_t(v[i].peer)]++;
+				most = std::max(most, idx[i] + 1);
+			}
+			return most;
+		};
+		std::vector<size_t> si, ri;
+		const size_t rounds = (std::max(rank_in_peer(snd, si), rank_in_peer(rcv, ri)) + kPiecesPerGroup - 1) /
+		                      kPiecesPerGroup;
+		if (rounds <= 1) {
+			NCCL_CHECK(ncclGroupStart());
+			for (const auto& m : snd) NCCL_CHECK(ncclSend(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
+			for (const auto& m : rcv) NCCL_CHECK(ncclRecv(m.p, m.n, ncclUint8, m.peer, g.nccl, s));
+			NCCL_CHECK(ncclGroupEnd());
+			return;
+		}
+		for (size_t j = 0; j < rounds; j++) {
+			const size_t lo = j * kPiecesPerGroup, hi = lo + kPiecesPerGroup;
+			NCCL_CHECK(ncclGroupStart());
+			for (size_t i = 0; i < snd.size(); i++)
+				if (si[i] >= lo && si[i] < hi) NCCL_CHECK(ncclSend(snd[i].p, snd[i].n, ncclUint8, snd[i].peer, g.nccl, s));
+			for (size_t i = 0; i < rcv.size(); i++)
+				if (ri[i] >= lo && ri[i] < hi) NCCL_CHECK(ncclRecv(rcv[i].p, rcv[i].n, ncclUint8, rcv[i].peer, g.nccl, s));
+			NCCL_CHECK(ncclGroupEnd());
+		}
 		return;
 	}
+	// the host exchange carries one byte stream per peer and direction, so
+	// piece boundaries are this side's own business: contiguous pieces are
+	// copied at once (a single-field halo under send_single_cells is one copy
+	// per peer, not one per cell)
+	coalesce(snd);
+	coalesce(rcv);
 	const size_t P = size_t(g.size);
 	std::vector<size_t> sb(P, 0), rb(P, 0);
 	for (const auto& m : msgs) DX_REQUIRE(m.peer >= 0 && m.peer < g.size && m.peer != g.rank, "message to an invalid peer");
@@ -128,10 +183,13 @@ void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t 
 }
 
 // one message to this rank itself through the RCCL branch of the byte mover
-// (a grouped ncclSend / ncclRecv pair; a host exchange has no self peer)
-void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, hipStream_t s) {
+// (a grouped ncclSend / ncclRecv pair; a host exchange has no self peer);
+// `cell` > 0: a run of cells of that many bytes each, which send_single_cells
+// puts on the wire cell by cell
+void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, size_t cell, hipStream_t s) {
 	DX_REQUIRE(g.nccl && !g.xfn, "loopback needs the RCCL transport");
-	move_bytes(g, {DevMsg{g.rank, static_cast<const uint8_t*>(send), bytes, static_cast<uint8_t*>(recv), bytes}}, s);
+	move_bytes(g, {DevMsg{g.rank, static_cast<const uint8_t*>(send), bytes, static_cast<uint8_t*>(recv), bytes, cell}},
+	           s);
 }
 
 // every rank's `bytes` bytes at `mine` into all[p * bytes] (device), own

@@ -301,8 +301,18 @@ struct Field {
 	// velocity / length reset): the local part is left unwritten, the rest
 	// zeroed; the flag is dropped by that rebuild
 	bool no_carry = false;
+	// write tracking for caches derived from the payloads (the advection
+	// sweep's neighbor records, NbRecords): `epoch` goes up with every write
+	// the library makes or is asked to make (field_written); `external` is set
+	// once the device pointer was handed out (writes then untracked, so no
+	// cache is built from the field until the next structural change moves
+	// the array and voids that pointer)
+	uint64_t epoch = 0;
+	bool external = false;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
+
+inline void field_written(Field& f) { f.epoch++; }
 
 // ---- Poisson BiCG (tests/poisson/poisson_solve.hpp) ------------------------
 // device pointers of one solve: user fields rhs / solution, the solver's own
@@ -618,6 +628,24 @@ struct Grid {
 	// another (then tmeta's); empty with tmeta
 	DBuf<uint32_t> tfused;
 	size_t tfused_n[2] = {0, 0};
+	uint64_t tiles_gen = 0;  // bumped by every tile build
+	// Neighbor records of the tile sweeps (sweep_kernels.hip, built by
+	// ensure_nbrec): per axis a and slot s one 24-B record {l_a, l_b * l_c,
+	// v_a} (b < c the other two axes, the product as the reference forms the
+	// face area) at r[(3 a n_slots + 3 s) ..], so an out-of-tile face neighbor
+	// costs its density and one record instead of five field lines.  Built
+	// from the velocity / length fields of the sweep, kept while their ids,
+	// epochs and arrays and the tiles are unchanged.
+	struct NbRecords {
+		DBuf<double> r;
+		int fid[6] = {-1, -1, -1, -1, -1, -1};
+		uint64_t epoch[6] = {0, 0, 0, 0, 0, 0};
+		const void* ptr[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+		uint64_t tiles_gen = 0;
+		size_t n_slots = 0;
+		bool valid = false;
+	} nbrec;
+	std::vector<int> halo_fields;  // fixed-size fields of the halo in flight (written again when it lands)
 	std::map<int, UserHood> uhoods;  // add_neighborhood ids
 	GolAmrTables gola;  // refined game of life: per-mesh tables (gol_amr.hip)
 	// uniform game of life: the regions as plane boxes (gol_slab_plan), built lazily
@@ -669,7 +697,7 @@ struct DevMsg {
 // one grouped point-to-point round of device messages (the same message list
 // for every transport; see comm.hip)
 void comm_device_transfer(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s);
-void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, hipStream_t s);
+void comm_loopback(Grid& g, const void* send, void* recv, size_t bytes, size_t cell, hipStream_t s);
 // every rank's `bytes` at `mine` into all[p * bytes] on the device (own slot included)
 void comm_allgather_dev(Grid& g, const void* mine, size_t bytes, uint8_t* all, hipStream_t s);
 // P x count values, rank-major, combined in rank order (op 0 sum, 1 min, 2 max)
@@ -853,7 +881,13 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
                  size_t s0, size_t s1, double dt, hipStream_t s);
 // tiled advection sweep over the regular and the irregular tiles of one run
 // (run 0 inner, 1 outer: tiles never straddle the two)
-void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s);
+void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s,
+                       const double* nbrec = nullptr);
+// the neighbor records for the sweep of fields fids (rho vx vy vz lx ly lz),
+// rebuilt when stale; nullptr when a velocity / length field is external
+// (or DCCRGX_NBREC=0): the sweeps then read the fields
+const double* ensure_nbrec(Grid& g, const int fids[7]);
+void k_nbrec(const double* const f[7], size_t n, double* r, hipStream_t s);
 void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
                      size_t s1, double dt, hipStream_t s);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);

@@ -109,6 +109,7 @@ void commit(Grid& g, Field& f) {
 		HIP_CHECK(hipMemcpyAsync(f.scratch.p + g.n_local * f.elem, f.data.p + g.n_local * f.elem, halo,
 		                         hipMemcpyDeviceToDevice, g.s_comp));
 	f.data.swap(f.scratch);
+	field_written(f);
 }
 
 void region_range(const Grid& g, int region, size_t& s0, size_t& s1) {
@@ -218,6 +219,14 @@ static void var_halo(Grid& g, HaloPlan& H, hipStream_t s) {
 
 static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 	if (transfer_fields(g).empty()) return;
+	// every transferred field is written by this exchange (its remote
+	// copies), now and again when it lands (halo_wait): a cache built from a
+	// field while its copies are in flight is rebuilt after
+	g.halo_fields.clear();
+	for (Field* f : transfer_fields(g)) {
+		field_written(*f);
+		g.halo_fields.push_back(int(f - g.fields.data()));
+	}
 	const std::vector<Field*> tf = fixed_transfer_fields(g);
 	if (tf.empty()) {
 		// variable-size payloads only: synchronous (their byte counts travel first)
@@ -271,6 +280,9 @@ void halo_wait(Grid& g) {
 	if (!g.halo_in_flight) return;
 	HIP_CHECK(hipStreamWaitEvent(g.s_comp, g.ev_halo, 0));
 	g.halo_in_flight = false;
+	for (int fid : g.halo_fields)
+		if (fid >= 0 && size_t(fid) < g.fields.size()) field_written(g.fields[size_t(fid)]);
+	g.halo_fields.clear();
 }
 
 // --------------------------------------------------------------------------- user neighborhoods
@@ -395,6 +407,7 @@ void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t byt
 			HIP_CHECK(hipMemcpyAsync(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, buf + o, b, hipMemcpyDefault, g.s_comp));
 		k_place(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, tf[k]->elem, tf[k]->win_off, tf[k]->win_len,
 		        H.recv_slots.p + ro, nr, tf[k]->data.p, g.s_comp);
+		field_written(*tf[k]);
 		o += b;
 	}
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
@@ -978,6 +991,7 @@ void finish_balance_load_impl(Grid& g) {
 		for (auto& f : g.fields) {
 			if (f.var) continue;
 			k_place(M.recvbuf.p + o, f.elem, 0, f.elem, sl.p, kv.second.size(), f.data.p, s);
+			field_written(f);
 			o += kv.second.size() * f.elem;
 		}
 	}

@@ -496,6 +496,8 @@ void rebuild(Grid& g, Mesh& nm) {
 	M.carry.release();
 	for (auto& f : g.fields) {
 		f.local_zero = false;
+		field_written(f);
+		f.external = false;  // the array moves: a pointer handed out before is void
 		if (f.var) {  // children and new copies start empty (the reference default-constructs them)
 			var_remap(f, old_slot_ids.p, old_slot_ids.p ? old_n_local : 0, dm, g.n_slots, s);
 			continue;
@@ -663,6 +665,23 @@ void ensure_tiles(Grid& g) {
 		r[5] = tb.fine_n[t];
 		if (r[3] > 1024u || r[5] > 512u || r[1] > 512u) fits = false;
 	}
+	if (std::getenv("DCCRGX_TILE_REASONS") && ni) {  // diagnostics: the irregular tiles' ext lists
+		std::map<uint32_t, size_t> hist;
+		uint32_t emax = 0;
+		size_t etot = 0, ax_n[4] = {0, 0, 0, 0};
+		const auto pk = download(g.ext_pk.p, g.total_ext, g.s_comp);
+		for (size_t i = 0; i < ni; i++) {
+			const uint32_t e = rec[8 * i + 3];
+			hist[e / 128u * 128u]++;
+			emax = std::max(emax, e);
+			etot += e;
+			for (uint32_t k = 0; k < e; k++) ax_n[__builtin_popcount(pk[rec[8 * i + 2] + k] >> 29)]++;
+		}
+		std::fprintf(stderr, "[tiles] irregular: %zu tiles, ext total %zu, max %u (all tiles: max %zu)\n", ni, etot, emax,
+		             g.max_ext);
+		for (auto& kv : hist) std::fprintf(stderr, "[tiles] ext %u..%u: %zu tiles\n", kv.first, kv.first + 127, kv.second);
+		std::fprintf(stderr, "[tiles] ext axes per entry: 0:%zu 1:%zu 2:%zu 3:%zu\n", ax_n[0], ax_n[1], ax_n[2], ax_n[3]);
+	}
 	g.tmeta.release();
 	if (fits && ni) upload(g.tmeta, rec, g.s_comp);
 	// the same records merged with the regular tiles' in tile order (only for
@@ -699,6 +718,7 @@ void ensure_tiles(Grid& g) {
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));
 	DX_LAP("tiles.3_meta");
 	g.tiles_valid = true;
+	g.tiles_gen++;
 }
 
 const std::vector<uint64_t>& slot_ids_host(Grid& g) {

@@ -493,10 +493,49 @@ struct StaticTiles {
 	__device__ __forceinline__ uint32_t next(uint32_t t) const { return t + B; }
 };
 
-template <int MINW>
+// Neighbor records (Grid::NbRecords): per axis a and slot s the 24-B record
+// {l_a, l_b * l_c, v_a} at r[3 a n + 3 s], b < c the two other axes, the
+// product formed as the reference forms a face's area (solve.hpp:142-161).
+// An out-of-tile face neighbor across an a-face then costs its density and
+// this record (one line or two) instead of its density, three lengths and
+// v_a from five arrays.  The sweeps stage such a neighbor into LDS with its
+// length along a in row l_a, the area in the row of the first transverse
+// length (nb_area_row) and 1.0 in the other (nb_one_row): every flux
+// expression then forms nb * nc = area * 1.0 = area exactly, so the fluxes
+// are bitwise those from the fields.
+__global__ void nbrec_kernel(const double* __restrict__ lx, const double* __restrict__ ly,
+                             const double* __restrict__ lz, const double* __restrict__ vx,
+                             const double* __restrict__ vy, const double* __restrict__ vz, size_t n,
+                             double* __restrict__ r) {
+#pragma clang fp contract(off)
+	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
+		const double x = lx[s], y = ly[s], z = lz[s];
+		double* r0 = r + 3 * s;
+		double* r1 = r + 3 * n + 3 * s;
+		double* r2 = r + 6 * n + 3 * s;
+		r0[0] = x;
+		r0[1] = y * z;
+		r0[2] = vx[s];
+		r1[0] = y;
+		r1[1] = x * z;
+		r1[2] = vy[s];
+		r2[0] = z;
+		r2[1] = x * y;
+		r2[2] = vz[s];
+	}
+}
+
+// LDS / register rows (4 lx, 5 ly, 6 lz) of a record-staged neighbor across
+// an a-face: the area in the row of nb, 1.0 in the row of nc, where
+// adv_face_g / adv_face_flux take (nb, nc) = (ly, lz), (lx, lz), (lx, ly)
+__device__ __forceinline__ uint32_t nb_area_row(uint32_t a) { return a == 0 ? 5u : 4u; }
+__device__ __forceinline__ uint32_t nb_one_row(uint32_t a) { return a == 2 ? 5u : 6u; }
+
+template <int MINW, bool REC>
 __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs P, double* __restrict__ rho_out,
                                                                          const RegTileMeta* __restrict__ meta,
-                                                                         uint32_t ntiles, double dt) {
+                                                                         uint32_t ntiles, double dt,
+                                                                         const double* __restrict__ R, size_t nrec) {
 #pragma clang fp contract(off)
 	// rows rho, vx, vy, vz, lx, ly, lz; columns 0..511 the tile's own cells,
 	// 512 + 64 d + (face cell) the out-of-tile neighbor across side d (only
@@ -560,13 +599,20 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);  // wave-uniform
 			r.e[i] = 0;
-			if (row >= 30u) continue;
-			const uint32_t d = row / 5u, val = row - 5u * d, a = d >> 1;
+			if (row >= (REC ? 24u : 30u)) continue;
+			const uint32_t d = REC ? row >> 2 : row / 5u, val = REC ? row & 3u : row - 5u * d, a = d >> 1;
 			const int32_t st = mt.nst(d);
 			if (st < 0) continue;
 			const uint32_t u = lane & 7u, v = lane >> 3, side = (d & 1u) ? 0u : 7u;
 			const uint32_t q0 = a == 0 ? side : u, q1 = a == 1 ? side : (a == 0 ? u : v), q2 = a == 2 ? side : v;
-			r.e[i] = ldo(P.p[val == 4 ? 4 + a : val], (uint32_t(st) + m9(q0, q1, q2)) << 3);
+			const uint32_t sl = uint32_t(st) + m9(q0, q1, q2);
+			if (REC) {
+				// rows (side, 0 rho | 1 l_a | 2 area | 3 v_a): the density from
+				// its field, the rest from the side's axis record
+				r.e[i] = val == 0 ? ldo(rho, sl << 3) : R[size_t(a) * 3 * nrec + 3 * size_t(sl) + (val - 1)];
+			} else {
+				r.e[i] = ldo(P.p[val == 4 ? 4 + a : val], sl << 3);
+			}
 		}
 	};
 	// a loaded tile into LDS (after the barrier that ends the previous tile's reads)
@@ -576,7 +622,14 @@ __global__ __launch_bounds__(512, MINW) void advection_regular_pp_kernel(AdvPtrs
 #pragma unroll
 		for (int i = 0; i < 4; i++) {
 			const uint32_t row = w + 8u * uint32_t(i);
-			if (row < 30u) {
+			if (REC) {
+				if (row < 24u) {
+					const uint32_t d = row >> 2, val = row & 3u, a = d >> 1, col = 512u + 64u * d + lane;
+					const uint32_t k = val == 0 ? 0u : (val == 1 ? 4u + a : (val == 2 ? nb_area_row(a) : 1u + a));
+					shd[k][col] = r.e[i];
+					if (val == 2) shd[nb_one_row(a)][col] = 1.0;
+				}
+			} else if (row < 30u) {
 				const uint32_t d = row / 5u, val = row - 5u * d;
 				shd[vrow(val, d >> 1)][512u + 64u * d + lane] = r.e[i];
 			}
@@ -862,11 +915,11 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW>
+template <int MINW, bool REC>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, uint32_t tplane,
     const uint32_t* __restrict__ ext, const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta,
-    uint32_t ntiles, uint32_t ecap, double dt) {
+    uint32_t ntiles, uint32_t ecap, double dt, const double* __restrict__ R, size_t nrec) {
 #pragma clang fp contract(off)
 	constexpr uint32_t T = 512;
 	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
@@ -895,8 +948,24 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 	// ext = slot | axis mask << 29: density and lengths, and only the
 	// velocity components along the axes its faces cross
 	auto load5 = [&](uint32_t q, double (&v)[7]) {
-		const uint32_t o = (q & 0x1fffffffu) << 3, ax = q >> 29;
-		v[0] = ldo(rho, o); v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
+		const uint32_t sl = q & 0x1fffffffu, o = sl << 3, ax = q >> 29;
+		v[0] = ldo(rho, o);
+		if (REC && (ax == 1u || ax == 2u || ax == 4u)) {
+			// reached through faces of one axis (all but ~0.3 % on config 3):
+			// its density and that axis' record, staged in the rows of
+			// nb_area_row / nb_one_row (bitwise the same fluxes)
+			const uint32_t a = ax >> 1;
+			const double* r = R + size_t(a) * 3 * nrec + 3 * size_t(sl);
+			const double la = r[0], ar = r[1], vv = r[2];
+			v[4] = a == 0 ? la : ar;
+			v[5] = a == 0 ? ar : (a == 1 ? la : 1.0);
+			v[6] = a == 2 ? la : 1.0;
+			v[1] = a == 0 ? vv : 0.0;
+			v[2] = a == 1 ? vv : 0.0;
+			v[3] = a == 2 ? vv : 0.0;
+			return;
+		}
+		v[4] = ldo(lx, o); v[5] = ldo(ly, o); v[6] = ldo(lz, o);
 		v[1] = (ax & 1u) ? ldo(vx, o) : 0.0;
 		v[2] = (ax & 2u) ? ldo(vy, o) : 0.0;
 		v[3] = (ax & 4u) ? ldo(vz, o) : 0.0;
@@ -1661,7 +1730,8 @@ void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* e
 	HIP_CHECK(hipGetLastError());
 }
 
-void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s) {
+void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int run, double dt, hipStream_t s,
+                       const double* nbrec) {
 	const size_t n_reg = g.tcount[run], n_irr = g.tcount[2 + run];
 	const AdvPtrs P{{f[0], f[4], f[5], f[6], f[1], f[2], f[3]}};
 	if (n_irr && !g.tmeta.n) {
@@ -1692,7 +1762,12 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 			advection_regular3_kernel<6><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
 		} else {
 			const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_reg + 7) / 8 * 8));
-			advection_regular_pp_kernel<4><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt);
+			if (nbrec)
+				advection_regular_pp_kernel<4, true><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, nbrec,
+				                                                          g.n_slots);
+			else
+				advection_regular_pp_kernel<4, false><<<nblk, 512, 0, s>>>(P, rho_out, meta, uint32_t(n_reg), dt, nullptr,
+				                                                           0);
 		}
 		HIP_CHECK(hipGetLastError());
 	}
@@ -1701,11 +1776,22 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 		const uint32_t ecap = uint32_t(g.max_ext);
 		const size_t lds = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
-		advection_tiles_pp_kernel<4><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1), g.ext_pk.p,
-		                                                    g.tfine.p, meta,
-		                                                    uint32_t(n_irr), ecap, dt);
+		if (nbrec)
+			advection_tiles_pp_kernel<4, true><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1),
+			                                                          g.ext_pk.p, g.tfine.p, meta, uint32_t(n_irr), ecap,
+			                                                          dt, nbrec, g.n_slots);
+		else
+			advection_tiles_pp_kernel<4, false><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1),
+			                                                           g.ext_pk.p, g.tfine.p, meta, uint32_t(n_irr), ecap,
+			                                                           dt, nullptr, 0);
 		HIP_CHECK(hipGetLastError());
 	}
+}
+
+void k_nbrec(const double* const f[7], size_t n, double* r, hipStream_t s) {
+	if (!n) return;
+	nbrec_kernel<<<grid_for(n, 256), 256, 0, s>>>(f[4], f[5], f[6], f[1], f[2], f[3], n, r);
+	HIP_CHECK(hipGetLastError());
 }
 
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s) {

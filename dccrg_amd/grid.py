@@ -859,10 +859,10 @@ class Dccrg:
     def advection_layout(self):
         """Tile layout of the advection sweep and its algorithmic HBM bytes per
         sweep over all local cells (see include/dccrgx.h)."""
-        out = (C.c_uint64 * 10)()
+        out = (C.c_uint64 * 12)()
         check(lib().dccrgx_advection_layout(self.h, out))
         keys = ("tile", "tiles", "ext_total", "ext_max", "finer_faces", "face_entries", "alg_bytes",
-                "alg_bytes_core", "regular_tiles", "regular_cells")
+                "alg_bytes_core", "regular_tiles", "regular_cells", "ext_regular", "bytes_needed")
         return dict(zip(keys, (int(v) for v in out)))
 
     def advection_check_adaptation(self, density, diff_increase, diff_threshold=0.25, unrefine_sensitivity=0.5):

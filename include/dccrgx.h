@@ -471,9 +471,15 @@ int dccrgx_advection_adapt(dccrgx_grid* g, const int fields[7], uint64_t out[2])
  * of one sweep over all local cells as SURVEY §8(d) fixes them (64 B per cell
  * + 4 B per face entry + 4 B per row pointer), [7] the 64 B-per-cell core
  * alone, [8] regular tiles (aligned uniform boxes swept without face rows),
- * [9] cells in regular tiles.  No reference counterpart (roofline
- * introspection). */
-int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[10]);
+ * [9] cells in regular tiles, [10] out-of-tile face neighbors of the regular
+ * tiles (64 per existing side), [11] the bytes the sweep kernels need per
+ * sweep, each value read once: the 64-B core, per cell of an irregular tile
+ * its 12 B of face codes, per out-of-tile neighbor its density, three
+ * lengths and the velocity along the face (40 B; 32 B with the experimental
+ * neighbor records) plus 4 B of list entry in an irregular tile, 8 B per
+ * finer face, 32 B per tile record (ABI 9: out[12]).
+ * No reference counterpart (roofline introspection). */
+int dccrgx_advection_layout(dccrgx_grid* g, uint64_t out[12]);
 
 /* ---- Poisson solver (tests/poisson/poisson_solve.hpp:156-1056) ----------
  * dccrgx_poisson_cache = Poisson_Solve::cache_system_info (827-971): local
@@ -522,7 +528,9 @@ int dccrgx_get_transport(dccrgx_grid* g, int* kind, int* comm_ranks);
  * received straight into slots [dst_slot0, dst_slot0 + n) of the same field,
  * through the grid's RCCL byte mover (one grouped ncclSend / ncclRecv, the
  * path of every halo and migration message; a grid created with an RCCL id,
- * also at size 1).  DCCRGX_EINVAL on a host-exchange or detached grid. */
+ * also at size 1).  Under send_single_cells the n elements go out as n
+ * messages, as a halo's cells do (ABI 9).  DCCRGX_EINVAL on a host-exchange
+ * or detached grid. */
 int dccrgx_comm_loopback(dccrgx_grid* g, int field_id, size_t slot0, size_t n, size_t dst_slot0);
 
 /* ---- stream / timing ----------------------------------------------------- */

@@ -293,3 +293,63 @@ def test_tile_cut_matches_restatement(gpu, base, R):
     assert lay["regular_tiles"] == int(np.sum(reason == 1))
     assert lay["regular_cells"] == 512 * lay["regular_tiles"]
     g.close()
+
+
+def _steps_with(base, R, steps, external=(), edit=None):
+    """`steps` sweeps on a fresh pre-refined grid (tiles from the second
+    step on); `external`: fields whose device pointer is taken first (the
+    sweeps then read the fields, not the neighbor records); `edit(f, k)` runs
+    before step k."""
+    g, f = gpu_grid(base, R)
+    prerefine(g, f, R)
+    for k in external:
+        f[k].device_ptr()
+    dt = g.advection_max_time_step(f)
+    out = []
+    for k in range(steps):
+        if edit is not None:
+            edit(f, k)
+        g.advection_step(f, 0.5 * dt)
+        g.advection_commit(f[0])
+        out.append(f[0].get(0, g.n_local))
+    g.close()
+    return out
+
+
+@pytest.fixture
+def nbrec_on(monkeypatch):
+    """The neighbor records are an opt-in experiment (DCCRGX_NBREC=1; it lost
+    its paired A/B) kept for reproducing it: parity with it on."""
+    monkeypatch.setenv("DCCRGX_NBREC", "1")
+    yield
+    monkeypatch.delenv("DCCRGX_NBREC", raising=False)
+
+
+@pytest.mark.parametrize("base,R", [((32, 32, 8), 2), ((12, 12, 3), 2), ((10, 10, 4), 1)])
+def test_neighbor_records_bitwise_equal_fields(gpu, nbrec_on, base, R):
+    """The tile sweeps read an out-of-tile neighbor's length, face area and
+    velocity from its per-axis record (NbRecords, sweep_kernels.hip) instead
+    of the fields; staged as (l_a, area, 1.0) every flux forms the same
+    products, so the densities are bitwise those of the field reads (here
+    forced by handing out a velocity field's device pointer)."""
+    a = _steps_with(base, R, 4)
+    b = _steps_with(base, R, 4, external=(1,))
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("k_field", [1, 2, 3, 4, 5, 6])
+def test_neighbor_records_follow_field_writes(gpu, nbrec_on, k_field):
+    """A write of any velocity or length field between steps (here an
+    upload) invalidates the records: the next sweep rebuilds them, so the
+    densities stay bitwise those of the field reads."""
+    def edit(f, k):
+        if k == 3:
+            v = f[k_field].get()
+            f[k_field].set(v * 0.5 + 0.01 if k_field <= 3 else v * 1.25)
+    a = _steps_with((16, 16, 4), 2, 6, edit=edit)
+    b = _steps_with((16, 16, 4), 2, 6, external=(k_field,), edit=edit)
+    c = _steps_with((16, 16, 4), 2, 6)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert not np.array_equal(a[-1], c[-1])  # the edit mattered

@@ -44,3 +44,23 @@ def test_rccl_self_send_recv(gpu):
         d.comm_loopback(fd, 0, 1, 4)
     g.close()
     d.close()
+
+
+def test_rccl_self_send_recv_single_cells(gpu):
+    """send_single_cells on: one ncclSend / ncclRecv pair per element, 9000
+    of them, posted in rounds of at most 4096 per group (comm.hip
+    kPiecesPerGroup); the bytes land as with one message."""
+    g = dccrg_amd.Dccrg(0, 1, 0, dccrg_amd.Dccrg.unique_id())
+    g.set_initial_length((32, 32, 20)).set_neighborhood_length(1).initialize()
+    n = g.n_slots
+    assert n == 20480
+    f = g.add_field("payload", np.float64)
+    vals = np.random.default_rng(5).standard_normal(n)
+    f.set(vals)
+    g.set_send_single_cells(True)
+    g.comm_loopback(f, 11, 9000, 10000)
+    exp = vals.copy()
+    exp[10000:19000] = vals[11:9011]
+    assert np.array_equal(f.get(), exp)
+    g.set_send_single_cells(False)
+    g.close()

@@ -143,6 +143,39 @@ def sc_gol(rank, world, explicit=False):
     return {"equal": ok, "outer": outer}
 
 
+def sc_single_cells_plane(rank, world):
+    """send_single_cells at config 5's plane size over the host transport: a
+    1024 x 1024 x (2 world) uniform grid, hood 1, z slabs, so every rank sends
+    and receives whole 1024 x 1024 planes (~10^6 cells per peer).  The halo
+    with the flag on - one wire piece per cell, coalesced by the host
+    exchange where they continue each other (comm.hip) - places exactly the
+    bytes of the halo with the flag off (the per-cell path at this
+    size must not fall off a cliff); both timed."""
+    length = (1024, 1024, 2 * world)
+    g = _grid(length, 0, (True, True, True), 1)
+    st = g.add_field("is_alive", np.uint32)
+    sl = g.slot_ids()
+    st.set(val(sl[: g.n_local]))
+    res = {}
+    got = {}
+    for flag in (False, True):
+        g.set_send_single_cells(flag)
+        st.set(np.zeros(g.n_slots - g.n_local, np.uint32), g.n_local)
+        g.synchronize()
+        t0 = time.perf_counter()
+        g.update_copies_of_remote_neighbors()
+        g.synchronize()
+        res[f"seconds_{int(flag)}"] = time.perf_counter() - t0
+        got[flag] = st.get(g.n_local, g.n_slots - g.n_local)
+    g.set_send_single_cells(False)
+    res["recv_cells"] = int(g.n_slots - g.n_local)
+    res["big"] = res["recv_cells"] >= 1024 * 1024
+    res["equal"] = bool(np.array_equal(got[True], got[False]) and np.array_equal(got[False], val(sl[g.n_local:])))
+    res["fast"] = res["seconds_1"] < 30.0
+    g.close()
+    return res
+
+
 def sc_gol_explicit(rank, world):
     return sc_gol(rank, world, explicit=True)
 
@@ -1049,7 +1082,8 @@ def sc_gol_amr_turn(rank, world):
 
 
 SCENARIOS = {
-    2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson", "sc_gol_halfshift", "sc_poisson1d"],
+    2: ["sc_config1", "sc_gol_explicit", "sc_rcb", "sc_poisson", "sc_gol_halfshift", "sc_poisson1d",
+        "sc_single_cells_plane"],
     3: ["sc_gol", "sc_advection", "sc_migration", "sc_migration_explicit", "sc_pins", "sc_save", "sc_iterators",
         "sc_rcb", "sc_unrefine", "sc_advection_adapt", "sc_variable", "sc_poisson", "sc_gol_halfshift",
         "sc_poisson1d", "sc_gol_amr_turn"],
@@ -1134,6 +1168,10 @@ def _check(results, name, keys):
 def test_gol_library_halo(transport_results):
     _check(transport_results, "sc_gol", ["equal"])
     assert any(o["outer"] > 0 for _, o in transport_results["sc_gol"].values())
+
+
+def test_send_single_cells_at_plane_size(transport_results):
+    _check(transport_results, "sc_single_cells_plane", ["big", "equal", "fast"])
 
 
 def test_gol_explicit_pack_place(transport_results):

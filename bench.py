@@ -301,14 +301,22 @@ def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
 def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     """the refined game emulating the level-0 game
     (tests/game_of_life/solve.hpp get_live_neighbors, as unrefined2d.cpp
-    plays it) on a 2048 x 2048 x 1 level-0 grid, max refinement level 1, a
-    seeded quarter of the level-0 cells refined (children inherit the state),
-    p = 0.3 live.  One step = collect + spread over every leaf (1 GPU: the
-    halo between them is a no-op).
+    plays it) on a 2048 x 2048 x 1 level-0 grid per GPU, max refinement level
+    1, a seeded quarter of the level-0 cells refined (children inherit the
+    state), p = 0.3 live.
 
-    One process, so the turn is the level-0 game (gol_amr.hip): the
-    roofline bytes are the ones its two passes move (below)."""
+    One process: one step = collect + spread over every leaf, which on one
+    process is the level-0 game (gol_amr.hip): the roofline bytes are the
+    ones its two passes move (below).  N > 1: one partitioned grid of
+    2048 x 2048 N (the block partition: a 2048 x 2048 slab per rank, each
+    rank refining a seeded quarter of its own cells), and one step is the
+    reference's turn across processes (unrefined2d.cpp:186-218): the copies
+    of remote neighbors refreshed, then get_live_neighbors (geometric collect,
+    its own halo of the collected lists, spread + rule); the roofline bytes
+    are SURVEY §8(d)'s CSR/AMR figure."""
     n = 2048
+    if world > 1:
+        return gol_amr_partitioned(a, dccrgx_mod, torch, dist, rank, world, uid, n)
     g = dccrgx_mod.Dccrg(0, 1, 0).set_initial_length((n, n, 1)).set_neighborhood_length(1)
     g.set_maximum_refinement_level(1).initialize()
     rng = np.random.default_rng(7)
@@ -322,33 +330,24 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
     st = g.add_field("is_alive", np.uint32)
     ls = g.add_field("gol_list", np.dtype((np.uint64, 8)))
     slots = g.slot_ids()[: g.n_local]
-    lvl = (slots > np.uint64(n * n)).astype(np.int64)
-    c1 = slots.astype(np.int64) - 1 - n * n
-    x1, y1 = c1 % (2 * n), (c1 // (2 * n)) % (2 * n)
-    par = np.where(lvl == 0, slots.astype(np.int64) - 1, (y1 // 2) * n + x1 // 2)
-    st.set(live0[par].astype(np.uint32))
+    st.set(live0[level0_index(slots, n, n)].astype(np.uint32))
     for _ in range(a.warmup):
         g.get_live_neighbors(st, ls)
-    # one process per grid: at N > 1 every rank plays its own replica, timed
-    # between the same barriers (value = all ranks' leaves / the slowest rank)
     el, kms, kn = timed(g, torch, dist, world, lambda: g.get_live_neighbors(st, ls), a.steps)
     nl = g.n_local
-    mx, sm = reduce_stats(torch, dist, world, [el, float(nl)])
-    el, total = mx[0], int(sm[1])
+    total = nl
     kbar = g.neighbor_entries("of") / nl
-    f1 = float(np.mean(lvl == 1))
     # roofline: the bytes the turn's kernels must move over the turn's kernel
     # time, so `achieved` / `frac` are a share of HBM bandwidth.  The grid is
-    # one process (a replica per GPU), so the turn is the level-0 game
-    # (gol_amr.hip lg_table_kernel + lg_game_kernel, one row per level-0
-    # cell): per leaf its state read by the table pass and read + written by
-    # the game pass (12 B), per level-0 cell the row's slot, octant byte and
-    # packed level-0 coordinates read by both passes (2 x 9 B) and its table
-    # byte written once and read once (2 B).  SURVEY §8(d)'s fixed CSR/AMR
-    # figure (8 B + 4 B per neighbor entry + 4 B row pointer) counts
-    # neighbor-entry reads this path does not make; it is reported beside it
-    # as model_throughput_GBs / frac_model, a throughput figure, not
-    # bandwidth.
+    # one process, so the turn is the level-0 game (gol_amr.hip lg_table_kernel
+    # + lg_game_kernel, one row per level-0 cell): per leaf its state read by
+    # the table pass and read + written by the game pass (12 B), per level-0
+    # cell the row's slot, octant byte and packed level-0 coordinates read by
+    # both passes (2 x 9 B) and its table byte written once and read once
+    # (2 B).  SURVEY §8(d)'s fixed CSR/AMR figure (8 B + 4 B per neighbor entry
+    # + 4 B row pointer) counts neighbor-entry reads this path does not make;
+    # it is reported beside it as model_throughput_GBs / frac_model, a
+    # throughput figure, not bandwidth.
     per_cell = 8 + 4 * kbar + 4
     moved_step = 12 * nl + 20 * n * n
     kern = "lg_table_kernel + lg_game_kernel"
@@ -370,8 +369,68 @@ def gol_amr_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                         "model_bytes_per_leaf": per_cell, "model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
                         "model_throughput_GBs": model, "frac_model": model / PEAK_HBM_GBS if model else None,
                         "kernel_ms_per_step": kms / a.steps, "launches_per_step": kn / a.steps}
-    line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("gol_amr", a.cpu_seconds)
+    line["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline("gol_amr", a.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    g.close()
+
+
+def level0_index(ids, nx, ny):
+    """0-based level-0 parent index (raster) of level-0 / level-1 leaves of
+    an nx x ny x 1 grid with max refinement level 1."""
+    ids = ids.astype(np.int64)
+    n0 = nx * ny
+    lvl = ids > n0
+    c1 = ids - 1 - n0
+    x1, y1 = c1 % (2 * nx), (c1 // (2 * nx)) % (2 * ny)
+    return np.where(lvl, (y1 // 2) * nx + x1 // 2, ids - 1)
+
+
+def gol_amr_partitioned(a, dccrgx_mod, torch, dist, rank, world, uid, n):
+    """The refined game at N > 1 on one partitioned grid (gol_amr_main)."""
+    nx, ny = n, n * world
+    g = make_grid(dccrgx_mod, rank, world, uid)
+    g.set_initial_length((nx, ny, 1)).set_neighborhood_length(1).set_maximum_refinement_level(1).initialize()
+    live0 = np.random.default_rng(7).random(nx * ny) < 0.3
+    t_setup = time.perf_counter()
+    loc = g.local_cells()
+    for c in np.random.default_rng(7 + rank).choice(loc, size=loc.size // 4, replace=False):
+        g.refine_completely(int(c))
+    g.stop_refining()
+    setup_s = time.perf_counter() - t_setup
+    st = g.add_field("is_alive", np.uint32)
+    ls = g.add_field("gol_list", np.dtype((np.uint64, 8)))
+    slots = g.slot_ids()[: g.n_local]
+    st.set(live0[level0_index(slots, nx, ny)].astype(np.uint32))
+
+    def step():
+        # unrefined2d.cpp:186-218: the copies of remote neighbors refreshed,
+        # then the turn (its own halo of the collected lists inside)
+        g.update_copies_of_remote_neighbors()
+        g.get_live_neighbors(st, ls)
+
+    for _ in range(a.warmup):
+        step()
+    el, kms, kn = timed(g, torch, dist, world, step, a.steps)
+    nl = g.n_local
+    kbar = g.neighbor_entries("of") / nl
+    per_cell = 8 + 4 * kbar + 4
+    mx, sm = reduce_stats(torch, dist, world, [el, float(nl), kms, float(g.get_number_of_update_send_cells())])
     if rank == 0:
+        line = line_base("cell-updates/s, refined game of life emulating the level-0 game (SURVEY a14)",
+                         sm[1] * a.steps / mx[0], world, a, mx[0] / a.steps * 1e3, "u32",
+                         "synthetic: seeded level-0 states (p=0.3), a seeded quarter of every rank's cells refined",
+                         {"workload": f"get_live_neighbors, {nx}x{ny}x1 level-0 (block partition, a {nx}x{n} slab "
+                                      "per rank), max_ref_lvl 1, neighborhood 1; step = state halo + turn",
+                          "cells_rank0": nl, "cells_total": int(sm[1]), "neighbor_entries_per_leaf": kbar,
+                          "setup_s": setup_s, "parallelism": f"domain decomposition x{world}"}, g=g)
+        ach = per_cell * nl * a.steps / (mx[2] / 1e3) / 1e9 if mx[2] > 0 else None
+        line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": ach / PEAK_HBM_GBS if ach else None, "traffic": None,
+                            "kernel": "gol_amr geometric collect + spread (+ exact collect when a family disagrees)",
+                            "alg_bytes_per_leaf": per_cell, "model": "SURVEY 8(d) GoL CSR/AMR: 8 + 4 k + 4",
+                            "kernel_ms_per_step_max_rank": mx[2] / a.steps, "launches_per_step": kn / a.steps}
+        line["halo"] = {"send_cells_max_rank": mx[3]}
+        line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
     g.close()
 

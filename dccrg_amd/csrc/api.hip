@@ -661,6 +661,19 @@ static void adv_fields(Grid& g, const int fids[7], const double* f[7]) {
 	}
 }
 
+// the block minima now in g.dt_part (nb of them) belong to fields fids as
+// they are now (Grid::DtCache)
+static void dt_cache_set(Grid& g, const int fids[7], size_t nb) {
+	Grid::DtCache& C = g.dt_cache;
+	for (int k = 1; k < 7; k++) {
+		C.fid[k - 1] = fids[k];
+		C.epoch[k - 1] = field(g, fids[k]).epoch;
+	}
+	C.n_local = g.n_local;
+	C.nb = nb;
+	C.valid = nb > 0;
+}
+
 // The neighbor records of the tile sweeps (Grid::NbRecords) for the fields
 // fids: kept while the six velocity / length fields are the same fields with
 // the same write epochs and arrays and the tiles are the same; rebuilt
@@ -745,9 +758,11 @@ namespace {
 struct PhaseTable {
 	std::map<std::string, std::pair<double, long>> t;
 	~PhaseTable() {
+		const char* r = std::getenv("RANK");
 		for (auto& kv : t)
-			std::fprintf(stderr, "[phase] %-28s %10.3f ms total %7ld calls %9.3f ms/call\n", kv.first.c_str(),
-			             kv.second.first * 1e3, kv.second.second, kv.second.first * 1e3 / double(kv.second.second));
+			std::fprintf(stderr, "[phase r%s] %-28s %10.3f ms total %7ld calls %9.3f ms/call\n", r ? r : "0",
+			             kv.first.c_str(), kv.second.first * 1e3, kv.second.second,
+			             kv.second.first * 1e3 / double(kv.second.second));
 	}
 };
 PhaseTable& phase_table() {
@@ -900,6 +915,7 @@ int dccrgx_destroy(dccrgx_grid* gp) {
 		(void)hipDeviceSynchronize();
 		drain_timing(g);
 		if (g.nccl) ncclCommDestroy(g.nccl);
+		if (g.pin_stage) (void)hipHostFree(g.pin_stage);
 		if (g.ev_comp) (void)hipEventDestroy(g.ev_comp);
 		if (g.ev_halo) (void)hipEventDestroy(g.ev_halo);
 		if (g.s_comp) (void)hipStreamDestroy(g.s_comp);
@@ -2567,16 +2583,28 @@ int dccrgx_advection_initialize(dccrgx_grid* gp, const int fids[7]) {
 	});
 }
 
+// the block minima of the time-step bound of fields fids in g.dt_part (their
+// count): the cached ones while the six velocity / length fields are
+// unwritten since (advection_adapt's reset pass leaves them), else one pass
+static size_t dt_partials(Grid& g, const int fids[7]) {
+	const double* f[7];
+	adv_fields(g, fids, f);
+	Grid::DtCache& C = g.dt_cache;
+	bool ok = C.valid && C.n_local == g.n_local && C.nb > 0;
+	for (int k = 1; k < 7 && ok; k++) ok = C.fid[k - 1] == fids[k] && C.epoch[k - 1] == field(g, fids[k]).epoch;
+	if (ok) return C.nb;
+	const size_t nb = 512;
+	g.dt_part.reserve(kDtPartials);
+	k_adv_dt(f, g.n_local, g.dt_part.p, nb, g.s_comp);
+	dt_cache_set(g, fids, nb);
+	return nb;
+}
+
 int dccrgx_advection_max_time_step(dccrgx_grid* gp, const int fids[7], double* out) {
 	return guard([&] {
 		GRID_OR_FAIL(gp);
-		const double* f[7];
-		adv_fields(g, fids, f);
-		const size_t nb = 512;
-		DBuf<double> part;
-		part.alloc(nb);
-		k_adv_dt(f, g.n_local, part.p, nb, g.s_comp);
-		auto h = download(part.p, nb, g.s_comp);
+		const size_t nb = dt_partials(g, fids);
+		auto h = download(g.dt_part.p, nb, g.s_comp);
 		*out = *std::min_element(h.begin(), h.end());
 		return 0;
 	});
@@ -2586,11 +2614,7 @@ int dccrgx_advection_max_time_step_device(dccrgx_grid* gp, const int fids[7], do
 	return guard([&] {
 		GRID_OR_FAIL(gp);
 		DX_REQUIRE(d_out != nullptr, "null device pointer");
-		const double* f[7];
-		adv_fields(g, fids, f);
-		const size_t nb = 512;
-		g.dt_part.reserve(nb);
-		k_adv_dt(f, g.n_local, g.dt_part.p, nb, g.s_comp);
+		const size_t nb = dt_partials(g, fids);
 		k_min_partials(g.dt_part.p, nb, d_out, g.s_comp);
 		comm_allreduce_f64_dev(g, d_out, d_out, 1, 1, g.s_comp);
 		return 0;
@@ -2791,7 +2815,10 @@ int dccrgx_advection_adapt(dccrgx_grid* gp, const int fids[7], uint64_t out[2]) 
 		k_adv_merge_parents(g.m, g.dm(), g.n_local, g.removed_ids, f[0], (const double*)field(g, fids[0]).removed.p, s,
 		                    g.merged_dev.p, g.n_merged);
 		DX_LAP("adapt.2_parents");
-		k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s);
+		// the reset pass also leaves the next time step's block minima
+		g.dt_part.reserve(kDtPartials);
+		const size_t nb = k_adv_reset(g.m, g.slot_ids.p, g.n_local, g.start, g.l0, f, s, g.dt_part.p);
+		dt_cache_set(g, fids, nb);
 		HIP_CHECK(hipStreamSynchronize(s));
 		DX_LAP("adapt.3_reset");
 		// transfer_all_data: every field of the seven in this halo

@@ -14,6 +14,7 @@
 // slot of a leaf is one 16-byte probe sequence in the rank's hash table (or
 // the block-partition formula on the initial level-0 grid).
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_merge.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -186,6 +187,46 @@ __global__ void remote_flags_kernel(MapCtx m, const int32_t* hood, const int32_t
 		}
 		const bool any = __any(remote);
 		if (lane_id() == 0) flag[w] = any ? 1u : 0u;
+	}
+}
+
+// The same classification with one thread per cell, for small hoods (the
+// face hood: 6 neighbors_of items + 60 neighbors_to candidates per cell): a
+// wave then holds 64 cells whose lookups are independent, where the wave per
+// cell above issues its cell's 66 lookups as two dependent rounds and leaves
+// 62 lanes idle in the second.  The walk stops at the first remote neighbor.
+__global__ __launch_bounds__(256) void remote_flags_thread_kernel(MapCtx m, const int32_t* __restrict__ hood,
+                                                                  const int32_t* __restrict__ hood_to, int nh,
+                                                                  DevMesh M, int rank, const uint64_t* __restrict__ cells,
+                                                                  size_t n, uint32_t* __restrict__ flag,
+                                                                  const uint8_t* __restrict__ near, uint64_t near_lo,
+                                                                  uint64_t near_n) {
+	const DevExists ex{M};
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		if (near) {
+			const uint64_t q = map_level0_parent(m, cells[i]) - near_lo;
+			if (q < near_n && !near[q]) {
+				flag[i] = 0u;
+				continue;
+			}
+		}
+		uint64_t c[3];
+		int lvl;
+		cell_coords(m, cells[i], c, lvl);
+		bool remote = false;
+		for (int k = 0; k < nh && !remote; k++) {
+			ItemOut o;
+			nof_item(m, c, lvl, hood + 3 * k, ex, o);
+			for (int j = 0; j < o.n; j++) {
+				const int32_t ow = dm_owner(M, o.id[j]);
+				if (ow >= 0 && ow != rank) remote = true;
+			}
+		}
+		for (int k = 0; k < 10 * nh && !remote; k++) {
+			const uint64_t f = nto_candidate(m, c, lvl, hood_to, nh, k, ex);
+			if (f != error_cell && dm_owner(M, f) != rank) remote = true;
+		}
+		flag[i] = remote ? 1u : 0u;
 	}
 }
 
@@ -1082,10 +1123,103 @@ void k_lookup(const DevMesh& M, const uint64_t* ids, size_t n, int32_t* owner, i
 }
 
 void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M, int rank,
-                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s) {
+                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s, const uint8_t* near,
+                    uint64_t near_lo, size_t near_n) {
 	if (!n) return;
-	remote_flags_kernel<<<grid_for(n, 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, cells, n, flag);
+	static const char* env = std::getenv("DCCRGX_FLAGS_WAVE");  // A/B: the wave-per-cell form
+	if ((nh <= 6 || near) && !(env && env[0] == '1'))
+		remote_flags_thread_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, cells, n, flag, near,
+		                                                            near_lo, near_n);
+	else
+		remote_flags_kernel<<<grid_for(n, 4), 256, 0, s>>>(m, hood, hood_to, nh, M, rank, cells, n, flag);
 	HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+// min / max level-0 parent of the ids: wave then block reduction, one
+// atomic pair per block (per wave, 134 K pairs on one address cost 0.75 ms)
+__global__ __launch_bounds__(256) void level0_span_kernel(MapCtx m, const uint64_t* __restrict__ ids, size_t n,
+                                                          unsigned long long* mm) {
+	__shared__ unsigned long long slo[256 / WAVE], shi[256 / WAVE];
+	unsigned long long lo = ~0ull, hi = 0;
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const unsigned long long p = map_level0_parent(m, ids[i]);
+		lo = p < lo ? p : lo;
+		hi = p > hi ? p : hi;
+	}
+	for (int o = WAVE / 2; o > 0; o >>= 1) {
+		const unsigned long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+		lo = a < lo ? a : lo;
+		hi = b > hi ? b : hi;
+	}
+	if (lane_id() == 0) {
+		slo[threadIdx.x / WAVE] = lo;
+		shi[threadIdx.x / WAVE] = hi;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < 256 / WAVE; w++) {
+			lo = slo[w] < lo ? slo[w] : lo;
+			hi = shi[w] > hi ? shi[w] : hi;
+		}
+		if (lo <= hi) {
+			atomicMin(mm, lo);
+			atomicMax(mm + 1, hi);
+		}
+	}
+}
+
+// mark the level-0 cells within r of every ghost leaf's level-0 parent
+__global__ void level0_near_kernel(MapCtx m, MapCtx m0, const uint64_t* __restrict__ kid,
+                                   const int32_t* __restrict__ kown, size_t n, int rank, int r, uint64_t lo,
+                                   uint64_t span, uint8_t* __restrict__ near) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		if (kown[i] == rank) continue;
+		uint64_t x, y, z;
+		map_indices(m0, map_level0_parent(m, kid[i]), x, y, z);
+		for (int dz = -r; dz <= r; dz++) {
+			uint64_t wz;
+			if (!map_wrap(m0, 2, int64_t(z) + dz, wz)) continue;
+			for (int dy = -r; dy <= r; dy++) {
+				uint64_t wy;
+				if (!map_wrap(m0, 1, int64_t(y) + dy, wy)) continue;
+				for (int dx = -r; dx <= r; dx++) {
+					uint64_t wx;
+					if (!map_wrap(m0, 0, int64_t(x) + dx, wx)) continue;
+					const uint64_t q = map_from_indices(m0, wx, wy, wz, 0) - lo;
+					if (q < span) near[q] = 1;
+				}
+			}
+		}
+	}
+}
+}  // namespace
+
+bool k_level0_near(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n_known, int rank, int radius,
+                   DBuf<uint8_t>& near, uint64_t& near_lo, hipStream_t s) {
+	if (!n_known) return false;
+	DBuf<unsigned long long> mm;
+	mm.alloc(2);
+	const unsigned long long init[2] = {~0ull, 0ull};
+	h2d(mm.p, init, sizeof(init), s);
+	level0_span_kernel<<<grid_for(n_known, 256, 1024), 256, 0, s>>>(m, kid, n_known, mm.p);
+	HIP_CHECK(hipGetLastError());
+	unsigned long long h[2] = {0, 0};
+	d2h_small(h, mm.p, sizeof(h), s);
+	if (h[0] > h[1]) return false;
+	const uint64_t span = h[1] - h[0] + 1;
+	if (span > 8 * uint64_t(n_known) + (uint64_t(1) << 24)) return false;
+	near.alloc(size_t(span));
+	HIP_CHECK(hipMemsetAsync(near.p, 0, size_t(span), s));
+	MapCtx m0;
+	const uint64_t len[3] = {m.len[0], m.len[1], m.len[2]};
+	const int per[3] = {m.periodic[0], m.periodic[1], m.periodic[2]};
+	map_init(m0, len, 0, per);
+	level0_near_kernel<<<grid_for(n_known, 256), 256, 0, s>>>(m, m0, kid, kown, n_known, rank, radius, h[0], span,
+	                                                          near.p);
+	HIP_CHECK(hipGetLastError());
+	near_lo = h[0];
+	return true;
 }
 
 void k_assign_slots2(const uint32_t* flag, const uint32_t* scan_outer, size_t n, size_t n_inner, const uint64_t* cells,
@@ -1142,7 +1276,11 @@ static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t 
 	out.clear();
 	if (!n) return;
 	if (!owners) {
-		n = sort_unique_u64(keys, n, s);
+		// keys = owner * stride + id < size * stride: only those bits sorted
+		int bits = 1;
+		const uint64_t top = uint64_t(size) * stride;
+		while (bits < 64 && (top >> bits)) bits++;
+		n = sort_unique_u64(keys, n, s, bits);
 		for (uint64_t k : download(keys, n, s)) out[int(k / stride)].push_back(k % stride);
 		return;
 	}
@@ -1410,11 +1548,37 @@ void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s) {
 	ids2.alloc(n);
 	morton_keys_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, ids, n, keys.p);
 	HIP_CHECK(hipGetLastError());
+	// the keys' bits: 3 per level of the finest index (9 levels on a 512-wide
+	// finest grid: 27 bits, 4 radix passes instead of 8)
+	int b = 1;
+	while (b < 21 && (uint64_t(1) << b) < std::max(m.glen[0], std::max(m.glen[1], m.glen[2]))) b++;
+	const int end_bit = std::min(63, 3 * b);
 	size_t bytes = 0;
-	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, 63, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, end_bit, s));
 	DBuf<uint8_t> temp;
 	temp.alloc(bytes);
-	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, 63, s));
+	HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp.p, bytes, keys.p, keys2.p, ids, ids2.p, n, 0, end_bit, s));
+	HIP_CHECK(hipMemcpyAsync(ids, ids2.p, n * 8, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ids[0, run1) and ids[run1, n) each in Morton order -> ids in Morton order:
+// one merge pass (rocprim::merge over the Morton keys) instead of a sort
+void k_morton_merge2(const MapCtx& m, uint64_t* ids, size_t n, size_t run1, hipStream_t s) {
+	if (run1 == 0 || run1 >= n) return;
+	DBuf<uint64_t> keys, keys2, ids2;
+	keys.alloc(n);
+	keys2.alloc(n);
+	ids2.alloc(n);
+	morton_keys_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, ids, n, keys.p);
+	HIP_CHECK(hipGetLastError());
+	size_t bytes = 0;
+	HIP_CHECK(rocprim::merge(nullptr, bytes, keys.p, keys.p + run1, keys2.p, ids, ids + run1, ids2.p, run1, n - run1,
+	                         rocprim::less<uint64_t>(), s));
+	DBuf<uint8_t> temp;
+	temp.alloc(bytes + 1);
+	HIP_CHECK(rocprim::merge(temp.p, bytes, keys.p, keys.p + run1, keys2.p, ids, ids + run1, ids2.p, run1, n - run1,
+	                         rocprim::less<uint64_t>(), s));
 	HIP_CHECK(hipMemcpyAsync(ids, ids2.p, n * 8, hipMemcpyDeviceToDevice, s));
 	HIP_CHECK(hipStreamSynchronize(s));
 }

@@ -141,6 +141,7 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 	// piece boundaries are this side's own business: contiguous pieces are
 	// copied at once (a single-field halo under send_single_cells is one copy
 	// per peer, not one per cell)
+	DX_PHASE("comm.host_move_bytes", s);
 	coalesce(snd);
 	coalesce(rcv);
 	const size_t P = size_t(g.size);
@@ -148,29 +149,52 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 	for (const auto& m : msgs) DX_REQUIRE(m.peer >= 0 && m.peer < g.size && m.peer != g.rank, "message to an invalid peer");
 	for (const auto& m : snd) sb[size_t(m.peer)] += m.n;
 	for (const auto& m : rcv) rb[size_t(m.peer)] += m.n;
-	std::vector<std::vector<uint8_t>> hs(P), hr(P);
-	std::vector<size_t> so(P, 0), ro(P, 0);
+	// one pinned staging area: the send bytes of every peer, then the
+	// receive bytes (grow-only, kept by the grid)
+	std::vector<size_t> sbase(P, 0), rbase(P, 0);
+	size_t tot = 0;
 	for (size_t p = 0; p < P; p++) {
-		hs[p].resize(sb[p]);
-		hr[p].resize(rb[p]);
+		sbase[p] = tot;
+		tot += sb[p];
 	}
+	for (size_t p = 0; p < P; p++) {
+		rbase[p] = tot;
+		tot += rb[p];
+	}
+	if (tot > g.pin_stage_cap) {
+		HIP_CHECK(hipStreamSynchronize(s));
+		if (g.pin_stage) HIP_CHECK(hipHostFree(g.pin_stage));
+		g.pin_stage = nullptr;
+		g.pin_stage_cap = 0;
+		const size_t cap = std::max(tot + tot / 4, size_t(1) << 20);
+		HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g.pin_stage), cap, hipHostMallocDefault));
+		g.pin_stage_cap = cap;
+	}
+	uint8_t* const pin = g.pin_stage;
+	std::vector<size_t> so(P, 0), ro(P, 0);
 	HIP_CHECK(hipStreamSynchronize(s));  // the send buffers are complete
 	for (const auto& m : snd) {
 		const size_t p = size_t(m.peer);
-		HIP_CHECK(hipMemcpyAsync(hs[p].data() + so[p], m.p, m.n, hipMemcpyDefault, s));
+		HIP_CHECK(hipMemcpyAsync(pin + sbase[p] + so[p], m.p, m.n, hipMemcpyDefault, s));
 		so[p] += m.n;
 	}
 	HIP_CHECK(hipStreamSynchronize(s));
 	std::vector<const void*> sp(P, nullptr);
 	std::vector<void*> rp(P, nullptr);
 	for (size_t p = 0; p < P; p++) {
-		sp[p] = hs[p].data();
-		rp[p] = hr[p].data();
+		sp[p] = pin + sbase[p];
+		rp[p] = pin + rbase[p];
 	}
+#if DCCRGX_PHASE_TIMING
+	const double tx0 = PhaseScope::now();
+#endif
 	DX_REQUIRE(g.xfn(g.xctx, sp.data(), sb.data(), rp.data(), rb.data()) == 0, "exchange function failed");
+#if DCCRGX_PHASE_TIMING
+	phase_add("comm.xfn_wait", PhaseScope::now() - tx0);
+#endif
 	for (const auto& m : rcv) {
 		const size_t p = size_t(m.peer);
-		HIP_CHECK(hipMemcpyAsync(m.p, hr[p].data() + ro[p], m.n, hipMemcpyDefault, s));
+		HIP_CHECK(hipMemcpyAsync(m.p, pin + rbase[p] + ro[p], m.n, hipMemcpyDefault, s));
 		ro[p] += m.n;
 	}
 	HIP_CHECK(hipStreamSynchronize(s));

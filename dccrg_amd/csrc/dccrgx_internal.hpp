@@ -558,7 +558,22 @@ struct Grid {
 	DBuf<int2> rmap_full;
 	bool rmap_full_clean = true;  // every entry {-1, -1}
 	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev (s_comp only)
-	DBuf<double> dt_part;  // block minima of dccrgx_advection_max_time_step_device
+	// pinned host staging of the host-exchange transport (comm.hip
+	// move_bytes), grow-only, freed with the grid: the device <-> host legs
+	// then run on the copy engines instead of the runtime's pageable path
+	uint8_t* pin_stage = nullptr;
+	size_t pin_stage_cap = 0;
+	DBuf<double> dt_part;  // block minima of the advection time step (dt_cache)
+	// the block minima in dt_part are those of the velocity / length fields
+	// fid with these write epochs over n_local cells (nb of them): the time
+	// step of advection_adapt's reset pass (fused into it), or of the last
+	// max_time_step, reused until one of the fields is written again
+	struct DtCache {
+		bool valid = false;
+		int fid[6] = {-1, -1, -1, -1, -1, -1};
+		uint64_t epoch[6] = {0, 0, 0, 0, 0, 0};
+		size_t n_local = 0, nb = 0;
+	} dt_cache;
 
 	// local layout
 	size_t n_inner = 0, n_outer = 0, n_local = 0, n_recv = 0, n_slots = 0;
@@ -754,9 +769,21 @@ void k_hash_insert(HashEntry* tab, uint64_t mask, uint32_t shift, const uint64_t
                    int32_t owner_const, size_t n, hipStream_t s, size_t slot_upto = 0);
 void k_hash_set_slots(const DevMesh& M, const uint64_t* slot_ids, size_t n, int32_t* err, hipStream_t s);
 void k_lookup(const DevMesh& M, const uint64_t* ids, size_t n, int32_t* owner, int32_t* slot, hipStream_t s);
-// flag local cells that have a remote neighbors_of / neighbors_to entry
+// flag local cells that have a remote neighbors_of / neighbors_to entry;
+// with `near` (a byte per level-0 id in [near_lo, near_lo + near_n), see
+// k_level0_near) only cells whose level-0 parent is marked are examined, the
+// others are inner
 void k_remote_flags(const MapCtx& m, const int32_t* hood, const int32_t* hood_to, int nh, const DevMesh& M, int rank,
-                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s);
+                    const uint64_t* cells, size_t n, uint32_t* flag, hipStream_t s, const uint8_t* near = nullptr,
+                    uint64_t near_lo = 0, size_t near_n = 0);
+// Level-0 cells within `radius` level-0 cells of a ghost leaf's level-0
+// parent, marked in a byte map over the level-0 span of the known leaves
+// (every neighbors_of / neighbors_to entry of a leaf lies under the level-0
+// cells within that radius of its level-0 parent, so a leaf under an
+// unmarked level-0 cell has no remote neighbor).  False when the span is too
+// sparse for a map (then no filter).
+bool k_level0_near(const MapCtx& m, const uint64_t* kid, const int32_t* kown, size_t n_known, int rank, int radius,
+                   DBuf<uint8_t>& near, uint64_t& near_lo, hipStream_t s);
 // local ids -> slots: inner first, outer second, both in the input order
 void k_assign_slots2(const uint32_t* flag, const uint32_t* scan_outer, size_t n, size_t n_inner, const uint64_t* cells,
                      uint64_t* slot_ids, hipStream_t s);
@@ -784,6 +811,7 @@ void host_sort_u64(std::vector<uint64_t>& v, bool unique, hipStream_t s);  // ho
 // (id, slot) of every slot sorted by id
 void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_t>& ids, std::vector<int32_t>& slots,
                          hipStream_t s);
+void k_morton_merge2(const MapCtx& m, uint64_t* ids, size_t n, size_t run1, hipStream_t s);
 void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
 void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s);
@@ -922,8 +950,11 @@ void k_adv_merge_parents(const MapCtx& m, const DevMesh& dm, size_t n_local, Laz
                          const double* removed_rho, hipStream_t s, const uint64_t* parents = nullptr, size_t np = 0);
 void k_adv_parent_density(double* rho, const int32_t* parent_slot, const int32_t* child_idx, const double* removed_rho,
                           size_t np, hipStream_t s);
-void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
-                 double* const f[7], hipStream_t s);
+// (dt_partial: when given, the block minima of the time-step bound of the
+// values written, as k_adv_dt computes them; returns their count)
+constexpr unsigned kDtPartials = 2048;  // block minima a reset pass leaves at most
+size_t k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
+                   double* const f[7], hipStream_t s, double* dt_partial = nullptr);
 void k_time_begin(Grid& g);
 void k_time_end(Grid& g);
 

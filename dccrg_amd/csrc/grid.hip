@@ -475,6 +475,68 @@ static bool close_set(Grid& g, std::vector<uint64_t>& S, bool finer, const uint6
 	return grew;
 }
 
+// Children of the merged families F that change process (10360-10410): one
+// thread per family looks up its eight children's owners; a child of this
+// rank whose parent goes to another (child 0's owner) is sent there, a child
+// of another rank whose parent stays here is received from it.  Only those
+// (the families on process boundaries) are appended, as (id, peer * 2 +
+// 0 send / 1 receive); everything else stays on the device.
+__global__ void moving_children_kernel(MapCtx m, DevMesh M, const uint64_t* __restrict__ F, size_t nf, int rank,
+                                       uint64_t* __restrict__ out_id, int32_t* __restrict__ out_peer,
+                                       unsigned long long* __restrict__ cnt, unsigned long long cap) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < nf; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t ch[8];
+		map_all_children(m, F[i], ch);
+		int32_t o[8];
+		for (int k = 0; k < 8; k++) o[k] = dm_owner(M, ch[k]);
+		const int32_t po = o[0];
+		for (int k = 0; k < 8; k++) {
+			int32_t peer = -1, kind = 0;
+			if (o[k] == rank && po != rank) {
+				peer = po;
+			} else if (o[k] != rank && po == rank && o[k] >= 0) {
+				peer = o[k];
+				kind = 1;
+			}
+			if (peer < 0) continue;
+			const unsigned long long at = atomicAdd(cnt, 1ull);
+			if (at < cap) {
+				out_id[at] = ch[k];
+				out_peer[at] = peer * 2 + kind;
+			}
+		}
+	}
+}
+
+static void k_moving_children(Grid& g, const uint64_t* dF, size_t nf, std::map<int, std::vector<uint64_t>>& send_ids,
+                              std::map<int, std::vector<uint64_t>>& recv_ids, hipStream_t s) {
+	if (!nf) return;
+	DBuf<unsigned long long> cnt;
+	cnt.alloc(1);
+	size_t cap = std::max<size_t>(4096, nf);  // most families do not straddle ranks; once more when short
+	for (int pass = 0; pass < 2; pass++) {
+		DBuf<uint64_t> id;
+		DBuf<int32_t> peer;
+		id.alloc(cap);
+		peer.alloc(cap);
+		HIP_CHECK(hipMemsetAsync(cnt.p, 0, 8, s));
+		moving_children_kernel<<<grid_for(nf, 256), 256, 0, s>>>(g.m, g.dm(), dF, nf, g.rank, id.p, peer.p, cnt.p,
+		                                                        (unsigned long long)cap);
+		HIP_CHECK(hipGetLastError());
+		unsigned long long n = 0;
+		d2h_small(&n, cnt.p, 8, s);
+		if (n > cap) {
+			cap = size_t(n);
+			continue;
+		}
+		const std::vector<uint64_t> hi = download(id.p, size_t(n), s);
+		const std::vector<int32_t> hp = download(peer.p, size_t(n), s);
+		for (size_t k = 0; k < size_t(n); k++) (hp[k] & 1 ? recv_ids : send_ids)[hp[k] >> 1].push_back(hi[k]);
+		return;
+	}
+	DX_REQUIRE(false, "internal error: moving children beyond their count");
+}
+
 // stop_refining (3461-3485) = override_refines, induce_refines,
 // override_unrefines, execute_refines, distributed:
 //  * override_refines (9991-10038): dont_refine cells spread to their finer
@@ -606,7 +668,12 @@ void stop_refining_impl(Grid& g) {
 		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, dF.p);
 		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
-		if (g.size > 1 || attrs) {
+		if (g.size > 1 && !attrs) {
+			// the device scan of the children that change process
+			k_moving_children(g, dF.p, F.size(), send_ids, recv_ids, s);
+			for (auto* mp : {&send_ids, &recv_ids})
+				for (auto& kv : *mp) std::sort(kv.second.begin(), kv.second.end());
+		} else if (attrs) {
 			// the children leaving / arriving, and the weights / pins of the
 			// removed local ones
 			std::vector<uint64_t> ch_all(8 * F.size());

@@ -349,6 +349,12 @@ void rebuild(Grid& g, Mesh& nm) {
 			d_local.alloc(g.n_local + 1);
 			HIP_CHECK(hipMemcpyAsync(d_local.p, M.kid.p, g.n_local * 8, hipMemcpyDeviceToDevice, s));
 			prefix_sorted = M.prefix_run1 == M.n_prefix;
+			if (!prefix_sorted && M.prefix_run1 > 0) {
+				// two runs: merged once here, the stable inner / outer split
+				// below then keeps both parts in Morton order (no sorts)
+				k_morton_merge2(m, d_local.p, g.n_local, M.prefix_run1, s);
+				prefix_sorted = true;
+			}
 		} else {
 			d_local.alloc(M.n_known + 1);
 			DBuf<unsigned long long> ctr;
@@ -379,7 +385,19 @@ void rebuild(Grid& g, Mesh& nm) {
 		flag.alloc(nl + 1);
 		scan.alloc(nl + 1);
 		HIP_CHECK(hipMemsetAsync(flag.p, 0, (nl + 1) * sizeof(uint32_t), s));
-		if (g.size > 1) k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.rank, d_local.p, nl, flag.p, s);
+		if (g.size > 1) {
+			// only leaves near a ghost leaf can have a remote neighbor
+			// (DCCRGX_NEAR_FILTER=0: examine every leaf, for A/Bs)
+			static const char* nf = std::getenv("DCCRGX_NEAR_FILTER");
+			DBuf<uint8_t> near;
+			uint64_t near_lo = 0;
+			const bool use = !M.implicit && !(nf && nf[0] == '0') &&
+			                 k_level0_near(m, M.kid.p, M.kown.p, M.n_known, g.rank, ghost_radius(g), near, near_lo, s);
+			DX_LAP("rb.2a0_near");
+			k_remote_flags(m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.rank, d_local.p, nl, flag.p, s,
+			               use ? near.p : nullptr, near_lo, use ? near.n : 0);
+		}
+		DX_LAP("rb.2a_remote_flags");
 		g.n_outer = scan_exclusive_u32(flag.p, scan.p, nl, s);
 		g.n_inner = nl - g.n_outer;
 		local_slots.alloc(nl + 1);
@@ -387,11 +405,17 @@ void rebuild(Grid& g, Mesh& nm) {
 		d_local.release();
 	}
 	const uint64_t* lsp = solo ? M.kid.p : local_slots.p;  // the own leaves in slot order
+	DX_LAP("rb.2b_scan_assign");
 	if (g.morton_slots && !prefix_sorted) {
 		// (a Morton-ordered d_local stays so in both runs: the split is stable)
 		k_morton_sort(m, local_slots.p, g.n_inner, s);
 		k_morton_sort(m, local_slots.p + g.n_inner, g.n_outer, s);
 	}
+#if DCCRGX_PHASE_TIMING
+	if (std::getenv("DCCRGX_MESH_NOTES"))
+		std::fprintf(stderr, "[mesh r%d] local %zu inner %zu outer %zu known %zu prefix %zu run1 %zu sorted %d range-map levels %d\n",
+		             g.rank, nl, g.n_inner, g.n_outer, M.n_known, M.n_prefix, M.prefix_run1, int(prefix_sorted), M.rlev);
+#endif
 
 	DX_LAP("rb.2_classify_sort");
 	// 3. neighbor lists of outer cells -> send / receive lists (8590-8752)
@@ -416,6 +440,7 @@ void rebuild(Grid& g, Mesh& nm) {
 		to_id.alloc(t_to + 1);
 		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, lsp, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
 		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, p_to.p, to_id.p, s);
+		DX_LAP("rb.3a_outer_rows");
 		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s);
 		k_send_by_owner(to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
 		std::map<int, std::vector<uint64_t>> rem_to;

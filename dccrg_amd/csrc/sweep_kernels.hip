@@ -1628,12 +1628,17 @@ __global__ void check_rows_kernel(const int32_t* __restrict__ cidx, const int32_
 // adapt_grid (adapter.hpp:294-305): velocity (solve.hpp:336-342) and lengths
 // (Cartesian_Geometry get_center / get_length, dccrg_cartesian_geometry.hpp:
 // 282-362) of every local cell
-__global__ void adv_reset_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, size_t n, double s0, double s1,
-                                 double l00, double l01, double l02, double* vx, double* vy, double* vz, double* lx,
-                                 double* ly, double* lz) {
+// (+ the block minima of adv_dt_kernel's bound over the values written, when
+// dt_partial is given: the next max_time_step needs no pass of its own)
+__global__ __launch_bounds__(256) void adv_reset_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids, size_t n,
+                                                        double s0, double s1, double l00, double l01, double l02,
+                                                        double* vx, double* vy, double* vz, double* lx, double* ly,
+                                                        double* lz, double* dt_partial) {
 #pragma clang fp contract(off)
+	__shared__ double red[256];
 	const double st[3] = {s0, s1, 0.0};
 	const double l0[3] = {l00, l01, l02};
+	double mn = 1.7976931348623157e308;
 	for (size_t s = blockIdx.x * size_t(blockDim.x) + threadIdx.x; s < n; s += size_t(gridDim.x) * blockDim.x) {
 		uint64_t ind[3];
 		const int lvl = map_indices(m, slot_ids[s], ind[0], ind[1], ind[2]);
@@ -1641,13 +1646,29 @@ __global__ void adv_reset_kernel(MapCtx m, const uint64_t* __restrict__ slot_ids
 		double L[3], c[2];
 		for (int d = 0; d < 3; d++) L[d] = l0[d] * sf;
 		for (int d = 0; d < 2; d++) c[d] = st[d] + double(ind[d]) * l0[d] / double(uint64_t(1) << m.R) + L[d] / 2;
-		vx[s] = -c[1] + 0.5;
-		vy[s] = +c[0] - 0.5;
-		vz[s] = 0;
+		const double v[3] = {-c[1] + 0.5, +c[0] - 0.5, 0.0};
+		vx[s] = v[0];
+		vy[s] = v[1];
+		vz[s] = v[2];
 		lx[s] = L[0];
 		ly[s] = L[1];
 		lz[s] = L[2];
+		if (dt_partial) {
+			// adv_dt_kernel's expression on the same values
+			const double a = L[0] / fabs(v[0]), b = L[1] / fabs(v[1]), cc = L[2] / fabs(v[2]);
+			if (__builtin_isnormal(a)) mn = fmin(mn, a);
+			if (__builtin_isnormal(b)) mn = fmin(mn, b);
+			if (__builtin_isnormal(cc)) mn = fmin(mn, cc);
+		}
 	}
+	if (!dt_partial) return;  // grid-uniform
+	red[threadIdx.x] = mn;
+	__syncthreads();
+	for (int k = blockDim.x / 2; k > 0; k >>= 1) {
+		if (threadIdx.x < k) red[threadIdx.x] = fmin(red[threadIdx.x], red[threadIdx.x + k]);
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) dt_partial[blockIdx.x] = red[0];
 }
 
 }  // namespace
@@ -1939,12 +1960,14 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	return out;
 }
 
-void k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
-                 double* const f[7], hipStream_t s) {
-	if (!n) return;
-	adv_reset_kernel<<<grid_for(n, 256), 256, 0, s>>>(m, slot_ids, n, start[0], start[1], l0[0], l0[1], l0[2], f[1],
-	                                                  f[2], f[3], f[4], f[5], f[6]);
+size_t k_adv_reset(const MapCtx& m, const uint64_t* slot_ids, size_t n, const double start[3], const double l0[3],
+                   double* const f[7], hipStream_t s, double* dt_partial) {
+	if (!n) return 0;
+	const unsigned nb = grid_for(n, 256, kDtPartials);
+	adv_reset_kernel<<<nb, 256, 0, s>>>(m, slot_ids, n, start[0], start[1], l0[0], l0[1], l0[2], f[1], f[2], f[3], f[4],
+	                                    f[5], f[6], dt_partial);
 	HIP_CHECK(hipGetLastError());
+	return nb;
 }
 
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,

@@ -915,16 +915,28 @@ struct TileMeta {
 	uint32_t ts, n, e0, ne, fb, nf, pad0, pad1;
 };
 
-template <int MINW, bool REC>
+// ONCE: a face between two cells of the tile whose codes point at each other
+// (a same-level pair: the minus cell's +a code is the plus cell, the plus
+// cell's -a code the minus cell) is evaluated once, by its minus cell, into
+// LDS (adv_face_g, as the regular kernel does), and the plus cell adds the
+// stored value: the same product with the same operands (the expression is
+// symmetric, see adv_face_g), so the densities are bitwise the two-sided
+// form's.  Faces to ext cells, finer lists and coarser neighbors are still
+// evaluated by each side.
+template <int MINW, bool REC, bool ONCE>
 __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
     AdvPtrs P, double* __restrict__ rho_out, const uint32_t* __restrict__ tell, uint32_t tplane,
     const uint32_t* __restrict__ ext, const uint32_t* __restrict__ tfine, const TileMeta* __restrict__ meta,
     uint32_t ntiles, uint32_t ecap, double dt, const double* __restrict__ R, size_t nrec) {
 #pragma clang fp contract(off)
 	constexpr uint32_t T = 512;
-	extern __shared__ double shd[];  // [7][T + ecap] (rho vx vy vz lx ly lz), then 2 x T u32 finer-face pairs
+	// [7][T + ecap] doubles (rho vx vy vz lx ly lz); ONCE: 3 x T doubles of
+	// +a face fluxes; 2 x T u32 finer-face pairs; ONCE: 3 x T flags
+	extern __shared__ double shd[];
 	const uint32_t W = T + ecap;
-	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W);
+	double* shg = shd + 7 * W;
+	uint32_t* shf = reinterpret_cast<uint32_t*>(shd + 7 * W + (ONCE ? 3 * T : 0));
+	uint8_t* shok = reinterpret_cast<uint8_t*>(shf + 2 * T);
 	const StaticTiles tk(ntiles);
 	const uint32_t t1 = tk.t1;
 	uint32_t t = tk.first();
@@ -1030,18 +1042,57 @@ __global__ __launch_bounds__(512, MINW) void advection_tiles_pp_kernel(
 			const uint32_t tnn = tk.next(tn);
 			rec = tnn < t1 ? tile_record_word(meta, tnn, lane) : 0u;
 		}
-		if (tid < n) {
-			const double cd = shd[tid], cvx = shd[W + tid], cvy = shd[2 * W + tid], cvz = shd[3 * W + tid],
-			             clx = shd[4 * W + tid], cly = shd[5 * W + tid], clz = shd[6 * W + tid];
-			auto fetch = [&](uint32_t li, int d) -> AdvNb {
-				return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
-			};
-			const uint32_t rr[3] = {r0, r1, r2};
+		const bool own = tid < n;
+		double cd = 0, cvx = 0, cvy = 0, cvz = 0, clx = 1, cly = 1, clz = 1;
+		if (own) {
+			cd = shd[tid];
+			cvx = shd[W + tid];
+			cvy = shd[2 * W + tid];
+			cvz = shd[3 * W + tid];
+			clx = shd[4 * W + tid];
+			cly = shd[5 * W + tid];
+			clz = shd[6 * W + tid];
+		}
+		auto fetch = [&](uint32_t li, int d) -> AdvNb {
+			return AdvNb{shd[li], shd[4 * W + li], shd[5 * W + li], shd[6 * W + li], shd[(1 + (d >> 1)) * W + li]};
+		};
+		const uint32_t rr[3] = {r0, r1, r2};
+		// ONCE, pass 1: the +a faces to a cell of the tile (direct codes)
+		double gp[3] = {0, 0, 0};
+		bool hp[3] = {false, false, false};
+		if (ONCE) {
+			if (own) {
+				const double cva[3] = {cvx, cvy, cvz};
+#pragma unroll
+				for (int a = 0; a < 3; a++) {
+					const uint32_t code = rr[a] >> 16;
+					hp[a] = code < n;  // (0xffff none and 0x8000 | k finer lists are >= n)
+					if (hp[a]) {
+						gp[a] = adv_face_g(a, cd, clx, cly, clz, cva[a], fetch(code, 2 * a + 1), dt);
+						shg[a * T + tid] = gp[a];
+					}
+					shok[a * T + tid] = hp[a] ? 1 : 0;
+				}
+			}
+			__syncthreads();
+		}
+		if (own) {
 			double acc = 0;
 #pragma unroll
 			for (int d = 0; d < 6; d++) {
 				const uint32_t code = (rr[d >> 1] >> (16 * (d & 1))) & 0xffffu;
 				if (code == 0xffffu) continue;
+				if (ONCE) {
+					const int a = d >> 1;
+					if ((d & 1) && hp[a]) {
+						acc += -gp[a];
+						continue;
+					}
+					if (!(d & 1) && code < n && shok[a * T + code]) {
+						acc += shg[a * T + code];
+						continue;
+					}
+				}
 				if (code & 0x8000u) {
 					const uint32_t fk = code & 0x7fffu;
 					const uint32_t q0 = shf[2 * fk], q1 = shf[2 * fk + 1];
@@ -1795,16 +1846,31 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 	if (n_irr) {
 		const TileMeta* meta = reinterpret_cast<const TileMeta*>(g.tmeta.p) + (run == 0 ? 0 : g.tcount[2]);
 		const uint32_t ecap = uint32_t(g.max_ext);
-		const size_t lds = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t);
+		// DCCRGX_FACE_ONCE=1: in-tile same-level faces evaluated once (lost
+		// its paired A/B: 0.184 -> 0.194 ms per sweep, the extra barrier costs
+		// more than the halved flux arithmetic)
+		static const char* fo = std::getenv("DCCRGX_FACE_ONCE");
+		const bool once = fo && fo[0] == '1';
+		const size_t lds = size_t(7) * (512 + ecap) * sizeof(double) + size_t(2) * 512 * sizeof(uint32_t) +
+		                   (once ? size_t(3) * 512 * (sizeof(double) + 1) : 0);
 		const unsigned nblk = unsigned(std::min<size_t>(size_t(256) * 2, (n_irr + 7) / 8 * 8));
-		if (nbrec)
-			advection_tiles_pp_kernel<4, true><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1),
-			                                                          g.ext_pk.p, g.tfine.p, meta, uint32_t(n_irr), ecap,
-			                                                          dt, nbrec, g.n_slots);
+		const uint32_t tp = uint32_t(g.n_local + 1);
+		if (nbrec && once)
+			advection_tiles_pp_kernel<4, true, true><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, tp, g.ext_pk.p, g.tfine.p,
+			                                                                meta, uint32_t(n_irr), ecap, dt, nbrec,
+			                                                                g.n_slots);
+		else if (nbrec)
+			advection_tiles_pp_kernel<4, true, false><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, tp, g.ext_pk.p,
+			                                                                 g.tfine.p, meta, uint32_t(n_irr), ecap, dt,
+			                                                                 nbrec, g.n_slots);
+		else if (once)
+			advection_tiles_pp_kernel<4, false, true><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, tp, g.ext_pk.p,
+			                                                                 g.tfine.p, meta, uint32_t(n_irr), ecap, dt,
+			                                                                 nullptr, 0);
 		else
-			advection_tiles_pp_kernel<4, false><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, uint32_t(g.n_local + 1),
-			                                                           g.ext_pk.p, g.tfine.p, meta, uint32_t(n_irr), ecap,
-			                                                           dt, nullptr, 0);
+			advection_tiles_pp_kernel<4, false, false><<<nblk, 512, lds, s>>>(P, rho_out, g.tell.p, tp, g.ext_pk.p,
+			                                                                  g.tfine.p, meta, uint32_t(n_irr), ecap, dt,
+			                                                                  nullptr, 0);
 		HIP_CHECK(hipGetLastError());
 	}
 }

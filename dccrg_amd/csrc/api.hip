@@ -1514,25 +1514,6 @@ static void flush_bulk_requests(Grid& g) {
 	g.unrefine_bulk.clear();
 }
 
-// whether the leaf `d` is one of neighbors_of(cell) in the default
-// neighborhood, for a `d` at least as large as the cell: it overlaps one of
-// the cell-sized boxes at the neighborhood's offsets (find_neighbors_of
-// 4339-4680 lists exactly the leaves overlapping those boxes)
-static bool in_neighbors_of(const Grid& g, uint64_t cell, uint64_t d) {
-	uint64_t c[3], o[3];
-	if (map_indices(g.m, cell, c[0], c[1], c[2]) < 0 || map_indices(g.m, d, o[0], o[1], o[2]) < 0) return false;
-	const uint64_t cl = map_cell_len(g.m, cell), dl = map_cell_len(g.m, d);
-	for (size_t k = 0; k + 2 < g.hood.size(); k += 3) {
-		bool hit = true;
-		for (int a = 0; a < 3 && hit; a++) {
-			uint64_t w = 0;
-			if (!map_wrap(g.m, a, int64_t(c[a]) + int64_t(g.hood[k + size_t(a)]) * int64_t(cl), w)) hit = false;
-			else hit = w < o[a] + dl && o[a] < w + cl;
-		}
-		if (hit) return true;
-	}
-	return false;
-}
 
 // refine_completely (2434-2530): only local leaves; at the maximum level it
 // is dont_unrefine (2472-2475); refused (false) when the cell, or a coarser
@@ -1558,10 +1539,26 @@ int dccrgx_refine_completely(dccrgx_grid* gp, uint64_t cell) {
 		}
 		if (!g.dont_refine_cells.empty()) {
 			if (g.dont_refine_cells.count(cell)) return DCCRGX_ENOTFOUND;
-			for (uint64_t d : g.dont_refine_cells)
-				if (map_level(g.m, d) >= 0 && map_level(g.m, d) < lvl && in_neighbors_of(g, cell, d) &&
-				    lookup_owner(g, d) >= 0)
-					return DCCRGX_ENOTFOUND;
+			// a coarser neighbors_of entry in the set (2480-2490): per hood item
+			// the level lvl - 1 leaf holding the item box's min corner (nof_item:
+			// the coarser neighbor of a 2:1-balanced mesh), tested against the
+			// set first and looked up only when it is in it (not a
+			// walk of the whole set per call)
+			if (lvl > 0) {
+				uint64_t c[3];
+				map_indices(g.m, cell, c[0], c[1], c[2]);
+				const int64_t len = int64_t(1) << (g.R - lvl);
+				for (size_t k = 0; k + 2 < g.hood.size(); k += 3) {
+					uint64_t w[3];
+					bool inside = true;
+					for (int a = 0; a < 3 && inside; a++)
+						inside = map_wrap(g.m, a, int64_t(c[a]) + int64_t(g.hood[k + size_t(a)]) * len, w[a]);
+					if (!inside) continue;
+					const uint64_t pl = uint64_t(len) * 2;
+					const uint64_t p = map_from_indices(g.m, w[0] & ~(pl - 1), w[1] & ~(pl - 1), w[2] & ~(pl - 1), lvl - 1);
+					if (g.dont_refine_cells.count(p) && lookup_owner(g, p) >= 0) return DCCRGX_ENOTFOUND;
+				}
+			}
 		}
 		g.refine_requests.insert(cell);
 		return 0;

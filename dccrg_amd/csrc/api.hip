@@ -779,6 +779,10 @@ void phase_add(const char* name, double seconds) {
 	e.second += 1;
 }
 void phase_reset() { phase_table().t.clear(); }
+double& phase_comm_total() {
+	static double t = 0;
+	return t;
+}
 #endif
 
 }  // namespace dccrgx

@@ -141,7 +141,7 @@ static void move_bytes(Grid& g, const std::vector<DevMsg>& msgs, hipStream_t s) 
 	// piece boundaries are this side's own business: contiguous pieces are
 	// copied at once (a single-field halo under send_single_cells is one copy
 	// per peer, not one per cell)
-	DX_PHASE("comm.host_move_bytes", s);
+	DX_PHASE_COMM("comm.host_move_bytes", s);
 	coalesce(snd);
 	coalesce(rcv);
 	const size_t P = size_t(g.size);

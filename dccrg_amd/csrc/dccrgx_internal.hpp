@@ -53,38 +53,51 @@ struct Error : std::runtime_error {
 #if DCCRGX_PHASE_TIMING
 void phase_add(const char* name, double seconds);
 void phase_reset();
+// seconds spent in the transport's byte mover so far (comm.hip), so that a
+// lap can book its time without the transport under "<name>.net"
+double& phase_comm_total();
 struct PhaseScope {
 	const char* name;
 	hipStream_t s;
 	double t0;
+	bool comm;
 	static double now();
-	PhaseScope(const char* n, hipStream_t st) : name(n), s(st), t0(now()) {}
+	PhaseScope(const char* n, hipStream_t st, bool is_comm = false) : name(n), s(st), t0(now()), comm(is_comm) {}
 	~PhaseScope() {
 		(void)hipStreamSynchronize(s);
-		phase_add(name, now() - t0);
+		const double d = now() - t0;
+		phase_add(name, d);
+		if (comm) phase_comm_total() += d;
 	}
 };
 // laps: DX_LAPS(stream) starts a lap clock in this scope, DX_LAP("name")
-// books the time since the previous lap (stream drained) under name
+// books the time since the previous lap (stream drained) under name, and
+// that time less the transport's inside it under "name.net"
 struct PhaseLaps {
 	hipStream_t s;
-	double t;
-	explicit PhaseLaps(hipStream_t st) : s(st), t(PhaseScope::now()) {}
+	double t, c;
+	explicit PhaseLaps(hipStream_t st) : s(st), t(PhaseScope::now()), c(phase_comm_total()) {}
 	void lap(const char* name) {
 		(void)hipStreamSynchronize(s);
-		const double n = PhaseScope::now();
+		const double n = PhaseScope::now(), cn = phase_comm_total();
 		phase_add(name, n - t);
+		if (cn > c) phase_add((std::string(name) + ".net").c_str(), (n - t) - (cn - c));
 		t = n;
+		c = cn;
 	}
 };
 #define DX_PHASE_CAT2(a, b) a##b
 #define DX_PHASE_CAT(a, b) DX_PHASE_CAT2(a, b)
 #define DX_PHASE(name, s) ::dccrgx::PhaseScope DX_PHASE_CAT(dx_phase_, __LINE__)(name, s)
+#define DX_PHASE_COMM(name, s) ::dccrgx::PhaseScope DX_PHASE_CAT(dx_phase_, __LINE__)(name, s, true)
 #define DX_LAPS(s) ::dccrgx::PhaseLaps dx_laps_(s)
 #define DX_LAP(name) dx_laps_.lap(name)
 #else
 #define DX_PHASE(name, s) \
 	do {                  \
+	} while (0)
+#define DX_PHASE_COMM(name, s) \
+	do {                       \
 	} while (0)
 #define DX_LAPS(s) \
 	do {           \
@@ -174,7 +187,9 @@ struct DBuf {
 
 // bytes from the device into host memory, s drained first (copy + sync);
 // reads of up to kSmallRead bytes go through a pinned staging buffer
-constexpr size_t kSmallRead = 64 * 1024;
+// (round 6: 4 MiB, the adaptive step's request lists of ~200 KB took 45-65 us
+// each through pageable memory)
+constexpr size_t kSmallRead = 4 * 1024 * 1024;
 void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s);
 // bytes from host memory to the device on s (list-sized ones staged through
 // pinned memory and completed on return); the host buffer may be reused on

@@ -137,13 +137,14 @@ void pool_free(void* raw, size_t cap) {
 	P.held += cap;
 }
 
-// Small device -> host reads (counters, totals, error flags) through a pinned
-// staging buffer per host thread: a pageable destination costs ~15 us more
-// per read than a pinned one on MI355X (scripts/microbench/d2h_small.hip:
-// 27 vs 15 us per kernel + read + sync, 12 for the sync alone), and an
-// adaptive step makes a few dozen such reads.  The buffer is kept for the
-// thread's life (never freed: a thread_local destructor may run after the
-// HIP runtime is gone).
+// Device -> host reads of up to kSmallRead bytes (counters, totals, error
+// flags, the adaptive step's lists) through a pinned staging buffer per host
+// thread: a pageable destination costs ~15 us more per small read than a
+// pinned one on MI355X (scripts/microbench/d2h_small.hip: 27 vs 15 us per
+// kernel + read + sync, 12 for the sync alone), and list-sized reads (~200
+// KB) 45-65 us through pageable memory in the adaptive step's HIP trace
+// (r06m).  The buffer is kept for the thread's life (never freed: a
+// thread_local destructor may run after the HIP runtime is gone).
 void d2h_small(void* host, const void* dev, size_t bytes, hipStream_t s) {
 	if (!bytes) return;
 	thread_local void* stage = nullptr;

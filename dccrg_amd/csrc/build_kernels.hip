@@ -398,6 +398,30 @@ __global__ void extract_send_kernel(const uint64_t* nto_id, const uint32_t* nto_
 	}
 }
 
+// the remote ids of a neighbors_to list whose (owner, id) key is not among
+// the sorted neighbors_of keys: cells that only this rank's cells' neighbors_to
+// reach (the reference's remote neighbors_to-only copies)
+__global__ void extract_extra_kernel(const uint64_t* ids, size_t n, DevMesh M, int rank, uint64_t stride,
+                                     const uint64_t* of_keys, size_t n_of, uint64_t* out, unsigned long long* counter) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		const uint64_t id = ids[i];
+		if (id == error_cell) continue;
+		const int32_t o = dm_owner(M, id);
+		if (o < 0 || o == rank) continue;
+		const uint64_t key = uint64_t(o) * stride + id;
+		size_t lo = 0, hi = n_of;
+		while (lo < hi) {
+			const size_t mid = (lo + hi) >> 1;
+			if (of_keys[mid] < key)
+				lo = mid + 1;
+			else
+				hi = mid;
+		}
+		if (lo < n_of && of_keys[lo] == key) continue;
+		out[atomicAdd(counter, 1ull)] = id;
+	}
+}
+
 // 1 where a (owner, id) pair differs from the one before it
 __global__ void pair_heads_kernel(const uint64_t* ids, const uint32_t* owners, size_t n, uint8_t* head) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
@@ -1271,10 +1295,10 @@ static void zero_counter(DBuf<unsigned long long>& ctr, hipStream_t s) {
 // the n extracted entries grouped by owner, each group's ids ascending and
 // unique: one 64-bit key sort, or for pairs a sort by id then a stable sort
 // by owner and a select of the pair heads
-static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t stride, int size,
-                           std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
+static size_t group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t stride, int size,
+                             std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
 	out.clear();
-	if (!n) return;
+	if (!n) return 0;
 	if (!owners) {
 		// keys = owner * stride + id < size * stride: only those bits sorted
 		int bits = 1;
@@ -1282,7 +1306,7 @@ static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t 
 		while (bits < 64 && (top >> bits)) bits++;
 		n = sort_unique_u64(keys, n, s, bits);
 		for (uint64_t k : download(keys, n, s)) out[int(k / stride)].push_back(k % stride);
-		return;
+		return n;
 	}
 	DBuf<uint64_t> k2;
 	DBuf<uint32_t> o2;
@@ -1312,11 +1336,13 @@ static void group_by_owner(uint64_t* keys, uint32_t* owners, size_t n, uint64_t 
 	const std::vector<uint64_t> ids = download(k2.p, u, s);
 	const std::vector<uint32_t> own = download(o2.p, u, s);
 	for (size_t i = 0; i < u; i++) out[int(own[i])].push_back(ids[i]);
+	return u;
 }
 
 void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size,
-                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s) {
+                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s, DBuf<uint64_t>* keep, size_t* keep_n) {
 	out.clear();
+	if (keep_n) *keep_n = 0;
 	if (!n) return;
 	const uint64_t stride = M.last + 1;
 	const bool pairs = uint64_t(size) > ~uint64_t(0) / stride;
@@ -1328,7 +1354,32 @@ void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank
 	zero_counter(ctr, s);
 	extract_remote_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, rank, stride, keys.p, owners.p, ctr.p);
 	HIP_CHECK(hipGetLastError());
-	group_by_owner(keys.p, owners.p, read_counter(ctr, s), stride, size, out, s);
+	const size_t u = group_by_owner(keys.p, owners.p, read_counter(ctr, s), stride, size, out, s);
+	if (keep && !pairs) {
+		keep->swap(keys);  // sorted unique (owner * stride + id) keys
+		*keep_n = u;
+	}
+}
+
+bool k_remote_extra(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size, const uint64_t* of_keys,
+                    size_t n_of, std::vector<uint64_t>& out, hipStream_t s) {
+	out.clear();
+	const uint64_t stride = M.last + 1;
+	if (uint64_t(size) > ~uint64_t(0) / stride) return false;  // keys would overflow: the caller's pair path
+	if (!n) return true;
+	DBuf<uint64_t> ex;
+	ex.alloc(n);
+	DBuf<unsigned long long> ctr;
+	zero_counter(ctr, s);
+	extract_extra_kernel<<<grid_for(n, 256), 256, 0, s>>>(ids, n, M, rank, stride, of_keys, n_of, ex.p, ctr.p);
+	HIP_CHECK(hipGetLastError());
+	const size_t k = read_counter(ctr, s);
+	if (k) {
+		out = download(ex.p, k, s);
+		std::sort(out.begin(), out.end());
+		out.erase(std::unique(out.begin(), out.end()), out.end());
+	}
+	return true;
 }
 
 void k_send_by_owner(const uint64_t* nto_id, const uint32_t* nto_ptr, size_t n_entries, const uint64_t* slot_ids,

@@ -572,6 +572,13 @@ struct Grid {
 	// own instead of clearing the whole map
 	DBuf<int2> rmap_full;
 	bool rmap_full_clean = true;  // every entry {-1, -1}
+	// a cleared per-level range map (every entry {-1, -1}) over rmap_spare_rl:
+	// the previous explicit mesh's map, its entries cleared one by one at the
+	// end of rebuild, taken by the next mesh whose level ranges it covers (no
+	// memset of the ranges; slabs of several processes)
+	DBuf<int2> rmap_spare;
+	RangeLevel rmap_spare_rl[kRangeLevels] = {};
+	int rmap_spare_rlev = 0;
 	DBuf<double> red_all;  // P x count all-gathered values of comm_allreduce_f64_dev (s_comp only)
 	// pinned host staging of the host-exchange transport (comm.hip
 	// move_bytes), grow-only, freed with the grid: the device <-> host legs
@@ -743,7 +750,7 @@ void mesh_materialize(Grid& g, Mesh& out);
 // after a repartition: own leaves known, ghosts fetched from their owners
 void mesh_from_local(Grid& g, Mesh& out, DBuf<uint64_t>& local, size_t n_local);
 // (entries i < slot_upto get slot i, the others -1)
-void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
+void mesh_build_range(Grid& g, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
                       size_t slot_upto);
 bool k_level_ranges(const MapCtx& m, const uint64_t* ids, size_t n, uint64_t* lo, uint64_t* hi, hipStream_t s);
 void k_range_insert(int2* rmap, const DevMesh& M, const uint64_t* ids, const int32_t* owners, size_t n, size_t slot_upto,
@@ -813,8 +820,16 @@ int max_hood_items();  // largest stencil the neighbors_to dedupe can hold in LD
 // the entries of an id array owned by another process, grouped by owner
 // (each group ascending, unique); device sorts of owner * (last + 1) + id
 // keys, or of (owner, id) pairs when the ids leave no room for the owner
+// remote ids of `ids` grouped by owner, each group ascending; `keep` (when
+// given) receives the sorted unique (owner * (last + 1) + id) keys on the
+// device and `keep_n` their count (0 and no keys when the keys would overflow)
 void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size,
-                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s);
+                       std::map<int, std::vector<uint64_t>>& out, hipStream_t s, DBuf<uint64_t>* keep = nullptr,
+                       size_t* keep_n = nullptr);
+// the remote ids of `ids` whose key is not among `of_keys` (kept by
+// k_remote_by_owner), ascending; false when keys would overflow
+bool k_remote_extra(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size, const uint64_t* of_keys,
+                    size_t n_of, std::vector<uint64_t>& out, hipStream_t s);
 // the send side: for each neighbors_to entry (n_entries in all) with a remote
 // owner, the row's own id under that owner
 void k_send_by_owner(const uint64_t* nto_id, const uint32_t* nto_ptr, size_t n_entries, const uint64_t* slot_ids,

@@ -83,34 +83,89 @@ void mesh_build_hash(Mesh& M, const uint64_t* ids, const int32_t* owners, size_t
 
 // The range map (dccrgx_mesh.hpp) when the known ids' per-level ranges hold
 // at most 32 ids per known leaf (+16 M) - one process, or slab partitions -
-// else the hash table.  DCCRGX_RANGE_MAP=0 forces the table.
-void mesh_build_range(const MapCtx& m, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
+// else the hash table.  DCCRGX_RANGE_MAP=0 forces the table.  The grid's
+// cleared spare map (the previous mesh's, Grid::rmap_spare) is taken when its
+// ranges cover these, so a mesh that changes every step (adaptive runs on
+// slabs) writes only its own entries; a map made afresh gets a quarter of
+// each level's range as room on either side (within the level, and the
+// 32-per-leaf bound) so that the next meshes' ranges fit in it too.
+// DCCRGX_RANGE_SPARE=0 always makes the map afresh, without room.
+void mesh_build_range(Grid& g, Mesh& M, const uint64_t* ids, const int32_t* owners, size_t n, hipStream_t s,
                       size_t slot_upto) {
 	static const char* env = std::getenv("DCCRGX_RANGE_MAP");
+	static const char* senv = std::getenv("DCCRGX_RANGE_SPARE");
 	const bool allowed = !(env && env[0] == '0');
+	const bool spare_ok = !(senv && senv[0] == '0');
+	const MapCtx& m = g.m;
 	uint64_t lo[kRangeLevels], hi[kRangeLevels];
 	M.rmap.release();
 	M.rlev = 0;
-	if (allowed && n && k_level_ranges(m, ids, n, lo, hi, s)) {
-		uint64_t total = 0;
-		std::vector<RangeLevel> rl;
-		for (int L = 0; L < kRangeLevels; L++) {
-			if (hi[L] == 0) continue;  // no id of this level
-			rl.push_back(RangeLevel{lo[L], hi[L] + 1, total});
-			total += hi[L] + 1 - lo[L];
+	bool ranged;
+	{
+		DX_PHASE("rb.1a0_level_ranges", s);
+		ranged = allowed && n && k_level_ranges(m, ids, n, lo, hi, s);
+	}
+	if (ranged) {
+		const uint64_t limit = 32 * uint64_t(n) + (uint64_t(1) << 24);
+		// the spare covers every level's range: take it as it is
+		bool covered = spare_ok && g.rmap_spare.p && g.rmap_spare_rlev > 0;
+		for (int L = 0; covered && L < kRangeLevels; L++) {
+			if (hi[L] == 0) continue;
+			bool in = false;
+			for (int q = 0; q < g.rmap_spare_rlev; q++)
+				in = in || (g.rmap_spare_rl[q].lo <= lo[L] && hi[L] < g.rmap_spare_rl[q].hi);
+			covered = in;
 		}
-		if (total <= 32 * uint64_t(n) + (uint64_t(1) << 24) && total < (uint64_t(1) << 31)) {
-			M.rlev = int(rl.size());
-			for (int L = 0; L < M.rlev; L++) M.rl[L] = rl[size_t(L)];
-			M.rmap.alloc(size_t(total));
-			HIP_CHECK(hipMemsetAsync(M.rmap.p, 0xff, size_t(total) * sizeof(int2), s));
+		if (covered && g.rmap_spare.n <= 2 * limit) {
+			M.rmap.swap(g.rmap_spare);
+			M.rlev = g.rmap_spare_rlev;
+			for (int L = 0; L < M.rlev; L++) M.rl[L] = g.rmap_spare_rl[L];
+			g.rmap_spare_rlev = 0;
 			M.tab.release();
 			M.mask = 0;
 			k_range_insert(M.rmap.p, M.dev(m.last), ids, owners, n, slot_upto, s);
 			return;
 		}
+		g.rmap_spare.release();
+		g.rmap_spare_rlev = 0;
+		for (int room = spare_ok ? 1 : 0; room >= 0; room--) {
+			uint64_t total = 0;
+			std::vector<RangeLevel> rl;
+			for (int L = 0; L < kRangeLevels; L++) {
+				if (hi[L] == 0) continue;  // no id of this level
+				uint64_t a = lo[L], b = hi[L] + 1;
+				if (room && L <= m.R) {
+					const uint64_t w = (b - a) / 4;
+					a = std::max<uint64_t>(m.first[L], a > w ? a - w : 0);
+					b = std::min<uint64_t>(m.first[L + 1], b + w);
+				}
+				rl.push_back(RangeLevel{a, b, total});
+				total += b - a;
+			}
+			if (total <= limit && total < (uint64_t(1) << 31)) {
+				M.rlev = int(rl.size());
+				for (int L = 0; L < M.rlev; L++) M.rl[L] = rl[size_t(L)];
+				M.rmap.alloc(size_t(total));
+				HIP_CHECK(hipMemsetAsync(M.rmap.p, 0xff, size_t(total) * sizeof(int2), s));
+				M.tab.release();
+				M.mask = 0;
+				k_range_insert(M.rmap.p, M.dev(m.last), ids, owners, n, slot_upto, s);
+				return;
+			}
+		}
 	}
 	mesh_build_hash(M, ids, owners, n, s, slot_upto);
+}
+
+// the retiring mesh's own range map, its entries cleared, as the grid's spare
+static void mesh_retire_range(Grid& g, Mesh& old, hipStream_t s) {
+	static const char* senv = std::getenv("DCCRGX_RANGE_SPARE");
+	if ((senv && senv[0] == '0') || !old.rmap.p || old.rmap_shared || old.implicit || !old.rlev) return;
+	if (old.n_known) k_range_clear(old.rmap.p, old.dev(g.m.last), old.kid.p, old.n_known, s);
+	g.rmap_spare.swap(old.rmap);
+	old.rmap.release();
+	for (int L = 0; L < old.rlev; L++) g.rmap_spare_rl[L] = old.rl[L];
+	g.rmap_spare_rlev = old.rlev;
 }
 
 // rebuild's direct mode (one process, the own leaves in slot order): the
@@ -335,7 +390,7 @@ void rebuild(Grid& g, Mesh& nm) {
 			// a mesh of its own; the shared map (if the previous mesh used it)
 			// keeps that mesh's entries
 			if (old.rmap_shared) g.rmap_full_clean = false;
-			mesh_build_range(m, M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
+			mesh_build_range(g, M, M.kid.p, M.kown.p, M.n_known, s, direct ? M.n_prefix : 0);
 		}
 		DX_LAP("rb.1a_hash");
 		solo = direct && g.size == 1;
@@ -441,18 +496,36 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, lsp, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
 		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, p_to.p, to_id.p, s);
 		DX_LAP("rb.3a_outer_rows");
-		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s);
+		DBuf<uint64_t> of_keys;
+		size_t n_of_keys = 0;
+		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s, &of_keys, &n_of_keys);
+		DX_LAP("rb.3b_recv_lists");
 		k_send_by_owner(to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
-		std::map<int, std::vector<uint64_t>> rem_to;
-		k_remote_by_owner(to_id.p, t_to, dm, g.rank, g.size, rem_to, s);
+		DX_LAP("rb.3c_send_lists");
+		// remote neighbors_to that are no neighbors_of: found on the device
+		// (none for a symmetric neighborhood), the pairs path on the host
 		std::vector<uint64_t> extra;
-		for (auto& kv : rem_to) {
-			const auto it = H.recv_ids.find(kv.first);
-			for (uint64_t id : kv.second)
-				if (it == H.recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id))
-					extra.push_back(id);
+		if (!k_remote_extra(to_id.p, t_to, dm, g.rank, g.size, of_keys.p, n_of_keys, extra, s)) {
+			std::map<int, std::vector<uint64_t>> rem_to;
+			k_remote_by_owner(to_id.p, t_to, dm, g.rank, g.size, rem_to, s);
+			for (auto& kv : rem_to) {
+				const auto it = H.recv_ids.find(kv.first);
+				for (uint64_t id : kv.second)
+					if (it == H.recv_ids.end() || !std::binary_search(it->second.begin(), it->second.end(), id))
+						extra.push_back(id);
+			}
+			std::sort(extra.begin(), extra.end());
 		}
-		std::sort(extra.begin(), extra.end());
+		DX_LAP("rb.3d_extra");
+#if DCCRGX_PHASE_TIMING
+		if (std::getenv("DCCRGX_MESH_NOTES")) {
+			size_t nr = 0, ns = 0;
+			for (auto& kv : H.recv_ids) nr += kv.second.size();
+			for (auto& kv : H.send_ids) ns += kv.second.size();
+			std::fprintf(stderr, "[mesh r%d] of entries %zu to entries %zu recv %zu send %zu extra %zu\n", g.rank, t_of,
+			             t_to, nr, ns, extra.size());
+		}
+#endif
 		g.extra_remote = extra;
 	}
 	g.peers = H.peers();
@@ -575,6 +648,8 @@ void rebuild(Grid& g, Mesh& nm) {
 		HIP_CHECK(hipStreamSynchronize(s));
 	}
 	DX_LAP("rb.7_known_order");
+	mesh_retire_range(g, old, s);  // after the carry step, the last reader of the old map
+	DX_LAP("rb.8_retire_map");
 	g.csr_valid = false;
 	g.face_valid = false;
 	g.tiles_valid = false;

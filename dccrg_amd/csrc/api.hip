@@ -2710,7 +2710,8 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			// on the device: refine requests, whole-family decisions, partial runs
 			// one process with Morton-ordered slots: each family's leaves are one run
 			const bool solo = g.size == 1 && g.morton_slots;
-			AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.s_comp);
+			AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.rank, g.s_comp);
+			DX_LAP("chk.2a_device_requests");
 			// 2434-2520 (bulk lists: no set hashing of ~20 K ids per step)
 			g.refine_bulk.insert(g.refine_bulk.end(), q.refine.begin(), q.refine.end());
 			if (g.refine_requests.empty() && !q.refine.empty()) {

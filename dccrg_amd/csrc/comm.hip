@@ -240,6 +240,33 @@ std::vector<std::vector<uint8_t>> comm_exchange(Grid& g, const std::vector<std::
 	hipStream_t s = g.s_comm;
 	std::vector<uint64_t> ssz(size_t(P), 0);
 	for (int p = 0; p < P; p++) ssz[size_t(p)] = p == g.rank ? 0 : send[size_t(p)].size();
+	if (g.xfn) {
+		// the host exchange moves host bytes: the lists go to it as they are
+		// (no device staging), the sizes first
+		DX_PHASE_COMM("comm.host_exchange_lists", s);
+		static uint64_t none = 0;
+		std::vector<uint64_t> rsz(size_t(P), 0);
+		std::vector<const void*> sp(size_t(P), &none);
+		std::vector<void*> rp(size_t(P), &none);
+		std::vector<size_t> sb(size_t(P), 0), rb(size_t(P), 0);
+		for (int p = 0; p < P; p++) {
+			if (p == g.rank) continue;
+			sp[size_t(p)] = &ssz[size_t(p)];
+			rp[size_t(p)] = &rsz[size_t(p)];
+			sb[size_t(p)] = rb[size_t(p)] = 8;
+		}
+		DX_REQUIRE(g.xfn(g.xctx, sp.data(), sb.data(), rp.data(), rb.data()) == 0, "exchange function failed");
+		for (int p = 0; p < P; p++) {
+			if (p == g.rank) continue;
+			recv[size_t(p)].resize(size_t(rsz[size_t(p)]));
+			sp[size_t(p)] = ssz[size_t(p)] ? static_cast<const void*>(send[size_t(p)].data()) : &none;
+			rp[size_t(p)] = rsz[size_t(p)] ? static_cast<void*>(recv[size_t(p)].data()) : &none;
+			sb[size_t(p)] = size_t(ssz[size_t(p)]);
+			rb[size_t(p)] = size_t(rsz[size_t(p)]);
+		}
+		DX_REQUIRE(g.xfn(g.xctx, sp.data(), sb.data(), rp.data(), rb.data()) == 0, "exchange function failed");
+		return recv;
+	}
 	DBuf<uint64_t> dsz, drsz;
 	upload(dsz, ssz, s);
 	drsz.alloc(size_t(P));

@@ -969,7 +969,7 @@ struct AdvRequests {
 	std::vector<uint8_t> part_bands;
 };
 AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
-                           bool solo, hipStream_t s);
+                           bool solo, int rank, hipStream_t s);
 void k_adv_bands(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,
                  double diff_increase, double diff_threshold, double unrefine_sensitivity, uint8_t* band,
                  hipStream_t s);

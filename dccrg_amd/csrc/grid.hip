@@ -423,6 +423,27 @@ void halo_message_size(Grid& g, int hood, int peer, size_t& sb, size_t& rb) {
 
 // --------------------------------------------------------------------------- refinement
 static std::vector<uint64_t> union_sorted(Grid& g, const std::vector<std::vector<uint64_t>>& all) {
+	// every rank's list ascending (as gather_union's callers give them): merged
+	// pairwise on the host, O(n log P), no device round trip
+	bool sorted = true;
+	for (const auto& v : all) sorted = sorted && std::is_sorted(v.begin(), v.end());
+	if (sorted) {
+		std::vector<std::vector<uint64_t>> parts(all.begin(), all.end());
+		while (parts.size() > 1) {
+			std::vector<std::vector<uint64_t>> next;
+			for (size_t i = 0; i + 1 < parts.size(); i += 2) {
+				std::vector<uint64_t> mg;
+				mg.reserve(parts[i].size() + parts[i + 1].size());
+				std::merge(parts[i].begin(), parts[i].end(), parts[i + 1].begin(), parts[i + 1].end(), std::back_inserter(mg));
+				next.push_back(std::move(mg));
+			}
+			if (parts.size() % 2) next.push_back(std::move(parts.back()));
+			parts.swap(next);
+		}
+		std::vector<uint64_t> u = parts.empty() ? std::vector<uint64_t>{} : std::move(parts[0]);
+		u.erase(std::unique(u.begin(), u.end()), u.end());
+		return u;
+	}
 	std::vector<uint64_t> u;
 	for (const auto& v : all) u.insert(u.end(), v.begin(), v.end());
 	host_sort_u64(u, true, g.s_comp);
@@ -459,11 +480,20 @@ static bool close_set(Grid& g, std::vector<uint64_t>& S, bool finer, const uint6
 	std::vector<uint64_t> fresh = S;
 	bool grew = false;
 	while (true) {
-		const std::vector<uint64_t> found = k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh,
-		                                                      g.s_comp, finer, grew ? nullptr : dS);
+		DX_PHASE("cs.round", g.s_comp);
+		std::vector<uint64_t> found;
+		{
+			DX_PHASE("cs.induced", g.s_comp);
+			found = k_induced_refines(g.m, g.d_hood.p, g.d_hood_to.p, nh, g.dm(), g.rank, fresh, g.s_comp, finer,
+			                          grew ? nullptr : dS);
+		}
 		std::vector<uint64_t> mine_new;
 		std::set_difference(found.begin(), found.end(), S.begin(), S.end(), std::back_inserter(mine_new));
-		const std::vector<uint64_t> all = gather_union(g, std::move(mine_new));
+		std::vector<uint64_t> all;
+		{
+			DX_PHASE("cs.gather", g.s_comp);
+			all = gather_union(g, std::move(mine_new));
+		}
 		fresh.clear();
 		std::set_difference(all.begin(), all.end(), S.begin(), S.end(), std::back_inserter(fresh));
 		if (fresh.empty()) break;

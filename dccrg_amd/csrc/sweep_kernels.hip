@@ -1514,7 +1514,7 @@ __device__ __forceinline__ void block_reserve4(unsigned long long* __restrict__ 
 template <int BS>
 __global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, const uint64_t* __restrict__ ids,
                                                                const uint8_t* __restrict__ band, size_t n, bool solo,
-                                                               uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
+                                                               int rank, uint64_t* __restrict__ ref, uint64_t* __restrict__ unref,
                                                                uint32_t* __restrict__ part,
                                                                unsigned long long* __restrict__ cnt) {
 	constexpr int kJ = 8;
@@ -1575,12 +1575,49 @@ __global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, c
 				k++;
 			}
 			bool whole = !solo;  // every child of p is a leaf (some held elsewhere)
+			// every child of p a local leaf (a family split between the inner
+			// and outer runs): decided here, by the run headed by the first child
+			// (-1: not local, 1: this run decides, 2: another run does)
+			int local = 0;
+			bool keep8 = false;
+			if (k < 8 && whole) {
+				// the slot just before or just after the run holding a child of a
+				// sibling (a grandchild of p) settles it without lookups
+				uint64_t after = ~uint64_t(0);
+#pragma unroll
+				for (int q = 1; q < 8; q++)
+					if (uint32_t(q) == k) after = nx[q - 1];
+				auto grandchild_of_p = [&](uint64_t par_of_slot) {
+					return par_of_slot != ~uint64_t(0) && map_level(m, par_of_slot) > 0 && map_parent(m, par_of_slot) == p;
+				};
+				if (grandchild_of_p(prev) || grandchild_of_p(after)) whole = false;
+			}
 			if (k < 8 && whole) {
 				uint64_t ch[8];
 				map_all_children(m, p, ch);
-				for (int i = 0; i < 8; i++) whole = whole && dm_owner(M, ch[i]) >= 0;
+				local = 1;
+				for (int i = 0; i < 8; i++) {
+					int32_t o = -1, sl = -1;
+					if (!dm_lookup(M, ch[i], o, sl)) {
+						whole = false;
+						break;
+					}
+					if (o != rank || sl < 0 || size_t(sl) >= n) local = -1;
+					else keep8 = keep8 || band[sl] >= 1;
+				}
+				if (local == 1 && ids[sj] != ch[0]) local = 2;
 			}
-			if (k < 8 && !whole) {
+			if (k < 8 && whole && local == 2) {
+				// counted by the run of the first child
+			} else if (k < 8 && whole && local == 1) {
+				// 2679-2733 as decide() on the host: a kept family is counted, a
+				// whole local family not kept is unrefined (its first child's id)
+				if (keep8) ck++;
+				else {
+					what |= 8;
+					cu++;
+				}
+			} else if (k < 8 && !whole) {
 				// a sibling has children: the family cannot be unrefined in
 				// this round (unrefine_completely refuses, a dont_unrefine mark
 				// changes nothing), so the host never sees it; counted as the
@@ -1976,7 +2013,7 @@ static void k_gather_ids_bands(const uint64_t* ids, const uint8_t* band, const u
 }
 
 AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* slot_ids, const uint8_t* band, size_t n,
-                           bool solo, hipStream_t s) {
+                           bool solo, int rank, hipStream_t s) {
 	AdvRequests out;
 	if (!n) return out;
 	DX_REQUIRE(n < (size_t(1) << 28), "too many local cells for the request runs");
@@ -1989,7 +2026,7 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	cnt.alloc(4);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
 	adv_requests_kernel<1024><<<unsigned((n + 1024 * 8 - 1) / (1024 * 8)), 1024, 0, s>>>(m, dm, slot_ids, band, n, solo,
-	                                                                                    ref.p, unref.p, part.p, cnt.p);
+	                                                                                    rank, ref.p, unref.p, part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	d2h_small(h, cnt.p, sizeof(h), s);

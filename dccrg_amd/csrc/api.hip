@@ -2719,7 +2719,7 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 				g.refine_dev = std::move(q.refine_dev);
 				g.refine_dev_valid = true;
 			}
-			if (solo && g.unrefine_requests.empty() && !q.unrefine.empty()) {
+			if (g.unrefine_requests.empty() && !q.unrefine.empty()) {
 				g.unrefine_dev = std::move(q.unrefine_dev);
 				g.unrefine_dev_valid = true;
 			}

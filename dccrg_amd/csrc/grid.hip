@@ -625,7 +625,9 @@ void stop_refining_impl(Grid& g) {
 	}
 	g.refine_requests.clear();
 	g.refine_bulk.clear();
+	DX_LAP("sr.2a_mine");
 	std::vector<uint64_t> S = gather_union(g, std::move(mine));
+	DX_LAP("sr.2b_gather_S");
 	bool s_on_dev = dev_rq && !S.empty();
 	if (!S.empty() && close_set(g, S, false, s_on_dev ? dS.p : nullptr)) s_on_dev = false;
 	DX_LAP("sr.2_induce_refines");
@@ -636,7 +638,7 @@ void stop_refining_impl(Grid& g) {
 	// (the requests exactly check_for_adaptation's device list of family
 	// heads: read there, no upload, no sort of their parents)
 	DBuf<uint64_t> dUR;
-	const bool dev_ur = g.unrefine_dev_valid && g.unrefine_requests.empty() && g.size == 1;
+	const bool dev_ur = g.unrefine_dev_valid && g.unrefine_requests.empty();
 	if (dev_ur) dUR = std::move(g.unrefine_dev);
 	g.unrefine_dev_valid = false;
 	g.unrefine_dev.release();
@@ -649,8 +651,10 @@ void stop_refining_impl(Grid& g) {
 	DX_LAP("sr.3a_requests");
 	// S is final: one device copy for the passes below
 	if (!s_on_dev) upload(dS, S, s);
+	DX_LAP("sr.3b_upload_S");
 	const std::vector<uint64_t> fmine =
 	    k_unrefine_families(g.m, g.d_hood.p, nh, g.dm(), req, S, DU, s, dS.p, dev_ur ? dUR.p : nullptr);
+	DX_LAP("sr.3c_families");
 	const std::vector<uint64_t> F = gather_union(g, fmine);
 	DBuf<uint64_t> dF;
 	upload(dF, F, s);

@@ -2478,8 +2478,26 @@ int dccrgx_advection_step(dccrgx_grid* gp, const int fids[7], double dt, int reg
 			if (s0 < g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 0, dt, g.s_comp, rec);
 			if (s1 > g.n_inner) k_advection_tiles(f, (double*)rho.scratch.p, g, 1, dt, g.s_comp, rec);
 		} else {
+			// the bands of the check that follows computed by the sweep (with the
+			// last check's parameters), recorded per run for band_cache_ok
+			const char* bc = std::getenv("DCCRGX_BAND_CACHE");  // read per call: tests switch it
+			const bool bands = g.band_params_valid && !(bc && bc[0] == '0') && !rho.external;
+			BandArgs B{};
+			if (bands) {
+				if (g.band_cache.n < g.n_local + 1) {
+					g.band_cache.alloc(g.n_local + 1);
+					g.band_rec[0].valid = g.band_rec[1].valid = false;
+				}
+				B = BandArgs{g.m, g.slot_lvl.p, g.slot_ids.p, g.band_inc, g.band_thr, g.band_uns, g.band_cache.p};
+				for (int run = 0; run < 2; run++) {
+					const size_t r0 = run == 0 ? 0 : g.n_inner, r1 = run == 0 ? g.n_inner : g.n_local;
+					if (r1 > r0 && s0 <= r0 && s1 >= r1)
+						g.band_rec[run] = Grid::BandRec{true, g.face_gen, rho.epoch, rho.local_epoch, rho.data.p};
+				}
+			}
 			k_time_begin(g);
-			k_advection_ell(f, (double*)rho.scratch.p, g.face_ell.p, g.face_fine.p, s0, s1, dt, g.s_comp);
+			k_advection_ell(f, (double*)rho.scratch.p, g.face_ell.p, g.face_fine.p, s0, s1, dt, g.s_comp,
+			                bands ? &B : nullptr);
 		}
 		k_time_end(g);
 		DX_LAP("step.1_sweep");
@@ -2639,6 +2657,24 @@ int dccrgx_advection_refine_candidates(dccrgx_grid* gp, int df, double diff_incr
 	});
 }
 
+// The sweep's bands (advection_step) stand for adv_bands_kernel's when the
+// same parameters were given, the face table is the one swept, and the
+// density array has not been written since: the inner run reads no remote
+// copy, so only local writes matter there; the outer run's rows read the
+// copies the halo placed before it.
+static bool band_cache_ok(Grid& g, const Field& F, double inc, double thr, double uns) {
+	if (!g.band_params_valid || g.band_inc != inc || g.band_thr != thr || g.band_uns != uns || F.external) return false;
+	if (g.band_cache.n < g.n_local + 1 || !g.face_valid) return false;
+	for (int run = 0; run < 2; run++) {
+		const size_t r0 = run == 0 ? 0 : g.n_inner, r1 = run == 0 ? g.n_inner : g.n_local;
+		if (r1 <= r0) continue;
+		const Grid::BandRec& R = g.band_rec[run];
+		if (!R.valid || R.face_gen != g.face_gen || R.rho != F.data.p || R.local_epoch != F.local_epoch) return false;
+		if (run == 1 && R.epoch != F.epoch) return false;
+	}
+	return true;
+}
+
 // check_for_adaptation (tests/advection/adapter.hpp:47-178) + the requests
 // adapt_grid makes from its sets (187-231): per local cell the band of its
 // max_diff; band-2 cells are refined, a family with a band-1 member is kept
@@ -2662,11 +2698,22 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		ensure_face(g);
 		DX_LAP("chk.0_face");
 		const size_t n = g.n_local;
-		DBuf<uint8_t> band;
-		band.alloc(n + 1);
-		const FaceView fv{g.face_ell.p, g.face_fine.p, g.slot_ids.p, g.n_local};
-		k_adv_bands(g.m, (const double*)F.data.p, fv, g.slot_lvl.p, n, diff_increase, diff_threshold,
-		            unrefine_sensitivity, band.p, g.s_comp);
+		DBuf<uint8_t> band_own;
+		const uint8_t* band = nullptr;
+		if (band_cache_ok(g, F, diff_increase, diff_threshold, unrefine_sensitivity)) {
+			band = g.band_cache.p;  // the sweep's (advection_step)
+		} else {
+			band_own.alloc(n + 1);
+			const FaceView fv{g.face_ell.p, g.face_fine.p, g.slot_ids.p, g.n_local};
+			k_adv_bands(g.m, (const double*)F.data.p, fv, g.slot_lvl.p, n, diff_increase, diff_threshold,
+			            unrefine_sensitivity, band_own.p, g.s_comp);
+			band = band_own.p;
+		}
+		g.band_rec[0].valid = g.band_rec[1].valid = false;
+		g.band_params_valid = true;  // the next sweeps compute the bands with these
+		g.band_inc = diff_increase;
+		g.band_thr = diff_threshold;
+		g.band_uns = unrefine_sensitivity;
 		DX_LAP("chk.1_bands");
 		uint64_t nref = 0, nkeep = 0, nunref = 0;
 		// decide one family from its local members (bands bb, ids ii, k of
@@ -2710,7 +2757,7 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 			// on the device: refine requests, whole-family decisions, partial runs
 			// one process with Morton-ordered slots: each family's leaves are one run
 			const bool solo = g.size == 1 && g.morton_slots;
-			AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band.p, n, solo, g.rank, g.s_comp);
+			AdvRequests q = k_adv_requests(g.m, g.dm(), g.slot_ids.p, band, n, solo, g.rank, g.s_comp);
 			DX_LAP("chk.2a_device_requests");
 			// 2434-2520 (bulk lists: no set hashing of ~20 K ids per step)
 			g.refine_bulk.insert(g.refine_bulk.end(), q.refine.begin(), q.refine.end());
@@ -2735,7 +2782,7 @@ int dccrgx_advection_check_adaptation(dccrgx_grid* gp, int df, double diff_incre
 		} else {
 			// unrefine requests pending from before (or more local cells than
 			// the device runs encode): the same walk on the host
-			const std::vector<uint8_t> b = download(band.p, n, g.s_comp);
+			const std::vector<uint8_t> b = download(band, n, g.s_comp);
 			const auto& ids = slot_ids_host(g);
 			std::vector<uint8_t> rb;
 			std::vector<uint64_t> ri;

@@ -323,11 +323,19 @@ struct Field {
 	// cache is built from the field until the next structural change moves
 	// the array and voids that pointer)
 	uint64_t epoch = 0;
+	// writes of local slots only (epoch counts remote-copy writes too): a
+	// cache over the inner cells, which read no remote copy, checks this one
+	uint64_t local_epoch = 0;
 	bool external = false;
 	bool full_window() const { return win_off == 0 && win_len == elem; }
 };
 
-inline void field_written(Field& f) { f.epoch++; }
+inline void field_written(Field& f) {
+	f.epoch++;
+	f.local_epoch++;
+}
+// a write of the field's remote copies only (halo receives)
+inline void field_halo_written(Field& f) { f.epoch++; }
 
 // ---- Poisson BiCG (tests/poisson/poisson_solve.hpp) ------------------------
 // device pointers of one solve: user fields rhs / solution, the solver's own
@@ -596,6 +604,20 @@ struct Grid {
 		uint64_t epoch[6] = {0, 0, 0, 0, 0, 0};
 		size_t n_local = 0, nb = 0;
 	} dt_cache;
+	// check_for_adaptation's bands computed by the face-table sweep
+	// (advection_ell_lds_kernel<true>) with the parameters of the last check
+	// call, per run (0 inner, 1 outer): valid for the check that follows when
+	// the face table, the density array and its writes since are the ones the
+	// sweep saw (DCCRGX_BAND_CACHE=0: always the separate bands kernel)
+	DBuf<uint8_t> band_cache;
+	struct BandRec {
+		bool valid = false;
+		uint64_t face_gen = 0, epoch = 0, local_epoch = 0;
+		const void* rho = nullptr;
+	} band_rec[2];
+	bool band_params_valid = false;
+	double band_inc = 0, band_thr = 0, band_uns = 0;
+	uint64_t face_gen = 0;  // bumped by every face table build (ensure_face)
 
 	// local layout
 	size_t n_inner = 0, n_outer = 0, n_local = 0, n_recv = 0, n_slots = 0;
@@ -946,8 +968,17 @@ void k_advection_tiles(const double* const f[7], double* rho_out, Grid& g, int r
 // (or DCCRGX_NBREC=0): the sweeps then read the fields
 const double* ensure_nbrec(Grid& g, const int fids[7]);
 void k_nbrec(const double* const f[7], size_t n, double* r, hipStream_t s);
+// the bands of check_for_adaptation (adv_bands_kernel) written by the sweep
+// as well, for rows [s0, s1) of `band`
+struct BandArgs {
+	MapCtx m;
+	const uint8_t* lvl8;
+	const uint64_t* slot_ids;
+	double inc, thr, uns;
+	uint8_t* band;
+};
 void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
-                     size_t s1, double dt, hipStream_t s);
+                     size_t s1, double dt, hipStream_t s, const BandArgs* bands = nullptr);
 void k_adv_dt(const double* const f[7], size_t n, double* partial, size_t nblocks, hipStream_t s);
 void k_min_partials(const double* partial, size_t n, double* out, hipStream_t s);
 size_t k_adv_candidates(const MapCtx& m, const double* rho, const FaceView& F, const uint8_t* lvl8, size_t n,

@@ -224,7 +224,7 @@ static void plan_start(Grid& g, HaloPlan& H, bool direct) {
 	// field while its copies are in flight is rebuilt after
 	g.halo_fields.clear();
 	for (Field* f : transfer_fields(g)) {
-		field_written(*f);
+		field_halo_written(*f);
 		g.halo_fields.push_back(int(f - g.fields.data()));
 	}
 	const std::vector<Field*> tf = fixed_transfer_fields(g);
@@ -281,7 +281,7 @@ void halo_wait(Grid& g) {
 	HIP_CHECK(hipStreamWaitEvent(g.s_comp, g.ev_halo, 0));
 	g.halo_in_flight = false;
 	for (int fid : g.halo_fields)
-		if (fid >= 0 && size_t(fid) < g.fields.size()) field_written(g.fields[size_t(fid)]);
+		if (fid >= 0 && size_t(fid) < g.fields.size()) field_halo_written(g.fields[size_t(fid)]);
 	g.halo_fields.clear();
 }
 
@@ -407,7 +407,7 @@ void halo_place_peer(Grid& g, int hood, int peer, const uint8_t* buf, size_t byt
 			HIP_CHECK(hipMemcpyAsync(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, buf + o, b, hipMemcpyDefault, g.s_comp));
 		k_place(H.recvbuf.p + L.rfo[k] + ro * tf[k]->win_len, tf[k]->elem, tf[k]->win_off, tf[k]->win_len,
 		        H.recv_slots.p + ro, nr, tf[k]->data.p, g.s_comp);
-		field_written(*tf[k]);
+		field_halo_written(*tf[k]);
 		o += b;
 	}
 	HIP_CHECK(hipStreamSynchronize(g.s_comp));

@@ -721,6 +721,7 @@ void ensure_face(Grid& g) {
 	DX_REQUIRE(herr == 0, "face neighbor without a local slot or remote copy");
 	g.face_valid = true;
 	g.face_csr_valid = false;
+	g.face_gen++;
 }
 
 void ensure_face_csr(Grid& g) {

@@ -339,15 +339,22 @@ __global__ __launch_bounds__(256) void advection_ell_kernel(const double* __rest
 // cells' seven values once, coalesced, and takes every neighbor inside the
 // block from LDS; the others are gathered as before.  The same values in the
 // same order: bitwise the densities of advection_ell_kernel.
+// BANDS: check_for_adaptation's band of every swept cell as well (the
+// densities it compares are the ones the sweep reads): adv_max_diff's
+// comparisons in its order - a coarser single neighbor only from the corner
+// of its face, of a finer face only the first cell - and adv_bands_kernel's
+// thresholds, so the bytes are that kernel's.
+template <bool BANDS>
 __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
     const double* __restrict__ rho, const double* __restrict__ vx, const double* __restrict__ vy,
     const double* __restrict__ vz, const double* __restrict__ lx, const double* __restrict__ ly,
     const double* __restrict__ lz, double* __restrict__ rho_out, const int32_t* __restrict__ ell,
-    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt) {
+    const int32_t* __restrict__ fine, size_t s0, size_t s1, double dt, BandArgs B) {
 #pragma clang fp contract(off)
 	typedef int i2v __attribute__((ext_vector_type(2)));
 	typedef int i4v __attribute__((ext_vector_type(4)));
 	__shared__ double sd[256], svx[256], svy[256], svz[256], slx[256], sly[256], slz[256];
+	__shared__ uint8_t slv[BANDS ? 256 : 1];
 	const unsigned t = threadIdx.x;
 	for (size_t b0 = s0 + blockIdx.x * size_t(256); b0 < s1; b0 += size_t(gridDim.x) * 256) {
 		const size_t s = b0 + t;
@@ -355,6 +362,7 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 		const uint32_t nb_in = uint32_t(min(size_t(256), s1 - b0));
 		double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
 		int32_t e6[6] = {-1, -1, -1, -1, -1, -1};
+		int lvl = 0;
 		if (live) {
 			cd = rho[s];
 			clx = lx[s];
@@ -363,6 +371,7 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 			cvx = vx[s];
 			cvy = vy[s];
 			cvz = vz[s];
+			if (BANDS) lvl = B.lvl8[s];
 			const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
 #pragma unroll
 			for (int j = 0; j < 3; j++) {
@@ -379,6 +388,7 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 		slx[t] = clx;
 		sly[t] = cly;
 		slz[t] = clz;
+		if (BANDS) slv[t] = uint8_t(lvl);
 		__syncthreads();
 		if (!live) continue;
 		auto nb = [&](int32_t n, int dir) {
@@ -390,22 +400,51 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 			const double nv = dir < 2 ? vx[n] : (dir < 4 ? vy[n] : vz[n]);
 			return AdvNb{rho[n], lx[n], ly[n], lz[n], nv};
 		};
-		double acc = 0;
+		double acc = 0, md = 0;
+		bool have_c = false;
+		uint64_t c3[3] = {0, 0, 0};
+		auto band_cmp = [&](double b) {
+			const double diff = fabs(cd - b) / (fmin(cd, b) + B.thr);
+			md = fmax(diff, md);
+		};
 #pragma unroll
 		for (int dir = 0; dir < 6; dir++) {
 			const int32_t c = e6[dir];
 			if (c == -1) continue;
 			if (c >= 0) {
-				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(c, dir), dt);
+				const AdvNb q = nb(c, dir);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, q, dt);
+				if (BANDS) {
+					const uint32_t k = uint32_t(int64_t(c) - int64_t(b0));
+					const int nl = k < nb_in ? int(slv[k]) : int(B.lvl8[c]);
+					bool use = true;
+					if (nl < lvl) {
+						if (!have_c) {
+							map_indices(B.m, B.slot_ids[s], c3[0], c3[1], c3[2]);
+							have_c = true;
+						}
+						const uint64_t pl = (uint64_t(1) << (B.m.R - lvl)) * 2;
+						const int d = dir >> 1;
+						for (int kk = 0; kk < 3; kk++)
+							if (kk != d && (c3[kk] & (pl - 1)) != 0) use = false;
+					}
+					if (use) band_cmp(q.d);
+				}
 			} else {
 				const i4v q = *reinterpret_cast<const i4v*>(fine + 4 * size_t(-2 - c));
-				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.x, dir), dt);
+				const AdvNb first = nb(q.x, dir);
+				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, first, dt);
 				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.y, dir), dt);
 				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.z, dir), dt);
 				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, nb(q.w, dir), dt);
+				if (BANDS) band_cmp(first.d);
 			}
 		}
 		rho_out[s] = cd + acc / (clx * cly * clz);
+		if (BANDS) {
+			const double refine_diff = (lvl + 1) * B.inc, unrefine_diff = B.uns * refine_diff;
+			B.band[s] = md > refine_diff ? 2 : (md >= unrefine_diff ? 1 : 0);
+		}
 	}
 }
 
@@ -1827,15 +1866,18 @@ void k_advection(const double* const f[7], double* rho_out, const uint32_t* face
 // block, dynamic tickets and a second stream for the general sweep all tie
 // or lose against this schedule).
 void k_advection_ell(const double* const f[7], double* rho_out, const int32_t* ell, const int32_t* fine, size_t s0,
-                     size_t s1, double dt, hipStream_t s) {
+                     size_t s1, double dt, hipStream_t s, const BandArgs* bands) {
 	if (s1 <= s0) return;
 	static const bool plain = std::getenv("DCCRGX_ELL_LDS") && std::atoi(std::getenv("DCCRGX_ELL_LDS")) == 0;
-	if (plain)
+	if (bands)
+		advection_ell_lds_kernel<true><<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(
+		    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, ell, fine, s0, s1, dt, *bands);
+	else if (plain)
 		advection_ell_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5],
 		                                                                     f[6], rho_out, ell, fine, s0, s1, dt);
 	else
-		advection_ell_lds_kernel<<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(f[0], f[1], f[2], f[3], f[4], f[5],
-		                                                                         f[6], rho_out, ell, fine, s0, s1, dt);
+		advection_ell_lds_kernel<false><<<grid_for(s1 - s0, 256, 256u * 64u), 256, 0, s>>>(
+		    f[0], f[1], f[2], f[3], f[4], f[5], f[6], rho_out, ell, fine, s0, s1, dt, BandArgs{});
 	HIP_CHECK(hipGetLastError());
 }
 

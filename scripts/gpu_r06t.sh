@@ -1,0 +1,21 @@
+#!/bin/bash
+# Adaptive-step changes: the adaptive / advection / transport suites, then the
+# N=1 line, N=1 and N=2 phase tables and the N=2 line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-r06t}
+timeout -k 10 700 python -u -m pytest tests/test_gpu_advection_adapt.py tests/test_gpu_advection.py tests/test_gpu_transport.py \
+    tests/test_gpu_multirank.py tests/test_gpu_unrefine.py tests/test_gpu_balance.py tests/test_gpu_ref_advection.py \
+    -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_${TAG}.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_${TAG}.log; grep -E "FAILED|ERROR" gpurun_out/pytest_${TAG}.log | head
+[ $rc -eq 0 ] || exit $rc
+for n in 1 2; do
+  DCCRG_BENCH_TRANSPORT=host timeout -k 10 400 python -u bench.py --gpus $n --workload advection_adapt --steps 20 \
+      --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_adapt_n$n.json 2> gpurun_out/${TAG}_adapt_n$n.err || exit $?
+  python -c "import json; d=json.loads(open('gpurun_out/${TAG}_adapt_n$n.json').read().strip().splitlines()[-1]); print('n=$n', round(d['ms_per_step'],3), d['adaptation'])"
+  DCCRG_BENCH_TRANSPORT=host DCCRGX_LIB=libdccrgx_pt.so timeout -k 10 400 python -u bench.py --gpus $n \
+      --workload advection_adapt --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_adapt_pt_n$n.json \
+      2> gpurun_out/${TAG}_adapt_pt_n$n.err || exit $?
+done
+grep "phase r0" gpurun_out/${TAG}_adapt_pt_n1.err | grep -E "chk\.|step\.|face|adapt\."

@@ -94,3 +94,42 @@ def test_check_with_pending_unrefine_matches_device_decisions(gpu):
     assert issued > 0
     for g, _ in grids:
         g.close()
+
+
+@pytest.mark.parametrize("base,split", [((16, 16, 1), True), ((10, 10, 3), False)])
+def test_sweep_bands_match_bands_kernel(gpu, monkeypatch, base, split):
+    """The face-table sweep also writes check_for_adaptation's bands (with the
+    last check's parameters) and the check then takes them instead of running
+    its own bands kernel.  Two identical grids step together, the second with
+    that cache switched off (DCCRGX_BAND_CACHE=0: the sweep computes no bands):
+    every step's created / removed counts, leaf set and densities must be
+    bitwise the same.  Sweeps as inner + outer runs or as one whole-grid run."""
+    R, steps = 2, 12
+    grids = []
+    for _ in range(2):
+        g, f = gpu_grid(base, R)
+        prerefine(g, f, R)
+        grids.append((g, f))
+    di = 0.025 / R
+    for step in range(steps):
+        dt = 0.5 * grids[0][0].advection_max_time_step(grids[0][1])
+        out = []
+        for k, (g, f) in enumerate(grids):
+            if k == 1:
+                monkeypatch.setenv("DCCRGX_BAND_CACHE", "0")
+            else:
+                monkeypatch.delenv("DCCRGX_BAND_CACHE", raising=False)
+            if split:
+                g.advection_step(f, dt, "inner")
+                g.advection_step(f, dt, "outer")
+            else:
+                g.advection_step(f, dt)
+            g.advection_check_adaptation(f[0], di)
+            g.advection_commit(f[0])
+            out.append(g.advection_adapt(f))
+        assert out[0] == out[1], step
+        assert np.array_equal(grids[0][0].local_cells(), grids[1][0].local_cells()), step
+        assert np.array_equal(grids[0][1][0].get(0, grids[0][0].n_local), grids[1][1][0].get(0, grids[1][0].n_local))
+    monkeypatch.delenv("DCCRGX_BAND_CACHE", raising=False)
+    for g, _ in grids:
+        g.close()

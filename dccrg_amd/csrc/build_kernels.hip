@@ -174,10 +174,10 @@ __global__ void remote_flags_kernel(MapCtx m, const int32_t* hood, const int32_t
 		cell_coords(m, cells[w], c, lvl);
 		bool remote = false;
 		for (int k = lane_id(); k < nh; k += WAVE) {
-			ItemOut o;
-			nof_item(m, c, lvl, hood + 3 * k, ex, o);
-			for (int i = 0; i < o.n; i++) {
-				const int32_t ow = dm_owner(M, o.id[i]);
+			uint64_t w[3];
+			const int kind = nof_item_case(m, c, lvl, hood + 3 * k, ex, w);
+			for (int i = 0; i < item_count(kind); i++) {
+				const int32_t ow = dm_owner(M, item_id(m, lvl, hood + 3 * k, kind, w, i, nullptr));
 				if (ow >= 0 && ow != rank) remote = true;
 			}
 		}
@@ -215,10 +215,10 @@ __global__ __launch_bounds__(256) void remote_flags_thread_kernel(MapCtx m, cons
 		cell_coords(m, cells[i], c, lvl);
 		bool remote = false;
 		for (int k = 0; k < nh && !remote; k++) {
-			ItemOut o;
-			nof_item(m, c, lvl, hood + 3 * k, ex, o);
-			for (int j = 0; j < o.n; j++) {
-				const int32_t ow = dm_owner(M, o.id[j]);
+			uint64_t w[3];
+			const int kind = nof_item_case(m, c, lvl, hood + 3 * k, ex, w);
+			for (int j = 0; j < item_count(kind); j++) {
+				const int32_t ow = dm_owner(M, item_id(m, lvl, hood + 3 * k, kind, w, j, nullptr));
 				if (ow >= 0 && ow != rank) remote = true;
 			}
 		}
@@ -306,9 +306,8 @@ __global__ void count_rows_kernel(MapCtx m, const int32_t* hood, const int32_t* 
 		cell_coords(m, slot_ids[row0 + r], c, lvl);
 		int n = 0;
 		for (int k = lane_id(); k < nh; k += WAVE) {
-			ItemOut o;
-			nof_item(m, c, lvl, hood + 3 * k, ex, o);
-			n += o.n;
+			uint64_t w[3];
+			n += item_count(nof_item_case(m, c, lvl, hood + 3 * k, ex, w));
 		}
 		n = wave_sum(n);
 		const int t = nto_row(m, hood_to, nh, ex, c, lvl, lds, cap, nullptr);
@@ -331,16 +330,17 @@ __global__ void fill_nof_kernel(MapCtx m, const int32_t* hood, int nh, DevMesh M
 		size_t base = ptr[r];
 		for (int k0 = 0; k0 < nh; k0 += WAVE) {
 			const int k = k0 + lane_id();
-			ItemOut o;
-			o.n = 0;
-			if (k < nh) nof_item(m, c, lvl, hood + 3 * k, ex, o);
-			const int incl = wave_incl_scan(o.n);
-			const size_t pos = base + size_t(incl - o.n);
-			for (int i = 0; i < o.n; i++) {
-				ids[pos + i] = o.id[i];
-				offs[3 * (pos + i) + 0] = o.off[i][0];
-				offs[3 * (pos + i) + 1] = o.off[i][1];
-				offs[3 * (pos + i) + 2] = o.off[i][2];
+			uint64_t w[3] = {0, 0, 0};
+			const int kind = k < nh ? nof_item_case(m, c, lvl, hood + 3 * k, ex, w) : 0;
+			const int no = item_count(kind);
+			const int incl = wave_incl_scan(no);
+			const size_t pos = base + size_t(incl - no);
+			for (int i = 0; i < no; i++) {
+				int32_t off[3];
+				ids[pos + i] = item_id(m, lvl, hood + 3 * k, kind, w, i, off);
+				offs[3 * (pos + i) + 0] = off[0];
+				offs[3 * (pos + i) + 1] = off[1];
+				offs[3 * (pos + i) + 2] = off[2];
 			}
 			base += size_t(__shfl(incl, WAVE - 1, WAVE));
 		}
@@ -867,10 +867,11 @@ __global__ void induced_kernel(MapCtx m, const int32_t* hood, const int32_t* hoo
 			const unsigned long long pos = atomicAdd(counter, 1ull);
 			if (pos < cap) out[pos] = q;
 		};
+		// nof_item's leaves from the item's case (no ItemOut in private memory)
 		for (int k = lane_id(); k < nh; k += WAVE) {
-			ItemOut o;
-			nof_item(m, c, lvl, hood + 3 * k, ex, o);
-			for (int i = 0; i < o.n; i++) emit(o.id[i]);
+			uint64_t w[3];
+			const int kind = nof_item_case(m, c, lvl, hood + 3 * k, ex, w);
+			for (int i = 0; i < item_count(kind); i++) emit(item_id(m, lvl, hood + 3 * k, kind, w, i, nullptr));
 		}
 		for (int k = lane_id(); k < 10 * nh; k += WAVE) emit(nto_candidate(m, c, lvl, hood_to, nh, k, ex));
 	}

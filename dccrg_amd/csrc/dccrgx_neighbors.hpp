@@ -32,46 +32,58 @@ struct ItemOut {
 	int32_t off[8][3];
 };
 
+// The case of one stencil item (find_neighbors_of 4339-4460): 0 outside a
+// non-periodic boundary or no leaf, 1 the eight finer leaves, 2 the
+// same-size leaf, 3 the coarser one; w = the item's wrapped index.  Kernels
+// take the case and form the ids from it (item_id) instead of an ItemOut in
+// private memory.
+template <class Exists>
+DX_HD int nof_item_case(const MapCtx& m, const uint64_t c[3], int lvl, const int32_t h[3], const Exists& exists,
+                        uint64_t w[3]) {
+	const int64_t len = int64_t(1) << (m.R - lvl);
+	for (int d = 0; d < 3; d++) {
+		if (!map_wrap(m, d, int64_t(c[d]) + int64_t(h[d]) * len, w[d])) return 0;
+	}
+	if (lvl < m.R && exists(map_from_indices(m, w[0], w[1], w[2], lvl + 1))) return 1;
+	if (exists(map_from_indices(m, w[0], w[1], w[2], lvl))) return 2;
+	if (lvl > 0 && exists(map_from_indices(m, w[0], w[1], w[2], lvl - 1))) return 3;
+	return 0;
+}
+
+DX_HD int item_count(int kind) { return kind == 1 ? 8 : (kind ? 1 : 0); }
+
+// leaf i (< item_count) of an item's case and its offset (off may be null)
+DX_HD uint64_t item_id(const MapCtx& m, int lvl, const int32_t h[3], int kind, const uint64_t w[3], int i,
+                       int32_t* off) {
+	const int64_t len = int64_t(1) << (m.R - lvl);
+	if (kind == 1) {
+		const int64_t hl = len / 2;
+		const int dx = i & 1, dy = (i >> 1) & 1, dz = (i >> 2) & 1;
+		if (off) {
+			off[0] = int32_t(h[0] * len + dx * hl);
+			off[1] = int32_t(h[1] * len + dy * hl);
+			off[2] = int32_t(h[2] * len + dz * hl);
+		}
+		return map_from_indices(m, w[0] + dx * hl, w[1] + dy * hl, w[2] + dz * hl, lvl + 1);
+	}
+	if (kind == 2) {
+		if (off)
+			for (int d = 0; d < 3; d++) off[d] = int32_t(h[d] * len);
+		return map_from_indices(m, w[0], w[1], w[2], lvl);
+	}
+	const uint64_t pl = uint64_t(len) * 2;
+	if (off)
+		for (int d = 0; d < 3; d++) off[d] = int32_t(h[d] * len - int64_t(w[d] & (pl - 1)));
+	return map_from_indices(m, w[0], w[1], w[2], lvl - 1);
+}
+
 template <class Exists>
 DX_HD void nof_item(const MapCtx& m, const uint64_t c[3], int lvl, const int32_t h[3], const Exists& exists,
                     ItemOut& o) {
-	o.n = 0;
-	const int64_t len = int64_t(1) << (m.R - lvl);
 	uint64_t w[3];
-	for (int d = 0; d < 3; d++) {
-		if (!map_wrap(m, d, int64_t(c[d]) + int64_t(h[d]) * len, w[d])) return;
-	}
-	if (lvl < m.R) {
-		const uint64_t f = map_from_indices(m, w[0], w[1], w[2], lvl + 1);
-		if (exists(f)) {
-			const int64_t hl = len / 2;
-			for (int i = 0; i < 8; i++) {
-				const int dx = i & 1, dy = (i >> 1) & 1, dz = (i >> 2) & 1;
-				o.id[i] = map_from_indices(m, w[0] + dx * hl, w[1] + dy * hl, w[2] + dz * hl, lvl + 1);
-				o.off[i][0] = int32_t(h[0] * len + dx * hl);
-				o.off[i][1] = int32_t(h[1] * len + dy * hl);
-				o.off[i][2] = int32_t(h[2] * len + dz * hl);
-			}
-			o.n = 8;
-			return;
-		}
-	}
-	const uint64_t s = map_from_indices(m, w[0], w[1], w[2], lvl);
-	if (exists(s)) {
-		o.id[0] = s;
-		for (int d = 0; d < 3; d++) o.off[0][d] = int32_t(h[d] * len);
-		o.n = 1;
-		return;
-	}
-	if (lvl > 0) {
-		const uint64_t p = map_from_indices(m, w[0], w[1], w[2], lvl - 1);
-		if (exists(p)) {
-			const uint64_t pl = uint64_t(len) * 2;
-			o.id[0] = p;
-			for (int d = 0; d < 3; d++) o.off[0][d] = int32_t(h[d] * len - int64_t(w[d] & (pl - 1)));
-			o.n = 1;
-		}
-	}
+	const int kind = nof_item_case(m, c, lvl, h, exists, w);
+	o.n = item_count(kind);
+	for (int i = 0; i < o.n; i++) o.id[i] = item_id(m, lvl, h, kind, w, i, o.off[i]);
 }
 
 // indices_from_neighborhood (dccrg.hpp:4200-4316) for one hood item: the

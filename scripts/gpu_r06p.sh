@@ -17,4 +17,4 @@ DCCRG_BENCH_TRANSPORT=host DCCRGX_LIB=libdccrgx_pt.so DCCRGX_MESH_NOTES=1 timeou
     --workload advection_adapt --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_adapt_pt_n2.json \
     2> gpurun_out/${TAG}_adapt_pt_n2.err || exit $?
 grep "mesh r0" gpurun_out/${TAG}_adapt_pt_n2.err | tail -2
-grep "phase r0" gpurun_out/${TAG}_adapt_pt_n2.err | grep -E "rb\.|sr\.7"
+grep "phase r0" gpurun_out/${TAG}_adapt_pt_n2.err | grep -E "rb\.|sr\.|chk\.|cs\.|adapt\.|comm\."

@@ -783,6 +783,10 @@ double& phase_comm_total() {
 	static double t = 0;
 	return t;
 }
+long& phase_sync_count() {
+	static long k = 0;
+	return k;
+}
 #endif
 
 }  // namespace dccrgx

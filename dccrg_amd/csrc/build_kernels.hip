@@ -13,6 +13,7 @@
 // written in the reference's order without atomics.  Existence / owner /
 // slot of a leaf is one 16-byte probe sequence in the rank's hash table (or
 // the block-partition formula on the initial level-0 grid).
+#include <cstring>
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_merge.hpp>
 
@@ -1478,6 +1479,37 @@ size_t sort_unique_u64(uint64_t* keys, size_t n, hipStream_t s, int end_bit) {
 	return read_counter(nsel, s);
 }
 
+namespace {
+struct PickU32 {
+	size_t at[4];
+	int k;
+};
+__global__ void pick_u32_kernel(const uint32_t* __restrict__ v, PickU32 p, uint32_t* __restrict__ out) {
+	if (int(threadIdx.x) < p.k) out[threadIdx.x] = v[p.at[threadIdx.x]];
+}
+}  // namespace
+
+uint32_t scan_exclusive_u32_at(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s, const size_t* at, int k,
+                               uint32_t* vals) {
+	DX_REQUIRE(k >= 0 && k <= 3, "internal error: too many scan positions");
+	size_t bytes = 0;
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n + 1, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(bytes);
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in, out, n + 1, s));
+	// the total and the k positions in one read
+	PickU32 p{{n, 0, 0, 0}, k + 1};
+	for (int j = 0; j < k; j++) p.at[j + 1] = at[j];
+	DBuf<uint32_t> picked;
+	picked.alloc(4);
+	pick_u32_kernel<<<1, 64, 0, s>>>(out, p, picked.p);
+	HIP_CHECK(hipGetLastError());
+	uint32_t h[4] = {0, 0, 0, 0};
+	d2h_small(h, picked.p, sizeof(uint32_t) * size_t(k + 1), s);
+	for (int j = 0; j < k; j++) vals[j] = h[j + 1];
+	return h[0];
+}
+
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {
 	// scans n + 1 entries: out[n] = sum(in[0..n))
 	size_t bytes = 0;
@@ -1768,11 +1800,22 @@ std::vector<uint64_t> k_unrefine_families(const MapCtx& m, const int32_t* hood, 
 		unrefine_check_kernel<<<grid_for(n * size_t(nh), 256), 256, 0, s>>>(m, hood, nh, M, par.p, n, dSp, S.size(),
 		                                                                    ok.p);
 	HIP_CHECK(hipGetLastError());
-	const std::vector<uint64_t> cand = download(par.p, n, s);
-	const std::vector<uint32_t> h = download(ok.p, n, s);
+	// candidates and verdicts in one read
+	DBuf<uint8_t> stage;
+	stage.alloc(12 * n);
+	HIP_CHECK(hipMemcpyAsync(stage.p, par.p, 8 * n, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipMemcpyAsync(stage.p + 8 * n, ok.p, 4 * n, hipMemcpyDeviceToDevice, s));
+	const std::vector<uint8_t> hb = download(stage.p, 12 * n, s);
 	std::vector<uint64_t> out;
-	for (size_t i = 0; i < n; i++)
-		if (h[i]) out.push_back(cand[i]);
+	for (size_t i = 0; i < n; i++) {
+		uint32_t v;
+		std::memcpy(&v, hb.data() + 8 * n + 4 * i, 4);
+		if (v) {
+			uint64_t c;
+			std::memcpy(&c, hb.data() + 8 * i, 8);
+			out.push_back(c);
+		}
+	}
 	return out;
 }
 
@@ -1807,13 +1850,12 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 		                                                          cnt.p + np);
 		HIP_CHECK(hipGetLastError());
 	}
-	n_out = scan_exclusive_u32(cnt.p, pos.p, n, s);
-	// where input positions at[k] land (the expanded list's run boundaries)
-	for (int k = 0; k < n_at; k++) {
-		uint32_t v = 0;
-		d2h_small(&v, pos.p + at[k], 4, s);
-		pos_at[k] = v;
-	}
+	// the total and where input positions at[k] land (the expanded list's run
+	// boundaries), one read
+	DX_REQUIRE(n_at >= 0 && n_at <= 3, "internal error: too many run boundaries");
+	uint32_t landed[3] = {0, 0, 0};
+	n_out = scan_exclusive_u32_at(cnt.p, pos.p, n, s, at, n_at, landed);
+	for (int k = 0; k < n_at; k++) pos_at[k] = landed[k];
 	out_id.alloc(n_out + 1);
 	out_own.alloc(n_out + 1);
 	if (src) {
@@ -1830,7 +1872,8 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 		                                                         dF.p, F.size(), out_id.p, out_own.p);
 		HIP_CHECK(hipGetLastError());
 	}
-	HIP_CHECK(hipStreamSynchronize(s));
+	// stream-ordered for rebuild (its readers run on s); the temporaries go
+	// back to the pool, which holds them until a device sync
 }
 
 size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& S,

@@ -73,17 +73,26 @@ struct PhaseScope {
 // laps: DX_LAPS(stream) starts a lap clock in this scope, DX_LAP("name")
 // books the time since the previous lap (stream drained) under name, and
 // that time less the transport's inside it under "name.net"
+// stream syncs of the library since start (the pt build counts every
+// hipStreamSynchronize below this header's end; the laps' own drains not)
+long& phase_sync_count();
 struct PhaseLaps {
 	hipStream_t s;
 	double t, c;
-	explicit PhaseLaps(hipStream_t st) : s(st), t(PhaseScope::now()), c(phase_comm_total()) {}
+	long k;
+	explicit PhaseLaps(hipStream_t st) : s(st), t(PhaseScope::now()), c(phase_comm_total()), k(phase_sync_count()) {}
 	void lap(const char* name) {
 		(void)hipStreamSynchronize(s);
 		const double n = PhaseScope::now(), cn = phase_comm_total();
 		phase_add(name, n - t);
 		if (cn > c) phase_add((std::string(name) + ".net").c_str(), (n - t) - (cn - c));
+		// "<name>.syncs": the stream syncs inside the lap, booked as 1 ms each
+		// (the table's ms column is then the count)
+		const long kn = phase_sync_count();
+		if (kn > k) phase_add((std::string(name) + ".syncs").c_str(), 1e-3 * double(kn - k));
 		t = n;
 		c = cn;
+		k = kn;
 	}
 };
 #define DX_PHASE_CAT2(a, b) a##b
@@ -866,6 +875,9 @@ void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_
 void k_morton_merge2(const MapCtx& m, uint64_t* ids, size_t n, size_t run1, hipStream_t s);
 void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
+// the same, and out[at[j]] (j < k <= 3) into vals, all in one device read
+uint32_t scan_exclusive_u32_at(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s, const size_t* at, int k,
+                               uint32_t* vals);
 void k_lookup_slots(const uint64_t* ids, size_t n, const DevMesh& M, int32_t* out, int32_t* err_flag, hipStream_t s);
 // iterator ranges cell.neighbors_of (update_cell_pointers 11451-11500): pass
 // 0 classifies the neighbors_of entries into cls (one byte per entry) and
@@ -1067,3 +1079,14 @@ void k_po_reduce(int k, const double* part, unsigned nb, double* red, PoScalars*
 void k_po_scalar(const double* all, int P, int k, PoScalars* st, const PoParams& prm, int stage, hipStream_t s);
 
 }  // namespace dccrgx
+
+#if DCCRGX_PHASE_TIMING
+// the analysis build counts the library's stream syncs (PhaseLaps "<lap>.syncs")
+namespace dccrgx {
+inline hipError_t dx_counted_stream_sync(hipStream_t s) {
+	phase_sync_count()++;
+	return (hipStreamSynchronize)(s);
+}
+}  // namespace dccrgx
+#define hipStreamSynchronize(s) ::dccrgx::dx_counted_stream_sync(s)
+#endif

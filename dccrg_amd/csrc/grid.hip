@@ -781,7 +781,7 @@ void stop_refining_impl(Grid& g) {
 				o += kv.second.size() * f.elem;
 			}
 		}
-		HIP_CHECK(hipStreamSynchronize(s));
+		if (!send_ids.empty()) HIP_CHECK(hipStreamSynchronize(s));  // (the slot lists' host vectors)
 		std::vector<DevMsg> msgs;
 		i = 0;
 		size_t j = 0;
@@ -812,7 +812,7 @@ void stop_refining_impl(Grid& g) {
 			}
 			at += kv.second.size();
 		}
-		HIP_CHECK(hipStreamSynchronize(s));
+		if (g.size > 1) HIP_CHECK(hipStreamSynchronize(s));  // the messages' buffers end with this scope
 		// variable-size payloads: the kept children's, then the received ones
 		if (std::any_of(g.fields.begin(), g.fields.end(), [](const Field& f) { return f.var; })) {
 			std::vector<uint64_t> out_all;

@@ -7,6 +7,7 @@
 //                 the reference's scatter into two cells becomes a race-free
 //                 gather with no atomics)
 // All bandwidth-bound; no MFMA.
+#include <cstring>
 #include <cstdlib>
 
 #include "dccrgx_internal.hpp"
@@ -2076,12 +2077,25 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	// here before they leave the device
 	sort_u64(ref.p, size_t(h[0]), s, map_id_bits(m));
 	sort_u64(unref.p, size_t(h[1]), s, map_id_bits(m));
-	out.refine = download(ref.p, size_t(h[0]), s);
-	out.unrefine = download(unref.p, size_t(h[1]), s);
+	// the three lists gathered on the device and read at once
+	const size_t b0 = 8 * size_t(h[0]), b1 = 8 * size_t(h[1]), b3 = 4 * size_t(h[3]);
+	std::vector<uint32_t> runs(static_cast<size_t>(h[3]));
+	out.refine.resize(size_t(h[0]));
+	out.unrefine.resize(size_t(h[1]));
+	if (b0 + b1 + b3) {
+		DBuf<uint8_t> stage;
+		stage.alloc(b0 + b1 + b3);
+		if (b0) HIP_CHECK(hipMemcpyAsync(stage.p, ref.p, b0, hipMemcpyDeviceToDevice, s));
+		if (b1) HIP_CHECK(hipMemcpyAsync(stage.p + b0, unref.p, b1, hipMemcpyDeviceToDevice, s));
+		if (b3) HIP_CHECK(hipMemcpyAsync(stage.p + b0 + b1, part.p, b3, hipMemcpyDeviceToDevice, s));
+		const std::vector<uint8_t> hb = download(stage.p, b0 + b1 + b3, s);
+		if (b0) std::memcpy(out.refine.data(), hb.data(), b0);
+		if (b1) std::memcpy(out.unrefine.data(), hb.data() + b0, b1);
+		if (b3) std::memcpy(runs.data(), hb.data() + b0 + b1, b3);
+	}
 	out.refine_dev = std::move(ref);
 	out.unrefine_dev = std::move(unref);
 	out.kept = size_t(h[2]);
-	const std::vector<uint32_t> runs = download(part.p, size_t(h[3]), s);
 	// the partial runs' members: ids and bands
 	for (uint32_t r : runs) {
 		const size_t s0 = r & ((1u << 28) - 1u), k = r >> 28;

@@ -1065,6 +1065,52 @@ __global__ void kept_children_kernel(MapCtx m, DevMesh M, int rank, const uint64
 	out_slot[at] = sl;
 }
 
+// Every child of every merged family local (one process): the children in
+// ascending id without a sort.  F ascending, so its families come in level
+// groups, and within a group the children of one octant k ascend with their
+// parents (the id's (z, y, x) digits are the parent's doubled plus the
+// octant's bits), so a child's position is the number of smaller children of
+// each octant in its group, found by binary search of that octant's stream.
+struct LevelGroups {
+	uint32_t lo[kRangeLevels + 1];  // group g: families [lo[g], lo[g + 1])
+	int n;
+};
+__global__ void family_children_kernel(MapCtx m, const uint64_t* __restrict__ F, size_t nF, uint64_t* __restrict__ ch) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < nF; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t c[8];
+		map_all_children(m, F[i], c);
+#pragma unroll
+		for (int k = 0; k < 8; k++) ch[8 * i + k] = c[k];
+	}
+}
+__global__ void kept_ordered_kernel(DevMesh M, const uint64_t* __restrict__ ch, size_t nF, LevelGroups G,
+                                    uint64_t* __restrict__ out, int32_t* __restrict__ out_slot) {
+	for (size_t t = blockIdx.x * size_t(blockDim.x) + threadIdx.x; t < 8 * nF; t += size_t(gridDim.x) * blockDim.x) {
+		const uint32_t i = uint32_t(t >> 3);
+		const int k = int(t & 7);
+		uint32_t g0 = 0, g1 = uint32_t(nF);
+		for (int g = 0; g < G.n; g++)
+			if (i >= G.lo[g] && i < G.lo[g + 1]) {
+				g0 = G.lo[g];
+				g1 = G.lo[g + 1];
+			}
+		const uint64_t c = ch[t];
+		size_t pos = 8 * size_t(g0) + (i - g0);  // its own octant's smaller ones
+		for (int q = 0; q < 8; q++) {
+			if (q == k) continue;
+			uint32_t lo = g0, hi = g1;
+			while (lo < hi) {
+				const uint32_t mid = (lo + hi) >> 1;
+				if (ch[8 * size_t(mid) + q] < c) lo = mid + 1;
+				else hi = mid;
+			}
+			pos += lo - g0;
+		}
+		out[pos] = c;
+		out_slot[pos] = dm_slot(M, c);
+	}
+}
+
 __global__ void slot_levels_kernel(MapCtx m, const uint64_t* slot_ids, size_t n, uint8_t* lvl) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
 		lvl[i] = uint8_t(map_level(m, slot_ids[i]));
@@ -1896,7 +1942,8 @@ size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std
 }
 
 size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF_given) {
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF_given,
+                       bool all_local) {
 	ids.release();
 	slots.release();
 	if (F.empty()) return 0;
@@ -1907,6 +1954,27 @@ size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::v
 		const uint64_t* p;
 	} dF{dF_given ? dF_given : dF_own.p};
 	const size_t cap = 8 * F.size();
+	if (all_local && F.size() < (size_t(1) << 31)) {
+		LevelGroups G{};
+		G.n = 0;
+		int last = -1;
+		for (size_t i = 0; i < F.size(); i++) {
+			const int L = map_level(m, F[i]);
+			if (L != last) {
+				DX_REQUIRE(G.n < kRangeLevels && L > last, "internal error: merged families not ascending");
+				G.lo[G.n++] = uint32_t(i);
+				last = L;
+			}
+		}
+		G.lo[G.n] = uint32_t(F.size());
+		ids.alloc(cap + 1);
+		slots.alloc(cap + 1);
+		k1.alloc(cap + 1);
+		family_children_kernel<<<grid_for(F.size(), 256), 256, 0, s>>>(m, dF.p, F.size(), k1.p);
+		kept_ordered_kernel<<<grid_for(cap, 256), 256, 0, s>>>(M, k1.p, F.size(), G, ids.p, slots.p);
+		HIP_CHECK(hipGetLastError());
+		return cap;
+	}
 	k1.alloc(cap + 1);
 	k2.alloc(cap + 1);
 	v1.alloc(cap + 1);

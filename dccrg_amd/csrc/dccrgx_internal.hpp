@@ -928,8 +928,11 @@ size_t k_created_children(const MapCtx& m, const DevMesh& M, int rank, const std
 // the children of the merged families F staying on `rank` (owned here, like
 // the family's first child), ascending, into ids with their slots; returns
 // their count
+// all_local: every child of every family is a local leaf (one process):
+// ordered by ranks within octant streams instead of a sort
 size_t k_kept_children(const MapCtx& m, const DevMesh& M, int rank, const std::vector<uint64_t>& F,
-                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF = nullptr);
+                       DBuf<uint64_t>& ids, DBuf<int32_t>& slots, hipStream_t s, const uint64_t* dF = nullptr,
+                       bool all_local = false);
 // known list after refining the sorted set S and merging the families under
 // the sorted parents F: every known leaf in S is replaced by its 8 children
 // (same owner), the children of a parent in F by the parent (owner of the

@@ -699,7 +699,8 @@ void stop_refining_impl(Grid& g) {
 	DBuf<int32_t> ksl;        // and their slots
 	size_t n_keep = 0;
 	if (!F.empty()) {
-		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, dF.p);
+		n_keep = k_kept_children(g.m, g.dm(), g.rank, F, keep_ids, ksl, s, dF.p,
+		                         g.size == 1 && !std::getenv("DCCRGX_KEPT_SORT"));
 		DX_LAP("sr.5a_kept");
 		const bool attrs = !g.weights.empty() || !g.pins.empty();
 		if (g.size > 1 && !attrs) {

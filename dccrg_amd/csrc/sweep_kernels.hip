@@ -1558,60 +1558,47 @@ __global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, c
                                                                uint32_t* __restrict__ part,
                                                                unsigned long long* __restrict__ cnt) {
 	constexpr int kJ = 8;
-	const int lane = int(threadIdx.x & 63u);
-	const size_t wave = (size_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-	const size_t base = wave * 64 * kJ;
-	uint64_t par[kJ + 1];
-	uint32_t bnd[kJ + 1];
-	// every load issued before the parents are computed (id 0 = none)
-#pragma unroll
-	for (int j = 0; j <= kJ; j++) {
-		const size_t sj = base + 64 * size_t(j) + size_t(lane);
-		par[j] = sj < n ? ids[sj] : 0;
-		bnd[j] = sj < n ? uint32_t(band[sj]) : 0u;
+	constexpr int kSpan = BS * kJ;  // a block's slots: wave w takes [64 kJ w, 64 kJ (w + 1))
+	// the parents (~0: level 0 or none) and bands of the block's slots, of
+	// the slot before them and of the seven after them (entry i = slot
+	// base0 + i - 1): a run head reads its run from here, every other slot
+	// only its predecessor (round 5's form shuffled all seven neighbors of
+	// every slot)
+	__shared__ uint64_t sp[kSpan + 8];
+	__shared__ uint8_t sb[kSpan + 8];
+	const size_t base0 = size_t(blockIdx.x) * kSpan;
+	for (int i = int(threadIdx.x); i < kSpan + 8; i += BS) {
+		const bool ok = (base0 + size_t(i) >= 1) && base0 + size_t(i) - 1 < n;
+		const uint64_t id = ok ? ids[base0 + size_t(i) - 1] : 0;
+		sp[i] = map_level(m, id) > 0 ? map_parent(m, id) : ~uint64_t(0);
+		sb[i] = ok ? band[base0 + size_t(i) - 1] : uint8_t(0);
 	}
-	// the parent of the slot before the wave's first one
-	uint64_t before = base > 0 && base - 1 < n ? ids[base - 1] : 0;
-	before = map_level(m, before) > 0 ? map_parent(m, before) : ~uint64_t(0);
-#pragma unroll
-	for (int j = 0; j <= kJ; j++) par[j] = map_level(m, par[j]) > 0 ? map_parent(m, par[j]) : ~uint64_t(0);
+	__syncthreads();
+	const int lane = int(threadIdx.x & 63u);
+	const int w = int(threadIdx.x >> 6);
 	uint32_t flags = 0;  // per j, 4 bits: 1 refine, 2 partial run head, 4 kept family head, 8 unrefine head
 	uint32_t runk = 0;   // per j, 4 bits: the run length of a partial run head
 	unsigned cr = 0, cp = 0, ck = 0, cu = 0;
 #pragma unroll
 	for (int j = 0; j < kJ; j++) {
-		const size_t sj = base + 64 * size_t(j) + size_t(lane);
-		const uint64_t p = par[j];
-		// the previous slot's parent: lane - 1, or lane 63 of the chunk before
-		const uint64_t prev_in = __shfl(par[j], (lane + 63) & 63, 64);
-		const uint64_t prev_last = j > 0 ? __shfl(par[j - 1], 63, 64) : before;
-		const uint64_t prev = lane > 0 ? prev_in : prev_last;
-		// the next seven slots' parents and bands (every lane takes part)
-		uint64_t nx[7];
-		uint32_t nb[7];
-#pragma unroll
-		for (int q = 1; q <= 7; q++) {
-			const int L = lane + q;
-			const uint64_t a = __shfl(par[j], L & 63, 64), b = __shfl(par[j + 1], L & 63, 64);
-			const uint32_t ba = __shfl(bnd[j], L & 63, 64), bb = __shfl(bnd[j + 1], L & 63, 64);
-			nx[q - 1] = L < 64 ? a : b;
-			nb[q - 1] = L < 64 ? ba : bb;
-		}
+		const int li = 64 * kJ * w + 64 * j + lane;  // block-local slot; its entries li + 1 (own), li (before)
+		const size_t sj = base0 + size_t(li);
 		if (sj >= n) continue;
+		const uint64_t p = sp[li + 1];
+		const uint64_t prev = sp[li];
+		const uint32_t bj = sb[li + 1];
 		const int lvl = p == ~uint64_t(0) ? 0 : map_level(m, p) + 1;
 		uint32_t what = 0;
-		if (bnd[j] == 2 && lvl < int(m.R)) {
+		if (bj == 2 && lvl < int(m.R)) {
 			what |= 1;
 			cr++;
 		}
 		if (lvl > 0 && prev != p) {
 			uint32_t k = 1;
-			bool keep = bnd[j] >= 1;
-#pragma unroll
+			bool keep = bj >= 1;
 			for (int q = 1; q < 8; q++) {
-				if (k != uint32_t(q)) break;
-				if (nx[q - 1] != p) break;
-				keep = keep || nb[q - 1] >= 1;
+				if (sp[li + 1 + q] != p) break;
+				keep = keep || sb[li + 1 + q] >= 1;
 				k++;
 			}
 			bool whole = !solo;  // every child of p is a leaf (some held elsewhere)
@@ -1623,10 +1610,7 @@ __global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, c
 			if (k < 8 && whole) {
 				// the slot just before or just after the run holding a child of a
 				// sibling (a grandchild of p) settles it without lookups
-				uint64_t after = ~uint64_t(0);
-#pragma unroll
-				for (int q = 1; q < 8; q++)
-					if (uint32_t(q) == k) after = nx[q - 1];
+				const uint64_t after = sp[li + 1 + int(k)];
 				auto grandchild_of_p = [&](uint64_t par_of_slot) {
 					return par_of_slot != ~uint64_t(0) && map_level(m, par_of_slot) > 0 && map_parent(m, par_of_slot) == p;
 				};
@@ -1684,7 +1668,7 @@ __global__ __launch_bounds__(BS) void adv_requests_kernel(MapCtx m, DevMesh M, c
 	for (int j = 0; j < kJ; j++) {
 		const uint32_t what = (flags >> (4 * j)) & 15u;
 		if (!what) continue;
-		const size_t sj = base + 64 * size_t(j) + size_t(lane);
+		const size_t sj = base0 + size_t(64 * kJ * w + 64 * j + lane);
 		if (what & 1) ref[ar++] = ids[sj];
 		if (what & 2) part[ap++] = uint32_t(sj) | (((runk >> (4 * j)) & 15u) << 28);
 		if (what & 8) unref[au++] = ids[sj];

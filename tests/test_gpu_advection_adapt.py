@@ -133,3 +133,38 @@ def test_sweep_bands_match_bands_kernel(gpu, monkeypatch, base, split):
     monkeypatch.delenv("DCCRGX_BAND_CACHE", raising=False)
     for g, _ in grids:
         g.close()
+
+
+def test_kept_children_order_without_sort(gpu, monkeypatch):
+    """On one process the merged families' children (the removed store)
+    are put in ascending order by ranks within the eight octant streams
+    instead of a sort (k_kept_children, all_local).  Against the sorted form
+    (DCCRGX_KEPT_SORT=1) on a twin grid: the removed cells in the same order
+    (ascending), the merged parents' densities bitwise, every step."""
+    base, R, steps = (10, 10, 3), 2, 10
+    grids = []
+    for _ in range(2):
+        g, f = gpu_grid(base, R)
+        prerefine(g, f, R)
+        grids.append((g, f))
+    di = 0.025 / R
+    merged = 0
+    for step in range(steps):
+        dt = 0.5 * grids[0][0].advection_max_time_step(grids[0][1])
+        out, rem = [], []
+        for k, (g, f) in enumerate(grids):
+            if k == 1:
+                monkeypatch.setenv("DCCRGX_KEPT_SORT", "1")
+            else:
+                monkeypatch.delenv("DCCRGX_KEPT_SORT", raising=False)
+            out.append(product_step(g, f, dt, di))
+            rem.append(g.get_removed_cells())
+        monkeypatch.delenv("DCCRGX_KEPT_SORT", raising=False)
+        assert out[0] == out[1], step
+        assert np.array_equal(rem[0], rem[1]), step
+        assert np.all(np.diff(rem[0].astype(np.int64)) > 0), step
+        merged += len(rem[0])
+        assert np.array_equal(grids[0][1][0].get(0, grids[0][0].n_local), grids[1][1][0].get(0, grids[1][0].n_local))
+    assert merged > 0
+    for g, _ in grids:
+        g.close()

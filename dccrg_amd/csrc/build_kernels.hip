@@ -569,9 +569,14 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // coarser probe needed).  Otherwise, and for the misses, the probes of
 // face_dir.  The table is the same either way.  The loop runs whole waves
 // (wave_reserve needs every lane).
+// chunk_keys (non-null): a wave's 64 rows are one chunk (r / 64); its finer
+// faces' keys go to chunk_keys[384 c ...] in (row, direction) order and
+// their number to chunk_cnt[c], so a scan of the counts numbers every finer
+// face in (row, direction) order - no sort of the keys
+constexpr uint32_t kChunkKeys = 6 * 64;
 __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, size_t nrows, size_t run1,
                                   bool morton, int32_t* ell, unsigned long long* n_fine, uint32_t* fine_keys,
-                                  size_t key_cap, int32_t* err) {
+                                  size_t key_cap, int32_t* err, uint32_t* chunk_keys, uint32_t* chunk_cnt) {
 	const SlotExists ex{M};
 	const size_t stride = size_t(gridDim.x) * blockDim.x;
 	for (size_t r = blockIdx.x * size_t(blockDim.x) + threadIdx.x; r - lane_id() < nrows; r += stride) {
@@ -646,6 +651,16 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 #pragma unroll
 			for (int j = 0; j < 3; j++) ev[j] = i2v{o6[2 * j], o6[2 * j + 1]};
 		}
+		if (chunk_keys) {
+			const int incl = wave_incl_scan(int(kf));
+			const size_t c = (r - lane_id()) >> 6;
+			if (lane_id() == WAVE - 1) chunk_cnt[c] = uint32_t(incl);
+			uint32_t at = uint32_t(incl) - kf;
+			if (live)
+				for (int dir = 0; dir < 6; dir++)
+					if (o6[dir] == -2) chunk_keys[kChunkKeys * c + at++] = (uint32_t(r) << 3) | uint32_t(dir);
+			continue;
+		}
 		if (__ballot(kf != 0) == 0) continue;
 		unsigned long long at = wave_reserve(n_fine, kf);
 		if (live)
@@ -659,10 +674,23 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 
 // the finer faces in key order: f = the key's position
 __global__ void face_fine_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids, const uint32_t* fine_keys, size_t n,
-                                 int32_t* ell, int32_t* fine, int32_t* err) {
+                                 int32_t* ell, int32_t* fine, int32_t* err, const uint32_t* chunk_keys,
+                                 const uint32_t* chunk_off, uint32_t n_chunks) {
 	const DevExists ex{M};
 	for (size_t f = blockIdx.x * size_t(blockDim.x) + threadIdx.x; f < n; f += size_t(gridDim.x) * blockDim.x) {
-		const uint32_t key = fine_keys[f];
+		uint32_t key;
+		if (chunk_keys) {
+			// the chunk holding finer face f: the last offset <= f
+			uint32_t lo = 0, hi = n_chunks;
+			while (hi - lo > 1) {
+				const uint32_t mid = (lo + hi) >> 1;
+				if (chunk_off[mid] <= uint32_t(f)) lo = mid;
+				else hi = mid;
+			}
+			key = chunk_keys[size_t(kChunkKeys) * lo + (uint32_t(f) - chunk_off[lo])];
+		} else {
+			key = fine_keys[f];
+		}
 		const size_t r = size_t(key >> 3);
 		const int dir = int(key & 7);
 		uint64_t c[3];
@@ -1591,6 +1619,25 @@ void k_iterator_lists(const uint32_t* nof_ptr, const uint64_t* nof_id, const int
 size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids, size_t nrows, size_t run1,
                     bool morton, int32_t* ell, DBuf<int32_t>& fine, int32_t* err, hipStream_t s) {
 	DX_REQUIRE(nrows < (size_t(1) << 29), "too many local cells for the face keys");
+	if (nrows && !(std::getenv("DCCRGX_FACE_KEYS") && std::strcmp(std::getenv("DCCRGX_FACE_KEYS"), "sort") == 0)) {
+		// finer faces numbered by a scan of per-chunk counts (face_table_kernel)
+		const size_t nch = (nrows + 63) / 64;
+		DX_REQUIRE(nch * kChunkKeys < (size_t(1) << 32), "too many rows for the chunked face keys");
+		DBuf<uint32_t> ckeys, ccnt, coff;
+		ckeys.alloc(nch * kChunkKeys);
+		ccnt.alloc(nch + 1);
+		coff.alloc(nch + 1);
+		face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit, ell,
+		                                                       nullptr, nullptr, 0, err, ckeys.p, ccnt.p);
+		HIP_CHECK(hipGetLastError());
+		const size_t nf = scan_exclusive_u32(ccnt.p, coff.p, nch, s);
+		fine.alloc(4 * nf + 4);
+		if (!nf) return 0;
+		face_fine_kernel<<<grid_for(nf, 256), 256, 0, s>>>(m, M, slot_ids, nullptr, nf, ell, fine.p, err, ckeys.p, coff.p,
+		                                                   uint32_t(nch));
+		HIP_CHECK(hipGetLastError());
+		return nf;
+	}
 	DBuf<unsigned long long> n_fine;
 	n_fine.alloc(1);
 	HIP_CHECK(hipMemsetAsync(n_fine.p, 0, 8, s));
@@ -1606,7 +1653,7 @@ size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids,
 		keys.alloc(cap);
 		if (nrows)
 			face_table_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(m, M, slot_ids, nrows, run1, morton && !M.implicit,
-			                                                       ell, n_fine.p, keys.p, cap, err);
+			                                                       ell, n_fine.p, keys.p, cap, err, nullptr, nullptr);
 		HIP_CHECK(hipGetLastError());
 		nf = size_t(read_counter(n_fine, s));
 		if (nf <= cap) break;
@@ -1627,7 +1674,7 @@ size_t k_face_table(const MapCtx& m, const DevMesh& M, const uint64_t* slot_ids,
 		HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys.p, sorted.p, nf, 0, bits, s));
 		keys.swap(sorted);
 	}
-	face_fine_kernel<<<grid_for(nf, 256), 256, 0, s>>>(m, M, slot_ids, keys.p, nf, ell, fine.p, err);
+	face_fine_kernel<<<grid_for(nf, 256), 256, 0, s>>>(m, M, slot_ids, keys.p, nf, ell, fine.p, err, nullptr, nullptr, 0);
 	HIP_CHECK(hipGetLastError());
 	return nf;
 }

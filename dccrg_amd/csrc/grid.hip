@@ -606,7 +606,11 @@ void stop_refining_impl(Grid& g) {
 	// cells_not_to_refine = old_donts (10039-10040): the spread set, the same
 	// on every rank, stays for the next stop_refining and refine_completely
 	// (2477-2491) until balance_load (3812)
-	g.dont_refine_cells = std::unordered_set<uint64_t>(D.begin(), D.end());
+	// (clear() of an unordered_set costs its bucket count even when empty, and
+	// the request sets keep the buckets of their largest size: cleared only
+	// when they hold something)
+	if (!D.empty()) g.dont_refine_cells = std::unordered_set<uint64_t>(D.begin(), D.end());
+	else if (!g.dont_refine_cells.empty()) g.dont_refine_cells.clear();
 	DX_LAP("sr.1_override_refines");
 	// the request set is exactly check_for_adaptation's device list: S starts
 	// as it, on the device as well
@@ -623,7 +627,7 @@ void stop_refining_impl(Grid& g) {
 		if (D.empty()) mine = std::move(rq);
 		else std::set_difference(rq.begin(), rq.end(), D.begin(), D.end(), std::back_inserter(mine));
 	}
-	g.refine_requests.clear();
+	if (!g.refine_requests.empty()) g.refine_requests.clear();
 	g.refine_bulk.clear();
 	DX_LAP("sr.2a_mine");
 	std::vector<uint64_t> S = gather_union(g, std::move(mine));
@@ -644,10 +648,10 @@ void stop_refining_impl(Grid& g) {
 	g.unrefine_dev.release();
 	std::vector<uint64_t> req(g.unrefine_requests.begin(), g.unrefine_requests.end());
 	req.insert(req.end(), g.unrefine_bulk.begin(), g.unrefine_bulk.end());
-	g.unrefine_requests.clear();
+	if (!g.unrefine_requests.empty()) g.unrefine_requests.clear();
 	g.unrefine_bulk.clear();
 	const std::vector<uint64_t> DU = gather_union(g, sorted_unique(g, vec(g.dont_unrefine_cells)));
-	g.dont_unrefine_cells.clear();
+	if (!g.dont_unrefine_cells.empty()) g.dont_unrefine_cells.clear();
 	DX_LAP("sr.3a_requests");
 	// S is final: one device copy for the passes below
 	if (!s_on_dev) upload(dS, S, s);

@@ -140,13 +140,19 @@ def test_face_table_sweep_bitwise_equals_tiles(gpu, base, R):
 
 
 def test_face_table_second_pass_same_table(gpu, monkeypatch):
-    """The face table's finer-face keys get room for a quarter of the rows
-    first and the pass runs again with room for all of them when that was
-    too little (k_face_table): forced here with room for one key, the
-    densities of three table sweeps (which read the table, finer faces
-    included) are bitwise those of the one-pass build."""
+    """The face table numbers its finer faces in (row, direction) order by a
+    scan of per-wave counts (k_face_table's default); the sorted form
+    (DCCRGX_FACE_KEYS=sort) gives the keys room for a quarter of the rows
+    first and runs the pass again with room for all of them when that was too
+    little: forced here with room for one key.  The densities of three table
+    sweeps (which read the table, finer faces included) are bitwise the same
+    for all three builds."""
     out = []
-    for cap in (None, "1"):
+    for keys, cap in ((None, None), ("sort", None), ("sort", "1")):
+        if keys is None:
+            monkeypatch.delenv("DCCRGX_FACE_KEYS", raising=False)
+        else:
+            monkeypatch.setenv("DCCRGX_FACE_KEYS", keys)
         if cap is None:
             monkeypatch.delenv("DCCRGX_FACE_KEY_CAP", raising=False)
         else:
@@ -162,8 +168,9 @@ def test_face_table_second_pass_same_table(gpu, monkeypatch):
         out.append(rho)
         g.close()
     monkeypatch.delenv("DCCRGX_FACE_KEY_CAP", raising=False)
-    for a, b in zip(*out):
-        assert np.array_equal(a, b)
+    monkeypatch.delenv("DCCRGX_FACE_KEYS", raising=False)
+    for a, b, c in zip(*out):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
 
 
 def _run_parity_grid(base=(32, 32, 8), R=2, steps=100):

@@ -1953,7 +1953,10 @@ void k_apply_refines(const MapCtx& m, const uint64_t* kid, const int32_t* kown, 
 	out_own.alloc(n_out + 1);
 	if (src) {
 		src->alloc(n_out + 1);
-		HIP_CHECK(hipMemsetAsync(src->p, 0xff, (n_out + 1) * 4, s));
+		// prefix_fill_kernel writes every output of the prefix; only the rest
+		// (refine_fill_kernel writes no sources) starts at -1
+		if (np < n) HIP_CHECK(hipMemsetAsync(src->p, 0xff, (n_out + 1) * 4, s));
+		else HIP_CHECK(hipMemsetAsync(src->p + n_out, 0xff, 4, s));
 	}
 	if (np) {
 		prefix_fill_kernel<<<grid_for(np, 256), 256, 0, s>>>(m, kid, kown, cls.p, np, pos.p, out_id.p, out_own.p,

@@ -403,7 +403,9 @@ __global__ void extract_send_kernel(const uint64_t* nto_id, const uint32_t* nto_
 // the sorted neighbors_of keys: cells that only this rank's cells' neighbors_to
 // reach (the reference's remote neighbors_to-only copies)
 __global__ void extract_extra_kernel(const uint64_t* ids, size_t n, DevMesh M, int rank, uint64_t stride,
-                                     const uint64_t* of_keys, size_t n_of, uint64_t* out, unsigned long long* counter) {
+                                     const uint64_t* of_keys, size_t n_of, uint64_t* out, unsigned long long* counter,
+                                     const unsigned long long* n_of_dev = nullptr) {
+	if (n_of_dev) n_of = size_t(*n_of_dev);
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
 		const uint64_t id = ids[i];
 		if (id == error_cell) continue;
@@ -1477,6 +1479,126 @@ void k_send_by_owner(const uint64_t* nto_id, const uint32_t* nto_ptr, size_t n_e
 	group_by_owner(keys.p, owners.p, read_counter(ctr, s), stride, size, out, s);
 }
 
+namespace {
+__global__ void fill_u64_kernel(uint64_t* __restrict__ p, size_t n, uint64_t v) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) p[i] = v;
+}
+// a sorted unique list padded with one sentinel group: drop it from the count
+__global__ void drop_sentinel_kernel(const uint64_t* __restrict__ u, unsigned long long* __restrict__ cnt, uint64_t v) {
+	if (threadIdx.x == 0 && *cnt > 0 && u[*cnt - 1] == v) *cnt -= 1;
+}
+__global__ void strip_owner_kernel(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ cnt,
+                                   uint64_t stride, uint64_t* __restrict__ ids) {
+	const size_t n = size_t(*cnt);
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		ids[i] = keys[i] % stride;
+}
+}  // namespace
+
+// keys padded with sentinels to their capacity, sorted and made unique on
+// the device, the count left on the device (no host read)
+static void sort_unique_padded(DBuf<uint64_t>& keys, size_t cap, int bits, uint64_t sentinel, DBuf<uint64_t>& uniq,
+                               unsigned long long* d_count, hipStream_t s) {
+	DBuf<uint64_t> tmp;
+	tmp.alloc(cap + 1);
+	uniq.alloc(cap + 1);
+	size_t b1 = 0, b2 = 0;
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, keys.p, tmp.p, cap, 0, bits, s));
+	HIP_CHECK(hipcub::DeviceSelect::Unique(nullptr, b2, tmp.p, uniq.p, d_count, cap, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(std::max(b1, b2) + 1);
+	HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(temp.p, b1, keys.p, tmp.p, cap, 0, bits, s));
+	HIP_CHECK(hipcub::DeviceSelect::Unique(temp.p, b2, tmp.p, uniq.p, d_count, cap, s));
+	drop_sentinel_kernel<<<1, 64, 0, s>>>(uniq.p, d_count, sentinel);
+	HIP_CHECK(hipGetLastError());
+}
+
+bool k_halo_lists(const uint64_t* of_id, size_t t_of, const uint64_t* to_id, const uint32_t* p_to, size_t t_to,
+                  const uint64_t* slot_ids, size_t row0, size_t nrows, const DevMesh& M, int rank, int size,
+                  HaloLists& out, hipStream_t s) {
+	out.recv.clear();
+	out.send.clear();
+	out.extra.clear();
+	out.n_recv = out.n_send = 0;
+	const uint64_t stride = M.last + 1;
+	if (uint64_t(size) > ~uint64_t(0) / stride) return false;  // keys would overflow: the pair path
+	int bits = 1;
+	const uint64_t top = uint64_t(size) * stride;
+	while (bits < 64 && (top >> bits)) bits++;
+	const uint64_t sentinel = bits >= 64 ? ~uint64_t(0) : (uint64_t(1) << bits) - 1;  // > every key
+	DBuf<unsigned long long> cnt;  // 0 of keys, 1 to keys, 2 extra ids, 3 extract counter of, 4 of to
+	cnt.alloc(5);
+	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 5 * sizeof(unsigned long long), s));
+	DBuf<uint64_t> kof, kto;
+	const size_t cof = std::max<size_t>(t_of, 1), cto = std::max<size_t>(t_to, 1);
+	kof.alloc(cof + 1);
+	kto.alloc(cto + 1);
+	fill_u64_kernel<<<grid_for(cof, 256), 256, 0, s>>>(kof.p, cof, sentinel);
+	fill_u64_kernel<<<grid_for(cto, 256), 256, 0, s>>>(kto.p, cto, sentinel);
+	if (t_of)
+		extract_remote_kernel<<<grid_for(t_of, 256), 256, 0, s>>>(of_id, t_of, M, rank, stride, kof.p, nullptr, cnt.p + 3);
+	if (nrows && t_to)
+		extract_send_kernel<<<grid_for(nrows, 256), 256, 0, s>>>(to_id, p_to, slot_ids, row0, nrows, M, rank, stride, kto.p,
+		                                                         nullptr, cnt.p + 4);
+	HIP_CHECK(hipGetLastError());
+	// the extracted counts first: sorting the capacity (several times the
+	// remote entries) costs more than this read
+	unsigned long long ext[2] = {0, 0};
+	d2h_small(ext, cnt.p + 3, sizeof(ext), s);
+	if (ext[0]) sort_unique_padded(kof, size_t(ext[0]), bits, sentinel, out.recv_keys, cnt.p + 0, s);
+	else out.recv_keys.alloc(1);
+	if (ext[1]) sort_unique_padded(kto, size_t(ext[1]), bits, sentinel, out.send_keys, cnt.p + 1, s);
+	else out.send_keys.alloc(1);
+	// remote neighbors_to that are no neighbors_of (none for a symmetric hood)
+	DBuf<uint64_t> ex;
+	ex.alloc(cto + 1);
+	if (t_to)
+		extract_extra_kernel<<<grid_for(t_to, 256), 256, 0, s>>>(to_id, t_to, M, rank, stride, out.recv_keys.p, 0, ex.p,
+		                                                         cnt.p + 2, cnt.p + 0);
+	HIP_CHECK(hipGetLastError());
+	unsigned long long h[3] = {0, 0, 0};
+	d2h_small(h, cnt.p, sizeof(h), s);
+	out.n_recv = size_t(h[0]);
+	out.n_send = size_t(h[1]);
+	// the three lists in one read
+	const size_t b0 = 8 * size_t(h[0]), b1 = 8 * size_t(h[1]), b2 = 8 * size_t(h[2]);
+	std::vector<uint64_t> all((b0 + b1 + b2) / 8);
+	if (!all.empty()) {
+		DBuf<uint8_t> stage;
+		stage.alloc(b0 + b1 + b2);
+		if (b0) HIP_CHECK(hipMemcpyAsync(stage.p, out.recv_keys.p, b0, hipMemcpyDeviceToDevice, s));
+		if (b1) HIP_CHECK(hipMemcpyAsync(stage.p + b0, out.send_keys.p, b1, hipMemcpyDeviceToDevice, s));
+		if (b2) HIP_CHECK(hipMemcpyAsync(stage.p + b0 + b1, ex.p, b2, hipMemcpyDeviceToDevice, s));
+		d2h_small(all.data(), stage.p, b0 + b1 + b2, s);
+	}
+	for (size_t i = 0; i < size_t(h[0]); i++) out.recv[int(all[i] / stride)].push_back(all[i] % stride);
+	for (size_t i = 0; i < size_t(h[1]); i++) out.send[int(all[h[0] + i] / stride)].push_back(all[h[0] + i] % stride);
+	out.extra.assign(all.begin() + ptrdiff_t(h[0] + h[1]), all.end());
+	std::sort(out.extra.begin(), out.extra.end());
+	out.extra.erase(std::unique(out.extra.begin(), out.extra.end()), out.extra.end());
+	// the lists' ids on the device in wire order (peer, then id): halo slot
+	// ids and send cells without an upload
+	out.recv_ids.alloc(size_t(h[0]) + 1);
+	out.send_ids.alloc(size_t(h[1]) + 1);
+	if (h[0]) strip_owner_kernel<<<grid_for(size_t(h[0]), 256), 256, 0, s>>>(out.recv_keys.p, cnt.p + 0, stride, out.recv_ids.p);
+	if (h[1]) strip_owner_kernel<<<grid_for(size_t(h[1]), 256), 256, 0, s>>>(out.send_keys.p, cnt.p + 1, stride, out.send_ids.p);
+	HIP_CHECK(hipGetLastError());
+	return true;
+}
+
+namespace {
+__global__ void iota_i32_from_kernel(int32_t* out, size_t n, int32_t first) {
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+		out[i] = first + int32_t(i);
+}
+}  // namespace
+
+void k_iota_i32(int32_t* out, size_t n, int32_t first, hipStream_t s) {
+	if (!n) return;
+	iota_i32_from_kernel<<<grid_for(n, 256), 256, 0, s>>>(out, n, first);
+	HIP_CHECK(hipGetLastError());
+}
+
 __global__ void iota_i32_kernel(int32_t* out, size_t n) {
 	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
 		out[i] = int32_t(i);
@@ -1582,6 +1704,24 @@ uint32_t scan_exclusive_u32_at(const uint32_t* in, uint32_t* out, size_t n, hipS
 	d2h_small(h, picked.p, sizeof(uint32_t) * size_t(k + 1), s);
 	for (int j = 0; j < k; j++) vals[j] = h[j + 1];
 	return h[0];
+}
+
+void scan_exclusive_u32_pair(const uint32_t* in1, uint32_t* out1, const uint32_t* in2, uint32_t* out2, size_t n,
+                             hipStream_t s, size_t& t1, size_t& t2) {
+	size_t bytes = 0;
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in1, out1, n + 1, s));
+	DBuf<uint8_t> temp;
+	temp.alloc(bytes + 1);
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in1, out1, n + 1, s));
+	HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(temp.p, bytes, in2, out2, n + 1, s));
+	DBuf<uint32_t> tot;
+	tot.alloc(2);
+	HIP_CHECK(hipMemcpyAsync(tot.p, out1 + n, 4, hipMemcpyDeviceToDevice, s));
+	HIP_CHECK(hipMemcpyAsync(tot.p + 1, out2 + n, 4, hipMemcpyDeviceToDevice, s));
+	uint32_t h[2] = {0, 0};
+	d2h_small(h, tot.p, sizeof(h), s);
+	t1 = h[0];
+	t2 = h[1];
 }
 
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s) {

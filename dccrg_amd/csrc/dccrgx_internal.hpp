@@ -857,6 +857,20 @@ int max_hood_items();  // largest stencil the neighbors_to dedupe can hold in LD
 void k_remote_by_owner(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size,
                        std::map<int, std::vector<uint64_t>>& out, hipStream_t s, DBuf<uint64_t>* keep = nullptr,
                        size_t* keep_n = nullptr);
+// Rebuild step 3 in one device pass and two reads (the pair-free case): the
+// receive lists (remote neighbors_of), the send lists (local cells in whose
+// neighbors_to a remote cell appears) grouped by peer, ascending, the remote
+// neighbors_to-only ids, and both lists' ids on the device in wire order
+struct HaloLists {
+	std::map<int, std::vector<uint64_t>> recv, send;
+	std::vector<uint64_t> extra;
+	DBuf<uint64_t> recv_keys, send_keys, recv_ids, send_ids;
+	size_t n_recv = 0, n_send = 0;
+};
+bool k_halo_lists(const uint64_t* of_id, size_t t_of, const uint64_t* to_id, const uint32_t* p_to, size_t t_to,
+                  const uint64_t* slot_ids, size_t row0, size_t nrows, const DevMesh& M, int rank, int size,
+                  HaloLists& out, hipStream_t s);
+void k_iota_i32(int32_t* out, size_t n, int32_t first, hipStream_t s);
 // the remote ids of `ids` whose key is not among `of_keys` (kept by
 // k_remote_by_owner), ascending; false when keys would overflow
 bool k_remote_extra(const uint64_t* ids, size_t n, const DevMesh& M, int rank, int size, const uint64_t* of_keys,
@@ -875,6 +889,9 @@ void k_sorted_slot_index(const uint64_t* slot_ids, size_t n, std::vector<uint64_
 void k_morton_merge2(const MapCtx& m, uint64_t* ids, size_t n, size_t run1, hipStream_t s);
 void k_morton_sort(const MapCtx& m, uint64_t* ids, size_t n, hipStream_t s);
 uint32_t scan_exclusive_u32(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s);  // returns total
+// two scans of n + 1 entries (the same temp storage size), both totals in one read
+void scan_exclusive_u32_pair(const uint32_t* in1, uint32_t* out1, const uint32_t* in2, uint32_t* out2, size_t n,
+                             hipStream_t s, size_t& t1, size_t& t2);
 // the same, and out[at[j]] (j < k <= 3) into vals, all in one device read
 uint32_t scan_exclusive_u32_at(const uint32_t* in, uint32_t* out, size_t n, hipStream_t s, const size_t* at, int k,
                                uint32_t* vals);

@@ -478,6 +478,8 @@ void rebuild(Grid& g, Mesh& nm) {
 	H.send_ids.clear();
 	H.recv_ids.clear();
 	g.extra_remote.clear();
+	HaloLists HL;  // the lists' device copies (k_halo_lists), for steps 4 and 5
+	bool hl = false;
 	if (g.n_outer > 0) {
 		const size_t no = g.n_outer;
 		DBuf<uint32_t> c_of, c_to, p_of, p_to;
@@ -486,8 +488,8 @@ void rebuild(Grid& g, Mesh& nm) {
 		p_of.alloc(no + 1);
 		p_to.alloc(no + 1);
 		k_count_rows(m, g.d_hood.p, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, c_of.p, c_to.p, s);
-		const size_t t_of = scan_exclusive_u32(c_of.p, p_of.p, no, s);
-		const size_t t_to = scan_exclusive_u32(c_to.p, p_to.p, no, s);
+		size_t t_of = 0, t_to = 0;
+		scan_exclusive_u32_pair(c_of.p, p_of.p, c_to.p, p_to.p, no, s, t_of, t_to);
 		DBuf<uint64_t> of_id, to_id;
 		DBuf<int32_t> of_off;
 		of_id.alloc(t_of + 1);
@@ -496,16 +498,27 @@ void rebuild(Grid& g, Mesh& nm) {
 		k_fill_neighbors_of(m, g.d_hood.p, nh, dm, lsp, g.n_inner, no, p_of.p, of_id.p, of_off.p, s);
 		k_fill_neighbors_to(m, g.d_hood_to.p, nh, dm, lsp, g.n_inner, no, p_to.p, to_id.p, s);
 		DX_LAP("rb.3a_outer_rows");
+		std::vector<uint64_t> extra;
+		// the receive / send lists and the neighbors_to-only ids in one device
+		// pass and two reads (DCCRGX_HALO_LISTS=split: the three separate
+		// passes below)
+		const char* hls = std::getenv("DCCRGX_HALO_LISTS");
+		hl = !(hls && std::strcmp(hls, "split") == 0) &&
+		     k_halo_lists(of_id.p, t_of, to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, HL, s);
+		if (hl) {
+			H.recv_ids = std::move(HL.recv);
+			H.send_ids = std::move(HL.send);
+			extra = HL.extra;
+		}
 		DBuf<uint64_t> of_keys;
 		size_t n_of_keys = 0;
-		k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s, &of_keys, &n_of_keys);
+		if (!hl) k_remote_by_owner(of_id.p, t_of, dm, g.rank, g.size, H.recv_ids, s, &of_keys, &n_of_keys);
 		DX_LAP("rb.3b_recv_lists");
-		k_send_by_owner(to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
+		if (!hl) k_send_by_owner(to_id.p, p_to.p, t_to, lsp, g.n_inner, no, dm, g.rank, g.size, H.send_ids, s);
 		DX_LAP("rb.3c_send_lists");
 		// remote neighbors_to that are no neighbors_of: found on the device
 		// (none for a symmetric neighborhood), the pairs path on the host
-		std::vector<uint64_t> extra;
-		if (!k_remote_extra(to_id.p, t_to, dm, g.rank, g.size, of_keys.p, n_of_keys, extra, s)) {
+		if (!hl && !k_remote_extra(to_id.p, t_to, dm, g.rank, g.size, of_keys.p, n_of_keys, extra, s)) {
 			std::map<int, std::vector<uint64_t>> rem_to;
 			k_remote_by_owner(to_id.p, t_to, dm, g.rank, g.size, rem_to, s);
 			for (auto& kv : rem_to) {
@@ -544,8 +557,16 @@ void rebuild(Grid& g, Mesh& nm) {
 	g.n_slots = nl + halo.size();
 	g.slot_ids.alloc(g.n_slots + 1);
 	if (nl) HIP_CHECK(hipMemcpyAsync(g.slot_ids.p, lsp, nl * 8, hipMemcpyDeviceToDevice, s));
-	if (!halo.empty())
+	if (hl && HL.n_recv == H.n_recv) {
+		// the receive ids already on the device in this order; the few
+		// neighbors_to-only ones uploaded
+		if (H.n_recv)
+			HIP_CHECK(hipMemcpyAsync(g.slot_ids.p + nl, HL.recv_ids.p, H.n_recv * 8, hipMemcpyDeviceToDevice, s));
+		if (!g.extra_remote.empty())
+			h2d(g.slot_ids.p + nl + H.n_recv, g.extra_remote.data(), g.extra_remote.size() * 8, s);
+	} else if (!halo.empty()) {
 		h2d(g.slot_ids.p + nl, halo.data(), halo.size() * 8, s);
+	}
 	DBuf<int32_t> err;
 	err.alloc(1);
 	HIP_CHECK(hipMemsetAsync(err.p, 0, 4, s));
@@ -553,11 +574,8 @@ void rebuild(Grid& g, Mesh& nm) {
 	dm = g.dm();
 	DX_REQUIRE(!direct || (g.n_slots == nl && g.n_inner == nl), "internal error: direct slots with halo or outer cells");
 	if (!direct) k_hash_set_slots(dm, g.slot_ids.p, g.n_slots, err.p, s);
-	{
-		std::vector<int32_t> rs(H.n_recv);
-		std::iota(rs.begin(), rs.end(), int32_t(nl));
-		upload(H.recv_slots, rs, s);
-	}
+	H.recv_slots.alloc(H.n_recv + 1);
+	k_iota_i32(H.recv_slots.p, H.n_recv, int32_t(nl), s);
 
 	DX_LAP("rb.4_slots_hash");
 	// 5. send slots (ascending id per peer = wire order)
@@ -570,9 +588,15 @@ void rebuild(Grid& g, Mesh& nm) {
 	H.n_send = sids.size();
 	{
 		DBuf<uint64_t> d;
-		upload(d, sids, s);
+		const uint64_t* dsid = nullptr;
+		if (hl && HL.n_send == sids.size()) {
+			dsid = HL.send_ids.p;  // the send cells already on the device in this order
+		} else {
+			upload(d, sids, s);
+			dsid = d.p;
+		}
 		H.send_slots.alloc(sids.size() + 1);
-		k_lookup_slots(d.p, sids.size(), dm, H.send_slots.p, err.p, s);
+		k_lookup_slots(dsid, sids.size(), dm, H.send_slots.p, err.p, s);
 		// (direct slots without send cells: nothing above can set the flag)
 		if (!(direct && sids.empty())) {
 			int32_t herr = 0;
@@ -680,8 +704,8 @@ void ensure_csr(Grid& g) {
 	g.nto_ptr.alloc(nl + 1);
 	g.it_ptr.alloc(nl + 1);
 	k_count_rows(g.m, g.d_hood.p, g.d_hood_to.p, nh, dm, g.slot_ids.p, 0, nl, c_of.p, c_to.p, s);
-	const size_t t_of = scan_exclusive_u32(c_of.p, g.nof_ptr.p, nl, s);
-	const size_t t_to = scan_exclusive_u32(c_to.p, g.nto_ptr.p, nl, s);
+	size_t t_of = 0, t_to = 0;
+	scan_exclusive_u32_pair(c_of.p, g.nof_ptr.p, c_to.p, g.nto_ptr.p, nl, s, t_of, t_to);
 	g.nof_id.alloc(t_of + 1);
 	g.nof_off.alloc(3 * t_of + 3);
 	g.nof_slot.alloc(t_of + 1);

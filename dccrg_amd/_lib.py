@@ -47,6 +47,8 @@ _SIGS = {
     "dccrgx_get_initial_length": (C.c_int, [vp, vp]),
     "dccrgx_get_periodic": (C.c_int, [vp, vp]),
     "dccrgx_get_geometry": (C.c_int, [vp, vp, vp]),
+    "dccrgx_set_geometry_block": (C.c_int, [vp, vp, sz]),
+    "dccrgx_get_geometry_block": (C.c_int, [vp, vp, sz, P(sz)]),
     "dccrgx_set_periodic": (C.c_int, [vp, C.c_int, C.c_int, C.c_int]),
     "dccrgx_set_neighborhood_length": (C.c_int, [vp, C.c_uint]),
     "dccrgx_initialize": (C.c_int, [vp]),

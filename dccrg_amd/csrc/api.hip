@@ -294,6 +294,24 @@ static PoScalars po_solve(Grid& g, const PoParams& prm, bool failsafe) {
 // pwrite at offsets derived from the all-gathered per-rank cell counts.
 static constexpr uint64_t kEndianCheck = 0x1234567890abcdefULL;
 static constexpr int kCartesianGeometryId = 1;
+static constexpr int kStretchedGeometryId = 2;
+
+// bytes of a Stretched_Cartesian_Geometry block (write 652-715: int id 2, 3 x
+// uint64 coordinate counts, then each dimension's coordinates as doubles)
+// given its first 28 bytes; 0 when they are no such block
+static size_t stretched_block_bytes(const uint8_t* head) {
+	int32_t id = 0;
+	uint64_t cnt[3];
+	std::memcpy(&id, head, 4);
+	std::memcpy(cnt, head + 4, 24);
+	if (id != kStretchedGeometryId) return 0;
+	uint64_t tot = 0;
+	for (int d = 0; d < 3; d++) {
+		if (cnt[d] < 2 || cnt[d] > (uint64_t(1) << 40)) return 0;  // the reference's set() needs two per dimension
+		tot += cnt[d];
+	}
+	return 28 + size_t(8 * tot);
+}
 
 static std::vector<uint8_t> grid_block(const Grid& g) {
 	std::vector<uint8_t> b;
@@ -308,6 +326,10 @@ static std::vector<uint8_t> grid_block(const Grid& g) {
 	put(&hood, 4);
 	const uint8_t per[3] = {uint8_t(g.per[0] != 0), uint8_t(g.per[1] != 0), uint8_t(g.per[2] != 0)};
 	put(per, 3);
+	if (!g.geo_block.empty()) {
+		put(g.geo_block.data(), g.geo_block.size());  // the stretched geometry's block
+		return b;
+	}
 	const int32_t gid = kCartesianGeometryId;
 	put(&gid, 4);
 	put(g.start, 24);
@@ -446,9 +468,10 @@ static void start_load_impl(Grid& g, const char* path, uint64_t offset, size_t h
 	pread_all(fd, &endian, 8, off);
 	DX_REQUIRE(endian == kEndianCheck, "grid file endianness check failed");
 	off += 8;
+	// mapping + neighborhood length + topology (35 B), then the geometry block:
+	// Cartesian (id 1, 52 B) or stretched (id 2, 28 B + the coordinates)
 	uint8_t blk[87];
-	pread_all(fd, blk, sizeof(blk), off);
-	off += sizeof(blk);
+	pread_all(fd, blk, 63, off);
 	uint64_t len[3];
 	int32_t R, gid;
 	uint32_t hood;
@@ -457,9 +480,34 @@ static void start_load_impl(Grid& g, const char* path, uint64_t offset, size_t h
 	std::memcpy(&R, blk + 24, 4);
 	std::memcpy(&hood, blk + 28, 4);
 	std::memcpy(&gid, blk + 35, 4);
-	std::memcpy(start, blk + 39, 24);
-	std::memcpy(l0, blk + 63, 24);
-	DX_REQUIRE(gid == kCartesianGeometryId, "grid file geometry is not Cartesian_Geometry");
+	std::vector<uint8_t> geo;
+	if (gid == kStretchedGeometryId) {
+		const size_t nb = stretched_block_bytes(blk + 35);
+		DX_REQUIRE(nb > 0 && nb <= uint64_t(file_end) - (off + 35), "grid file: invalid stretched geometry block");
+		geo.resize(nb);
+		pread_all(fd, geo.data(), nb, off + 35);
+		uint64_t cnt[3];
+		std::memcpy(cnt, geo.data() + 4, 24);
+		std::vector<double> c(size_t(cnt[0] + cnt[1] + cnt[2]));
+		std::memcpy(c.data(), geo.data() + 28, c.size() * 8);
+		// the library's device geometry: each dimension's start and first
+		// level-0 cell length (exact for evenly spaced coordinates; uneven
+		// spacing stays with the facade's host-side geometry)
+		size_t at = 0;
+		for (int d = 0; d < 3; d++) {
+			start[d] = c[at];
+			l0[d] = c[at + 1] - c[at];
+			at += size_t(cnt[d]);
+		}
+		off += 35 + nb;
+	} else {
+		DX_REQUIRE(gid == kCartesianGeometryId,
+		           "grid file geometry is neither Cartesian_Geometry nor Stretched_Cartesian_Geometry");
+		pread_all(fd, blk + 63, 24, off + 63);
+		std::memcpy(start, blk + 39, 24);
+		std::memcpy(l0, blk + 63, 24);
+		off += sizeof(blk);
+	}
 	// the same checks as the setters (a foreign or corrupt file must not
 	// reach the builders)
 	for (int d = 0; d < 3; d++) DX_REQUIRE(len[d] > 0, "grid file: grid length must be > 0");
@@ -474,6 +522,7 @@ static void start_load_impl(Grid& g, const char* path, uint64_t offset, size_t h
 	}
 	g.R = R;
 	g.hood_len = hood;
+	g.geo_block = std::move(geo);
 	init_impl(g);
 	uint64_t total = 0;
 	pread_all(fd, &total, 8, off);
@@ -1037,6 +1086,33 @@ int dccrgx_get_geometry(dccrgx_grid* gp, double start[3], double l0[3]) {
 			if (start) start[d] = g.start[d];
 			if (l0) l0[d] = g.l0[d];
 		}
+		return 0;
+	});
+}
+
+int dccrgx_set_geometry_block(dccrgx_grid* gp, const void* bytes, size_t n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		if (n == 0) {
+			g.geo_block.clear();
+			return 0;
+		}
+		DX_REQUIRE(bytes != nullptr && n >= 28, "geometry block too short");
+		const uint8_t* b = static_cast<const uint8_t*>(bytes);
+		DX_REQUIRE(stretched_block_bytes(b) == n, "not a Stretched_Cartesian_Geometry block (id 2, counts, coordinates)");
+		g.geo_block.assign(b, b + n);
+		return 0;
+	});
+}
+
+int dccrgx_get_geometry_block(dccrgx_grid* gp, void* out, size_t cap, size_t* n) {
+	return guard([&] {
+		GRID_OR_FAIL(gp);
+		DX_REQUIRE(n != nullptr, "null count");
+		*n = g.geo_block.size();
+		if (!out) return 0;
+		DX_REQUIRE(cap >= g.geo_block.size(), "buffer too small for the geometry block");
+		if (!g.geo_block.empty()) std::memcpy(out, g.geo_block.data(), g.geo_block.size());
 		return 0;
 	});
 }

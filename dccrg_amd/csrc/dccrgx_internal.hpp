@@ -546,6 +546,11 @@ struct Grid {
 	std::vector<int32_t> hood;     // neighborhood_of, 3 per item
 	std::vector<int32_t> hood_to;  // neighborhood_to (negated)
 	double start[3] = {0, 0, 0}, l0[3] = {1, 1, 1};
+	// a grid file's geometry block other than the Cartesian one (the bytes
+	// Stretched_Cartesian_Geometry::write makes, id 2): written by
+	// save_grid_data instead of start / l0, read back by load_grid_data
+	// (dccrgx_set_geometry_block / dccrgx_get_geometry_block); empty: Cartesian
+	std::vector<uint8_t> geo_block;
 
 	Mesh mesh;
 	std::unordered_map<uint64_t, int> pins;  // local cells pinned to a process (pin 5832-5909)

@@ -275,6 +275,25 @@ class Dccrg:
         check(lib().dccrgx_set_geometry(self.h, s, l0))
         return self
 
+    def set_geometry_block(self, block: bytes):
+        """The grid file's geometry block of a Stretched_Cartesian_Geometry
+        (dccrg_stretched_cartesian_geometry.hpp:652-715), written by
+        save_grid_data instead of the Cartesian block; b"" restores that."""
+        b = bytes(block)
+        buf = C.create_string_buffer(b, len(b)) if b else None
+        check(lib().dccrgx_set_geometry_block(self.h, buf, len(b)))
+        return self
+
+    def geometry_block(self) -> bytes:
+        """The stretched geometry block a load read (b"" for a Cartesian file)."""
+        n = C.c_size_t()
+        check(lib().dccrgx_get_geometry_block(self.h, None, 0, C.byref(n)))
+        if not n.value:
+            return b""
+        buf = C.create_string_buffer(n.value)
+        check(lib().dccrgx_get_geometry_block(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[: n.value]
+
     def geometry(self, cells):
         """(centers, lengths), each (n, 3): Cartesian_Geometry get_center /
         get_length (dccrg_cartesian_geometry.hpp:282-362) of many cells."""

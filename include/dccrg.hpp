@@ -333,6 +333,15 @@ public:
 		topology_ = t;
 	}
 	bool set(const Parameters&) { return true; }
+	// the geometry block save_grid_data writes (empty: the library's
+	// Cartesian block) and the check of the block a load found (empty: a
+	// Cartesian file), the reference's write / read of each geometry
+	std::vector<char> file_block() const { return {}; }
+	bool from_file_block(const std::vector<char>& b) {
+		if (b.empty()) return true;
+		std::cerr << "Wrong geometry: 2 (Stretched_Cartesian_Geometry) in the grid file" << std::endl;
+		return false;
+	}
 	std::array<double, 3> get_length(uint64_t cell) const { return batch(cell, false); }
 	std::array<double, 3> get_center(uint64_t cell) const { return batch(cell, true); }
 
@@ -946,6 +955,8 @@ public:
 	                    const size_t header_bytes = 0) {
 		sync_window();  // the bytes get_mpi_datatype describes now
 		upload_local();
+		const std::vector<char> geo = geometry_rw.file_block();  // Geometry::write's bytes (empty: Cartesian)
+		if (dccrgx_set_geometry_block(g_, geo.empty() ? nullptr : geo.data(), geo.size()) != DCCRGX_OK) return false;
 		return dccrgx_save_grid_data(g_, name.c_str(), offset, header, header_bytes) == DCCRGX_OK;
 	}
 	// the reference's form: the header is (address, count, datatype), written
@@ -1208,6 +1219,14 @@ private:
 			mapping_rw.length.set({{len[0], len[1], len[2]}});
 		}
 		geometry_rw.sync_from_library();
+		{
+			// Geometry::read: the file's geometry block (none for a Cartesian file)
+			size_t n = 0;
+			detail::check(dccrgx_get_geometry_block(g_, nullptr, 0, &n));
+			std::vector<char> geo(n);
+			if (n) detail::check(dccrgx_get_geometry_block(g_, geo.data(), n, &n));
+			if (!geometry_rw.from_file_block(geo)) return false;
+		}
 		refresh();
 		return true;
 	}
@@ -1677,6 +1696,11 @@ private:
 		void sync_from_library() {
 			Geometry::sync_from_library();
 			params_ = Geometry::get();
+		}
+		bool from_file_block(const std::vector<char>& b) {
+			if (!Geometry::from_file_block(b)) return false;
+			params_ = Geometry::get();
+			return true;
 		}
 		bool set(const typename Geometry::Parameters& p) {
 			params_ = p;

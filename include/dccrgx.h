@@ -37,7 +37,7 @@ extern "C" {
 
 typedef struct dccrgx_grid dccrgx_grid;
 
-#define DCCRGX_ABI_VERSION 9 /* dccrgx_abi_version() of a matching library */
+#define DCCRGX_ABI_VERSION 10 /* dccrgx_abi_version() of a matching library */
 
 #define DCCRGX_OK 0
 #define DCCRGX_EINVAL -1   /* bad argument / wrong state  (std::invalid_argument) */
@@ -110,6 +110,17 @@ int dccrgx_set_geometry(dccrgx_grid* g, const double start[3], const double leve
 /* Cartesian_Geometry::get_start / get_level_0_cell_length (ABI 8); either
  * output may be NULL */
 int dccrgx_get_geometry(dccrgx_grid* g, double start[3], double level_0_cell_length[3]);
+/* The grid file's geometry block of a Stretched_Cartesian_Geometry
+ * (Stretched_Cartesian_Geometry::write / read,
+ * dccrg_stretched_cartesian_geometry.hpp:652-800: int id 2, 3 x uint64
+ * coordinate counts, the coordinates as doubles), which save_grid_data then
+ * writes instead of the Cartesian block (n = 0: the Cartesian block again);
+ * DCCRGX_EINVAL for other bytes.  After load_grid_data of a file with such a
+ * block, dccrgx_get_geometry_block returns it (*n = 0 for a Cartesian file;
+ * out = NULL: the size only) and the library's own geometry takes each
+ * dimension's start and first cell length (ABI 10). */
+int dccrgx_set_geometry_block(dccrgx_grid* g, const void* bytes, size_t n);
+int dccrgx_get_geometry_block(dccrgx_grid* g, void* out, size_t cap, size_t* n);
 int dccrgx_geometry_batch(dccrgx_grid* g, const uint64_t* ids, size_t n, double* center, double* length);
 
 /* ---- mapping (dccrg_mapping.hpp) — host-side scalar queries -------------- */

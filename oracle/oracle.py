@@ -371,6 +371,28 @@ def grid_block_bytes(length, R, hood, periodic, start, l0):
             + struct.pack("<i3d3d", 1, *[float(v) for v in start], *[float(v) for v in l0]))
 
 
+def stretched_geometry_block(coordinates):
+    """Stretched_Cartesian_Geometry::write (dccrg_stretched_cartesian_geometry.hpp:
+    652-715): int geometry id 2, the three coordinate counts as uint64, then
+    each dimension's coordinates as doubles (data_size 808-817)."""
+    import struct
+
+    out = struct.pack("<i", 2) + struct.pack("<3Q", *[len(c) for c in coordinates])
+    for c in coordinates:
+        out += struct.pack("<%dd" % len(c), *[float(v) for v in c])
+    return out
+
+
+def grid_block_stretched_bytes(length, R, hood, periodic, coordinates):
+    """grid_block_bytes with the stretched geometry's block in place of the
+    Cartesian one (the reference's save_grid_data writes geometry.write's bytes
+    there, dccrg.hpp:1216-1231)."""
+    import struct
+
+    return (struct.pack("<3Qi", *[int(v) for v in length], int(R)) + struct.pack("<I", int(hood))
+            + struct.pack("<3B", *[1 if p else 0 for p in periodic]) + stretched_geometry_block(coordinates))
+
+
 def grid_file_bytes(block, header, offset, cells_by_rank, data_of):
     """A whole grid file as save_grid_data lays it out: `offset` zero bytes
     (untouched by the writer), the user header, uint64 0x1234567890abcdef,

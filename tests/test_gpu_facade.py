@@ -217,3 +217,23 @@ def test_variable_restart(gpu, tmp_path, Ps, Pl):
     out = mpirun("variable_restart", Pl, ["load", path])
     assert out.count("PASS") == Pl, out
     assert sum(int(m) for m in re.findall(r"PASS \d+ (\d+)", out)) == 20
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_stretched_geometry_restart(gpu, tmp_path, P):
+    """A Stretched_Cartesian_Geometry grid saved and loaded through the facade
+    (examples/stretched_restart.cpp): the file's geometry block is the
+    reference's Stretched_Cartesian_Geometry::write bytes
+    (dccrg_stretched_cartesian_geometry.hpp:652-715: id 2, the coordinate
+    counts, the coordinates), and the loaded grid has the same unevenly
+    spaced coordinates, payloads and cell centers / lengths."""
+    import struct
+
+    path = tmp_path / "stretched.dc"
+    out = mpirun("stretched_restart", P, [path])
+    assert out.count("PASS") == P, out
+    raw = open(path, "rb").read()
+    coords = [[0.0, 0.5, 1.5, 3.0, 5.0, 5.25], [-2.0, -1.0, 0.25, 4.0, 4.5], [10.0, 10.5, 12.0, 12.125]]
+    block = O.stretched_geometry_block(coords)
+    assert struct.unpack_from("<Q", raw, 0)[0] == 0x1234567890ABCDEF
+    assert raw[8 + 35:8 + 35 + len(block)] == block

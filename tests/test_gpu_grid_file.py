@@ -292,3 +292,51 @@ def test_save_over_longer_file_variable_size(gpu, tmp_path):
     assert all(np.array_equal(a, np.arange(int(n), dtype=np.int32) + 7) for a, n in zip(got, k))
     for x in (big, g, h, h1):
         x.close()
+
+
+def test_stretched_geometry_block_file_and_round_trip(gpu, tmp_path):
+    """A grid saved with a Stretched_Cartesian_Geometry carries that
+    geometry's block (dccrg_stretched_cartesian_geometry.hpp:652-715: id 2,
+    the coordinate counts, the coordinates) where a Cartesian grid has its
+    Cartesian block: the file is byte for byte the oracle's layout with that
+    block, and loading it returns the block and the payloads; a block of
+    another shape is refused."""
+    length, R, periodic, hood = (4, 3, 2), 1, (False, True, False), 1
+    g, _ = make_pair(length, R, periodic, hood, 1, 0.2, 3)
+    coords = [[0.0, 0.5, 1.5, 3.0, 5.0], [-2.0, -1.0, 0.25, 4.0], [10.0, 10.5, 12.0]]
+    block = O.stretched_geometry_block(coords)
+    g.set_geometry_block(block)
+    fill(g, 7)
+    path = tmp_path / "stretched.dc"
+    g.save_grid_data(path)
+    got = open(path, "rb").read()
+    exp = O.grid_file_bytes(O.grid_block_stretched_bytes(length, R, hood, periodic, coords), b"", 0,
+                            [g.local_cells()], lambda c: payload(c, 7))
+    assert got == exp
+    h = dccrg_amd.Dccrg(0, 1, 0)
+    a = h.add_field("a", np.uint32)
+    b = h.add_field("b", np.float64)
+    h.add_field("c", np.float64, False)
+    h.load_grid_data(path)
+    assert h.geometry_block() == block
+    assert np.array_equal(h.local_cells(), g.local_cells())
+    ids = h.slot_ids()[: h.n_local]
+    assert np.array_equal(a.get(0, h.n_local), (ids * np.uint64(2654435761) + np.uint64(7)).astype(np.uint32))
+    assert np.array_equal(b.get(0, h.n_local), np.sin(ids.astype(np.float64) * 0.37 + 7))
+    # a Cartesian file reads back without a block
+    g.set_geometry_block(b"")
+    g.save_grid_data(tmp_path / "cart.dc")
+    k = dccrg_amd.Dccrg(0, 1, 0)
+    for n, t in (("a", np.uint32), ("b", np.float64)):
+        k.add_field(n, t)
+    k.add_field("c", np.float64, False)
+    k.load_grid_data(tmp_path / "cart.dc")
+    assert k.geometry_block() == b""
+    with pytest.raises(dccrgx_error()):
+        g.set_geometry_block(block[:-8])  # the counts promise one more coordinate
+    for x in (g, h, k):
+        x.close()
+
+
+def dccrgx_error():
+    return dccrg_amd.DccrgError

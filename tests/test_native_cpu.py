@@ -26,7 +26,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_error_string():
     L = dccrg_amd.lib()
-    assert L.dccrgx_abi_version() == 9
+    assert L.dccrgx_abi_version() == 10
     assert isinstance(L.dccrgx_last_error(), bytes)
 
 

@@ -225,6 +225,147 @@ __global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t
 	}
 }
 
+// gol_structured_v3 with YR consecutive y rows per wave (DCCRGX_GOL_YR=2 or
+// 4, an A/B): a plane's YR + 2 rows are loaded once per wave for YR output
+// rows (v3: 3 row loads per output row), so the L2 reads of the y+-1 rows
+// drop from 12 B to 4 (YR + 2) / YR B per cell.  Same sums, same states.
+template <int DEPTH, int YR>
+__global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_yr(const uint32_t* __restrict__ st,
+                                                                 uint32_t* __restrict__ out, int nx, int ny, int nz,
+                                                                 int px, int py, int pz, int zc, unsigned nbx,
+                                                                 unsigned nby, unsigned nb,
+                                                                 const uint32_t* __restrict__ lo,
+                                                                 const uint32_t* __restrict__ hi) {
+	constexpr int NR = YR + 2;
+	const unsigned per_xcd = gridDim.x >> 3;
+	const unsigned L = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+	if (L >= nb) return;  // block-uniform
+	const unsigned bx = L % nbx, r = L / nbx, by = r % nby, bz = r / nby;
+	const int lane = threadIdx.x & 63;
+	const int y0 = (int(by) * G3_ROWS + int(threadIdx.x >> 6)) * YR;
+	if (y0 >= ny) return;  // wave-uniform
+	const int x0 = int(bx) * 256;
+	const int x = x0 + 4 * lane;
+	// row i of a plane is y0 - 1 + i, wrapped or absent (-1)
+	size_t orow[NR];
+	bool rin[NR];
+#pragma unroll
+	for (int i = 0; i < NR; i++) {
+		int y = y0 - 1 + i;
+		bool in = true;
+		if (y < 0) {
+			if (py) y += ny;
+			else in = false;
+		} else if (y >= ny) {
+			if (py) y -= ny;
+			else in = false;
+		}
+		rin[i] = in;
+		orow[i] = in ? size_t(y) * nx : 0;
+	}
+	int xe = -1;
+	if (lane == 0) xe = x0 > 0 ? x0 - 1 : (px ? nx - 1 : -1);
+	if (lane == 63) xe = x0 + 256 < nx ? x0 + 256 : (px ? 0 : -1);
+	const size_t plane = size_t(nx) * ny;
+	struct P {
+		uint4 v[NR];
+		uint32_t e[NR];
+	};
+	auto load = [&](int z, P& Q) {
+#pragma unroll
+		for (int i = 0; i < NR; i++) {
+			Q.v[i] = make_uint4(0, 0, 0, 0);
+			Q.e[i] = 0;
+		}
+		const uint32_t* p;
+		if (z < 0) p = lo ? lo : (pz ? st + size_t(z + nz) * plane : nullptr);
+		else if (z >= nz) p = hi ? hi : (pz ? st + size_t(z - nz) * plane : nullptr);
+		else p = st + size_t(z) * plane;
+		if (!p) return;
+#pragma unroll
+		for (int i = 0; i < NR; i++)
+			if (rin[i]) Q.v[i] = *reinterpret_cast<const uint4*>(p + orow[i] + x);
+		if (xe >= 0) {
+#pragma unroll
+			for (int i = 0; i < NR; i++)
+				if (rin[i]) Q.e[i] = p[orow[i] + xe];
+		}
+	};
+	// per output row k the in-plane 3x3 sums at this lane's 4 x
+	auto psum = [&](const P& Q, uint32_t s[YR][4]) {
+		uint32_t c[NR][4], ce[NR];
+#pragma unroll
+		for (int i = 0; i < NR; i++) {
+			c[i][0] = Q.v[i].x > 0;
+			c[i][1] = Q.v[i].y > 0;
+			c[i][2] = Q.v[i].z > 0;
+			c[i][3] = Q.v[i].w > 0;
+			ce[i] = Q.e[i] > 0;
+		}
+#pragma unroll
+		for (int k = 0; k < YR; k++) {
+			const uint32_t c0 = c[k][0] + c[k + 1][0] + c[k + 2][0], c1 = c[k][1] + c[k + 1][1] + c[k + 2][1],
+			               c2 = c[k][2] + c[k + 1][2] + c[k + 2][2], c3 = c[k][3] + c[k + 1][3] + c[k + 2][3];
+			const uint32_t cee = ce[k] + ce[k + 1] + ce[k + 2];
+			uint32_t l = __shfl_up(c3, 1, 64), rr = __shfl_down(c0, 1, 64);
+			if (lane == 0) l = cee;
+			if (lane == 63) rr = cee;
+			s[k][0] = l + c0 + c1;
+			s[k][1] = c0 + c1 + c2;
+			s[k][2] = c1 + c2 + c3;
+			s[k][3] = c2 + c3 + rr;
+		}
+	};
+	const int z0 = int(bz) * zc;
+	const int z1 = min(z0 + zc, nz);
+	P A, Q[DEPTH];
+	uint32_t sp[YR][4], sc[YR][4], sn[YR][4];
+	uint4 cur[YR];
+	load(z0 - 1, A);
+	psum(A, sp);
+	load(z0, A);
+	psum(A, sc);
+#pragma unroll
+	for (int k = 0; k < YR; k++) cur[k] = A.v[k + 1];
+#pragma unroll
+	for (int i = 0; i < DEPTH; i++)
+		if (z0 + 1 + i <= z1) load(z0 + 1 + i, Q[i]);
+	for (int z = z0; z < z1; z++) {
+		P E = Q[DEPTH - 1];
+		if (z + 1 + DEPTH <= z1) load(z + 1 + DEPTH, E);
+		psum(Q[0], sn);
+#pragma unroll
+		for (int k = 0; k < YR; k++) {
+			if (y0 + k >= ny) continue;
+			uint4 o;
+			uint32_t cnt;
+			cnt = sp[k][0] + sc[k][0] + sn[k][0] - (cur[k].x > 0);
+			o.x = cnt == 3 ? 1u : (cnt == 2 ? cur[k].x : 0u);
+			cnt = sp[k][1] + sc[k][1] + sn[k][1] - (cur[k].y > 0);
+			o.y = cnt == 3 ? 1u : (cnt == 2 ? cur[k].y : 0u);
+			cnt = sp[k][2] + sc[k][2] + sn[k][2] - (cur[k].z > 0);
+			o.z = cnt == 3 ? 1u : (cnt == 2 ? cur[k].z : 0u);
+			cnt = sp[k][3] + sc[k][3] + sn[k][3] - (cur[k].w > 0);
+			o.w = cnt == 3 ? 1u : (cnt == 2 ? cur[k].w : 0u);
+			typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+			u4v ov = {o.x, o.y, o.z, o.w};
+			__builtin_nontemporal_store(ov, reinterpret_cast<u4v*>(out + size_t(z) * plane + size_t(y0 + k) * nx + x));
+		}
+#pragma unroll
+		for (int k = 0; k < YR; k++) {
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				sp[k][i] = sc[k][i];
+				sc[k][i] = sn[k][i];
+			}
+			cur[k] = Q[0].v[k + 1];
+		}
+#pragma unroll
+		for (int i = 0; i + 1 < DEPTH; i++) Q[i] = Q[i + 1];
+		Q[DEPTH - 1] = E;
+	}
+}
+
 // ---------------------------------------------------------------------------
 // Face flux without the division by the cell volume (applied once per cell):
 // the face velocity and the upwind flux keep the reference's expression
@@ -1825,6 +1966,25 @@ bool k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 	// 64 planes per z chunk, 3 planes of loads in flight per wave (r01g/r01j
 	// sweeps over zc and the depth on config 2)
 	const int zc = int(std::min<uint64_t>(n[2], 64));
+	static const int yr = std::getenv("DCCRGX_GOL_YR") ? std::atoi(std::getenv("DCCRGX_GOL_YR")) : 1;
+	static const int ydepth = std::getenv("DCCRGX_GOL_YDEPTH") ? std::atoi(std::getenv("DCCRGX_GOL_YDEPTH")) : 2;
+	if (yr == 2 || yr == 4) {
+		const unsigned rows = unsigned(G3_ROWS * yr);
+		const unsigned nbx = unsigned(n[0] / 256), nby = unsigned((n[1] + rows - 1) / rows),
+		               nbz = unsigned((n[2] + zc - 1) / zc);
+		const size_t nb = size_t(nbx) * nby * nbz;
+		const unsigned grid = unsigned((nb + 7) / 8 * 8);
+#define DX_GOL_YR(D, Y)                                                                                                   \
+	gol_structured_yr<D, Y><<<grid, 64 * G3_ROWS, 0, s>>>(state, out, int(n[0]), int(n[1]), int(n[2]), per[0], per[1], \
+	                                                      per[2], zc, nbx, nby, unsigned(nb), lo, hi)
+		if (yr == 2 && ydepth == 3) DX_GOL_YR(3, 2);
+		else if (yr == 2) DX_GOL_YR(2, 2);
+		else if (ydepth == 1) DX_GOL_YR(1, 4);
+		else DX_GOL_YR(2, 4);
+#undef DX_GOL_YR
+		HIP_CHECK(hipGetLastError());
+		return true;
+	}
 	const unsigned nbx = unsigned(n[0] / 256), nby = unsigned((n[1] + G3_ROWS - 1) / G3_ROWS),
 	               nbz = unsigned((n[2] + zc - 1) / zc);
 	const size_t nb = size_t(nbx) * nby * nbz;

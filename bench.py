@@ -290,7 +290,7 @@ def gol_main(a, dccrgx_mod, torch, dist, rank, world, uid):
                                       f"{', z slabs' if world > 1 else ''})", "cells_rank0": n}, g=g)
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS, "traffic": measured_traffic("gol", n, 8 * n, world),
-                            "kernel": "gol_structured_v3",
+                            "kernel": "gol_structured_yr<2, 2> (gol_structured_v3 with two rows per wave)",
                             "alg_bytes_per_step": 8 * n, "kernel_ms_per_step": kms / a.steps}
         line["cpu_baseline"] = None if (a.no_cpu_baseline or world > 1) else cpu_baseline("gol", a.cpu_seconds)
         print(json.dumps(line), flush=True)
@@ -575,7 +575,7 @@ def scalability_main(a, dccrgx_mod, torch, dist, rank, world, uid):
         line["roofline"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": ach / PEAK_HBM_GBS if ach else None,
                             "traffic": measured_traffic("scalability", n, 8 * n, world),
-                            "kernel": "gol_structured_v3 (plane boxes)", "alg_bytes_per_step": 8 * n,
+                            "kernel": "gol_structured_yr<2, 2> (plane boxes)", "alg_bytes_per_step": 8 * n,
                             "kernel_ms_per_step": kms / a.steps}
         halo = {"ms_per_exchange_4B": mx[3] * 1e3, "ms_per_exchange_1B": mx[4] * 1e3,
                 "send_cells_max_rank": mx[6], "peers_rank0": peers}

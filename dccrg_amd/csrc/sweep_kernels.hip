@@ -225,8 +225,8 @@ __global__ __launch_bounds__(64 * G3_ROWS) void gol_structured_v3(const uint32_t
 	}
 }
 
-// gol_structured_v3 with YR consecutive y rows per wave (DCCRGX_GOL_YR=2 or
-// 4, an A/B): a plane's YR + 2 rows are loaded once per wave for YR output
+// gol_structured_v3 with YR consecutive y rows per wave (YR = 2 the default,
+// DCCRGX_GOL_YR=4 / 1 for A/Bs): a plane's YR + 2 rows are loaded once per wave for YR output
 // rows (v3: 3 row loads per output row), so the L2 reads of the y+-1 rows
 // drop from 12 B to 4 (YR + 2) / YR B per cell.  Same sums, same states.
 template <int DEPTH, int YR>
@@ -1966,7 +1966,9 @@ bool k_gol_structured(const uint32_t* state, uint32_t* out, const uint64_t n[3],
 	// 64 planes per z chunk, 3 planes of loads in flight per wave (r01g/r01j
 	// sweeps over zc and the depth on config 2)
 	const int zc = int(std::min<uint64_t>(n[2], 64));
-	static const int yr = std::getenv("DCCRGX_GOL_YR") ? std::atoi(std::getenv("DCCRGX_GOL_YR")) : 1;
+	// two rows per wave by default (paired A/B on config 2, profiles/r06ze_gol_yr_ab.txt:
+	// 0.1118 -> 0.1083 ms per sweep; four rows: 185 VGPRs, slower); DCCRGX_GOL_YR=1: v3
+	static const int yr = std::getenv("DCCRGX_GOL_YR") ? std::atoi(std::getenv("DCCRGX_GOL_YR")) : 2;
 	static const int ydepth = std::getenv("DCCRGX_GOL_YDEPTH") ? std::atoi(std::getenv("DCCRGX_GOL_YDEPTH")) : 2;
 	if (yr == 2 || yr == 4) {
 		const unsigned rows = unsigned(G3_ROWS * yr);

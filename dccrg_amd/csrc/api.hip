@@ -156,6 +156,7 @@ static PoArrays po_arrays(Grid& g) {
 	a.ap0 = d(P.ap0);
 	a.sf = d(P.sf);
 	for (int k = 0; k < 6; k++) a.f[k] = d(P.f[k]);
+	a.ft = P.valid && P.ft.p ? P.ft.p : nullptr;
 	return a;
 }
 
@@ -205,6 +206,16 @@ static void po_cache(Grid& g, int rhs, int sol, const uint64_t* solve, size_t ns
 	std::vector<int> geo{P.sf};  // GEOMETRY (969-970)
 	for (int k = 0; k < 6; k++) geo.push_back(P.f[k]);
 	halo_only(g, geo);
+	// the neighbors' factors toward each cell, once per cache pass (phase B
+	// reads them coalesced instead of gathering them every iteration;
+	// DCCRGX_PO_FT=0 keeps the gathers)
+	const char* ftv = std::getenv("DCCRGX_PO_FT");
+	if (!(ftv && ftv[0] == '0') && nl) {
+		P.ft.alloc(6 * nl);
+		k_po_transpose(po_arrays(g), nl, P.ft.p, s);
+	} else {
+		P.ft.release();
+	}
 	HIP_CHECK(hipStreamSynchronize(s));
 	P.valid = true;
 }

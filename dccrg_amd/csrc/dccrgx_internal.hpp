@@ -356,6 +356,10 @@ struct PoArrays {
 	const double* rhs;
 	double *sol, *best, *p0, *p1, *r0, *r1, *ap0, *sf;
 	double* f[6];  // f_x_neg, f_x_pos, f_y_neg, f_y_pos, f_z_neg, f_z_pos
+	// ft[dir * n + s]: the same-size / coarser neighbor's factor toward s
+	// (f[dir ^ 1][ell[6 s + dir]]), gathered once per cache pass for phase B's
+	// transpose product (null: phase B gathers it)
+	const double* ft;
 };
 
 struct PoParams {  // Poisson_Solve constructor, poisson_solve.hpp:187-201
@@ -379,6 +383,7 @@ struct PoissonState {
 	int type = -1;             // int32 field: classification / final type
 	int p0 = -1, p1 = -1, r0 = -1, r1 = -1, ap0 = -1, best = -1, sf = -1, f[6] = {-1, -1, -1, -1, -1, -1};
 	DBuf<int32_t> ell, fine;
+	DBuf<double> ft;               // PoArrays::ft
 	DBuf<double> part, red, gath;  // gath: P x 2 all-gathered per-rank sums
 	DBuf<PoScalars> st;
 	size_t n_cached = 0;       // local cells in cell_info
@@ -1093,6 +1098,7 @@ void k_gol_amr(int phase, GolAmrTables& T, size_t n_slots, size_t n_local, uint3
 
 // --- launchers implemented in poisson_kernels.hip ---------------------------
 unsigned k_po_blocks(size_t n);  // blocks (= partials) of a phase launch over n slots
+void k_po_transpose(const PoArrays& a, size_t n, double* ft, hipStream_t s);
 void k_po_cache(const MapCtx& m, const double l0[3], const uint64_t* slot_ids, const int32_t* cls,
                 const int32_t* face_ell, const int32_t* face_fine, size_t n, int32_t* po_ell, int32_t* po_fine,
                 int32_t* type, const PoArrays& a, hipStream_t s);

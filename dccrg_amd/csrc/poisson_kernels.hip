@@ -251,7 +251,7 @@ __global__ void po_phase_b_kernel(PoArrays a, size_t n, const PoScalars* st, dou
 			for (int dir = 0; dir < 6; dir++) ev[dir] = a.ell[6 * s + dir];
 #pragma unroll
 			for (int dir = 0; dir < 6; dir++) {
-				fv[dir] = ev[dir] >= 0 ? a.f[dir ^ 1][ev[dir]] : 0.0;
+				fv[dir] = ev[dir] >= 0 ? (a.ft ? a.ft[size_t(dir) * n + s] : a.f[dir ^ 1][ev[dir]]) : 0.0;
 				pv[dir] = ev[dir] >= 0 ? a.p1[ev[dir]] : 0.0;
 			}
 #pragma unroll
@@ -278,6 +278,18 @@ __global__ void po_phase_b_kernel(PoArrays a, size_t n, const PoScalars* st, dou
 		}
 	}
 	block_sum_store<1>(v, part);
+}
+
+// PoArrays::ft: per local cell and direction the single neighbor's factor in
+// the reversed direction (0 where there is none or it is finer)
+__global__ void po_transpose_kernel(PoArrays a, size_t n, double* __restrict__ ft) {
+	const size_t s = size_t(xcd_block()) * BS + threadIdx.x;
+	if (s >= n) return;
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) {
+		const int32_t e = a.ell[6 * s + dir];
+		ft[size_t(dir) * n + s] = e >= 0 ? a.f[dir ^ 1][e] : 0.0;
+	}
 }
 
 // p0 = r0 + beta p0, p1 = r1 + beta p1 (497-504)
@@ -473,6 +485,12 @@ void k_po_cache(const MapCtx& m, const double l0[3], const uint64_t* slot_ids, c
 	if (!n) return;
 	po_cache_kernel<<<po_blocks(n), BS, 0, s>>>(m, l0[0], l0[1], l0[2], slot_ids, cls, face_ell, face_fine, n, po_ell,
 	                                            po_fine, type, a);
+	HIP_CHECK(hipGetLastError());
+}
+
+void k_po_transpose(const PoArrays& a, size_t n, double* ft, hipStream_t s) {
+	if (!n) return;
+	po_transpose_kernel<<<po_blocks(n), BS, 0, s>>>(a, n, ft);
 	HIP_CHECK(hipGetLastError());
 }
 

@@ -1141,9 +1141,17 @@ __global__ void kept_ordered_kernel(DevMesh M, const uint64_t* __restrict__ ch, 
 	}
 }
 
+// bits 0-4: the level; bits 5-7: the cell's octant in its parent (bit k set
+// when its index along axis k is odd at its level; 0 at level 0), which is
+// the corner test of adapter.hpp:84-102 without the cell's indices
 __global__ void slot_levels_kernel(MapCtx m, const uint64_t* slot_ids, size_t n, uint8_t* lvl) {
-	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-		lvl[i] = uint8_t(map_level(m, slot_ids[i]));
+	for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
+		uint64_t x, y, z;
+		const int l = map_indices(m, slot_ids[i], x, y, z);
+		const int sh = m.R - l;
+		const unsigned oct = l ? unsigned(((x >> sh) & 1) | (((y >> sh) & 1) << 1) | (((z >> sh) & 1) << 2)) : 0u;
+		lvl[i] = uint8_t(unsigned(l) | (oct << 5));
+	}
 }
 
 }  // namespace

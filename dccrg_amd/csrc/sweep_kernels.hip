@@ -505,6 +505,7 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 		double cd = 0, clx = 1, cly = 1, clz = 1, cvx = 0, cvy = 0, cvz = 0;
 		int32_t e6[6] = {-1, -1, -1, -1, -1, -1};
 		int lvl = 0;
+		unsigned oct = 0;
 		if (live) {
 			cd = rho[s];
 			clx = lx[s];
@@ -513,7 +514,11 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 			cvx = vx[s];
 			cvy = vy[s];
 			cvz = vz[s];
-			if (BANDS) lvl = B.lvl8[s];
+			if (BANDS) {
+				const unsigned v = B.lvl8[s];
+				lvl = int(v & 31u);
+				oct = v >> 5;
+			}
 			const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
 #pragma unroll
 			for (int j = 0; j < 3; j++) {
@@ -543,8 +548,6 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 			return AdvNb{rho[n], lx[n], ly[n], lz[n], nv};
 		};
 		double acc = 0, md = 0;
-		bool have_c = false;
-		uint64_t c3[3] = {0, 0, 0};
 		auto band_cmp = [&](double b) {
 			const double diff = fabs(cd - b) / (fmin(cd, b) + B.thr);
 			md = fmax(diff, md);
@@ -558,19 +561,10 @@ __global__ __launch_bounds__(256) void advection_ell_lds_kernel(
 				acc += adv_face_flux_d(dir, cd, clx, cly, clz, cvx, cvy, cvz, q, dt);
 				if (BANDS) {
 					const uint32_t k = uint32_t(int64_t(c) - int64_t(b0));
-					const int nl = k < nb_in ? int(slv[k]) : int(B.lvl8[c]);
-					bool use = true;
-					if (nl < lvl) {
-						if (!have_c) {
-							map_indices(B.m, B.slot_ids[s], c3[0], c3[1], c3[2]);
-							have_c = true;
-						}
-						const uint64_t pl = (uint64_t(1) << (B.m.R - lvl)) * 2;
-						const int d = dir >> 1;
-						for (int kk = 0; kk < 3; kk++)
-							if (kk != d && (c3[kk] & (pl - 1)) != 0) use = false;
-					}
-					if (use) band_cmp(q.d);
+					const int nl = k < nb_in ? int(slv[k]) : int(B.lvl8[c] & 31u);
+					// coarser: only from the corner of its face, i.e. the
+					// cell's octant bits across the face axis are zero
+					if (nl >= lvl || (oct & ~(1u << (dir >> 1))) == 0) band_cmp(q.d);
 				}
 			} else {
 				const i4v q = *reinterpret_cast<const i4v*>(fine + 4 * size_t(-2 - c));
@@ -1564,7 +1558,9 @@ __device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const i
                                const int32_t* __restrict__ fine, const uint8_t* __restrict__ lvl8,
                                const uint64_t* __restrict__ slot_ids, size_t s, double diff_threshold, int& lvl) {
 	typedef int i2v __attribute__((ext_vector_type(2)));
-	lvl = lvl8[s];
+	const unsigned lv = lvl8[s];
+	lvl = int(lv & 31u);
+	const unsigned oct = lv >> 5;
 	int32_t e6[6];
 	const i2v* ev = reinterpret_cast<const i2v*>(ell + 6 * s);
 #pragma unroll
@@ -1575,8 +1571,6 @@ __device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const i
 	}
 	const double a = rho[s];
 	double md = 0;
-	bool have_c = false;
-	uint64_t c[3] = {0, 0, 0};
 #pragma unroll
 	for (int dir = 0; dir < 6; dir++) {
 		const int32_t e = e6[dir];
@@ -1584,18 +1578,8 @@ __device__ double adv_max_diff(MapCtx m, const double* __restrict__ rho, const i
 		int32_t nsl;
 		if (e >= 0) {
 			nsl = e;
-			if (int(lvl8[e]) < lvl) {
-				if (!have_c) {
-					map_indices(m, slot_ids[s], c[0], c[1], c[2]);
-					have_c = true;
-				}
-				const uint64_t pl = (uint64_t(1) << (m.R - lvl)) * 2;
-				const int d = dir >> 1;
-				bool zero = true;
-				for (int k = 0; k < 3; k++)
-					if (k != d && (c[k] & (pl - 1)) != 0) zero = false;
-				if (!zero) continue;
-			}
+			// coarser: only when the cell sits at the corner of its face
+			if (int(lvl8[e] & 31u) < lvl && (oct & ~(1u << (dir >> 1))) != 0) continue;
 		} else {
 			nsl = fine[4 * size_t(-2 - e)];
 		}

@@ -568,9 +568,56 @@ __device__ __forceinline__ uint64_t morton3(const uint64_t c[3]) {
 // is predicted at the row its Morton distance away - exact whenever every
 // leaf between the two has that size - and taken when the row holds its id:
 // a same-size leaf is the one face neighbor in that direction (no finer or
-// coarser probe needed).  Otherwise, and for the misses, the probes of
-// face_dir.  The table is the same either way.  The loop runs whole waves
-// (wave_reserve needs every lane).
+// coarser probe needed).  o6[dir] = -1 (no face neighbor), the predicted row,
+// or kFaceMiss (the probes of face_dir decide).
+constexpr int32_t kFaceMiss = -3;
+__device__ __forceinline__ void face_predict(const MapCtx& m, const uint64_t* __restrict__ slot_ids, size_t r,
+                                             size_t run1, size_t nrows, uint64_t id, const uint64_t c[3], int lvl,
+                                             int32_t o6[6]) {
+	int32_t h[6];
+	uint64_t want[6], got[6];
+	bool probe[6];
+	const int sh = 3 * (m.R - lvl);
+	const uint64_t len = uint64_t(1) << (m.R - lvl);
+	const uint64_t key = morton3(c) >> sh;
+	const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
+	// the neighbor's id and Morton key from this cell's: one step along d is
+	// +-stride[d] in the id and a dilated +-1 in the key (no re-interleave,
+	// no index -> id products); a periodic wrap takes the general form
+	const uint64_t lx = m.len[0] << lvl, ly = m.len[1] << lvl;
+	const uint64_t stride[3] = {1, lx, lx * ly};
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) {
+		const int d = dir >> 1;
+		uint64_t p[3];
+		h[dir] = -1;
+		want[dir] = ~uint64_t(0);
+		probe[dir] = face_probe(m, c, lvl, dir, p);
+		if (!probe[dir]) continue;
+		p[d] &= ~(len - 1);  // the other two are c's, aligned
+		const uint64_t M = uint64_t(0x1249249249249249ull) << d, u = uint64_t(1) << d;
+		uint64_t nkey;
+		if ((dir & 1) ? p[d] == c[d] + len : p[d] + len == c[d])
+			nkey = (dir & 1) ? ((((key | ~M) + u) & M) | (key & ~M)) : ((((key & M) - u) & M) | (key & ~M));
+		else
+			nkey = morton3(p) >> sh;
+		const int64_t q = int64_t(r) + (int64_t(nkey) - int64_t(key));
+		if (q >= lo && q < hi) {
+			h[dir] = int32_t(q);
+			want[dir] = id + ((p[d] >> (m.R - lvl)) - (c[d] >> (m.R - lvl))) * stride[d];
+		}
+	}
+	// the six row loads in flight together
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
+#pragma unroll
+	for (int dir = 0; dir < 6; dir++)
+		o6[dir] = !probe[dir] ? -1 : (h[dir] >= 0 && got[dir] == want[dir] ? h[dir] : kFaceMiss);
+}
+
+// One thread per row: the predictions, then face_dir's probes for the
+// directions they leave open.  The loop runs whole waves (wave_reserve needs
+// every lane).
 // chunk_keys (non-null): a wave's 64 rows are one chunk (r / 64); its finer
 // faces' keys go to chunk_keys[384 c ...] in (row, direction) order and
 // their number to chunk_cnt[c], so a scan of the counts numbers every finer
@@ -590,57 +637,10 @@ __global__ void face_table_kernel(MapCtx m, DevMesh M, const uint64_t* slot_ids,
 			int lvl;
 			const uint64_t id = slot_ids[r];
 			cell_coords(m, id, c, lvl);
-			// the six predictions first, their six row loads in flight together
-			int32_t h[6];
-			uint64_t want[6], got[6];
-			bool probe[6];
-			if (morton) {
-				const int sh = 3 * (m.R - lvl);
-				const uint64_t len = uint64_t(1) << (m.R - lvl);
-				const uint64_t key = morton3(c) >> sh;
-				const int64_t lo = r < run1 ? 0 : int64_t(run1), hi = r < run1 ? int64_t(run1) : int64_t(nrows);
-				// the neighbor's id and Morton key from this cell's: one step
-				// along d is +-stride[d] in the id and a dilated +-1 in the key
-				// (no re-interleave, no index -> id products); a periodic wrap
-				// takes the general form
-				const uint64_t lx = m.len[0] << lvl, ly = m.len[1] << lvl;
-				const uint64_t stride[3] = {1, lx, lx * ly};
-#pragma unroll
-				for (int dir = 0; dir < 6; dir++) {
-					const int d = dir >> 1;
-					uint64_t p[3];
-					h[dir] = -1;
-					want[dir] = ~uint64_t(0);
-					probe[dir] = face_probe(m, c, lvl, dir, p);
-					if (!probe[dir]) continue;
-					p[d] &= ~(len - 1);  // the other two are c's, aligned
-					const uint64_t M = uint64_t(0x1249249249249249ull) << d, u = uint64_t(1) << d;
-					uint64_t nkey;
-					if ((dir & 1) ? p[d] == c[d] + len : p[d] + len == c[d])
-						nkey = (dir & 1) ? ((((key | ~M) + u) & M) | (key & ~M)) : ((((key & M) - u) & M) | (key & ~M));
-					else
-						nkey = morton3(p) >> sh;
-					const int64_t q = int64_t(r) + (int64_t(nkey) - int64_t(key));
-					if (q >= lo && q < hi) {
-						h[dir] = int32_t(q);
-						want[dir] = id + ((p[d] >> (m.R - lvl)) - (c[d] >> (m.R - lvl))) * stride[d];
-					}
-				}
-#pragma unroll
-				for (int dir = 0; dir < 6; dir++) got[dir] = h[dir] >= 0 ? slot_ids[h[dir]] : 0;
-			}
+			if (morton) face_predict(m, slot_ids, r, run1, nrows, id, c, lvl, o6);
 #pragma unroll
 			for (int dir = 0; dir < 6; dir++) {
-				if (morton) {
-					if (!probe[dir]) {
-						o6[dir] = -1;
-						continue;
-					}
-					if (h[dir] >= 0 && got[dir] == want[dir]) {
-						o6[dir] = h[dir];
-						continue;
-					}
-				}
+				if (morton && o6[dir] != kFaceMiss) continue;
 				uint64_t out[4];
 				const int nf = face_dir(m, c, lvl, dir, ex, out);
 				// a single neighbor was the last cell found (face_dir returns on it)

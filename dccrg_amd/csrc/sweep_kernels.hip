@@ -2198,8 +2198,21 @@ AdvRequests k_adv_requests(const MapCtx& m, const DevMesh& dm, const uint64_t* s
 	part.alloc(n);
 	cnt.alloc(4);
 	HIP_CHECK(hipMemsetAsync(cnt.p, 0, 4 * sizeof(unsigned long long), s));
-	adv_requests_kernel<1024><<<unsigned((n + 1024 * 8 - 1) / (1024 * 8)), 1024, 0, s>>>(m, dm, slot_ids, band, n, solo,
-	                                                                                    rank, ref.p, unref.p, part.p, cnt.p);
+	// 512 threads (4096 slots, 37 KB of LDS, four blocks per CU): a config-3
+	// step's ~2100 blocks end in a shorter partial last round than 1024's
+	// ~1050 two-per-CU blocks (122 -> 92 us; r06zj_requests_bs_ab.txt).
+	// DCCRGX_REQ_BS=256 / 1024: the other sizes measured
+	const char* rb = std::getenv("DCCRGX_REQ_BS");
+	const int bs = rb && *rb ? std::atoi(rb) : 512;
+	if (bs == 256)
+		adv_requests_kernel<256><<<unsigned((n + 256 * 8 - 1) / (256 * 8)), 256, 0, s>>>(m, dm, slot_ids, band, n, solo,
+		                                                                                rank, ref.p, unref.p, part.p, cnt.p);
+	else if (bs == 512)
+		adv_requests_kernel<512><<<unsigned((n + 512 * 8 - 1) / (512 * 8)), 512, 0, s>>>(m, dm, slot_ids, band, n, solo,
+		                                                                                rank, ref.p, unref.p, part.p, cnt.p);
+	else
+		adv_requests_kernel<1024><<<unsigned((n + 1024 * 8 - 1) / (1024 * 8)), 1024, 0, s>>>(m, dm, slot_ids, band, n, solo,
+		                                                                                    rank, ref.p, unref.p, part.p, cnt.p);
 	HIP_CHECK(hipGetLastError());
 	unsigned long long h[4];
 	d2h_small(h, cnt.p, sizeof(h), s);
